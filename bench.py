@@ -1,0 +1,184 @@
+"""Benchmark: ForwardTacotron.generate() mel-frames/s on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
+
+Workload (BASELINE.json configs[2], "c3"): ForwardTacotron LJSpeech config, batch = 64
+synthetic phoneme sequences per GPU (lengths U{50..200}, ids U{1..134}, pad 0; seed =
+rank), synthetic weights (forwardtacotron_amd.synthetic, no checkpoint download), fp32.
+A step is one full `generate()` call on one batch whose tokens are already resident in HBM
+(pitch / energy identity callbacks, alpha = 1).  Frames = B * T_mel of the returned
+mel_post (padded frames, as the reference returns them).
+
+Multi-GPU: each rank runs its own batch of 64 utterances (weak scaling, no data-path
+collective: utterances are independent); barrier + synchronize around the K timed steps,
+max elapsed over ranks, value = all frames of all ranks / that time.
+
+The JSON line also carries
+  roofline     the dominant kernel (largest device time inside the timed steps, measured
+               with HIP events on the launch stream): algorithmic FLOPs (or bytes) per launch
+               / its average duration, against the fp32 MFMA (or HBM) peak of MI355X;
+  cpu_baseline rank 0, N = 1: the torch-CPU restatement of the reference (oracle/
+               ft_torch_cpu.py, same ATen CPU kernels as the reference) on the same batch;
+  parity       mean / max |mel_post GPU - CPU| on that batch, and LR counts equality.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from forwardtacotron_amd.forward_tacotron import ForwardTacotron  # noqa: E402
+from forwardtacotron_amd.probe import KernelProbe  # noqa: E402
+from forwardtacotron_amd.synthetic import default_config, synthetic_state_dict, synthetic_tokens  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA == vector rate), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--batch', type=int, default=64)
+    ap.add_argument('--tmax', type=int, default=200)
+    ap.add_argument('--tmin', type=int, default=50)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--kernels', action='store_true', help='print the per-kernel table to stderr')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+
+    model = ForwardTacotron.from_config(default_config())
+    sd = synthetic_state_dict(model, seed=0)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model = model.to(dev).eval()
+    x_np = synthetic_tokens(args.batch, args.tmax, seed=rank, min_len=args.tmin)
+    x = torch.from_numpy(x_np).to(dev)
+
+    for _ in range(args.warmup):
+        model.generate(x)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    frames = 0
+    with KernelProbe() as probe:
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = model.generate(x)
+            frames += out['mel_post'].size(0) * out['mel_post'].size(2)
+        torch.cuda.synchronize()
+        barrier()
+        t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern = probe.summary()
+
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        f = torch.tensor([frames], device=dev, dtype=torch.float64)
+        dist.all_reduce(f, op=dist.ReduceOp.SUM)
+        frames = int(f.item())
+
+    if rank == 0:
+        # dominant kernel = largest device time inside the timed region
+        dom_label, dom = max(kern.items(), key=lambda kv: kv[1]['total_ms'])
+        total_dev_ms = sum(v['total_ms'] for v in kern.values())
+        if args.kernels:
+            log(f'{"kernel":60s} {"n":>4s} {"avg ms":>9s} {"share":>6s} {"TFLOP/s":>8s} {"GB/s":>8s}')
+            for lab, v in sorted(kern.items(), key=lambda kv: -kv[1]['total_ms']):
+                s = v['avg_ms'] / 1e3
+                log(f'{lab:60s} {v["launches"]:4d} {v["avg_ms"]:9.3f} {v["total_ms"] / total_dev_ms:6.1%} '
+                    f'{v["flops"] / s / 1e12:8.2f} {v["bytes"] / s / 1e9:8.1f}')
+        s = dom['avg_ms'] / 1e3
+        if dom['flops'] > 0:
+            achieved = dom['flops'] / s / 1e12
+            roof = {'kernel': dom_label, 'bound': 'mfma', 'achieved': round(achieved, 3),
+                    'peak': PEAK_FP32_TFLOPS, 'unit': 'TFLOP/s',
+                    'frac': round(achieved / PEAK_FP32_TFLOPS, 4),
+                    'algorithmic_per_launch': dom['flops'], 'avg_launch_ms': round(dom['avg_ms'], 4),
+                    'launches': dom['launches'], 'share_of_device_time': round(dom['total_ms'] / total_dev_ms, 4),
+                    'traffic': None}
+        else:
+            achieved = dom['bytes'] / s / 1e9
+            roof = {'kernel': dom_label, 'bound': 'hbm', 'achieved': round(achieved, 1),
+                    'peak': PEAK_HBM_GBS, 'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 4),
+                    'algorithmic_per_launch': dom['bytes'], 'avg_launch_ms': round(dom['avg_ms'], 4),
+                    'launches': dom['launches'], 'traffic': None}
+
+        value = frames / elapsed
+        line = {
+            'metric': 'mel-frames/sec at batch=64 LJSpeech shapes (ForwardTacotron.generate, B*T_mel per s)',
+            'value': round(value, 1), 'unit': 'mel-frames/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+            'data': 'synthetic (seeded LJSpeech-shaped phoneme batches, synthetic weights)',
+            'config': {'workload': f'c3: ForwardTacotron generate, batch={args.batch} per GPU, '
+                                   f'phoneme lengths U{{{args.tmin}..{args.tmax}}}',
+                       'global_batch': args.batch * world, 'T_phonemes': int(x_np.shape[1]),
+                       'T_mel': int(out['mel_post'].size(2)), 'parallelism': f'dp{world}'},
+            'roofline': roof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line['cpu_baseline'], line['parity'] = cpu_baseline(sd, x_np, out)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sd, x_np, out):
+    """Time the torch-CPU restatement of the reference on the same batch (bounded: one call)."""
+    from oracle import ft_oracle, ft_torch_cpu
+    sdt = ft_torch_cpu.to_torch(sd)
+    xt = torch.from_numpy(x_np)
+    ft_torch_cpu.generate(sdt, xt[:1, :20])  # warm the CPU kernels
+    t0 = time.perf_counter()
+    ref = ft_torch_cpu.generate(sdt, xt)
+    dt = time.perf_counter() - t0
+    frames = ref['mel_post'].size(0) * ref['mel_post'].size(2)
+    got = out['mel_post'].float().cpu().numpy()
+    r = ref['mel_post'].numpy()
+    same_shape = got.shape == r.shape
+    d = np.abs(got - r) if same_shape else None
+    counts_equal = bool(np.array_equal(ft_oracle.duration_counts(out['dur'].cpu().numpy()),
+                                       ft_oracle.duration_counts(ref['dur'].numpy())))
+    base = {'value': round(frames / dt, 1), 'unit': 'mel-frames/s', 'cores': torch.get_num_threads(),
+            'kind': 'port',
+            'sample': f'one generate() of the same batch ({x_np.shape[0]} x {x_np.shape[1]} phonemes, '
+                      f'T_mel {r.shape[2]}) with oracle/ft_torch_cpu.py (the reference\'s ATen CPU '
+                      f'kernels), {dt:.2f} s'}
+    parity = {'mel_post_mean_abs': float(d.mean()) if same_shape else None,
+              'mel_post_max_abs': float(d.max()) if same_shape else None,
+              'lr_counts_equal': counts_equal}
+    return base, parity
+
+
+if __name__ == '__main__':
+    main()

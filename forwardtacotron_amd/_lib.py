@@ -1,0 +1,89 @@
+"""ctypes binding of libftmi.so (declarations: include/ftmi.h).
+
+The library is loaded lazily on first use.  torch is imported first so that the HIP
+runtime torch ships (SONAME libamdhip64.so.7) is the one libftmi.so binds to: device
+pointers and streams are then shared with torch without any interop layer.
+
+There is no fallback: if the library is missing or fails to load, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+_LIB_PATH = Path(os.environ.get('FTMI_LIB', Path(__file__).resolve().parent / 'libftmi.so'))
+_lib = None
+
+c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+P = c_void_p  # every device pointer travels as void*
+
+
+class ConvArgs(ctypes.Structure):
+    """Mirror of ftmi_conv_args (include/ftmi.h)."""
+    _fields_ = [
+        ('x', P), ('x_stride', c_int64), ('B', c_int), ('T', c_int), ('Cin', c_int),
+        ('w', P), ('N', c_int), ('k', c_int), ('pad', c_int),
+        ('bias', P), ('relu', c_int), ('bn_scale', P), ('bn_shift', P), ('maxpool', c_int),
+        ('residual', P), ('res_stride', c_int64),
+        ('y', P), ('y_stride', c_int64), ('yt', P), ('T_out', c_int),
+    ]
+
+
+# name -> (restype, argtypes); the exact export list of include/ftmi.h
+SIGNATURES = {
+    'ftmi_abi_version': (c_int, []),
+    'ftmi_strerror': (ctypes.c_char_p, [c_int]),
+    'ftmi_embedding': (c_int, [P, c_int64, P, c_int64, c_int64, P, P, P]),
+    'ftmi_conv1d': (c_int, [ctypes.POINTER(ConvArgs), P]),
+    'ftmi_conv_bank': (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, c_int, P, P, P, c_int64, P]),
+    'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, c_int64, P]),
+    'ftmi_rnn_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
+    'ftmi_rnn_error_offset': (c_int64, [c_int]),
+    'ftmi_rnn_bidir': (c_int, [c_int, c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,
+                               c_float, P, c_int64, P, P]),
+    'ftmi_duration_counts': (c_int, [P, c_int, c_int, c_int, c_float, P, P, P, P]),
+    'ftmi_lr_index': (c_int, [P, c_int, c_int, c_int, P, P]),
+    'ftmi_length_regulate': (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, P, c_int64, P]),
+    'ftmi_series_proj_add': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, P, c_float, P, P, P,
+                                     c_float, P]),
+    'ftmi_rowdot': (c_int, [P, c_int64, c_int64, c_int, P, P, c_float, P, P]),
+}
+
+
+class FtmiError(RuntimeError):
+    pass
+
+
+def lib_path() -> Path:
+    return _LIB_PATH
+
+
+def load():
+    """Load libftmi.so and bind every exported symbol; raises if anything is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not _LIB_PATH.exists():
+        raise FtmiError(f'libftmi.so not found at {_LIB_PATH}; run `python -m forwardtacotron_amd.build` '
+                        '(there is no CPU fallback)')
+    lib = ctypes.CDLL(str(_LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError if the export is missing
+        fn.restype = res
+        fn.argtypes = args
+    if lib.ftmi_abi_version() != 1:
+        raise FtmiError('libftmi.so ABI version mismatch')
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    """Invoke an ftmi entry point and raise FtmiError on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.ftmi_strerror(rc).decode()
+        raise FtmiError(f'{name} failed with status {rc}: {msg}')

@@ -1,0 +1,279 @@
+"""Layers of the reference (`models/common_layers.py`, `models/forward_tacotron.py:14-71`)
+re-built on libftmi.so.
+
+Every module declares exactly the parameters / buffers of its reference counterpart, under
+the same names, so ``state_dict()`` keys and shapes are identical and reference checkpoints
+load with ``load_state_dict`` unchanged.  The modules hold no torch compute layers: the
+math runs in HIP kernels through :mod:`forwardtacotron_amd.ops`.
+
+Internally activations are channels-last (B, T, C) (``*_cl`` methods).  The public
+``forward`` methods keep the reference's argument layout and return values so they can be
+used (and tested) one layer at a time.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+
+# --------------------------------------------------------------------------------------
+# parameter holders (same tensors as nn.Conv1d / nn.BatchNorm1d / nn.Linear / nn.GRU / nn.LSTM)
+
+
+def _uniform_(t: torch.Tensor, bound: float) -> None:
+    with torch.no_grad():
+        t.uniform_(-bound, bound)
+
+
+class Conv1dParams(nn.Module):
+    """Parameters of nn.Conv1d(cin, cout, k, bias=...)."""
+
+    def __init__(self, cin: int, cout: int, k: int, bias: bool) -> None:
+        super().__init__()
+        self.in_channels, self.out_channels, self.kernel_size = cin, cout, k
+        self.weight = nn.Parameter(torch.empty(cout, cin, k))
+        self.bias = nn.Parameter(torch.empty(cout)) if bias else None
+        b = 1.0 / math.sqrt(cin * k)
+        _uniform_(self.weight, b)
+        if self.bias is not None:
+            _uniform_(self.bias, b)
+
+
+class BatchNorm1dParams(nn.Module):
+    """Parameters and running statistics of nn.BatchNorm1d(c) (eval mode only)."""
+
+    def __init__(self, c: int, eps: float = 1e-5) -> None:
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(c))
+        self.bias = nn.Parameter(torch.zeros(c))
+        self.register_buffer('running_mean', torch.zeros(c))
+        self.register_buffer('running_var', torch.ones(c))
+        self.register_buffer('num_batches_tracked', torch.tensor(0, dtype=torch.long))
+
+    def folded(self):
+        """(scale, shift) with y = x*scale + shift == (x - mean)/sqrt(var + eps)*w + b."""
+        invstd = 1.0 / torch.sqrt(self.running_var + self.eps)
+        scale = invstd * self.weight
+        shift = self.bias - self.running_mean * scale
+        return scale.detach().float().contiguous(), shift.detach().float().contiguous()
+
+
+class LinearParams(nn.Module):
+    """Parameters of nn.Linear(fin, fout, bias=...)."""
+
+    def __init__(self, fin: int, fout: int, bias: bool = True) -> None:
+        super().__init__()
+        self.in_features, self.out_features = fin, fout
+        self.weight = nn.Parameter(torch.empty(fout, fin))
+        self.bias = nn.Parameter(torch.empty(fout)) if bias else None
+        b = 1.0 / math.sqrt(fin)
+        _uniform_(self.weight, b)
+        if self.bias is not None:
+            _uniform_(self.bias, b)
+
+
+def pack_conv(w: torch.Tensor) -> torch.Tensor:
+    """nn.Conv1d weight (N, Cin, k) -> kernel layout [N][k*Cin] (tap-major K)."""
+    return w.detach().permute(0, 2, 1).contiguous().reshape(w.size(0), -1)
+
+
+# --------------------------------------------------------------------------------------
+# packed-weight cache: rebuilt whenever a parameter / buffer changes (load_state_dict, .to)
+
+class Packed(nn.Module):
+    """Base class: caches kernel-layout weights, keyed by the identity/version of params."""
+
+    def _pack_key(self):
+        return tuple((t.data_ptr(), t._version, t.device) for t in
+                     list(self.parameters()) + list(self.buffers()))
+
+    def packed_weights(self):
+        key = self._pack_key()
+        cache = self.__dict__.get('_ftmi_pack')
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                cache = (key, self._pack())
+            self.__dict__['_ftmi_pack'] = cache
+        return cache[1]
+
+    def _pack(self):  # pragma: no cover - abstract
+        raise NotImplementedError
+
+
+# --------------------------------------------------------------------------------------
+# reference layers
+
+class LengthRegulator(nn.Module):
+    """`models/common_layers.py:7-19`: dur[dur<0]=0 (in place), repeat each frame
+    int64(dur+0.5) times, zero-pad to the longest sequence."""
+
+    def forward(self, x: torch.Tensor, dur: torch.Tensor) -> torch.Tensor:
+        dur_c = dur if (dur.is_contiguous() and dur.dtype == torch.float32) else dur.float().contiguous()
+        offsets, totals, _ = ops.duration_counts(dur_c, apply_fill=False)
+        if dur_c is not dur:
+            dur.copy_(dur_c)
+        T_mel = int(totals.max().item()) if totals.numel() else 0
+        index = ops.lr_index(offsets, T_mel)
+        return ops.length_regulate(x.contiguous(), index)
+
+
+class BatchNormConv(Packed):
+    """Conv1d_s1 (pad k//2, no bias) -> (ReLU) -> BatchNorm1d(eval).
+    `models/forward_tacotron.py:58-71` and `models/common_layers.py:38-52`."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel: int, relu: bool = True) -> None:
+        super().__init__()
+        self.conv = Conv1dParams(in_channels, out_channels, kernel, bias=False)
+        self.bnorm = BatchNorm1dParams(out_channels)
+        self.relu = relu
+        self.kernel = kernel
+
+    def _pack(self):
+        return pack_conv(self.conv.weight), self.bnorm.folded()
+
+    def forward_cl(self, x: torch.Tensor, T_out: int = 0, residual=None, maxpool=False) -> torch.Tensor:
+        w, bn = self.packed_weights()
+        y, _ = ops.conv1d(x, w, self.kernel, self.kernel // 2, relu=self.relu, bn=bn,
+                          residual=residual, maxpool=maxpool, T_out=T_out)
+        return y
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """(B, Cin, T) -> (B, Cout, T + 1 - k % 2), like the reference."""
+        T = x.size(2)
+        To = T + 2 * (self.kernel // 2) - self.kernel + 1
+        y = self.forward_cl(x.transpose(1, 2).contiguous(), T_out=To)
+        return y.transpose(1, 2)
+
+
+class HighwayNetwork(Packed):
+    """`models/common_layers.py:22-35`: y = g*relu(W1 x + b1) + (1-g)*x, g = sigmoid(W2 x + b2)."""
+
+    def __init__(self, size: int) -> None:
+        super().__init__()
+        self.W1 = LinearParams(size, size)
+        self.W2 = LinearParams(size, size)
+        with torch.no_grad():
+            self.W1.bias.zero_()
+
+    def _pack(self):
+        C = self.W1.weight.size(0)
+        w1 = self.W1.weight.detach().reshape(C // 32, 32, C)
+        w2 = self.W2.weight.detach().reshape(C // 32, 32, C)
+        w12 = torch.stack([w1, w2], 1).reshape(2 * C, C).contiguous()
+        return w12, self.W1.bias.detach().contiguous(), self.W2.bias.detach().contiguous()
+
+    def forward_cl(self, x: torch.Tensor, out=None) -> torch.Tensor:
+        w12, b1, b2 = self.packed_weights()
+        return ops.highway(x, w12, b1, b2, out=out)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        shp = x.shape
+        y = self.forward_cl(x.reshape(1, -1, shp[-1]).contiguous())
+        return y.reshape(shp)
+
+
+class BiRNN(Packed):
+    """1-layer bidirectional GRU (gates r,z,n) / LSTM (gates i,f,g,o), batch_first, holding
+    exactly the parameters of nn.GRU / nn.LSTM (weight_ih_l0, weight_hh_l0, bias_ih_l0,
+    bias_hh_l0 and their _reverse twins)."""
+
+    def __init__(self, fin: int, hidden: int, cell: str) -> None:
+        super().__init__()
+        self.cell = 0 if cell == 'gru' else 1
+        self.input_size, self.hidden = fin, hidden
+        gh = (3 if self.cell == 0 else 4) * hidden
+        b = 1.0 / math.sqrt(hidden)
+        for sfx in ('', '_reverse'):
+            for name, shape in (('weight_ih_l0', (gh, fin)), ('weight_hh_l0', (gh, hidden)),
+                                ('bias_ih_l0', (gh,)), ('bias_hh_l0', (gh,))):
+                prm = nn.Parameter(torch.empty(*shape))
+                _uniform_(prm, b)
+                self.register_parameter(name + sfx, prm)
+
+    def _pack(self):
+        """W_ih both directions [2*G*H][In], input bias [2*G*H], b_hh [2*G*H], W_hh [2][G*H][H]."""
+        w_ih = torch.cat([self.weight_ih_l0, self.weight_ih_l0_reverse], 0).detach().contiguous()
+        b_ih = torch.cat([self.bias_ih_l0, self.bias_ih_l0_reverse], 0).detach().contiguous()
+        b_hh = torch.cat([self.bias_hh_l0, self.bias_hh_l0_reverse], 0).detach().contiguous()
+        w_hh = torch.stack([self.weight_hh_l0, self.weight_hh_l0_reverse], 0).detach().contiguous()
+        if self.cell == 1:  # LSTM: both biases folded into the input projection
+            return w_ih, (b_ih + b_hh).contiguous(), None, w_hh
+        return w_ih, b_ih, b_hh, w_hh
+
+    def forward_cl(self, x: torch.Tensor, T: Optional[int] = None, index=None, lengths=None,
+                   pad_value: float = 0.0) -> torch.Tensor:
+        """x: (B, T_src, In) channels-last; with index, frame t reads row index[b, t]."""
+        w_ih, b_in, b_hh, w_hh = self.packed_weights()
+        xp, _ = ops.conv1d(x, w_ih, 1, 0, bias=b_in)
+        return ops.rnn_bidir(self.cell, xp, self.hidden, w_hh, b_hh, T=T, index=index,
+                             xp_zero=b_in if index is not None else None, lengths=lengths,
+                             pad_value=pad_value)
+
+    def forward(self, x: torch.Tensor):
+        """(B, T, In) -> ((B, T, 2H), None) like nn.GRU/LSTM(batch_first=True) without h0."""
+        return self.forward_cl(x.contiguous()), None
+
+
+class CBHG(Packed):
+    """`models/common_layers.py:55-119`: conv bank (k = 1..K) -> maxpool -> proj1 -> proj2
+    + residual -> pre_highway -> highways -> bidirectional GRU."""
+
+    def __init__(self, K: int, in_channels: int, channels: int, proj_channels: List[int],
+                 num_highways: int, dropout: float = 0.5) -> None:
+        super().__init__()
+        self.dropout = dropout
+        self.K = K
+        self.channels = channels
+        self.bank_kernels = list(range(1, K + 1))
+        self.conv1d_bank = nn.ModuleList(
+            [BatchNormConv(in_channels, channels, k) for k in self.bank_kernels])
+        self.conv_project1 = BatchNormConv(K * channels, proj_channels[0], 3)
+        self.conv_project2 = BatchNormConv(proj_channels[0], proj_channels[1], 3, relu=False)
+        self.pre_highway = LinearParams(proj_channels[-1], channels, bias=False)
+        self.highways = nn.ModuleList([HighwayNetwork(channels) for _ in range(num_highways)])
+        self.rnn = GRUParamsModule(channels, channels)
+
+    def _pack(self):
+        ws = [pack_conv(c.conv.weight) for c in self.conv1d_bank]
+        bank_w = torch.cat([w.reshape(-1) for w in ws]).contiguous()
+        folds = [c.bnorm.folded() for c in self.conv1d_bank]
+        scale = torch.cat([f[0] for f in folds]).contiguous()
+        shift = torch.cat([f[1] for f in folds]).contiguous()
+        return bank_w, scale, shift, self.pre_highway.weight.detach().contiguous()
+
+    def forward_cl(self, x: torch.Tensor) -> torch.Tensor:
+        """(B, T, Cin) channels-last -> (B, T, 2*channels)."""
+        bank_w, scale, shift, w_pre = self.packed_weights()
+        bank = ops.conv_bank(x, bank_w, self.K, self.channels, scale, shift)
+        y = self.conv_project1.forward_cl(bank, maxpool=True)
+        del bank
+        y = self.conv_project2.forward_cl(y, residual=x)
+        h, _ = ops.conv1d(y, w_pre, 1, 0)
+        h2 = torch.empty_like(h)
+        for hw in self.highways:
+            hw.forward_cl(h, out=h2)
+            h, h2 = h2, h
+        return self.rnn.forward_cl(h)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """(B, Cin, T) -> (B, T, 2*channels), like the reference."""
+        return self.forward_cl(x.transpose(1, 2).contiguous())
+
+
+class GRUParamsModule(BiRNN):
+    """nn.GRU(fin, hidden, batch_first=True, bidirectional=True) parameters + HIP forward."""
+
+    def __init__(self, fin: int, hidden: int) -> None:
+        super().__init__(fin, hidden, 'gru')
+
+
+class LSTMParamsModule(BiRNN):
+    """nn.LSTM(fin, hidden, batch_first=True, bidirectional=True) parameters + HIP forward."""
+
+    def __init__(self, fin: int, hidden: int) -> None:
+        super().__init__(fin, hidden, 'lstm')

@@ -1,0 +1,360 @@
+// Implicit-GEMM Conv1d / Linear / CBHG-bank / Highway kernels on fp32 MFMA (gfx950).
+//
+// One kernel template covers every dense contraction of the ForwardTacotron forward pass:
+//   BatchNormConv (k = 1..16, pad k//2, ReLU -> BN)   models/common_layers.py:38-52,
+//                                                     models/forward_tacotron.py:58-71
+//   CBHG bank (K convs in one launch, concatenated)   models/common_layers.py:67-71,92-97
+//   CBHG maxpool fused into proj1's operand load      models/common_layers.py:73,100
+//   proj2 + residual                                  models/common_layers.py:106-109
+//   Linear layers (k = 1)                             pre_highway, lin, post_proj, RNN W_ih
+//   Highway layer (W1 | W2 in one GEMM, gating epilogue) models/common_layers.py:22-35
+//
+// Numerics: exact fp32 (v_mfma_f32_32x32x2_f32 is a k-ordered fmaf chain), no reduced
+// precision anywhere.  Tiling: 128x128 block tile, BK = 16, 4 waves each owning a 64x64
+// sub-tile = 2x2 MFMA 32x32 tiles; operands staged through LDS (double buffered, one
+// barrier per K-step, global loads for step k+1 issued before the MFMAs of step k).
+// Inside a BK = 16 chunk lane half h consumes k = 8h + s at MFMA s (s = 0..7) for both
+// operands, so every lane reads its fragments with two ds_read_b128 per operand; the
+// LDS row stride of 20 floats makes those reads bank-conflict free (5i mod 16 distinct).
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128;
+constexpr int BN = 128;
+constexpr int BK = 16;
+constexpr int LDS_STRIDE = 20;  // floats per staged row (16 + 4 pad)
+constexpr int MAX_GROUPS = 16;
+
+enum { EPI_CONV = 0, EPI_HIGHWAY = 1 };
+
+struct GemmGroup {
+  const float *w;  // [N][Ktot]
+  const float *bias;
+  const float *scale;
+  const float *shift;
+  int N, k, pad, Ktot;
+  int ycol0;   // first output column of this group
+  int ntiles;  // number of BN tiles
+  int tile0;   // first linear block index of this group
+};
+
+struct GemmParams {
+  const float *x;
+  int64_t x_stride;
+  int B, T, Cin, M;
+  int To;  // output frames per sequence (rows of y are (b, t < To))
+  int relu, ngroups;
+  const float *residual;
+  int64_t res_stride;
+  float *y;
+  int64_t y_stride;
+  float *yt;
+  int yt_channels;
+  // highway epilogue
+  const float *b1;
+  const float *b2;
+  GemmGroup g[MAX_GROUPS];
+};
+
+__device__ __forceinline__ f32x4 fmax4(f32x4 a, f32x4 b) {
+  f32x4 r;
+  r.x = fmaxf(a.x, b.x);
+  r.y = fmaxf(a.y, b.y);
+  r.z = fmaxf(a.z, b.z);
+  r.w = fmaxf(a.w, b.w);
+  return r;
+}
+
+template <int EPI, bool MAXPOOL>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(const GemmParams p) {
+  __shared__ __attribute__((aligned(16))) float lds[2][2][BM * LDS_STRIDE];
+
+  // ---- locate (group, m-tile, n-tile); groups are ordered heaviest first -------------
+  const int tile = blockIdx.x;
+  int gi = 0;
+  while (gi + 1 < p.ngroups && tile >= p.g[gi + 1].tile0) ++gi;
+  const GemmGroup &G = p.g[gi];
+  const int lt = tile - G.tile0;
+  const int mt = lt / G.ntiles;
+  const int nt = lt - mt * G.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- loader assignment: rows lr and lr+64 of both A and B tiles, float4 #lq ------
+  const int lr = tid >> 2, lq = tid & 3;
+  int ab[2], at[2];
+  bool aok[2], bok[2];
+  const float *wrow[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int m = m0 + lr + 64 * q;
+    aok[q] = m < p.M;
+    const int mm = aok[q] ? m : 0;
+    ab[q] = mm / p.To;
+    at[q] = mm - ab[q] * p.To;
+    const int n = n0 + lr + 64 * q;
+    bok[q] = n < G.N;
+    wrow[q] = G.w + (int64_t)(bok[q] ? n : 0) * G.Ktot + 4 * lq;
+  }
+
+  const int nk = G.Ktot / BK;
+  f32x4 ra[2], rb[2];
+
+  auto gload = [&](int kc) {
+    const int kk = kc * BK;
+    const int j = kk / p.Cin;
+    const int c0 = kk - j * p.Cin;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int ts = at[q] + j - G.pad;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (aok[q] && ts >= 0 && ts < p.T) {
+        const float *src = p.x + ((int64_t)ab[q] * p.T + ts) * p.x_stride + c0 + 4 * lq;
+        v = *(const f32x4 *)src;
+        if (MAXPOOL && ts > 0) v = fmax4(v, *(const f32x4 *)(src - p.x_stride));
+      }
+      ra[q] = v;
+      f32x4 w = {0.f, 0.f, 0.f, 0.f};
+      if (bok[q]) w = *(const f32x4 *)(wrow[q] + kk);
+      rb[q] = w;
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      *(f32x4 *)&lds[buf][0][(lr + 64 * q) * LDS_STRIDE + 4 * lq] = ra[q];
+      *(f32x4 *)&lds[buf][1][(lr + 64 * q) * LDS_STRIDE + 4 * lq] = rb[q];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int fi = lane & 31, fh = lane >> 5;
+  auto compute = [&](int buf) {
+    const float *As = lds[buf][0];
+    const float *Bs = lds[buf][1];
+    f32x4 a[2][2], b[2][2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+        a[mi][v] = *(const f32x4 *)&As[(wm * 64 + mi * 32 + fi) * LDS_STRIDE + 8 * fh + 4 * v];
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+        b[ni][v] = *(const f32x4 *)&Bs[(wn * 64 + ni * 32 + fi) * LDS_STRIDE + 8 * fh + 4 * v];
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mi][s >> 2][s & 3],
+                                                             b[ni][s >> 2][s & 3],
+                                                             acc[mi][ni], 0, 0, 0);
+  };
+
+  // ---- main loop: one barrier per K-step ---------------------------------------------
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int cur = kc & 1;
+    if (kc + 1 < nk) gload(kc + 1);
+    compute(cur);
+    if (kc + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ---------------------------------------------------------------------
+  if constexpr (EPI == EPI_CONV) {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int col = n0 + wn * 64 + ni * 32 + fi;
+        if (col >= G.N) continue;
+        const float bias = G.bias ? G.bias[col] : 0.f;
+        const float sc = G.scale ? G.scale[col] : 1.f;
+        const float sh = G.scale ? G.shift[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          if (row >= p.M) continue;
+          float v = acc[mi][ni][r];
+          if (G.bias) v += bias;
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (G.scale) v = v * sc + sh;
+          if (p.residual) v += p.residual[(int64_t)row * p.res_stride + col];
+          if (p.y) p.y[(int64_t)row * p.y_stride + G.ycol0 + col] = v;
+          if (p.yt) {
+            const int b = row / p.To, t = row - b * p.To;
+            p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = v;
+          }
+        }
+      }
+  } else {
+    // Highway: packed column block pair (2q, 2q+1) = (W1, W2) rows 32q..32q+31.
+    if (n0 + wn * 64 >= G.N) return;
+    const int col = (n0 + wn * 64) / 2 + fi;
+    const float b1 = p.b1[col], b2 = p.b2[col];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        if (row >= p.M) continue;
+        const float x1 = acc[mi][0][r] + b1;
+        const float x2 = acc[mi][1][r] + b2;
+        const float g = ftmi_sigmoid(x2);
+        const float xin = p.x[(int64_t)row * p.x_stride + col];
+        p.y[(int64_t)row * p.y_stride + col] = g * fmaxf(x1, 0.f) + (1.f - g) * xin;
+      }
+  }
+}
+
+int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, hipStream_t s) {
+  if (nblocks <= 0) return FTMI_OK;
+  dim3 grid(nblocks), block(256);
+  if (epi == EPI_HIGHWAY)
+    hipLaunchKernelGGL((conv_gemm_kernel<EPI_HIGHWAY, false>), grid, block, 0, s, p);
+  else if (maxpool)
+    hipLaunchKernelGGL((conv_gemm_kernel<EPI_CONV, true>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<EPI_CONV, false>), grid, block, 0, s, p);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+}  // namespace
+
+extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
+  if (!a || !a->x || !a->w || (!a->y && !a->yt)) return FTMI_E_ARG;
+  if (a->B <= 0 || a->T <= 0 || a->Cin <= 0 || a->N <= 0 || a->k <= 0) return FTMI_E_ARG;
+  if (a->Cin % 16 != 0) return FTMI_E_SHAPE;
+  if (a->pad < 0 || a->pad >= a->k + a->T) return FTMI_E_SHAPE;
+  if ((a->bn_scale == nullptr) != (a->bn_shift == nullptr)) return FTMI_E_ARG;
+  if (!ftmi_aligned16(a->x) || !ftmi_aligned16(a->w) || (a->x_stride & 3)) return FTMI_E_ALIGN;
+  const int To = a->T_out > 0 ? a->T_out : a->T;
+  if ((int64_t)a->B * To > INT32_MAX) return FTMI_E_SHAPE;
+  GemmParams p = {};
+  p.x = a->x;
+  p.x_stride = a->x_stride;
+  p.B = a->B;
+  p.T = a->T;
+  p.To = To;
+  p.Cin = a->Cin;
+  p.M = a->B * To;
+  p.relu = a->relu;
+  p.ngroups = 1;
+  p.residual = a->residual;
+  p.res_stride = a->res_stride;
+  p.y = a->y;
+  p.y_stride = a->y_stride;
+  p.yt = a->yt;
+  p.yt_channels = a->N;
+  GemmGroup &g = p.g[0];
+  g.w = a->w;
+  g.bias = a->bias;
+  g.scale = a->bn_scale;
+  g.shift = a->bn_shift;
+  g.N = a->N;
+  g.k = a->k;
+  g.pad = a->pad;
+  g.Ktot = a->k * a->Cin;
+  g.ycol0 = 0;
+  g.ntiles = (a->N + BN - 1) / BN;
+  g.tile0 = 0;
+  const int mtiles = (p.M + BM - 1) / BM;
+  return launch(p, EPI_CONV, a->maxpool != 0, mtiles * g.ntiles, ftmi_hs(stream));
+}
+
+extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T,
+                              int32_t Cin, const float *w, int32_t K, int32_t Cout,
+                              const float *bn_scale, const float *bn_shift, float *y,
+                              int64_t y_stride, ftmi_stream_t stream) {
+  if (!x || !w || !bn_scale || !bn_shift || !y) return FTMI_E_ARG;
+  if (B <= 0 || T <= 0 || Cin <= 0 || Cout <= 0 || K <= 0) return FTMI_E_ARG;
+  if (K > MAX_GROUPS) return FTMI_E_UNSUPPORTED;
+  if (Cin % 16 != 0) return FTMI_E_SHAPE;
+  if (!ftmi_aligned16(x) || !ftmi_aligned16(w) || (x_stride & 3)) return FTMI_E_ALIGN;
+  if ((int64_t)B * T > INT32_MAX) return FTMI_E_SHAPE;
+  GemmParams p = {};
+  p.x = x;
+  p.x_stride = x_stride;
+  p.B = B;
+  p.T = T;
+  p.To = T;
+  p.Cin = Cin;
+  p.M = B * T;
+  p.relu = 1;
+  p.ngroups = K;
+  p.y = y;
+  p.y_stride = y_stride;
+  const int mtiles = (p.M + BM - 1) / BM;
+  const int ntiles = (Cout + BN - 1) / BN;
+  int tile0 = 0;
+  for (int gi = 0; gi < K; ++gi) {
+    const int ks = K - gi;  // heaviest group first
+    const int gidx = ks - 1;
+    GemmGroup &g = p.g[gi];
+    g.w = w + (int64_t)Cout * Cin * gidx * (gidx + 1) / 2;
+    g.bias = nullptr;
+    g.scale = bn_scale + (int64_t)gidx * Cout;
+    g.shift = bn_shift + (int64_t)gidx * Cout;
+    g.N = Cout;
+    g.k = ks;
+    g.pad = ks / 2;
+    g.Ktot = ks * Cin;
+    g.ycol0 = gidx * Cout;
+    g.ntiles = ntiles;
+    g.tile0 = tile0;
+    tile0 += mtiles * ntiles;
+  }
+  return launch(p, EPI_CONV, false, tile0, ftmi_hs(stream));
+}
+
+extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t C,
+                            const float *w12, const float *b1, const float *b2, float *y,
+                            int64_t y_stride, ftmi_stream_t stream) {
+  if (!x || !w12 || !b1 || !b2 || !y) return FTMI_E_ARG;
+  if (M <= 0 || C <= 0) return FTMI_E_ARG;
+  if (C % 32 != 0 || C % 16 != 0) return FTMI_E_SHAPE;
+  if (M > INT32_MAX) return FTMI_E_SHAPE;
+  if (!ftmi_aligned16(x) || !ftmi_aligned16(w12) || (x_stride & 3)) return FTMI_E_ALIGN;
+  if (x == y) return FTMI_E_ARG;
+  GemmParams p = {};
+  p.x = x;
+  p.x_stride = x_stride;
+  p.B = 1;
+  p.T = (int)M;
+  p.To = (int)M;
+  p.Cin = C;
+  p.M = (int)M;
+  p.ngroups = 1;
+  p.y = y;
+  p.y_stride = y_stride;
+  p.b1 = b1;
+  p.b2 = b2;
+  GemmGroup &g = p.g[0];
+  g.w = w12;
+  g.N = 2 * C;
+  g.k = 1;
+  g.pad = 0;
+  g.Ktot = C;
+  g.ntiles = (2 * C + BN - 1) / BN;
+  g.tile0 = 0;
+  const int mtiles = (p.M + BM - 1) / BM;
+  return launch(p, EPI_HIGHWAY, false, mtiles * g.ntiles, ftmi_hs(stream));
+}

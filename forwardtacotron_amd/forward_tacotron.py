@@ -1,0 +1,271 @@
+"""ForwardTacotron (V2: pitch + energy) on MI355X — drop-in for `models/forward_tacotron.py`.
+
+Same constructor keywords (:93-118), same state_dict keys and shapes (checkpoints from the
+reference load unchanged), same ``generate`` / ``generate_jit`` / ``forward`` /
+``from_config`` / ``from_checkpoint`` / ``get_step`` surface and return dictionaries.
+All math runs in libftmi.so (HIP, gfx950, fp32); torch only allocates device buffers,
+moves tokens / results and runs the user's pitch / energy callbacks.
+
+Pipeline of ``generate`` (channels-last activations, one HIP stream):
+  predictors  embed -> 3x conv k5 (ReLU, BN) -> GRU in-proj GEMM -> GRU recurrence -> head
+  durations   fill-2 rule + clip + counts + scan in one kernel (bit-exact), one host sync
+              for T_mel (the reference syncs at the same point, :254 and common_layers.py:16)
+  encoder     embed -> CBHG(K=16) -> + pitch/energy conv projections
+  decoder     LSTM input projection at PHONEME rate (x W_ih^T + b), the recurrence reads
+              it through the LengthRegulator index map: LR(x) W_ih^T == LR(x W_ih^T), so the
+              expanded (B, T_mel, 512) tensor and 7x of the projection FLOPs are never needed;
+              lin (-> mel, written both channels-last and as (B, 80, T_mel))
+  postnet     CBHG(K=8) on the channels-last mel -> post_proj (-> mel_post (B, 80, T_mel))
+"""
+from __future__ import annotations
+
+from pathlib import Path
+from typing import Any, Callable, Dict, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+from .common_layers import (CBHG, BatchNormConv, BiRNN, Conv1dParams, LengthRegulator,
+                            LinearParams, Packed, pack_conv)
+from .text.symbols import phonemes
+
+
+class Embedding(nn.Module):
+    """Parameters of nn.Embedding(num, dim)."""
+
+    def __init__(self, num: int, dim: int) -> None:
+        super().__init__()
+        self.num_embeddings, self.embedding_dim = num, dim
+        self.weight = nn.Parameter(torch.randn(num, dim))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return ops.embedding(x, self.weight.detach())
+
+
+class SeriesPredictor(Packed):
+    """`models/forward_tacotron.py:14-55`: embed -> [Conv1d k5 -> ReLU -> BN]x3 -> biGRU ->
+    Linear(2h -> 1) -> / alpha."""
+
+    def __init__(self, num_chars, emb_dim=64, conv_dims=256, rnn_dims=64, dropout=0.5):
+        super().__init__()
+        self.embedding = Embedding(num_chars, emb_dim)
+        self.convs = nn.ModuleList([
+            BatchNormConv(emb_dim, conv_dims, 5, relu=True),
+            BatchNormConv(conv_dims, conv_dims, 5, relu=True),
+            BatchNormConv(conv_dims, conv_dims, 5, relu=True),
+        ])
+        self.rnn = BiRNN(conv_dims, rnn_dims, 'gru')
+        self.lin = LinearParams(2 * rnn_dims, 1)
+        self.dropout = dropout
+
+    def _pack(self):
+        return self.lin.weight.detach().reshape(-1).contiguous(), self.lin.bias.detach().contiguous()
+
+    def forward_bt(self, x: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
+        """(B, T) ids -> (B, T) series (before the reference's trailing unsqueeze)."""
+        h = ops.embedding(x, self.embedding.weight.detach())
+        for conv in self.convs:
+            h = conv.forward_cl(h)
+        h = self.rnn.forward_cl(h)
+        w, b = self.packed_weights()
+        return ops.rowdot(h, w, b, alpha)
+
+    def forward(self, x: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
+        """(B, T) -> (B, T, 1), like the reference."""
+        return self.forward_bt(x, alpha).unsqueeze(-1)
+
+
+class ForwardTacotron(nn.Module):
+    """ForwardTacotron V2; see module docstring.  Reference: models/forward_tacotron.py:74-350."""
+
+    def __init__(self,
+                 embed_dims: int,
+                 series_embed_dims: int,
+                 num_chars: int,
+                 durpred_conv_dims: int,
+                 durpred_rnn_dims: int,
+                 durpred_dropout: float,
+                 pitch_conv_dims: int,
+                 pitch_rnn_dims: int,
+                 pitch_dropout: float,
+                 pitch_strength: float,
+                 energy_conv_dims: int,
+                 energy_rnn_dims: int,
+                 energy_dropout: float,
+                 energy_strength: float,
+                 rnn_dims: int,
+                 prenet_dims: int,
+                 prenet_k: int,
+                 postnet_num_highways: int,
+                 prenet_dropout: float,
+                 postnet_dims: int,
+                 postnet_k: int,
+                 prenet_num_highways: int,
+                 postnet_dropout: float,
+                 n_mels: int,
+                 padding_value=-11.5129):
+        super().__init__()
+        self.rnn_dims = rnn_dims
+        self.padding_value = padding_value
+        self.register_buffer('step', torch.zeros(1, dtype=torch.long))
+        # registration order follows the reference so state_dict() iterates identically
+        self.embedding = Embedding(num_chars, embed_dims)
+        self.prenet = CBHG(K=prenet_k, in_channels=embed_dims, channels=prenet_dims,
+                           proj_channels=[prenet_dims, embed_dims],
+                           num_highways=prenet_num_highways, dropout=prenet_dropout)
+        self.pitch_pred = SeriesPredictor(num_chars, series_embed_dims, pitch_conv_dims,
+                                          pitch_rnn_dims, pitch_dropout)
+        self.energy_pred = SeriesPredictor(num_chars, series_embed_dims, energy_conv_dims,
+                                           energy_rnn_dims, energy_dropout)
+        self.pitch_proj = Conv1dParams(1, 2 * prenet_dims, 3, bias=True)
+        self.energy_proj = Conv1dParams(1, 2 * prenet_dims, 3, bias=True)
+        self.pitch_strength = pitch_strength
+        self.energy_strength = energy_strength
+        self.lr = LengthRegulator()
+        self.dur_pred = SeriesPredictor(num_chars, series_embed_dims, durpred_conv_dims,
+                                        durpred_rnn_dims, durpred_dropout)
+        self.lstm = BiRNN(2 * prenet_dims, rnn_dims, 'lstm')
+        self.lin = LinearParams(2 * rnn_dims, n_mels)
+        self.postnet = CBHG(K=postnet_k, in_channels=n_mels, channels=postnet_dims,
+                            proj_channels=[postnet_dims, n_mels],
+                            num_highways=postnet_num_highways, dropout=postnet_dropout)
+        self.post_proj = LinearParams(2 * postnet_dims, n_mels, bias=False)
+        self.n_mels = n_mels
+
+    def __repr__(self):
+        num_params = sum([np.prod(p.size()) for p in self.parameters()])
+        return f'ForwardTacotron, num params: {num_params}'
+
+    # ---------------------------------------------------------------------------------
+    def _check_device(self, x: torch.Tensor) -> None:
+        if not self.embedding.weight.is_cuda:
+            raise RuntimeError('forwardtacotron_amd.ForwardTacotron runs on a HIP device only: '
+                               'call model.to("cuda") first (there is no CPU path)')
+        if x.device != self.embedding.weight.device:
+            raise RuntimeError(f'input on {x.device}, model on {self.embedding.weight.device}')
+
+    def _series_proj_weights(self):
+        return (self.pitch_proj.weight.detach().reshape(-1, 3).contiguous(),
+                self.pitch_proj.bias.detach().contiguous(),
+                self.energy_proj.weight.detach().reshape(-1, 3).contiguous(),
+                self.energy_proj.bias.detach().contiguous())
+
+    def _encode(self, x: torch.Tensor, pitch: torch.Tensor, energy: torch.Tensor) -> torch.Tensor:
+        """embedding -> prenet CBHG -> + pitch / energy projections: (B, T, 2*prenet_dims)."""
+        h = ops.embedding(x, self.embedding.weight.detach())
+        h = self.prenet.forward_cl(h)
+        wp, bp, we, be = self._series_proj_weights()
+        ops.series_proj_add(h, pitch, wp, bp, self.pitch_strength, energy, we, be,
+                            self.energy_strength)
+        return h
+
+    def _decode(self, enc: torch.Tensor, index: torch.Tensor, lengths=None, T_out=None):
+        """LSTM over LR(enc) (through the index map) -> lin -> postnet -> post_proj."""
+        B = enc.size(0)
+        T_mel = index.size(1)
+        lstm_out = self.lstm.forward_cl(enc, T=T_mel, index=index, lengths=lengths,
+                                        pad_value=self.padding_value)
+        mel_cl = torch.empty(B, T_mel, self.n_mels, device=enc.device)
+        mel = torch.empty(B, self.n_mels, T_mel, device=enc.device)
+        ops.conv1d(lstm_out, self.lin.weight.detach(), 1, 0, bias=self.lin.bias.detach(),
+                   out=mel_cl, out_t=mel)
+        del lstm_out
+        post = self.postnet.forward_cl(mel_cl)
+        mel_post = torch.empty(B, self.n_mels, T_mel, device=enc.device)
+        ops.conv1d(post, self.post_proj.weight.detach(), 1, 0, out_t=mel_post, want_y=False)
+        return mel, mel_post
+
+    # ---------------------------------------------------------------------------------
+    def forward(self, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """Teacher-forced pass (`models/forward_tacotron.py:184-242`), inference numerics."""
+        x = batch['x']
+        self._check_device(x)
+        mel = batch['mel']
+        mel_lens = batch['mel_len']
+        dur = batch['dur']
+        pitch = batch['pitch'].unsqueeze(1)
+        energy = batch['energy'].unsqueeze(1)
+        if self.training:
+            self.step += 1
+        with torch.no_grad():
+            dur_hat = self.dur_pred.forward_bt(x)
+            pitch_hat = self.pitch_pred.forward_bt(x).unsqueeze(1)
+            energy_hat = self.energy_pred.forward_bt(x).unsqueeze(1)
+            enc = self._encode(x, pitch, energy)
+            dur_c = dur.float().contiguous()
+            offsets, totals, _ = ops.duration_counts(dur_c, apply_fill=False)
+            if dur_c.data_ptr() != dur.data_ptr():
+                dur.copy_(dur_c)  # the reference's LR clips batch['dur'] in place
+            lens = mel_lens.to(torch.int64)
+            T_pack = int(lens.max().item())
+            if T_pack > int(totals.max().item()):
+                raise RuntimeError('mel_len exceeds the length-regulated sequence length')
+            index = ops.lr_index(offsets, T_pack)
+            x_mel, x_post = self._decode(enc, index, lengths=lens.to(x.device))
+            x_post = self._pad(x_post, mel.size(2))
+            x_mel = self._pad(x_mel, mel.size(2))
+        return {'mel': x_mel, 'mel_post': x_post,
+                'dur': dur_hat, 'pitch': pitch_hat, 'energy': energy_hat}
+
+    def generate(self,
+                 x: torch.Tensor,
+                 alpha=1.0,
+                 pitch_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x,
+                 energy_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x) -> Dict[str, torch.Tensor]:
+        """`models/forward_tacotron.py:244-268`."""
+        self.eval()
+        self._check_device(x)
+        with torch.no_grad():
+            dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
+            pitch_hat = self.pitch_pred.forward_bt(x).unsqueeze(1)
+            pitch_hat = pitch_function(pitch_hat)
+            energy_hat = self.energy_pred.forward_bt(x).unsqueeze(1)
+            energy_hat = energy_function(energy_hat)
+            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, apply_fill=True)
+
+    def generate_jit(self, x: torch.Tensor, alpha: float = 1.0, beta: float = 1.0) -> Dict[str, torch.Tensor]:
+        """`models/forward_tacotron.py:270-284` (pitch scaled by beta, no callbacks)."""
+        self._check_device(x)
+        with torch.no_grad():
+            dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
+            pitch_hat = self.pitch_pred.forward_bt(x).unsqueeze(1) * beta
+            energy_hat = self.energy_pred.forward_bt(x).unsqueeze(1)
+            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, apply_fill=True)
+
+    def get_step(self) -> int:
+        return self.step.data.item()
+
+    def _generate_mel(self, x, dur_hat, pitch_hat, energy_hat, apply_fill=False):
+        """`models/forward_tacotron.py:289-330` (+ the fill-2 rule of :254-255 when apply_fill)."""
+        enc = self._encode(x, pitch_hat, energy_hat)
+        offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=apply_fill)
+        T_mel = int(totals.max().item())  # the one host sync: output size is data dependent
+        index = ops.lr_index(offsets, T_mel)
+        mel, mel_post = self._decode(enc, index)
+        return {'mel': mel, 'mel_post': mel_post, 'dur': dur_hat,
+                'pitch': pitch_hat, 'energy': energy_hat}
+
+    def _pad(self, x: torch.Tensor, max_len: int) -> torch.Tensor:
+        """`models/forward_tacotron.py:332-335` (crop / pad the time axis with padding_value)."""
+        x = x[:, :, :max_len]
+        if x.size(2) < max_len:
+            pad = torch.full((x.size(0), x.size(1), max_len - x.size(2)), self.padding_value,
+                             device=x.device, dtype=x.dtype)
+            x = torch.cat([x, pad], 2)
+        return x
+
+    @classmethod
+    def from_config(cls, config: Dict[str, Any]) -> 'ForwardTacotron':
+        model_config = config['forward_tacotron']['model']
+        model_config['num_chars'] = len(phonemes)
+        model_config['n_mels'] = config['dsp']['num_mels']
+        return ForwardTacotron(**model_config)
+
+    @classmethod
+    def from_checkpoint(cls, path: Union[Path, str]) -> 'ForwardTacotron':
+        checkpoint = torch.load(path, map_location=torch.device('cpu'), weights_only=True)
+        model = ForwardTacotron.from_config(checkpoint['config'])
+        model.load_state_dict(checkpoint['model'])
+        return model

@@ -1,0 +1,231 @@
+"""Tensor-level wrappers over libftmi.so.
+
+Every function takes HIP device tensors (fp32 unless stated), allocates the outputs with
+torch's caching allocator (plumbing only), and enqueues ONE ftmi_* entry point on
+torch's current stream.  Nothing here computes on the host or falls back to torch ops:
+a CPU tensor or a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import ConvArgs
+from .probe import launch
+
+_f32 = torch.float32
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError('forwardtacotron_amd ops run on a HIP device only (got a CPU '
+                               'tensor); there is no CPU fallback')
+
+
+def _rows(x: torch.Tensor) -> Tuple[int, int, int, int]:
+    """(B, T, C, row_stride) of a channels-last (B, T, C) view with uniformly strided rows."""
+    if x.dim() != 3 or x.stride(2) != 1 or x.stride(0) != x.size(1) * x.stride(1):
+        raise ValueError(f'expected a (B, T, C) channels-last view with uniform row stride, got '
+                         f'shape {tuple(x.shape)} strides {x.stride()}')
+    if x.dtype != _f32:
+        raise TypeError('fp32 expected')
+    return x.size(0), x.size(1), x.size(2), x.stride(1)
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, err: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """nn.Embedding forward: (B, T) int64 -> (B, T, dim)."""
+    _dev(ids, table)
+    ids = ids.contiguous()
+    if ids.dtype != torch.int64:
+        ids = ids.long()
+    table = table.contiguous()
+    out = torch.empty(*ids.shape, table.size(1), device=table.device, dtype=_f32)
+    n, d = ids.numel(), table.size(1)
+    launch('ftmi_embedding', f'embedding[n={n},d={d}]', 0, n * 8 + 2 * n * d * 4,
+           ids.data_ptr(), n, table.data_ptr(), table.size(0), d, out.data_ptr(), _ptr(err),
+           _stream())
+    return out
+
+
+def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, relu=False,
+           bn=None, maxpool=False, residual=None, out=None, out_t=None, want_y=True,
+           T_out: int = 0):
+    """Fused Conv1d (+bias, ReLU, BN, residual) on a channels-last (B, T, Cin) view.
+
+    w: packed [N][k*Cin].  Returns (y, yt) where y is (B, T_out, N) (or `out`) and yt is
+    the optional (B, N, T_out) transposed copy (`out_t`).
+    """
+    _dev(x, w, bias, residual, out, out_t)
+    B, T, Cin, xs = _rows(x)
+    N = w.size(0)
+    To = T_out or T
+    if w.size(1) != k * Cin:
+        raise ValueError(f'packed weight {tuple(w.shape)} does not match k={k}, Cin={Cin}')
+    y = None
+    if want_y:
+        y = out if out is not None else torch.empty(B, To, N, device=x.device, dtype=_f32)
+        _rows(y)
+    if residual is not None:
+        _rows(residual)
+    a = ConvArgs()
+    a.x, a.x_stride, a.B, a.T, a.Cin = x.data_ptr(), xs, B, T, Cin
+    a.w, a.N, a.k, a.pad = w.data_ptr(), N, k, pad
+    a.bias = _ptr(bias)
+    a.relu = int(relu)
+    if bn is not None:
+        a.bn_scale, a.bn_shift = bn[0].data_ptr(), bn[1].data_ptr()
+    a.maxpool = int(maxpool)
+    if residual is not None:
+        a.residual, a.res_stride = residual.data_ptr(), residual.stride(1)
+    if y is not None:
+        a.y, a.y_stride = y.data_ptr(), y.stride(1)
+    a.yt = _ptr(out_t)
+    a.T_out = To
+    M = B * To
+    label = f'conv1d[M={M},N={N},K={k * Cin}{",maxpool" if maxpool else ""}]'
+    launch('ftmi_conv1d', label, 2.0 * M * N * k * Cin,
+           4.0 * (B * T * Cin + N * k * Cin + M * N * (1 + (residual is not None))),
+           ctypes.byref(a), _stream())
+    return y, out_t
+
+
+def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.Tensor,
+              shift: torch.Tensor) -> torch.Tensor:
+    """CBHG conv bank, (B, T, Cin) -> (B, T, K*Cout)."""
+    _dev(x, w, scale, shift)
+    B, T, Cin, xs = _rows(x)
+    y = torch.empty(B, T, K * Cout, device=x.device, dtype=_f32)
+    M = B * T
+    flops = 2.0 * M * Cout * Cin * K * (K + 1) / 2
+    launch('ftmi_conv_bank', f'conv_bank[M={M},K={K},Cin={Cin}]', flops,
+           4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
+           x.data_ptr(), xs, B, T, Cin, w.data_ptr(), K, Cout, scale.data_ptr(),
+           shift.data_ptr(), y.data_ptr(), y.stride(1), _stream())
+    return y
+
+
+def highway(x: torch.Tensor, w12: torch.Tensor, b1: torch.Tensor, b2: torch.Tensor,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(x, w12, b1, b2, out)
+    B, T, C, xs = _rows(x)
+    y = out if out is not None else torch.empty(B, T, C, device=x.device, dtype=_f32)
+    M = B * T
+    launch('ftmi_highway', f'highway[M={M},C={C}]', 2.0 * M * 2 * C * C,
+           4.0 * (2 * M * C + 2 * C * C),
+           x.data_ptr(), xs, M, C, w12.data_ptr(), b1.data_ptr(), b2.data_ptr(),
+           y.data_ptr(), y.stride(1), _stream())
+    return y
+
+
+class RnnTimeout(RuntimeError):
+    pass
+
+
+def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Optional[torch.Tensor],
+              T: Optional[int] = None, index: Optional[torch.Tensor] = None,
+              xp_zero: Optional[torch.Tensor] = None, lengths: Optional[torch.Tensor] = None,
+              pad_value: float = 0.0, check: bool = False) -> torch.Tensor:
+    """Bidirectional GRU (cell=0) / LSTM (cell=1) recurrence -> (B, T, 2H).
+
+    xp: (B, T_src, 2*G*H) input projections; index: (B, T) int32 frame -> row map.
+    check=True synchronises and raises RnnTimeout if a workgroup gave up waiting.
+    """
+    _dev(xp, w_hh, b_hh, index, xp_zero, lengths)
+    B, T_src, _, xs = _rows(xp)
+    T = T if T is not None else T_src
+    y = torch.empty(B, T, 2 * H, device=xp.device, dtype=_f32)
+    lib = _lib.load()
+    ws = torch.empty(int(lib.ftmi_rnn_workspace_bytes(B, H, cell)) // 4 + 4, device=xp.device,
+                     dtype=torch.int32)
+    if index is not None:
+        assert index.dtype == torch.int32 and index.is_contiguous() and index.shape == (B, T)
+    if lengths is not None:
+        lengths = lengths.to(device=xp.device, dtype=torch.int32).contiguous()
+    G = 4 if cell else 3
+    label = f'rnn_bidir[{"lstm" if cell else "gru"},B={B},T={T},H={H}]'
+    # recurrent contraction W_hh h per step and direction; bytes: xp rows read per frame,
+    # W_hh once, y written once
+    launch('ftmi_rnn_bidir', label, 2.0 * B * T * 2 * G * H * H,
+           4.0 * (B * T * 2 * G * H + 2 * G * H * H + B * T * 2 * H),
+           cell, B, T, H, xp.data_ptr(), xs, T_src, _ptr(index), _ptr(xp_zero),
+           w_hh.data_ptr(), _ptr(b_hh), _ptr(lengths), float(pad_value), y.data_ptr(), y.stride(1),
+           ws.data_ptr(), _stream())
+    if check:
+        torch.cuda.current_stream().synchronize()
+        off = int(lib.ftmi_rnn_error_offset(B)) // 4
+        if int(ws[off].item()) != 0:
+            raise RnnTimeout('ftmi_rnn_bidir: a workgroup timed out waiting for its group')
+    return y
+
+
+def duration_counts(dur: torch.Tensor, apply_fill: bool, fill_value: float = 2.0):
+    """In place: fill-2 rule (optional) + clip; returns (offsets (B,T+1), totals (B,), fill_flag)."""
+    _dev(dur)
+    if dur.dtype != _f32 or not dur.is_contiguous() or dur.dim() != 2:
+        raise ValueError('dur must be a contiguous (B, T) fp32 tensor')
+    B, T = dur.shape
+    offsets = torch.empty(B, T + 1, device=dur.device, dtype=torch.int32)
+    totals = torch.empty(B, device=dur.device, dtype=torch.int32)
+    flag = torch.empty(1, device=dur.device, dtype=torch.int32)
+    launch('ftmi_duration_counts', f'duration_counts[B={B},T={T}]', 0, B * T * 12,
+           dur.data_ptr(), B, T, int(apply_fill), float(fill_value),
+           offsets.data_ptr(), totals.data_ptr(), flag.data_ptr(), _stream())
+    return offsets, totals, flag
+
+
+def lr_index(offsets: torch.Tensor, T_mel: int) -> torch.Tensor:
+    _dev(offsets)
+    B, T1 = offsets.shape
+    index = torch.empty(B, T_mel, device=offsets.device, dtype=torch.int32)
+    launch('ftmi_lr_index', f'lr_index[B={B},T_mel={T_mel}]', 0, 4.0 * B * (T1 + T_mel),
+           offsets.data_ptr(), B, T1 - 1, T_mel, index.data_ptr(), _stream())
+    return index
+
+
+def length_regulate(x: torch.Tensor, index: torch.Tensor) -> torch.Tensor:
+    _dev(x, index)
+    B, T, C, xs = _rows(x)
+    T_mel = index.size(1)
+    y = torch.empty(B, T_mel, C, device=x.device, dtype=_f32)
+    launch('ftmi_length_regulate', f'length_regulate[B={B},T={T},T_mel={T_mel},C={C}]', 0,
+           4.0 * (B * T * C + B * T_mel * (C + 1)),
+           x.data_ptr(), xs, B, T, C, index.data_ptr(), T_mel, y.data_ptr(), y.stride(1), _stream())
+    return y
+
+
+def series_proj_add(x: torch.Tensor, pitch: torch.Tensor, wp, bp, ps: float, energy: torch.Tensor,
+                    we, be, es: float) -> torch.Tensor:
+    """In place on x (B, T, C): x += proj(pitch)*ps ; x += proj(energy)*es."""
+    _dev(x, pitch, energy, wp, bp, we, be)
+    B, T, C, xs = _rows(x)
+    pitch = pitch.reshape(B, T).to(_f32).contiguous()
+    energy = energy.reshape(B, T).to(_f32).contiguous()
+    launch('ftmi_series_proj_add', f'series_proj_add[B={B},T={T},C={C}]', 14.0 * B * T * C,
+           4.0 * (2 * B * T * C + 2 * B * T + 8 * C),
+           x.data_ptr(), xs, B, T, C, pitch.data_ptr(), wp.data_ptr(),
+           bp.data_ptr(), float(ps), energy.data_ptr(), we.data_ptr(), be.data_ptr(), float(es),
+           _stream())
+    return x
+
+
+def rowdot(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], alpha: float) -> torch.Tensor:
+    """(x . w + bias) / alpha over the last dim: (B, T, C) -> (B, T)."""
+    _dev(x, w, bias)
+    B, T, C, xs = _rows(x)
+    out = torch.empty(B, T, device=x.device, dtype=_f32)
+    launch('ftmi_rowdot', f'rowdot[M={B * T},C={C}]', 2.0 * B * T * C, 4.0 * (B * T * (C + 1) + C),
+           x.data_ptr(), xs, B * T, C, w.data_ptr(), _ptr(bias), float(alpha),
+           out.data_ptr(), _stream())
+    return out

@@ -1,0 +1,184 @@
+/*
+ * ftmi.h — C ABI of libftmi.so, the MI355X (gfx950) hot path of ForwardTacotron
+ * inference (reference: tarepan/ForwardTacotron, models/forward_tacotron.py).
+ *
+ * Every entry point:
+ *   - works on CALLER-OWNED device buffers (plain pointers + sizes, fp32 unless stated);
+ *   - enqueues on the given HIP stream (ftmi_stream_t = hipStream_t, NULL = null stream)
+ *     and never synchronises, allocates or frees;
+ *   - returns 0 on success, an FTMI_E_* code (>= 1000) for argument / shape errors
+ *     detected on the host, or a hipError_t (< 1000) if a launch failed.
+ *
+ * Layout convention: sequences are CHANNELS-LAST, (B, T, C) rows of C floats with a
+ * row stride given in floats. The reference's (B, C, T) tensors are produced only at
+ * the API edge (mel / mel_post outputs) through the transposed-store option.
+ *
+ * Each function names the reference code it replaces (file:line in the reference).
+ */
+#ifndef FTMI_H
+#define FTMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *ftmi_stream_t; /* hipStream_t */
+
+enum {
+  FTMI_OK = 0,
+  FTMI_E_ARG = 1001,         /* null pointer / non-positive size */
+  FTMI_E_SHAPE = 1002,       /* shape constraint violated (e.g. Cin % 16 != 0) */
+  FTMI_E_UNSUPPORTED = 1003, /* configuration without a compiled kernel */
+  FTMI_E_ALIGN = 1004        /* pointer / stride not 16-byte aligned */
+};
+
+/* ABI version; bumped on any signature change. */
+int ftmi_abi_version(void);
+/* Static string for an error code (FTMI_E_* or hipError_t). */
+const char *ftmi_strerror(int code);
+
+/* ------------------------------------------------------------------------------------
+ * Embedding gather.  out[n, :] = table[ids[n], :]
+ * Replaces nn.Embedding forward: models/forward_tacotron.py:125,304 and the predictor
+ * embeddings :31,47.  Ids outside [0, num_rows) produce a zero row and set *err = 1
+ * (the reference raises IndexError); err may be NULL.
+ * ---------------------------------------------------------------------------------- */
+int ftmi_embedding(const int64_t *ids, int64_t n, const float *table, int64_t num_rows,
+                   int64_t dim, float *out, int32_t *err, ftmi_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Fused Conv1d (implicit GEMM on fp32 MFMA) over channels-last sequences.
+ *   acc[b,t,n] = sum_{j<k} sum_c w[n, j*Cin + c] * xin[b, t + j - pad, c]   (zero outside [0,T))
+ *   for t in [0, T_out)
+ *   v = acc (+ bias[n]) ; relu? max(v,0) ; bn? v*bn_scale[n] + bn_shift[n] ; (+ residual)
+ *   xin[b,t,:] = x[b,t,:]                              if maxpool == 0
+ *              = max(x[b,t-1,:], x[b,t,:]) (t>0), x[b,0,:] (t==0)   if maxpool == 1
+ * Replaces BatchNormConv (models/forward_tacotron.py:58-71, models/common_layers.py:38-52),
+ * the CBHG maxpool+projections+residual (common_layers.py:100-109), nn.Linear layers
+ * (k = 1: pre_highway :113, lin / post_proj forward_tacotron.py:322,326, RNN input
+ * projections).  w is packed [N][k*Cin] (tap-major K).  Requires Cin % 16 == 0 and
+ * 16-byte aligned x / w / y with strides % 4 == 0.  yt (optional) receives the same
+ * values transposed to (B, N, T) — the reference's mel layout.
+ * ---------------------------------------------------------------------------------- */
+typedef struct ftmi_conv_args {
+  const float *x;
+  int64_t x_stride; /* floats between consecutive (b,t) rows of x */
+  int32_t B, T, Cin;
+  const float *w; /* [N][k*Cin] */
+  int32_t N, k, pad;
+  const float *bias;     /* [N] or NULL */
+  int32_t relu;          /* 0 / 1 */
+  const float *bn_scale; /* [N] or NULL (BN eval folded: gamma / sqrt(var + eps)) */
+  const float *bn_shift; /* [N] (beta - mean * scale) */
+  int32_t maxpool;       /* 0 / 1 */
+  const float *residual; /* (B,T,N) rows with res_stride, or NULL */
+  int64_t res_stride;
+  float *y; /* (B,T,N) rows with y_stride, or NULL if only yt is wanted */
+  int64_t y_stride;
+  float *yt; /* (B,N,T_out) or NULL */
+  int32_t T_out; /* output frames per sequence, 0 = T (even k in PyTorch gives T+1) */
+} ftmi_conv_args;
+
+int ftmi_conv1d(const ftmi_conv_args *args, ftmi_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * CBHG convolution bank: K BatchNormConvs with kernel sizes 1..K (pad k//2, ReLU then
+ * BN, output sliced to T), concatenated on channels (common_layers.py:67-71,92-97).
+ *   y[b,t, g*Cout + n] = BN_g(relu(sum_{j<=g} sum_c w_g[n, j*Cin+c] * x[b, t+j-(g+1)/2, c]))
+ * w: the K packed weights back to back, group g is [Cout][(g+1)*Cin] starting at float
+ * offset Cout*Cin*g*(g+1)/2.  bn_scale / bn_shift: [K*Cout].  y: (B,T,K*Cout) rows.
+ * ---------------------------------------------------------------------------------- */
+int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t Cin,
+                   const float *w, int32_t K, int32_t Cout, const float *bn_scale,
+                   const float *bn_shift, float *y, int64_t y_stride, ftmi_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * One highway layer (common_layers.py:22-35):
+ *   g = sigmoid(x W2^T + b2);  y = g * relu(x W1^T + b1) + (1 - g) * x
+ * w12: [2C][C] with rows interleaved in blocks of 32: rows 64q..64q+31 = W1 rows
+ * 32q..32q+31, rows 64q+32..64q+63 = W2 rows 32q..32q+31.  Requires C % 32 == 0.
+ * y must not alias x.
+ * ---------------------------------------------------------------------------------- */
+int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t C, const float *w12,
+                 const float *b1, const float *b2, float *y, int64_t y_stride,
+                 ftmi_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Bidirectional single-layer GRU / LSTM recurrence, PyTorch semantics, h0 = c0 = 0,
+ * both directions over the full padded length (no packing), output [fwd | bwd].
+ *   GRU  (cell = 0, gates r,z,n): common_layers.py:84,118 and forward_tacotron.py:39,53
+ *   LSTM (cell = 1, gates i,f,g,o): forward_tacotron.py:165-168,321
+ * xp: precomputed input projections, rows of 2*G*H floats ([dir][gate][unit]), already
+ *     including b_ih (GRU) or b_ih + b_hh (LSTM); row for (b, t) is
+ *       xp + (b*T_src + src)*xp_stride,  src = t if index == NULL else index[b*T + t];
+ *     src < 0 selects xp_zero (the projection of a zero input row: the biases), 2*G*H.
+ *     (index = LengthRegulator map: the LSTM reads phoneme-rate projections directly.)
+ * w_hh: [2][G*H][H] (PyTorch weight_hh_l0 then weight_hh_l0_reverse).
+ * b_hh: [2][G*H] for GRU (added inside the recurrence), ignored (may be NULL) for LSTM.
+ * lengths: int32 [B] or NULL.  Packed-sequence semantics (pack_padded_sequence +
+ *     pad_packed_sequence, forward_tacotron.py:224-230): frames t >= lengths[b] output
+ *     pad_value and the reverse direction starts from h = c = 0 at t = lengths[b]-1.
+ * y:    (B, T, 2H) rows with y_stride.
+ * sync: 16-byte aligned device workspace of ftmi_rnn_workspace_bytes() bytes (zeroed by
+ *     the call; holds the arrival counters and the h exchange buffer).  After the stream
+ *     has completed, the 32-bit word at byte offset ftmi_rnn_error_offset() is non-zero if
+ *     a workgroup timed out waiting for its group (not all workgroups resident).
+ * Supported H: GRU 64, 128, 256; LSTM 512 (the ForwardTacotron config).
+ * ---------------------------------------------------------------------------------- */
+int64_t ftmi_rnn_workspace_bytes(int32_t B, int32_t H, int32_t cell);
+int64_t ftmi_rnn_error_offset(int32_t B);
+int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, const float *xp,
+                   int64_t xp_stride, int32_t T_src, const int32_t *index,
+                   const float *xp_zero, const float *w_hh, const float *b_hh,
+                   const int32_t *lengths, float pad_value, float *y, int64_t y_stride,
+                   void *sync, ftmi_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Duration post-processing of ForwardTacotron.generate + LengthRegulator counts:
+ *   if sum_{b,t} trunc_int64(dur) <= 0: dur[:] = fill_value   (forward_tacotron.py:254-255,
+ *                                                               only when apply_fill != 0)
+ *   dur[dur < 0] = 0                    (in place, common_layers.py:13)
+ *   count = int64(trunc(fp32(dur + 0.5)))  (common_layers.py:16)
+ *   offsets[b, 0..T] = exclusive prefix sum of counts; totals[b] = offsets[b, T]
+ * Single launch, bit-exact. offsets: int32 [B][T+1]; totals: int32 [B];
+ * fill_flag (optional int32[1]) receives 1 if the fill rule fired.
+ * ---------------------------------------------------------------------------------- */
+int ftmi_duration_counts(float *dur, int32_t B, int32_t T, int32_t apply_fill,
+                         float fill_value, int32_t *offsets, int32_t *totals,
+                         int32_t *fill_flag, ftmi_stream_t stream);
+
+/* Frame -> phoneme index map of the LengthRegulator: index[b, f] = t such that
+ * offsets[b,t] <= f < offsets[b,t+1], or -1 for f >= totals[b] (zero padding,
+ * pad_sequence in common_layers.py:18).  index: int32 [B][T_mel]. */
+int ftmi_lr_index(const int32_t *offsets, int32_t B, int32_t T, int32_t T_mel,
+                  int32_t *index, ftmi_stream_t stream);
+
+/* LengthRegulator expansion (common_layers.py:12-19): y[b,f,:] = x[b,index[b,f],:] or 0. */
+int ftmi_length_regulate(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t C,
+                         const int32_t *index, int32_t T_mel, float *y, int64_t y_stride,
+                         ftmi_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * Pitch / energy conditioning (forward_tacotron.py:308-314):
+ *   x[b,t,c] = (x[b,t,c] + P[b,t,c] * pitch_strength) + E[b,t,c] * energy_strength
+ *   P = Conv1d(1 -> C, k=3, pad=1, bias)(pitch[b,:]) at t (same for E with energy).
+ * pitch / energy: (B, T) contiguous. wp / we: [C][3]; bp / be: [C].
+ * ---------------------------------------------------------------------------------- */
+int ftmi_series_proj_add(float *x, int64_t x_stride, int32_t B, int32_t T, int32_t C,
+                         const float *pitch, const float *wp, const float *bp,
+                         float pitch_strength, const float *energy, const float *we,
+                         const float *be, float energy_strength, ftmi_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * SeriesPredictor head (forward_tacotron.py:41,54-55): out[m] = (x[m,:] . w + bias[0]) / alpha
+ * x: M rows of C floats (row stride x_stride); bias: device float[1] or NULL; out: M floats.
+ * ---------------------------------------------------------------------------------- */
+int ftmi_rowdot(const float *x, int64_t x_stride, int64_t M, int32_t C, const float *w,
+                const float *bias, float alpha, float *out, ftmi_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FTMI_H */

