@@ -180,11 +180,14 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
       const int soff = ((t - 1) & 1) * hx_par;
 #pragma unroll
       for (int kb = 0; kb < KB; kb += 4) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + kb * 4, soff, 16);
-        hf[kb] = __builtin_bit_cast(float, v[0]);
-        hf[kb + 1] = __builtin_bit_cast(float, v[1]);
-        hf[kb + 2] = __builtin_bit_cast(float, v[2]);
-        hf[kb + 3] = __builtin_bit_cast(float, v[3]);
+        // NB: bit_cast the whole vector; extracting u32 lanes one by one and bit-casting
+        // each is miscompiled by ROCm 7.2 (every lane reads element 0).
+        const f32x4 v = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + kb * 4, soff, 16));
+        hf[kb] = v.x;
+        hf[kb + 1] = v.y;
+        hf[kb + 2] = v.z;
+        hf[kb + 3] = v.w;
       }
     }
 

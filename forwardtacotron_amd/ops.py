@@ -142,6 +142,8 @@ def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Opt
     xp: (B, T_src, 2*G*H) input projections; index: (B, T) int32 frame -> row map.
     check=True synchronises and raises RnnTimeout if a workgroup gave up waiting.
     """
+    if lengths is not None:  # host-side lengths (as pack_padded_sequence takes) are fine
+        lengths = lengths.to(device=xp.device, dtype=torch.int32).contiguous()
     _dev(xp, w_hh, b_hh, index, xp_zero, lengths)
     B, T_src, _, xs = _rows(xp)
     T = T if T is not None else T_src
@@ -151,8 +153,6 @@ def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Opt
                      dtype=torch.int32)
     if index is not None:
         assert index.dtype == torch.int32 and index.is_contiguous() and index.shape == (B, T)
-    if lengths is not None:
-        lengths = lengths.to(device=xp.device, dtype=torch.int32).contiguous()
     G = 4 if cell else 3
     label = f'rnn_bidir[{"lstm" if cell else "gru"},B={B},T={T},H={H}]'
     # recurrent contraction W_hh h per step and direction; bytes: xp rows read per frame,
