@@ -73,8 +73,33 @@ def build(force: bool = False, verbose: bool = False, extra=()) -> Path:
     return LIB
 
 
+def build_stamps() -> Path:
+    """Diagnostic library libftmi_stamps.so: the recurrence kernel with s_memtime phase
+    stamps (-DFTMI_RNN_STAMPS).  Never loaded by the package unless FTMI_LIB points at it."""
+    out = PKG / 'libftmi_stamps.so'
+    objs = []
+    for src in _sources():
+        obj = OBJ / (src.stem + ('_stamps.o' if src.stem == 'rnn' else '.o'))
+        if src.stem == 'rnn':
+            cmd = [HIPCC, *CFLAGS, '-DFTMI_RNN_STAMPS', '-c', str(src), '-o', str(obj)]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(r.stderr)
+        else:
+            _compile(src, False, [])
+        objs.append(obj)
+    r = subprocess.run([HIPCC, '-shared', f'--offload-arch={ARCH}', '-fPIC', *map(str, objs), '-o',
+                        str(out)], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr)
+    return out
+
+
 if __name__ == '__main__':
     ap = argparse.ArgumentParser()
     ap.add_argument('--force', action='store_true')
+    ap.add_argument('--stamps', action='store_true', help='also build libftmi_stamps.so')
     a = ap.parse_args()
     print(build(force=a.force, verbose=True))
+    if a.stamps:
+        print(build_stamps())

@@ -19,8 +19,10 @@
 // update to the U x 16 (unit, sequence) cells they own (c / h state lives in registers).
 //
 // Hand-off between the BPG workgroups of a group (MI355X_MICROARCH.md "Valid forms",
-// row 1): new h values go to a small exchange buffer hx[t & 1][seq][2H] in the call's
-// workspace (parity double buffering is race-free because a workgroup can only start
+// row 1): new h values go to a small exchange buffer hx[t & 1][group][16*H] in the call's
+// workspace, stored in MFMA-FRAGMENT ORDER ([wave][kb/4][lane][4]) so that every consumer
+// wave-instruction reads 1 KB of consecutive bytes (sc1 loads bypass L1: a row-major image
+// made each instruction touch 64 lines and fetch every line 8 times) (parity double buffering is race-free because a workgroup can only start
 // step t+1 after every workgroup of its group finished step t) with write-through (sc1)
 // stores; every storing wave drains
 // vmcnt(0); after a workgroup barrier ONE lane adds 1 to the group's arrival counter
@@ -35,6 +37,27 @@
 // Every spin is bounded; on timeout the call's error word is set and the workgroup leaves
 // the time loop.
 #include "common.h"
+
+// ---- diagnostic build only (-DFTMI_RNN_STAMPS): per-phase s_memtime sums per workgroup
+#ifdef FTMI_RNN_STAMPS
+__device__ unsigned long long ftmi_rnn_stamps[2048 * 8];
+#define STAMP(i)                                                                      \
+  do {                                                                                \
+    if (threadIdx.x == 0) {                                                           \
+      __builtin_amdgcn_sched_barrier(0);                                              \
+      unsigned long long now__;                                                       \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" \
+                   : "=s"(now__)::"memory");                                         \
+      __builtin_amdgcn_sched_barrier(0);                                              \
+      st_acc[i] += now__ - st_last;                                                   \
+      st_last = now__;                                                                \
+    }                                                                                 \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
 
 namespace {
 
@@ -125,34 +148,51 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
       bhh[j][g] = (CELL == 0) ? p.b_hh[dir * G * H + g * H + u0 + cu[j]] : 0.f;
   }
 
-  // ---- h operand source: this group's rows of the exchange buffer -------------------
-  float *hxbase = p.hx + (size_t)chunk * NB * (2 * H) + dir * H;
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(hxbase, (short)0, 0x7FFFFFF0, 0x00020000);
-  const unsigned hoff = (unsigned)((lc * (2 * H) + wave * KW + ls * KB) * 4);
+  // ---- h operand source: this group's fragment-ordered slab of the exchange buffer ---
+  // slab (16*H floats) = [wave 4][kbq KB/4][lane 64][4]; (seq bl, unit k) lives at
+  //   (((k / KW) * (KB/4) + (k % KB) / 4) * 64 + ((k % KW) / KB) * 16 + bl) * 4 + (k % 4)
+  const int gglob = 2 * chunk + dir;
+  const int slab = 16 * H;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.hx, (short)0, 0x7FFFFFF0, 0x00020000);
+  const unsigned hoff = (unsigned)(((gglob * slab) + wave * (KB / 4) * 256 + lane * 4) * 4);
   const int hx_par = p.nrows_hx * 2 * H * 4;  // bytes between the two parity halves
+  int hxo[CPT];  // this thread's cells in the slab
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int k = u0 + cu[j], bl = cb[j] - chunk * NB;
+    hxo[j] = gglob * slab + (((k / KW) * (KB / 4) + (k % KB) / 4) * 64 + ((k % KW) / KB) * 16 + bl) * 4 + (k % 4);
+  }
   int len[CPT];
 #pragma unroll
   for (int j = 0; j < CPT; ++j) len[j] = (p.lengths && cvalid[j]) ? p.lengths[cb[j]] : p.T;
 
   if (tid == 0) s_abort = 0;
   __syncthreads();
+#ifdef FTMI_RNN_STAMPS
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = 0;
+  if (tid == 0) st_last = __builtin_amdgcn_s_memtime();
+#endif
 
-  for (int t = 0; t < p.T; ++t) {
+  // input projections (independent of h): step t+1's rows are fetched during step t
+  auto load_gx = [&](int t, float (&g)[CPT][G]) {
     const int tt = dir ? (p.T - 1 - t) : t;
-
-    // input projections of this step (independent of h): issue before the wait
-    float gx[CPT][G];
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
       const int b = cvalid[j] ? cb[j] : 0;
       int src = tt;
       if (p.index) src = p.index[(size_t)b * p.T + tt];
-      const float *row = src >= 0 ? p.xp + ((size_t)b * p.T_src + src) * p.xp_stride
-                                  : p.xp_zero;
+      const float *row = src >= 0 ? p.xp + ((size_t)b * p.T_src + src) * p.xp_stride : p.xp_zero;
 #pragma unroll
-      for (int g = 0; g < G; ++g) gx[j][g] = row[dir * G * H + g * H + u0 + cu[j]];
+      for (int gi = 0; gi < G; ++gi) g[j][gi] = row[dir * G * H + gi * H + u0 + cu[j]];
     }
+  };
+  float gx[CPT][G], gxn[CPT][G];
+  load_gx(0, gx);
 
+  for (int t = 0; t < p.T; ++t) {
+    const int tt = dir ? (p.T - 1 - t) : t;
+
+    STAMP(0);  // xp gather issued (and landed, in the stamp build)
     // wait until every workgroup of the group has published h_{t-1}
     if (BPG > 1 && t > 0) {
       if (tid == 0) {
@@ -171,6 +211,7 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
       if (s_abort) break;
     }
 
+    STAMP(1);  // group arrival observed
     // h_{t-1} operand (sc1 loads), zero at t = 0
     float hf[KB];
     if (t == 0) {
@@ -183,7 +224,7 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
         // NB: bit_cast the whole vector; extracting u32 lanes one by one and bit-casting
         // each is miscompiled by ROCm 7.2 (every lane reads element 0).
         const f32x4 v = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + kb * 4, soff, 16));
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + kb * 256, soff, 16));
         hf[kb] = v.x;
         hf[kb + 1] = v.y;
         hf[kb + 2] = v.z;
@@ -191,6 +232,8 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
       }
     }
 
+    if (t + 1 < p.T) load_gx(t + 1, gxn);
+    STAMP(2);  // h operand landed
     // partial gates over this wave's quarter of K
     f32x4 acc[RB];
 #pragma unroll
@@ -207,6 +250,7 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
       for (int i = 0; i < 4; ++i)
         red[(wave * R + rb * 16 + ls * 4 + i) * RED_STRIDE + lc] = acc[rb][i];
     __syncthreads();
+    STAMP(3);  // MFMAs + partial sums in LDS
 
     // cell update
 #pragma unroll
@@ -243,18 +287,28 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
       }
       hstate[j] = hn;
       if (cvalid[j]) {
-        __hip_atomic_store(p.hx + ((size_t)(t & 1) * p.nrows_hx + cb[j]) * (2 * H) + dir * H + u0 + cu[j],
-                           hn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p.hx + (size_t)(t & 1) * p.nrows_hx * 2 * H + hxo[j], hn,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         p.y[((size_t)cb[j] * p.T + tt) * p.y_stride + dir * H + u0 + cu[j]] = yout;
       }
     }
 
+#pragma unroll
+    for (int j = 0; j < CPT; ++j)
+#pragma unroll
+      for (int gi = 0; gi < G; ++gi) gx[j][gi] = gxn[j][gi];
+    STAMP(4);  // cell update + stores issued
     // publish: every storing wave drains, barrier, one lane arrives
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (BPG > 1 && tid == 0)
       __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    STAMP(5);  // drained + arrived
   }
+#ifdef FTMI_RNN_STAMPS
+  if (tid == 0)
+    for (int i = 0; i < 6; ++i) ftmi_rnn_stamps[blockIdx.x * 8 + i] = st_acc[i];
+#endif
 }
 
 template <int CELL, int H, int U>
@@ -341,3 +395,10 @@ extern "C" int64_t ftmi_rnn_error_offset(int32_t B) {
   const int64_t nchunks = (B + NB - 1) / NB;
   return 2 * nchunks * CNT_PAD * (int64_t)sizeof(unsigned);
 }
+
+#ifdef FTMI_RNN_STAMPS
+extern "C" int ftmi_debug_rnn_stamps(unsigned long long *host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ftmi_rnn_stamps),
+                                  sizeof(unsigned long long) * (size_t)n, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -209,37 +209,66 @@ class ForwardTacotron(nn.Module):
         return {'mel': x_mel, 'mel_post': x_post,
                 'dur': dur_hat, 'pitch': pitch_hat, 'energy': energy_hat}
 
+    def _side_streams(self, device):
+        cache = self.__dict__.setdefault('_ftmi_streams', {})
+        if device not in cache:
+            cache[device] = [torch.cuda.Stream(device=device) for _ in range(3)]
+        return cache[device]
+
+    def _phoneme_phase(self, x, alpha, pitch_fn, energy_fn):
+        """Duration / pitch / energy predictors and the prenet CBHG are independent: they
+        run concurrently on three side streams next to the caller's stream (the predictor
+        recurrences occupy only 2*ceil(B/16) workgroups each).  Returns
+        (dur_hat, pitch_hat, energy_hat, prenet_out) ready on the caller's stream."""
+        main = torch.cuda.current_stream(x.device)
+        s_pitch, s_energy, s_prenet = self._side_streams(x.device)
+        for s in (s_pitch, s_energy, s_prenet):
+            s.wait_stream(main)
+        with torch.cuda.stream(s_pitch):
+            pitch_hat = pitch_fn(self.pitch_pred.forward_bt(x).unsqueeze(1))
+        with torch.cuda.stream(s_energy):
+            energy_hat = energy_fn(self.energy_pred.forward_bt(x).unsqueeze(1))
+        with torch.cuda.stream(s_prenet):
+            enc = self.prenet.forward_cl(ops.embedding(x, self.embedding.weight.detach()))
+        dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
+        for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat), (s_prenet, enc)):
+            main.wait_stream(s)
+            t.record_stream(main)
+        return dur_hat, pitch_hat, energy_hat, enc
+
     def generate(self,
                  x: torch.Tensor,
                  alpha=1.0,
                  pitch_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x,
                  energy_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x) -> Dict[str, torch.Tensor]:
-        """`models/forward_tacotron.py:244-268`."""
+        """`models/forward_tacotron.py:244-268`.  The callbacks run on the stream of their
+        predictor (torch ops issued inside them are ordered after the prediction)."""
         self.eval()
         self._check_device(x)
         with torch.no_grad():
-            dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
-            pitch_hat = self.pitch_pred.forward_bt(x).unsqueeze(1)
-            pitch_hat = pitch_function(pitch_hat)
-            energy_hat = self.energy_pred.forward_bt(x).unsqueeze(1)
-            energy_hat = energy_function(energy_hat)
-            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, apply_fill=True)
+            dur_hat, pitch_hat, energy_hat, enc = self._phoneme_phase(
+                x, alpha, pitch_function, energy_function)
+            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, apply_fill=True, enc=enc)
 
     def generate_jit(self, x: torch.Tensor, alpha: float = 1.0, beta: float = 1.0) -> Dict[str, torch.Tensor]:
         """`models/forward_tacotron.py:270-284` (pitch scaled by beta, no callbacks)."""
         self._check_device(x)
         with torch.no_grad():
-            dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
-            pitch_hat = self.pitch_pred.forward_bt(x).unsqueeze(1) * beta
-            energy_hat = self.energy_pred.forward_bt(x).unsqueeze(1)
-            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, apply_fill=True)
+            dur_hat, pitch_hat, energy_hat, enc = self._phoneme_phase(
+                x, alpha, lambda p: p * beta, lambda e: e)
+            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, apply_fill=True, enc=enc)
 
     def get_step(self) -> int:
         return self.step.data.item()
 
-    def _generate_mel(self, x, dur_hat, pitch_hat, energy_hat, apply_fill=False):
-        """`models/forward_tacotron.py:289-330` (+ the fill-2 rule of :254-255 when apply_fill)."""
-        enc = self._encode(x, pitch_hat, energy_hat)
+    def _generate_mel(self, x, dur_hat, pitch_hat, energy_hat, apply_fill=False, enc=None):
+        """`models/forward_tacotron.py:289-330` (+ the fill-2 rule of :254-255 when apply_fill).
+        enc: the prenet output if already computed (by _phoneme_phase)."""
+        if enc is None:
+            enc = self.prenet.forward_cl(ops.embedding(x, self.embedding.weight.detach()))
+        wp, bp, we, be = self._series_proj_weights()
+        ops.series_proj_add(enc, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
+                            self.energy_strength)
         offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=apply_fill)
         T_mel = int(totals.max().item())  # the one host sync: output size is data dependent
         index = ops.lr_index(offsets, T_mel)
