@@ -19,6 +19,8 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
+ABI_VERSION = 2
+MMA_F32, MMA_BF16X6 = 0, 1
 
 
 class ConvArgs(ctypes.Structure):
@@ -28,7 +30,7 @@ class ConvArgs(ctypes.Structure):
         ('w', P), ('N', c_int), ('k', c_int), ('pad', c_int),
         ('bias', P), ('relu', c_int), ('bn_scale', P), ('bn_shift', P), ('maxpool', c_int),
         ('residual', P), ('res_stride', c_int64),
-        ('y', P), ('y_stride', c_int64), ('yt', P), ('T_out', c_int),
+        ('y', P), ('y_stride', c_int64), ('yt', P), ('T_out', c_int), ('mma', c_int),
     ]
 
 
@@ -38,8 +40,9 @@ SIGNATURES = {
     'ftmi_strerror': (ctypes.c_char_p, [c_int]),
     'ftmi_embedding': (c_int, [P, c_int64, P, c_int64, c_int64, P, P, P]),
     'ftmi_conv1d': (c_int, [ctypes.POINTER(ConvArgs), P]),
-    'ftmi_conv_bank': (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, c_int, P, P, P, c_int64, P]),
-    'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, c_int64, P]),
+    'ftmi_conv_bank': (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, c_int, P, P, P, c_int64,
+                               c_int, P]),
+    'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, c_int64, c_int, P]),
     'ftmi_rnn_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
     'ftmi_rnn_error_offset': (c_int64, [c_int]),
     'ftmi_rnn_bidir': (c_int, [c_int, c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,
@@ -74,7 +77,7 @@ def load():
         fn = getattr(lib, name)  # AttributeError if the export is missing
         fn.restype = res
         fn.argtypes = args
-    if lib.ftmi_abi_version() != 1:
+    if lib.ftmi_abi_version() != ABI_VERSION:
         raise FtmiError('libftmi.so ABI version mismatch')
     _lib = lib
     return lib

@@ -16,6 +16,14 @@
 // Inside a BK = 16 chunk lane half h consumes k = 8h + s at MFMA s (s = 0..7) for both
 // operands, so every lane reads its fragments with two ds_read_b128 per operand; the
 // LDS row stride of 20 floats makes those reads bank-conflict free (5i mod 16 distinct).
+//
+// Second path, "x6" (mma = 1): the same contraction on the bf16 matrix pipe (16x the fp32
+// MFMA rate).  Both fp32 operands are split while staged into LDS, a = a1 + a2 + a3 with
+// a1 = bf16(a), a2 = bf16(a - a1), a3 = bf16(a - a1 - a2) (each difference is exact in
+// fp32), and every 16x16x32 tile accumulates the six cross products with i + j <= 4
+// (a1b1, a1b2, a2b1, a1b3, a2b2, a3b1) in fp32 — the dropped terms are < 2^-24 relative,
+// so the result is fp32-accurate (emulated: max err 5-7e-7 vs 2e-6 for a plain fp32 GEMM
+// at K = 256..6144) at 16/6 = 2.7x the fp32 MFMA rate.
 #include "common.h"
 
 namespace {
@@ -56,6 +64,14 @@ struct GemmParams {
   const float *b2;
   GemmGroup g[MAX_GROUPS];
 };
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int X6_BK = 32;
+constexpr int X6_STRIDE = 48;  // bf16 per staged row (32 + 16 pad): 96-B rows make the
+                               // ds_read_b128 fragment reads of 16x16x32 conflict free
+constexpr int X6_PIECE = BM * X6_STRIDE;  // bf16 per (operand, piece) image
 
 __device__ __forceinline__ f32x4 fmax4(f32x4 a, f32x4 b) {
   f32x4 r;
@@ -224,9 +240,202 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const GemmParams p) {
   }
 }
 
-int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, hipStream_t s) {
+
+// ---------------------------------------------------------------------------------------
+// bf16x6 path.  128x128 block tile, BK = 32, 4 waves (2x2) each owning 64x64 = 4x4 tiles of
+// v_mfma_f32_16x16x32_bf16.  LDS: [buffer 2][operand 2][piece 3][row 128][48] bf16 = 144 KB
+// (one workgroup per CU); global loads for chunk k+1 are issued before the MFMAs of chunk k.
+__device__ __forceinline__ void split3(f32x4 v, bf16x4 &h1, bf16x4 &h2, bf16x4 &h3) {
+  h1 = __builtin_convertvector(v, bf16x4);
+  const f32x4 r1 = v - __builtin_convertvector(h1, f32x4);
+  h2 = __builtin_convertvector(r1, bf16x4);
+  const f32x4 r2 = r1 - __builtin_convertvector(h2, f32x4);
+  h3 = __builtin_convertvector(r2, bf16x4);
+}
+
+template <int EPI, bool MAXPOOL>
+__global__ __launch_bounds__(256, 1) void conv_gemm_x6_kernel(const GemmParams p) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 2 * 3 * X6_PIECE];
+
+  const int tile = blockIdx.x;
+  int gi = 0;
+  while (gi + 1 < p.ngroups && tile >= p.g[gi + 1].tile0) ++gi;
+  const GemmGroup &G = p.g[gi];
+  const int lt = tile - G.tile0;
+  const int mt = lt / G.ntiles;
+  const int nt = lt - mt * G.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // loader: rows lr + 32q (q = 0..3) of both operands, float4 #lc of the 32-wide chunk
+  const int lr = tid >> 3, lc = tid & 7;
+  int ab[4], at[4];
+  bool aok[4], bok[4];
+  const float *wrow[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = m0 + lr + 32 * q;
+    aok[q] = m < p.M;
+    const int mm = aok[q] ? m : 0;
+    ab[q] = mm / p.To;
+    at[q] = mm - ab[q] * p.To;
+    const int n = n0 + lr + 32 * q;
+    bok[q] = n < G.N;
+    wrow[q] = G.w + (int64_t)(bok[q] ? n : 0) * G.Ktot;
+  }
+  const int nk = (G.Ktot + X6_BK - 1) / X6_BK;
+  f32x4 ra[4], rb[4];
+
+  auto gload = [&](int kc) {
+    const int k = kc * X6_BK + 4 * lc;  // this thread's 4 consecutive K indices
+    const bool kok = k < G.Ktot;
+    const int j = k / p.Cin;
+    const int c = k - j * p.Cin;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ts = at[q] + j - G.pad;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (kok && aok[q] && ts >= 0 && ts < p.T) {
+        const float *src = p.x + ((int64_t)ab[q] * p.T + ts) * p.x_stride + c;
+        v = *(const f32x4 *)src;
+        if (MAXPOOL && ts > 0) v = fmax4(v, *(const f32x4 *)(src - p.x_stride));
+      }
+      ra[q] = v;
+      f32x4 w = {0.f, 0.f, 0.f, 0.f};
+      if (kok && bok[q]) w = *(const f32x4 *)(wrow[q] + k);
+      rb[q] = w;
+    }
+  };
+  auto swrite = [&](int buf) {
+    __bf16 *base = lds + buf * (2 * 3 * X6_PIECE);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int off = (lr + 32 * q) * X6_STRIDE + 4 * lc;
+      bf16x4 h1, h2, h3;
+      split3(ra[q], h1, h2, h3);
+      *(bf16x4 *)(base + 0 * X6_PIECE + off) = h1;
+      *(bf16x4 *)(base + 1 * X6_PIECE + off) = h2;
+      *(bf16x4 *)(base + 2 * X6_PIECE + off) = h3;
+      split3(rb[q], h1, h2, h3);
+      *(bf16x4 *)(base + 3 * X6_PIECE + off) = h1;
+      *(bf16x4 *)(base + 4 * X6_PIECE + off) = h2;
+      *(bf16x4 *)(base + 5 * X6_PIECE + off) = h3;
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  auto compute = [&](int buf) {
+    const __bf16 *base = lds + buf * (2 * 3 * X6_PIECE);
+    bf16x8 a[4][3], b[4][3];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+        a[mi][pc] = *(const bf16x8 *)(base + pc * X6_PIECE + (wm * 64 + mi * 16 + fr) * X6_STRIDE + fk);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+        b[ni][pc] = *(const bf16x8 *)(base + (3 + pc) * X6_PIECE + (wn * 64 + ni * 16 + fr) * X6_STRIDE + fk);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        f32x4 c = acc[mi][ni];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][2], b[ni][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][1], b[ni][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][0], b[ni][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][1], b[ni][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][0], b[ni][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][0], b[ni][0], c, 0, 0, 0);
+        acc[mi][ni] = c;
+      }
+  };
+
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int cur = kc & 1;
+    if (kc + 1 < nk) gload(kc + 1);
+    compute(cur);
+    if (kc + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: tile (mi, ni) element (row 4*(lane>>4) + i, col lane & 15)
+  const int er = 4 * (lane >> 4);
+  if constexpr (EPI == EPI_CONV) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int col = n0 + wn * 64 + ni * 16 + fr;
+      if (col >= G.N) continue;
+      const float bias = G.bias ? G.bias[col] : 0.f;
+      const float sc = G.scale ? G.scale[col] : 1.f;
+      const float sh = G.scale ? G.shift[col] : 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wm * 64 + mi * 16 + er + i;
+          if (row >= p.M) continue;
+          float v = acc[mi][ni][i];
+          if (G.bias) v += bias;
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (G.scale) v = v * sc + sh;
+          if (p.residual) v += p.residual[(int64_t)row * p.res_stride + col];
+          if (p.y) p.y[(int64_t)row * p.y_stride + G.ycol0 + col] = v;
+          if (p.yt) {
+            const int b = row / p.To, t = row - b * p.To;
+            p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = v;
+          }
+        }
+    }
+  } else {
+    // packed column blocks of 32: tiles ni = 0,1 are W1 columns, ni = 2,3 the matching W2
+    if (n0 + wn * 64 >= G.N) return;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int col = (n0 + wn * 64) / 2 + ni * 16 + fr;
+      const float b1 = p.b1[col], b2 = p.b2[col];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wm * 64 + mi * 16 + er + i;
+          if (row >= p.M) continue;
+          const float x1 = acc[mi][ni][i] + b1;
+          const float x2 = acc[mi][ni + 2][i] + b2;
+          const float g = ftmi_sigmoid(x2);
+          const float xin = p.x[(int64_t)row * p.x_stride + col];
+          p.y[(int64_t)row * p.y_stride + col] = g * fmaxf(x1, 0.f) + (1.f - g) * xin;
+        }
+    }
+  }
+}
+
+int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hipStream_t s) {
   if (nblocks <= 0) return FTMI_OK;
   dim3 grid(nblocks), block(256);
+  if (mma == 1) {
+    if (epi == EPI_HIGHWAY)
+      hipLaunchKernelGGL((conv_gemm_x6_kernel<EPI_HIGHWAY, false>), grid, block, 0, s, p);
+    else if (maxpool)
+      hipLaunchKernelGGL((conv_gemm_x6_kernel<EPI_CONV, true>), grid, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_gemm_x6_kernel<EPI_CONV, false>), grid, block, 0, s, p);
+    FTMI_CHECK_LAUNCH();
+    return FTMI_OK;
+  }
   if (epi == EPI_HIGHWAY)
     hipLaunchKernelGGL((conv_gemm_kernel<EPI_HIGHWAY, false>), grid, block, 0, s, p);
   else if (maxpool)
@@ -243,6 +452,7 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   if (!a || !a->x || !a->w || (!a->y && !a->yt)) return FTMI_E_ARG;
   if (a->B <= 0 || a->T <= 0 || a->Cin <= 0 || a->N <= 0 || a->k <= 0) return FTMI_E_ARG;
   if (a->Cin % 16 != 0) return FTMI_E_SHAPE;
+  if (a->mma != 0 && a->mma != 1) return FTMI_E_ARG;
   if (a->pad < 0 || a->pad >= a->k + a->T) return FTMI_E_SHAPE;
   if ((a->bn_scale == nullptr) != (a->bn_shift == nullptr)) return FTMI_E_ARG;
   if (!ftmi_aligned16(a->x) || !ftmi_aligned16(a->w) || (a->x_stride & 3)) return FTMI_E_ALIGN;
@@ -277,13 +487,13 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   g.ntiles = (a->N + BN - 1) / BN;
   g.tile0 = 0;
   const int mtiles = (p.M + BM - 1) / BM;
-  return launch(p, EPI_CONV, a->maxpool != 0, mtiles * g.ntiles, ftmi_hs(stream));
+  return launch(p, EPI_CONV, a->maxpool != 0, mtiles * g.ntiles, a->mma, ftmi_hs(stream));
 }
 
 extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T,
                               int32_t Cin, const float *w, int32_t K, int32_t Cout,
                               const float *bn_scale, const float *bn_shift, float *y,
-                              int64_t y_stride, ftmi_stream_t stream) {
+                              int64_t y_stride, int32_t mma, ftmi_stream_t stream) {
   if (!x || !w || !bn_scale || !bn_shift || !y) return FTMI_E_ARG;
   if (B <= 0 || T <= 0 || Cin <= 0 || Cout <= 0 || K <= 0) return FTMI_E_ARG;
   if (K > MAX_GROUPS) return FTMI_E_UNSUPPORTED;
@@ -322,12 +532,12 @@ extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32
     g.tile0 = tile0;
     tile0 += mtiles * ntiles;
   }
-  return launch(p, EPI_CONV, false, tile0, ftmi_hs(stream));
+  return launch(p, EPI_CONV, false, tile0, mma, ftmi_hs(stream));
 }
 
 extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t C,
                             const float *w12, const float *b1, const float *b2, float *y,
-                            int64_t y_stride, ftmi_stream_t stream) {
+                            int64_t y_stride, int32_t mma, ftmi_stream_t stream) {
   if (!x || !w12 || !b1 || !b2 || !y) return FTMI_E_ARG;
   if (M <= 0 || C <= 0) return FTMI_E_ARG;
   if (C % 32 != 0 || C % 16 != 0) return FTMI_E_SHAPE;
@@ -356,5 +566,5 @@ extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t
   g.ntiles = (2 * C + BN - 1) / BN;
   g.tile0 = 0;
   const int mtiles = (p.M + BM - 1) / BM;
-  return launch(p, EPI_HIGHWAY, false, mtiles * g.ntiles, ftmi_hs(stream));
+  return launch(p, EPI_HIGHWAY, false, mtiles * g.ntiles, mma, ftmi_hs(stream));
 }

@@ -8,6 +8,7 @@ a CPU tensor or a missing library raises.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -17,6 +18,10 @@ from ._lib import ConvArgs
 from .probe import launch
 
 _f32 = torch.float32
+
+# Matrix path of the dense contractions (include/ftmi.h FTMI_MMA_*): 1 = bf16x6 split
+# (fp32-accurate, 2.7x the fp32 MFMA rate), 0 = plain fp32 MFMA.  FTMI_MMA=0/1 overrides.
+MMA = int(os.environ.get('FTMI_MMA', '1'))
 
 
 def _stream() -> int:
@@ -61,7 +66,7 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, err: Optional[torch.Tensor
 
 def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, relu=False,
            bn=None, maxpool=False, residual=None, out=None, out_t=None, want_y=True,
-           T_out: int = 0):
+           T_out: int = 0, mma: Optional[int] = None):
     """Fused Conv1d (+bias, ReLU, BN, residual) on a channels-last (B, T, Cin) view.
 
     w: packed [N][k*Cin].  Returns (y, yt) where y is (B, T_out, N) (or `out`) and yt is
@@ -93,8 +98,9 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
         a.y, a.y_stride = y.data_ptr(), y.stride(1)
     a.yt = _ptr(out_t)
     a.T_out = To
+    a.mma = MMA if mma is None else mma
     M = B * To
-    label = f'conv1d[M={M},N={N},K={k * Cin}{",maxpool" if maxpool else ""}]'
+    label = f'conv1d[M={M},N={N},K={k * Cin}{",maxpool" if maxpool else ""},mma={a.mma}]'
     launch('ftmi_conv1d', label, 2.0 * M * N * k * Cin,
            4.0 * (B * T * Cin + N * k * Cin + M * N * (1 + (residual is not None))),
            ctypes.byref(a), _stream())
@@ -102,30 +108,32 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
 
 
 def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.Tensor,
-              shift: torch.Tensor) -> torch.Tensor:
+              shift: torch.Tensor, mma: Optional[int] = None) -> torch.Tensor:
     """CBHG conv bank, (B, T, Cin) -> (B, T, K*Cout)."""
     _dev(x, w, scale, shift)
     B, T, Cin, xs = _rows(x)
     y = torch.empty(B, T, K * Cout, device=x.device, dtype=_f32)
     M = B * T
     flops = 2.0 * M * Cout * Cin * K * (K + 1) / 2
-    launch('ftmi_conv_bank', f'conv_bank[M={M},K={K},Cin={Cin}]', flops,
+    mma = MMA if mma is None else mma
+    launch('ftmi_conv_bank', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}]', flops,
            4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
            x.data_ptr(), xs, B, T, Cin, w.data_ptr(), K, Cout, scale.data_ptr(),
-           shift.data_ptr(), y.data_ptr(), y.stride(1), _stream())
+           shift.data_ptr(), y.data_ptr(), y.stride(1), mma, _stream())
     return y
 
 
 def highway(x: torch.Tensor, w12: torch.Tensor, b1: torch.Tensor, b2: torch.Tensor,
-            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+            out: Optional[torch.Tensor] = None, mma: Optional[int] = None) -> torch.Tensor:
     _dev(x, w12, b1, b2, out)
     B, T, C, xs = _rows(x)
     y = out if out is not None else torch.empty(B, T, C, device=x.device, dtype=_f32)
     M = B * T
-    launch('ftmi_highway', f'highway[M={M},C={C}]', 2.0 * M * 2 * C * C,
+    mma = MMA if mma is None else mma
+    launch('ftmi_highway', f'highway[M={M},C={C},mma={mma}]', 2.0 * M * 2 * C * C,
            4.0 * (2 * M * C + 2 * C * C),
            x.data_ptr(), xs, M, C, w12.data_ptr(), b1.data_ptr(), b2.data_ptr(),
-           y.data_ptr(), y.stride(1), _stream())
+           y.data_ptr(), y.stride(1), mma, _stream())
     return y
 
 

@@ -34,6 +34,14 @@ enum {
   FTMI_E_ALIGN = 1004        /* pointer / stride not 16-byte aligned */
 };
 
+/* Matrix-core path of the dense contractions (conv1d / conv_bank / highway):
+ *   FTMI_MMA_F32     v_mfma_f32_32x32x2_f32: exact fp32 products, 157 TFLOP/s peak.
+ *   FTMI_MMA_BF16X6  each fp32 operand split into three bf16 pieces (a = a1+a2+a3, exact),
+ *                    the six cross products with i+j <= 4 on v_mfma_f32_16x16x32_bf16 with
+ *                    fp32 accumulation: fp32-accurate (dropped terms < 2^-24 relative) at
+ *                    16/6 of the fp32 MFMA rate. */
+enum { FTMI_MMA_F32 = 0, FTMI_MMA_BF16X6 = 1 };
+
 /* ABI version; bumped on any signature change. */
 int ftmi_abi_version(void);
 /* Static string for an error code (FTMI_E_* or hipError_t). */
@@ -79,6 +87,7 @@ typedef struct ftmi_conv_args {
   int64_t y_stride;
   float *yt; /* (B,N,T_out) or NULL */
   int32_t T_out; /* output frames per sequence, 0 = T (even k in PyTorch gives T+1) */
+  int32_t mma;   /* matrix path: FTMI_MMA_F32 or FTMI_MMA_BF16X6 (both fp32-accurate) */
 } ftmi_conv_args;
 
 int ftmi_conv1d(const ftmi_conv_args *args, ftmi_stream_t stream);
@@ -92,7 +101,8 @@ int ftmi_conv1d(const ftmi_conv_args *args, ftmi_stream_t stream);
  * ---------------------------------------------------------------------------------- */
 int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t Cin,
                    const float *w, int32_t K, int32_t Cout, const float *bn_scale,
-                   const float *bn_shift, float *y, int64_t y_stride, ftmi_stream_t stream);
+                   const float *bn_shift, float *y, int64_t y_stride, int32_t mma,
+                   ftmi_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * One highway layer (common_layers.py:22-35):
@@ -102,7 +112,7 @@ int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32
  * y must not alias x.
  * ---------------------------------------------------------------------------------- */
 int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t C, const float *w12,
-                 const float *b1, const float *b2, float *y, int64_t y_stride,
+                 const float *b1, const float *b2, float *y, int64_t y_stride, int32_t mma,
                  ftmi_stream_t stream);
 
 /* ------------------------------------------------------------------------------------

@@ -25,7 +25,7 @@ def test_library_exports_every_symbol():
     lib = _lib.load()
     for name in declared():
         assert hasattr(lib, name), name
-    assert lib.ftmi_abi_version() == 1
+    assert lib.ftmi_abi_version() == _lib.ABI_VERSION
 
 
 def test_exported_symbols_are_plain_c():
@@ -48,8 +48,8 @@ def test_strerror():
 @pytest.mark.parametrize('call,code', [
     (lambda L: L.ftmi_embedding(None, 4, None, 135, 256, None, None, None), 1001),
     (lambda L: L.ftmi_conv1d(None, None), 1001),
-    (lambda L: L.ftmi_conv_bank(None, 0, 1, 1, 16, None, 4, 8, None, None, None, 0, None), 1001),
-    (lambda L: L.ftmi_highway(None, 0, 1, 32, None, None, None, None, 0, None), 1001),
+    (lambda L: L.ftmi_conv_bank(None, 0, 1, 1, 16, None, 4, 8, None, None, None, 0, 1, None), 1001),
+    (lambda L: L.ftmi_highway(None, 0, 1, 32, None, None, None, None, 0, 1, None), 1001),
     (lambda L: L.ftmi_rnn_bidir(0, 1, 1, 64, None, 0, 1, None, None, None, None, None, 0.0, None, 0, None, None), 1001),
     (lambda L: L.ftmi_duration_counts(None, 1, 1, 1, 2.0, None, None, None, None), 1001),
     (lambda L: L.ftmi_lr_index(None, 1, 1, 1, None, None), 1001),
@@ -70,6 +70,8 @@ def test_conv_shape_errors():
     assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1002
     a.Cin, a.x_stride = 16, 18  # stride not a multiple of 4 floats
     assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1004
+    a.x_stride, a.mma = 16, 7  # unknown matrix path
+    assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1001
 
 
 def test_rnn_unsupported_hidden():

@@ -33,6 +33,10 @@ def rng():
 
 
 # ---------------------------------------------------------------- conv / GEMM family
+MMAS = pytest.mark.parametrize('mma', [0, 1], ids=['f32', 'bf16x6'])
+
+
+@MMAS
 @pytest.mark.parametrize('B,T,Cin,N,k,relu,bn,bias', [
     (2, 37, 64, 256, 5, True, True, False),     # SeriesPredictor conv 1
     (3, 50, 256, 256, 5, True, True, False),    # SeriesPredictor conv 2/3
@@ -40,7 +44,7 @@ def rng():
     (1, 7, 16, 40, 4, True, True, False),       # even k, tiny
     (2, 300, 80, 256, 8, True, True, False),    # postnet bank k=8
 ])
-def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng):
+def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma):
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
@@ -55,11 +59,12 @@ def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng):
         ref = ref * sc[None, :, None] + sh[None, :, None]
     y, _ = ops.conv1d(dev(x), pack_conv(torch.from_numpy(w)).cuda(), k, k // 2,
                       bias=dev(b) if bias else None, relu=relu,
-                      bn=(dev(sc), dev(sh)) if bn else None)
+                      bn=(dev(sc), dev(sh)) if bn else None, mma=mma)
     close(host(y), ref.transpose(0, 2, 1))
 
 
-def test_conv1d_maxpool_residual_transposed(rng):
+@MMAS
+def test_conv1d_maxpool_residual_transposed(rng, mma):
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     B, T, Cin, N = 2, 45, 128, 80
@@ -69,23 +74,25 @@ def test_conv1d_maxpool_residual_transposed(rng):
     ref = O.conv1d(O.maxpool_k2_s1_p1(x.transpose(0, 2, 1)), w, 1) + res.transpose(0, 2, 1)
     yt = torch.empty(B, N, T, device='cuda')
     y, _ = ops.conv1d(dev(x), pack_conv(torch.from_numpy(w)).cuda(), 3, 1, maxpool=True,
-                      residual=dev(res), out_t=yt)
+                      residual=dev(res), out_t=yt, mma=mma)
     close(host(y), ref.transpose(0, 2, 1))
     close(host(yt), ref)
 
 
-def test_conv1d_strided_input_view(rng):
+@MMAS
+def test_conv1d_strided_input_view(rng, mma):
     from forwardtacotron_amd import ops
     B, T, C = 2, 33, 64
     full = rng.normal(0, 1, (B, T, 2 * C)).astype(np.float32)
     w = rng.normal(0, 0.1, (48, C)).astype(np.float32)
     xt = dev(full)[:, :, C:]  # row stride 2C
-    y, _ = ops.conv1d(xt, dev(w), 1, 0)
+    y, _ = ops.conv1d(xt, dev(w), 1, 0, mma=mma)
     close(host(y), full[:, :, C:] @ w.T)
 
 
+@MMAS
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 2, 41), (8, 80, 2, 150)])
-def test_conv_bank(K, Cin, B, T, rng):
+def test_conv_bank(K, Cin, B, T, rng, mma):
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     C = 256
@@ -96,11 +103,12 @@ def test_conv_bank(K, Cin, B, T, rng):
     refs = [np.maximum(O.conv1d(x.transpose(0, 2, 1), w, w.shape[2] // 2)[:, :, :T], 0) for w in ws]
     ref = np.concatenate(refs, 1) * sc[None, :, None] + sh[None, :, None]
     wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
-    y = ops.conv_bank(dev(x), wp, K, C, dev(sc), dev(sh))
+    y = ops.conv_bank(dev(x), wp, K, C, dev(sc), dev(sh), mma=mma)
     close(host(y), ref.transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
 
 
-def test_highway(rng):
+@MMAS
+def test_highway(rng, mma):
     from forwardtacotron_amd.common_layers import HighwayNetwork
     C = 256
     hw = HighwayNetwork(C)
@@ -110,7 +118,9 @@ def test_highway(rng):
     hw = hw.cuda()
     x = rng.normal(0, 1, (3, 77, C)).astype(np.float32)
     ref = O.highway({'h.' + k: v.astype(np.float32) for k, v in sd.items()}, 'h', x, np.float32)
-    close(host(hw.forward_cl(dev(x))), ref)
+    w12, b1, b2 = hw.packed_weights()
+    from forwardtacotron_amd import ops
+    close(host(ops.highway(dev(x), w12, b1, b2, mma=mma)), ref)
 
 
 # ---------------------------------------------------------------- recurrences
