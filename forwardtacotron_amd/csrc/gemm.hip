@@ -243,8 +243,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const GemmParams p) {
 
 // ---------------------------------------------------------------------------------------
 // bf16x6 path.  128x128 block tile, BK = 32, 4 waves (2x2) each owning 64x64 = 4x4 tiles of
-// v_mfma_f32_16x16x32_bf16.  LDS: [buffer 2][operand 2][piece 3][row 128][48] bf16 = 144 KB
-// (one workgroup per CU); global loads for chunk k+1 are issued before the MFMAs of chunk k.
+// v_mfma_f32_16x16x32_bf16.  One LDS image [operand 2][piece 3][row 128][48] bf16 = 72 KB,
+// two workgroups per CU: while one splits / stages a chunk the other's MFMAs run.  Chunk
+// k+1's global loads are issued before chunk k's MFMAs (loads go to registers; their
+// split into pieces happens after the MFMAs, then one barrier pair per chunk).
+// Global loads are branch-free: out-of-range rows / taps / K read a clamped in-bounds
+// address and are zeroed by a select.
 __device__ __forceinline__ void split3(f32x4 v, bf16x4 &h1, bf16x4 &h2, bf16x4 &h3) {
   h1 = __builtin_convertvector(v, bf16x4);
   const f32x4 r1 = v - __builtin_convertvector(h1, f32x4);
@@ -253,9 +257,14 @@ __device__ __forceinline__ void split3(f32x4 v, bf16x4 &h1, bf16x4 &h2, bf16x4 &
   h3 = __builtin_convertvector(r2, bf16x4);
 }
 
+__device__ __forceinline__ f32x4 sel4(bool ok, f32x4 v) {
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  return ok ? v : z;
+}
+
 template <int EPI, bool MAXPOOL>
-__global__ __launch_bounds__(256, 1) void conv_gemm_x6_kernel(const GemmParams p) {
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 2 * 3 * X6_PIECE];
+__global__ __launch_bounds__(256, 2) void conv_gemm_x6_kernel(const GemmParams p) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 3 * X6_PIECE];
 
   const int tile = blockIdx.x;
   int gi = 0;
@@ -272,7 +281,8 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_x6_kernel(const GemmParams p
 
   // loader: rows lr + 32q (q = 0..3) of both operands, float4 #lc of the 32-wide chunk
   const int lr = tid >> 3, lc = tid & 7;
-  int ab[4], at[4];
+  const float *arow[4];  // sequence start of the A row (b, t = 0)
+  int at[4];
   bool aok[4], bok[4];
   const float *wrow[4];
 #pragma unroll
@@ -280,49 +290,54 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_x6_kernel(const GemmParams p
     const int m = m0 + lr + 32 * q;
     aok[q] = m < p.M;
     const int mm = aok[q] ? m : 0;
-    ab[q] = mm / p.To;
-    at[q] = mm - ab[q] * p.To;
+    const int b = mm / p.To;
+    at[q] = mm - b * p.To;
+    arow[q] = p.x + (int64_t)b * p.T * p.x_stride;
     const int n = n0 + lr + 32 * q;
     bok[q] = n < G.N;
     wrow[q] = G.w + (int64_t)(bok[q] ? n : 0) * G.Ktot;
   }
   const int nk = (G.Ktot + X6_BK - 1) / X6_BK;
   f32x4 ra[4], rb[4];
+  // this thread's K index k = kc*32 + 4*lc  ->  (tap j, channel c), advanced per chunk
+  int kk = 4 * lc, tj = kk / p.Cin, tc = kk - tj * p.Cin;
 
-  auto gload = [&](int kc) {
-    const int k = kc * X6_BK + 4 * lc;  // this thread's 4 consecutive K indices
-    const bool kok = k < G.Ktot;
-    const int j = k / p.Cin;
-    const int c = k - j * p.Cin;
+  auto gload = [&]() {
+    const bool kok = kk < G.Ktot;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int ts = at[q] + j - G.pad;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (kok && aok[q] && ts >= 0 && ts < p.T) {
-        const float *src = p.x + ((int64_t)ab[q] * p.T + ts) * p.x_stride + c;
-        v = *(const f32x4 *)src;
-        if (MAXPOOL && ts > 0) v = fmax4(v, *(const f32x4 *)(src - p.x_stride));
+      const int ts = at[q] + tj - G.pad;
+      const bool ok = kok && aok[q] && ts >= 0 && ts < p.T;
+      const float *src = arow[q] + (int64_t)(ok ? ts : 0) * p.x_stride + (ok ? tc : 0);
+      f32x4 v = *(const f32x4 *)src;
+      if (MAXPOOL) {
+        const bool okp = ok && ts > 0;
+        const f32x4 u = *(const f32x4 *)(src - (okp ? p.x_stride : 0));
+        v = fmax4(v, u);
       }
-      ra[q] = v;
-      f32x4 w = {0.f, 0.f, 0.f, 0.f};
-      if (kok && bok[q]) w = *(const f32x4 *)(wrow[q] + k);
-      rb[q] = w;
+      ra[q] = sel4(ok, v);
+      rb[q] = sel4(kok && bok[q], *(const f32x4 *)(wrow[q] + (kok ? kk : 0)));
+    }
+    kk += X6_BK;
+    tc += X6_BK;
+    while (tc >= p.Cin) {
+      tc -= p.Cin;
+      ++tj;
     }
   };
-  auto swrite = [&](int buf) {
-    __bf16 *base = lds + buf * (2 * 3 * X6_PIECE);
+  auto swrite = [&]() {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int off = (lr + 32 * q) * X6_STRIDE + 4 * lc;
       bf16x4 h1, h2, h3;
       split3(ra[q], h1, h2, h3);
-      *(bf16x4 *)(base + 0 * X6_PIECE + off) = h1;
-      *(bf16x4 *)(base + 1 * X6_PIECE + off) = h2;
-      *(bf16x4 *)(base + 2 * X6_PIECE + off) = h3;
+      *(bf16x4 *)(lds + 0 * X6_PIECE + off) = h1;
+      *(bf16x4 *)(lds + 1 * X6_PIECE + off) = h2;
+      *(bf16x4 *)(lds + 2 * X6_PIECE + off) = h3;
       split3(rb[q], h1, h2, h3);
-      *(bf16x4 *)(base + 3 * X6_PIECE + off) = h1;
-      *(bf16x4 *)(base + 4 * X6_PIECE + off) = h2;
-      *(bf16x4 *)(base + 5 * X6_PIECE + off) = h3;
+      *(bf16x4 *)(lds + 3 * X6_PIECE + off) = h1;
+      *(bf16x4 *)(lds + 4 * X6_PIECE + off) = h2;
+      *(bf16x4 *)(lds + 5 * X6_PIECE + off) = h3;
     }
   };
 
@@ -333,19 +348,18 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_x6_kernel(const GemmParams p
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fk = 8 * (lane >> 4);
-  auto compute = [&](int buf) {
-    const __bf16 *base = lds + buf * (2 * 3 * X6_PIECE);
+  auto compute = [&]() {
     bf16x8 a[4][3], b[4][3];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
       for (int pc = 0; pc < 3; ++pc)
-        a[mi][pc] = *(const bf16x8 *)(base + pc * X6_PIECE + (wm * 64 + mi * 16 + fr) * X6_STRIDE + fk);
+        a[mi][pc] = *(const bf16x8 *)(lds + pc * X6_PIECE + (wm * 64 + mi * 16 + fr) * X6_STRIDE + fk);
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
       for (int pc = 0; pc < 3; ++pc)
-        b[ni][pc] = *(const bf16x8 *)(base + (3 + pc) * X6_PIECE + (wn * 64 + ni * 16 + fr) * X6_STRIDE + fk);
+        b[ni][pc] = *(const bf16x8 *)(lds + (3 + pc) * X6_PIECE + (wn * 64 + ni * 16 + fr) * X6_STRIDE + fk);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -361,14 +375,12 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_x6_kernel(const GemmParams p
       }
   };
 
-  gload(0);
-  swrite(0);
-  __syncthreads();
+  gload();
   for (int kc = 0; kc < nk; ++kc) {
-    const int cur = kc & 1;
-    if (kc + 1 < nk) gload(kc + 1);
-    compute(cur);
-    if (kc + 1 < nk) swrite(cur ^ 1);
+    swrite();
+    __syncthreads();
+    if (kc + 1 < nk) gload();
+    compute();
     __syncthreads();
   }
 
