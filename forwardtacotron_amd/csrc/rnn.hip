@@ -1,4 +1,4 @@
-// Persistent bidirectional GRU / LSTM recurrence (gfx950, fp32 MFMA 16x16x4).
+// Persistent bidirectional GRU / LSTM recurrence (gfx950).
 //
 // Reference semantics: PyTorch nn.GRU / nn.LSTM, one layer, bidirectional, batch_first,
 // h0 = c0 = 0, both directions over the full padded length (no packing) — used by
@@ -10,32 +10,41 @@
 //
 // Decomposition.  The batch is cut into chunks of NB = 16 sequences; a GROUP is one
 // (direction, chunk) pair and owns an independent recurrence.  A group is spread over
-// BPG = H / U workgroups, each owning U hidden units (all G gates of them, R = G*U rows
-// of W_hh).  The workgroup keeps its W_hh slice in VGPRs for the whole sequence, laid out
-// as MFMA A-fragments: wave w covers k in [w*H/4, (w+1)*H/4) and lane slot s = lane>>4
-// takes k = w*KW + s*KB + kb at MFMA kb, so every lane's fragments (and its h operand) are
-// KB consecutive floats.  Per step each wave produces R x 16 partial gate sums over its
-// quarter of K, the four partials are summed through LDS, and 256 threads apply the cell
-// update to the U x 16 (unit, sequence) cells they own (c / h state lives in registers).
+// BPG = H / U workgroups, each owning U hidden units (all G gates: R = G*U rows of W_hh)
+// whose W_hh slice stays in VGPRs for the whole sequence.  The 4 waves of a workgroup are
+// WK (K-split) x WR (row-split); per step each wave computes its rows' partial gate sums over
+// its K range with MFMA, the WK partials are summed through LDS, and 256 threads apply the
+// cell update to the U x 16 (unit, sequence) cells they own (c / h state in registers).
 //
-// Hand-off between the BPG workgroups of a group (MI355X_MICROARCH.md "Valid forms",
-// row 1): new h values go to a small exchange buffer hx[t & 1][group][16*H] in the call's
-// workspace, stored in MFMA-FRAGMENT ORDER ([wave][kb/4][lane][4]) so that every consumer
-// wave-instruction reads 1 KB of consecutive bytes (sc1 loads bypass L1: a row-major image
-// made each instruction touch 64 lines and fetch every line 8 times) (parity double buffering is race-free because a workgroup can only start
-// step t+1 after every workgroup of its group finished step t) with write-through (sc1)
-// stores; every storing wave drains
-// vmcnt(0); after a workgroup barrier ONE lane adds 1 to the group's arrival counter
-// (agent-scope atomic).  Before step t, ONE lane polls that counter with relaxed sc1
-// loads until it reaches t*BPG, the workgroup barrier releases the other waves, and all
-// loads of the handed-off h are sc1 buffer loads.  The layer output y is written with
-// plain stores (nothing in the launch reads it back), so it may hold padding values.
+// Matrix path (X6 = true, default): W and h are split into three bf16 pieces each and the
+// six cross products with i + j <= 4 run on v_mfma_f32_16x16x32_bf16 with fp32
+// accumulation — fp32-accurate (see gemm.hip) at 16/6 of the fp32 MFMA rate.  X6 = false
+// keeps v_mfma_f32_16x16x4_f32.
+//
+// h hand-off between the BPG workgroups of a group.  New h values go to an exchange buffer
+// hx[t & 1][group][16*H] in MFMA-fragment order (every consumer wave-instruction reads
+// 1 KB of consecutive bytes); parity double buffering is race-free because a workgroup can
+// only start step t+1 after every workgroup of its group finished step t.  Every storing
+// wave drains vmcnt(0), a workgroup barrier, then ONE lane adds 1 to the group's arrival
+// counter (agent-scope atomic); before step t ONE lane polls that counter (relaxed sc1
+// loads) until it reaches t*BPG, a workgroup barrier releases the other waves, and every
+// load of handed-off h is an sc1 load (L1 bypassed).  Two modes, chosen per launch:
+//   XCD-local: a start-of-launch census reads each workgroup's XCC_ID (s_getreg) and, when
+//     every XCD received exactly the workgroups of whole groups, forms the groups from
+//     co-located workgroups.  h is then stored with PLAIN stores (kept in that XCD's L2)
+//     and read by sc1 loads served from the same L2, and the arrival counter is replaced by
+//     one flag word per workgroup (plain store of the step number after the drain + barrier,
+//     polled by one wave with a single sc1 load of all BPG flags) — no fabric round trip.
+//     Correct by construction because group membership comes from the measured XCD, never
+//     from an assumed dispatch order.
+//   global (fallback when the census is unbalanced, or disabled): sc1 write-through
+//     stores, groups by blockIdx (MI355X_MICROARCH.md "Valid forms", row 1).
+// BPG == 1 groups never leave the workgroup: h goes through LDS.  Every spin is bounded;
+// on timeout the call's error word is set and the workgroup leaves the time loop.
 //
 // Packed sequences (forward(), models/forward_tacotron.py:224-230): with lengths != NULL
 // frames t >= lengths[b] output pad_value, and the reverse direction keeps h = c = 0
 // until t = lengths[b]-1, exactly like pack_padded_sequence + pad_packed_sequence.
-// Every spin is bounded; on timeout the call's error word is set and the workgroup leaves
-// the time loop.
 #include "common.h"
 
 // ---- diagnostic build only (-DFTMI_RNN_STAMPS): per-phase s_memtime sums per workgroup
@@ -61,10 +70,19 @@ __device__ unsigned long long ftmi_rnn_stamps[2048 * 8];
 
 namespace {
 
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
 constexpr int NB = 16;              // sequences per group (MFMA 16x16 columns)
 constexpr int RED_STRIDE = NB + 1;  // LDS partial-sum row stride (floats)
 constexpr unsigned SPIN_LIMIT = 1u << 22;
-constexpr int CNT_PAD = 32;  // one 128-B line per group counter
+constexpr int CNT_PAD = 32;  // one 128-B line per counter
+// workspace word offsets (in 32-bit words) of the control block
+constexpr int WS_ERR = 0;
+constexpr int WS_CENSUS = 1 * CNT_PAD;   // 8 per-XCD slot counters, one line each
+constexpr int WS_ARRIVE = 9 * CNT_PAD;   // census barrier
+constexpr int WS_FLAGS = 10 * CNT_PAD;   // XCD-local mode: 64 flag words per group
+constexpr int FLAGS_PER_GROUP = 64;
+constexpr int WS_GROUPS_OF(int ngroups) { return WS_FLAGS + ngroups * FLAGS_PER_GROUP; }
 
 struct RnnParams {
   const float *xp;
@@ -78,100 +96,187 @@ struct RnnParams {
   int64_t y_stride;
   const int32_t *lengths;
   float pad_value;
-  float *hx;  // [2][nchunks*NB][2H]
+  float *hx;  // [2][ngroups_total][16*H]
   int B, T;
-  int nrows_hx;  // rows per parity half of hx (= nchunks * NB)
-  int chunk0;   // first batch chunk of this launch
-  int ngroups;  // groups in this launch
-  unsigned *cnt;
-  unsigned *err;
+  int ngroups_total;
+  int chunk0;     // first batch chunk of this launch
+  int ngroups;    // groups in this launch
+  int xcd_local;  // 1: try the census-based XCD-local mode
+  unsigned *ws;   // control words (see WS_*)
 };
 
-template <int CELL, int H, int U>
+__device__ __forceinline__ float fast_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ float fast_tanh(float x) { return 2.0f * fast_sigmoid(2.0f * x) - 1.0f; }
+
+__device__ __forceinline__ void split3x8(const float (&v)[8], bf16x8 &h1, bf16x8 &h2, bf16x8 &h3) {
+  typedef float f32x8 __attribute__((ext_vector_type(8)));
+  f32x8 x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[i] = v[i];
+  h1 = __builtin_convertvector(x, bf16x8);
+  const f32x8 r1 = x - __builtin_convertvector(h1, f32x8);
+  h2 = __builtin_convertvector(r1, bf16x8);
+  const f32x8 r2 = r1 - __builtin_convertvector(h2, f32x8);
+  h3 = __builtin_convertvector(r2, bf16x8);
+}
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 7u;
+}
+
+// bounded relaxed poll (one lane): returns false on timeout
+__device__ __forceinline__ bool poll_ge(unsigned *w, unsigned target) {
+  unsigned spins = 0;
+  while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > SPIN_LIMIT) return false;
+  }
+  return true;
+}
+
+template <int CELL, int H, int U, int WK, bool X6>
 __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
   constexpr int G = CELL ? 4 : 3;
   constexpr int R = G * U;
   constexpr int RB = R / 16;
-  constexpr int KW = H / 4;
-  constexpr int KB = KW / 4;
+  constexpr int WR = 4 / WK;
+  constexpr int RBW = RB / WR;  // row blocks per wave
+  constexpr int KW = H / WK;    // K range per wave
+  constexpr int NL = KW / 16;   // float4s of h operand per lane
+  constexpr int KS = KW / 32;   // bf16 k-steps per wave (X6)
+  constexpr int KB = KW / 4;    // f32 k-blocks per wave (!X6)
   constexpr int BPG = H / U;
+  constexpr bool LOCAL = BPG == 1;
   constexpr int CELLS = U * NB;
   constexpr int CPT = CELLS / 256;
-  static_assert(U % 16 == 0 && H % U == 0 && KB % 4 == 0 && CELLS % 256 == 0, "shape");
+  static_assert(U % 16 == 0 && H % U == 0 && RB % WR == 0 && CELLS % 256 == 0, "shape");
+  static_assert(X6 ? (KW % 32 == 0) : (KB % 4 == 0), "K split");
 
-  __shared__ __attribute__((aligned(16))) float red[4 * R * RED_STRIDE];
-  __shared__ int s_abort;
+  __shared__ __attribute__((aligned(16))) float red[WK * R * RED_STRIDE];
+  __shared__ __attribute__((aligned(16))) float hloc[LOCAL ? 2 * 16 * H : 4];
+  __shared__ int s_abort, s_group, s_bi, s_mode;
 
-  const int group = blockIdx.x % p.ngroups;
-  const int bi = blockIdx.x / p.ngroups;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wk = wave % WK, wr = wave / WK;
+  const int ls = lane >> 4, lc = lane & 15;
+
+  // ---- group assignment (census for the XCD-local mode) ----------------------------
+  if (tid == 0) {
+    int mode = 0, group = blockIdx.x % p.ngroups, bi = blockIdx.x / p.ngroups, abort = 0;
+    if (!LOCAL && p.xcd_local) {
+      const unsigned x = xcc_id();
+      const unsigned slot = __hip_atomic_fetch_add(p.ws + WS_CENSUS + x * CNT_PAD, 1u,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(p.ws + WS_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!poll_ge(p.ws + WS_ARRIVE, gridDim.x)) {
+        abort = 1;
+        __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (p.ngroups % 8 == 0) {
+        const unsigned per = (unsigned)(p.ngroups / 8) * BPG;
+        bool balanced = true;
+        for (int i = 0; i < 8; ++i)
+          balanced &= __hip_atomic_load(p.ws + WS_CENSUS + i * CNT_PAD, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT) == per;
+        if (balanced) {
+          mode = 1;
+          group = (int)(x * (p.ngroups / 8) + slot / BPG);
+          bi = (int)(slot % BPG);
+        }
+      }
+    }
+    s_mode = mode;
+    s_group = group;
+    s_bi = bi;
+    s_abort = abort;
+  }
+  __syncthreads();
+  if (s_abort) return;
+  const int group = s_group, bi = s_bi;
+  const bool xcd_mode = s_mode == 1;
   const int dir = group & 1;
   const int chunk = p.chunk0 + (group >> 1);
+  const int gglob = p.chunk0 * 2 + group;
   const int u0 = bi * U;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ls = lane >> 4, lc = lane & 15;
-  unsigned *cnt = p.cnt + (size_t)(p.chunk0 * 2 + group) * CNT_PAD;
+  unsigned *cnt = p.ws + WS_GROUPS_OF(p.ngroups_total) + gglob * CNT_PAD;
+  unsigned *flags = p.ws + WS_FLAGS + gglob * FLAGS_PER_GROUP;
+  static_assert(BPG <= FLAGS_PER_GROUP, "flags");
 
   // ---- W_hh slice -> VGPR A-fragments (loaded once) ---------------------------------
-  float wf[RB][KB];
-  {
-    const float *wdir = p.w_hh + (size_t)dir * (G * H) * H;
+  // row block rb = wr*RBW + i, lane row lc; X6: k = wk*KW + ks*32 + 8*ls + j (j < 8)
+  //                                        f32: k = wk*KW + ls*KB + kb
+  const float *wdir = p.w_hh + (size_t)dir * (G * H) * H;
+  bf16x8 wa[X6 ? RBW : 1][X6 ? KS : 1][3];
+  float wf[X6 ? 1 : RBW][X6 ? 1 : KB];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      const int lrow = rb * 16 + lc;
-      const int grow = (lrow / U) * H + u0 + (lrow % U);
-      const float *src = wdir + (size_t)grow * H + wave * KW + ls * KB;
+  for (int i = 0; i < RBW; ++i) {
+    const int lrow = (wr * RBW + i) * 16 + lc;
+    const int grow = (lrow / U) * H + u0 + (lrow % U);
+    const float *src = wdir + (size_t)grow * H + wk * KW;
+    if constexpr (X6) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        float v[8];
+        const f32x4 a = *(const f32x4 *)(src + ks * 32 + 8 * ls);
+        const f32x4 b = *(const f32x4 *)(src + ks * 32 + 8 * ls + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        split3x8(v, wa[i][ks][0], wa[i][ks][1], wa[i][ks][2]);
+      }
+    } else {
 #pragma unroll
       for (int kb = 0; kb < KB; kb += 4) {
-        const f32x4 v = *(const f32x4 *)(src + kb);
-        wf[rb][kb] = v.x;
-        wf[rb][kb + 1] = v.y;
-        wf[rb][kb + 2] = v.z;
-        wf[rb][kb + 3] = v.w;
+        const f32x4 v = *(const f32x4 *)(src + ls * KB + kb);
+        wf[i][kb] = v.x;
+        wf[i][kb + 1] = v.y;
+        wf[i][kb + 2] = v.z;
+        wf[i][kb + 3] = v.w;
       }
     }
   }
 
   // ---- per-thread cells: cell c = tid + 256*j -> (unit u = c % U, seq b = c / U) ------
-  int cu[CPT], cb[CPT];
+  int cu[CPT], cb[CPT], len[CPT], hxo[CPT];
   bool cvalid[CPT];
   float hstate[CPT], cstate[CPT], bhh[CPT][G];
 #pragma unroll
   for (int j = 0; j < CPT; ++j) {
     const int c = tid + 256 * j;
     cu[j] = c % U;
-    cb[j] = chunk * NB + c / U;
+    const int bl = c / U;
+    cb[j] = chunk * NB + bl;
     cvalid[j] = cb[j] < p.B;
     hstate[j] = 0.f;
     cstate[j] = 0.f;
+    len[j] = (p.lengths && cvalid[j]) ? p.lengths[cb[j]] : p.T;
 #pragma unroll
     for (int g = 0; g < G; ++g)
       bhh[j][g] = (CELL == 0) ? p.b_hh[dir * G * H + g * H + u0 + cu[j]] : 0.f;
+    // fragment-order position of (seq bl, unit k) in the group's 16*H slab
+    const int k = u0 + cu[j];
+    const int kwv = k / KW, r = k % KW;
+    int ln, idx4, e;
+    if constexpr (X6) {
+      const int q = r % 32;
+      ln = (q >> 3) * 16 + bl;
+      idx4 = (r / 32) * 2 + ((q & 7) >> 2);
+      e = q & 3;
+    } else {
+      ln = (r / KB) * 16 + bl;
+      idx4 = (r % KB) >> 2;
+      e = r & 3;
+    }
+    hxo[j] = ((kwv * NL + idx4) * 64 + ln) * 4 + e;
   }
 
-  // ---- h operand source: this group's fragment-ordered slab of the exchange buffer ---
-  // slab (16*H floats) = [wave 4][kbq KB/4][lane 64][4]; (seq bl, unit k) lives at
-  //   (((k / KW) * (KB/4) + (k % KB) / 4) * 64 + ((k % KW) / KB) * 16 + bl) * 4 + (k % 4)
-  const int gglob = 2 * chunk + dir;
+  // ---- h operand source ----------------------------------------------------------------
   const int slab = 16 * H;
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.hx, (short)0, 0x7FFFFFF0, 0x00020000);
-  const unsigned hoff = (unsigned)(((gglob * slab) + wave * (KB / 4) * 256 + lane * 4) * 4);
-  const int hx_par = p.nrows_hx * 2 * H * 4;  // bytes between the two parity halves
-  int hxo[CPT];  // this thread's cells in the slab
-#pragma unroll
-  for (int j = 0; j < CPT; ++j) {
-    const int k = u0 + cu[j], bl = cb[j] - chunk * NB;
-    hxo[j] = gglob * slab + (((k / KW) * (KB / 4) + (k % KB) / 4) * 64 + ((k % KW) / KB) * 16 + bl) * 4 + (k % 4);
-  }
-  int len[CPT];
-#pragma unroll
-  for (int j = 0; j < CPT; ++j) len[j] = (p.lengths && cvalid[j]) ? p.lengths[cb[j]] : p.T;
-
-  if (tid == 0) s_abort = 0;
-  __syncthreads();
-#ifdef FTMI_RNN_STAMPS
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = 0;
-  if (tid == 0) st_last = __builtin_amdgcn_s_memtime();
-#endif
+  const unsigned hoff = (unsigned)((gglob * slab + wk * NL * 256 + lane * 4) * 4);
+  const int hx_par = p.ngroups_total * slab * 4;  // bytes between the two parity halves
 
   // input projections (independent of h): step t+1's rows are fetched during step t
   auto load_gx = [&](int t, float (&g)[CPT][G]) {
@@ -186,71 +291,119 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
       for (int gi = 0; gi < G; ++gi) g[j][gi] = row[dir * G * H + gi * H + u0 + cu[j]];
     }
   };
-  float gx[CPT][G], gxn[CPT][G];
+  float gx[CPT][G], gxn[CPT][G], yo[CPT];
   load_gx(0, gx);
+  if (LOCAL)
+    for (int i = tid; i < 16 * H; i += 256) hloc[i] = 0.f;
+  __syncthreads();
+
+#ifdef FTMI_RNN_STAMPS
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = 0;
+  if (tid == 0) st_last = __builtin_amdgcn_s_memtime();
+#endif
 
   for (int t = 0; t < p.T; ++t) {
     const int tt = dir ? (p.T - 1 - t) : t;
-
-    STAMP(0);  // xp gather issued (and landed, in the stamp build)
+    STAMP(0);
     // wait until every workgroup of the group has published h_{t-1}
-    if (BPG > 1 && t > 0) {
-      if (tid == 0) {
-        const unsigned target = (unsigned)t * BPG;
-        unsigned spins = 0;
-        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > SPIN_LIMIT) {
-            s_abort = 1;
-            __hip_atomic_store(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
+    if (!LOCAL && t > 0) {
+      if (xcd_mode) {
+        if (wave == 0) {  // lane i watches workgroup i's flag (L2-served sc1 loads)
+          unsigned spins = 0;
+          for (;;) {
+            const unsigned f = lane < BPG ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT)
+                                          : (unsigned)t;
+            if (__all(f >= (unsigned)t)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > SPIN_LIMIT) {
+              if (lane == 0) {
+                s_abort = 1;
+                __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
+              break;
+            }
           }
         }
+      } else if (tid == 0 && !poll_ge(cnt, (unsigned)t * BPG)) {
+        s_abort = 1;
+        __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
       if (s_abort) break;
     }
+    STAMP(1);
 
-    STAMP(1);  // group arrival observed
-    // h_{t-1} operand (sc1 loads), zero at t = 0
-    float hf[KB];
+    // h_{t-1} operand: NL float4 per lane (fragment order), zero at t = 0
+    float hv[NL * 4];
     if (t == 0) {
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) hf[kb] = 0.f;
+      for (int i = 0; i < NL * 4; ++i) hv[i] = 0.f;
+    } else if constexpr (LOCAL) {
+      const float *hb = hloc + ((t - 1) & 1) * slab + wk * NL * 256 + lane * 4;
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const f32x4 v = *(const f32x4 *)(hb + i * 256);
+        hv[4 * i] = v.x;
+        hv[4 * i + 1] = v.y;
+        hv[4 * i + 2] = v.z;
+        hv[4 * i + 3] = v.w;
+      }
     } else {
       const int soff = ((t - 1) & 1) * hx_par;
 #pragma unroll
-      for (int kb = 0; kb < KB; kb += 4) {
+      for (int i = 0; i < NL; ++i) {
         // NB: bit_cast the whole vector; extracting u32 lanes one by one and bit-casting
         // each is miscompiled by ROCm 7.2 (every lane reads element 0).
         const f32x4 v = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + kb * 256, soff, 16));
-        hf[kb] = v.x;
-        hf[kb + 1] = v.y;
-        hf[kb + 2] = v.z;
-        hf[kb + 3] = v.w;
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + i * 1024, soff, 16));
+        hv[4 * i] = v.x;
+        hv[4 * i + 1] = v.y;
+        hv[4 * i + 2] = v.z;
+        hv[4 * i + 3] = v.w;
       }
     }
-
     if (t + 1 < p.T) load_gx(t + 1, gxn);
-    STAMP(2);  // h operand landed
-    // partial gates over this wave's quarter of K
-    f32x4 acc[RB];
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) acc[rb] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[rb][kb], hf[kb], acc[rb], 0, 0, 0);
+    STAMP(2);
 
+    // partial gates over this wave's K range
+    f32x4 acc[RBW];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
+    for (int i = 0; i < RBW; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if constexpr (X6) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        red[(wave * R + rb * 16 + ls * 4 + i) * RED_STRIDE + lc] = acc[rb][i];
+      for (int ks = 0; ks < KS; ++ks) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = hv[ks * 8 + e];
+        bf16x8 h1, h2, h3;
+        split3x8(v, h1, h2, h3);
+#pragma unroll
+        for (int i = 0; i < RBW; ++i) {
+          f32x4 c = acc[i];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][ks][2], h1, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][ks][1], h2, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][ks][0], h3, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][ks][1], h1, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][ks][0], h2, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][ks][0], h1, c, 0, 0, 0);
+          acc[i] = c;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int i = 0; i < RBW; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[i][kb], hv[kb], acc[i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RBW; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        red[(wk * R + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] = acc[i][e];
     __syncthreads();
-    STAMP(3);  // MFMAs + partial sums in LDS
+    STAMP(3);
 
     // cell update
 #pragma unroll
@@ -260,24 +413,26 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int row = g * U + cu[j];
-        gs[g] = red[(0 * R + row) * RED_STRIDE + bl] + red[(1 * R + row) * RED_STRIDE + bl] +
-                red[(2 * R + row) * RED_STRIDE + bl] + red[(3 * R + row) * RED_STRIDE + bl];
+        float sum = red[row * RED_STRIDE + bl];
+#pragma unroll
+        for (int w = 1; w < WK; ++w) sum += red[(w * R + row) * RED_STRIDE + bl];
+        gs[g] = sum;
       }
       float hn;
       if (CELL == 0) {
         // ATen GRU cell: r, z, n ; h' = n + z * (h - n)
-        const float r = ftmi_sigmoid(gx[j][0] + (gs[0] + bhh[j][0]));
-        const float z = ftmi_sigmoid(gx[j][1] + (gs[1] + bhh[j][1]));
-        const float n = tanhf(gx[j][2] + r * (gs[2] + bhh[j][2]));
+        const float r = fast_sigmoid(gx[j][0] + (gs[0] + bhh[j][0]));
+        const float z = fast_sigmoid(gx[j][1] + (gs[1] + bhh[j][1]));
+        const float n = fast_tanh(gx[j][2] + r * (gs[2] + bhh[j][2]));
         hn = n + z * (hstate[j] - n);
       } else {
         // LSTM cell: i, f, g, o
-        const float ig = ftmi_sigmoid(gx[j][0] + gs[0]);
-        const float fg = ftmi_sigmoid(gx[j][1] + gs[1]);
-        const float gg = tanhf(gx[j][2] + gs[2]);
-        const float og = ftmi_sigmoid(gx[j][3] + gs[3]);
+        const float ig = fast_sigmoid(gx[j][0] + gs[0]);
+        const float fg = fast_sigmoid(gx[j][1] + gs[1]);
+        const float gg = fast_tanh(gx[j][2] + gs[2]);
+        const float og = fast_sigmoid(gx[j][3] + gs[3]);
         cstate[j] = fg * cstate[j] + ig * gg;
-        hn = og * tanhf(cstate[j]);
+        hn = og * fast_tanh(cstate[j]);
       }
       float yout = hn;
       if (tt >= len[j]) {  // packed-sequence padding: reverse direction restarts from zero
@@ -287,23 +442,39 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
       }
       hstate[j] = hn;
       if (cvalid[j]) {
-        __hip_atomic_store(p.hx + (size_t)(t & 1) * p.nrows_hx * 2 * H + hxo[j], hn,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        p.y[((size_t)cb[j] * p.T + tt) * p.y_stride + dir * H + u0 + cu[j]] = yout;
+        if constexpr (LOCAL) {
+          hloc[(t & 1) * slab + hxo[j]] = hn;
+        } else {
+          float *dst = p.hx + (size_t)(t & 1) * p.ngroups_total * slab + gglob * slab + hxo[j];
+          if (xcd_mode)
+            *dst = hn;  // stays in this XCD's L2, read back by same-XCD sc1 loads
+          else
+            __hip_atomic_store(dst, hn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
+      yo[j] = yout;
     }
-
 #pragma unroll
     for (int j = 0; j < CPT; ++j)
 #pragma unroll
       for (int gi = 0; gi < G; ++gi) gx[j][gi] = gxn[j][gi];
-    STAMP(4);  // cell update + stores issued
+    STAMP(4);
+
     // publish: every storing wave drains, barrier, one lane arrives
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (!LOCAL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (BPG > 1 && tid == 0)
-      __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    STAMP(5);  // drained + arrived
+    if (!LOCAL && tid == 0) {
+      if (xcd_mode)
+        __hip_atomic_store(flags + bi, (unsigned)(t + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);  // plain store, stays in L2
+      else
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // layer output after the hand-off: nothing in this launch reads y
+#pragma unroll
+    for (int j = 0; j < CPT; ++j)
+      if (cvalid[j]) p.y[((size_t)cb[j] * p.T + tt) * p.y_stride + dir * H + u0 + cu[j]] = yo[j];
+    STAMP(5);
   }
 #ifdef FTMI_RNN_STAMPS
   if (tid == 0)
@@ -311,7 +482,7 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
 #endif
 }
 
-template <int CELL, int H, int U>
+template <int CELL, int H, int U, int WK, bool X6>
 int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
   constexpr int BPG = H / U;
   int max_groups = (max_blocks / BPG) & ~1;
@@ -320,7 +491,12 @@ int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
     const int nc = (nchunks - c0) < max_groups / 2 ? (nchunks - c0) : max_groups / 2;
     p.chunk0 = c0;
     p.ngroups = 2 * nc;
-    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U>), dim3(p.ngroups * BPG), dim3(256), 0, s, p);
+    if (c0 > 0) {  // the census words are per launch
+      hipError_t e = hipMemsetAsync(p.ws + WS_CENSUS, 0, (WS_FLAGS - WS_CENSUS) * 4, s);
+      if (e != hipSuccess) return (int)e;
+    }
+    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, X6>), dim3(p.ngroups * BPG), dim3(256),
+                       0, s, p);
     FTMI_CHECK_LAUNCH();
   }
   return FTMI_OK;
@@ -340,13 +516,21 @@ int device_cu_count() {
 
 }  // namespace
 
-// workspace: [counters: 2*nchunks lines][err: 1 line][hx: 2 * nchunks*NB * 2H floats]
+// workspace: [control: err, census, flags, counters][hx: 2 * 2*nchunks * 16*H floats]
+static int64_t ctl_bytes(int64_t nchunks) {
+  return (WS_GROUPS_OF((int)(2 * nchunks)) + 2 * nchunks * CNT_PAD) * (int64_t)sizeof(unsigned);
+}
+
 extern "C" int64_t ftmi_rnn_workspace_bytes(int32_t B, int32_t H, int32_t cell) {
   (void)cell;
   if (B <= 0 || H <= 0) return 0;
   const int64_t nchunks = (B + NB - 1) / NB;
-  return (2 * nchunks * CNT_PAD + CNT_PAD) * (int64_t)sizeof(unsigned) +
-         2 * nchunks * NB * 2 * (int64_t)H * (int64_t)sizeof(float);
+  return ctl_bytes(nchunks) + 2 * (2 * nchunks) * NB * (int64_t)H * (int64_t)sizeof(float);
+}
+
+extern "C" int64_t ftmi_rnn_error_offset(int32_t B) {
+  (void)B;
+  return WS_ERR * (int64_t)sizeof(unsigned);
 }
 
 extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, const float *xp,
@@ -362,9 +546,18 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   if (!ftmi_aligned16(w_hh) || !ftmi_aligned16(sync)) return FTMI_E_ALIGN;
   hipStream_t s = ftmi_hs(stream);
   const int nchunks = (B + NB - 1) / NB;
+  const int64_t ctl = ctl_bytes(nchunks);
   const int64_t wsb = ftmi_rnn_workspace_bytes(B, H, cell);
   hipError_t e = hipMemsetAsync(sync, 0, (size_t)wsb, s);
   if (e != hipSuccess) return (int)e;
+  static const int xcd_env = [] {
+    const char *v = getenv("FTMI_RNN_XCD_LOCAL");
+    return v ? atoi(v) : 1;
+  }();
+  static const int x6_env = [] {
+    const char *v = getenv("FTMI_RNN_MMA");
+    return v ? atoi(v) : 1;
+  }();
   RnnParams p = {};
   p.xp = xp;
   p.xp_stride = xp_stride;
@@ -379,21 +572,25 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   p.pad_value = pad_value;
   p.B = B;
   p.T = T;
-  p.nrows_hx = nchunks * NB;
-  p.cnt = (unsigned *)sync;
-  p.err = (unsigned *)sync + 2 * nchunks * CNT_PAD;
-  p.hx = (float *)((unsigned *)sync + (2 * nchunks + 1) * CNT_PAD);
+  p.ngroups_total = 2 * nchunks;
+  p.xcd_local = xcd_env;
+  p.ws = (unsigned *)sync;
+  p.hx = (float *)((char *)sync + ctl);
   const int maxb = device_cu_count();
-  if (cell == 0 && H == 64) return launch_rnn<0, 64, 64>(p, nchunks, maxb, s);
-  if (cell == 0 && H == 128) return launch_rnn<0, 128, 128>(p, nchunks, maxb, s);
-  if (cell == 0 && H == 256) return launch_rnn<0, 256, 16>(p, nchunks, maxb, s);
-  if (cell == 1 && H == 512) return launch_rnn<1, 512, 16>(p, nchunks, maxb, s);
+  const bool x6 = x6_env != 0;
+  if (cell == 0 && H == 64)
+    return x6 ? launch_rnn<0, 64, 64, 2, true>(p, nchunks, maxb, s)
+              : launch_rnn<0, 64, 64, 4, false>(p, nchunks, maxb, s);
+  if (cell == 0 && H == 128)
+    return x6 ? launch_rnn<0, 128, 64, 4, true>(p, nchunks, maxb, s)
+              : launch_rnn<0, 128, 64, 4, false>(p, nchunks, maxb, s);
+  if (cell == 0 && H == 256)
+    return x6 ? launch_rnn<0, 256, 16, 4, true>(p, nchunks, maxb, s)
+              : launch_rnn<0, 256, 16, 4, false>(p, nchunks, maxb, s);
+  if (cell == 1 && H == 512)
+    return x6 ? launch_rnn<1, 512, 16, 4, true>(p, nchunks, maxb, s)
+              : launch_rnn<1, 512, 16, 4, false>(p, nchunks, maxb, s);
   return FTMI_E_UNSUPPORTED;
-}
-
-extern "C" int64_t ftmi_rnn_error_offset(int32_t B) {
-  const int64_t nchunks = (B + NB - 1) / NB;
-  return 2 * nchunks * CNT_PAD * (int64_t)sizeof(unsigned);
 }
 
 #ifdef FTMI_RNN_STAMPS

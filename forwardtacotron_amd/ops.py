@@ -144,7 +144,8 @@ class RnnTimeout(RuntimeError):
 def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Optional[torch.Tensor],
               T: Optional[int] = None, index: Optional[torch.Tensor] = None,
               xp_zero: Optional[torch.Tensor] = None, lengths: Optional[torch.Tensor] = None,
-              pad_value: float = 0.0, check: bool = False) -> torch.Tensor:
+              pad_value: float = 0.0, check: bool = False,
+              ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Bidirectional GRU (cell=0) / LSTM (cell=1) recurrence -> (B, T, 2H).
 
     xp: (B, T_src, 2*G*H) input projections; index: (B, T) int32 frame -> row map.
@@ -157,8 +158,9 @@ def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Opt
     T = T if T is not None else T_src
     y = torch.empty(B, T, 2 * H, device=xp.device, dtype=_f32)
     lib = _lib.load()
-    ws = torch.empty(int(lib.ftmi_rnn_workspace_bytes(B, H, cell)) // 4 + 4, device=xp.device,
-                     dtype=torch.int32)
+    need = int(lib.ftmi_rnn_workspace_bytes(B, H, cell)) // 4 + 4
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, device=xp.device, dtype=torch.int32)
     if index is not None:
         assert index.dtype == torch.int32 and index.is_contiguous() and index.shape == (B, T)
     G = 4 if cell else 3

@@ -19,7 +19,7 @@ for cell, H, B, T in [(1, 512, 64, 1368), (0, 256, 64, 1368), (0, 128, 64, 200),
     torch.cuda.synchronize()
     t0 = time.perf_counter(); ops.rnn_bidir(cell, xp, H, w, bh if cell == 0 else None, check=True)
     dt = time.perf_counter() - t0
-    U = {512: 16, 256: 16, 128: 128, 64: 64}[H]
+    U = {512: 16, 256: 16, 128: 64, 64: 64}[H]
     nb = 2 * ((B + 15) // 16) * (H // U)
     buf = (ctypes.c_ulonglong * (nb * 8))()
     assert fn(buf, nb * 8) == 0
