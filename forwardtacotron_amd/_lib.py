@@ -31,6 +31,7 @@ class ConvArgs(ctypes.Structure):
         ('bias', P), ('relu', c_int), ('bn_scale', P), ('bn_shift', P), ('maxpool', c_int),
         ('residual', P), ('res_stride', c_int64),
         ('y', P), ('y_stride', c_int64), ('yt', P), ('T_out', c_int), ('mma', c_int),
+        ('split_k', c_int), ('split_ws', P),
     ]
 
 

@@ -62,6 +62,11 @@ struct GemmParams {
   // highway epilogue
   const float *b1;
   const float *b2;
+  // split-K: blocks with blockIdx.y = s accumulate K chunks [s*kc_per, (s+1)*kc_per) and
+  // store raw partial sums to part[s][M][N]; splitk_epilogue_kernel finishes the tile
+  int split;
+  int kc_per;
+  float *part;
   GemmGroup g[MAX_GROUPS];
 };
 
@@ -297,10 +302,15 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6_kernel(const GemmParams p
     bok[q] = n < G.N;
     wrow[q] = G.w + (int64_t)(bok[q] ? n : 0) * G.Ktot;
   }
-  const int nk = (G.Ktot + X6_BK - 1) / X6_BK;
+  int nk = (G.Ktot + X6_BK - 1) / X6_BK;
+  int kc0 = 0;
+  if (p.split > 1) {
+    kc0 = blockIdx.y * p.kc_per;
+    nk = min(nk - kc0, p.kc_per);
+  }
   f32x4 ra[4], rb[4];
   // this thread's K index k = kc*32 + 4*lc  ->  (tap j, channel c), advanced per chunk
-  int kk = 4 * lc, tj = kk / p.Cin, tc = kk - tj * p.Cin;
+  int kk = kc0 * X6_BK + 4 * lc, tj = kk / p.Cin, tc = kk - tj * p.Cin;
 
   auto gload = [&]() {
     const bool kok = kk < G.Ktot;
@@ -384,6 +394,23 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6_kernel(const GemmParams p
     __syncthreads();
   }
 
+  if (p.split > 1) {  // raw partial sums; the epilogue runs in splitk_epilogue_kernel
+    float *part = p.part + (size_t)blockIdx.y * p.M * G.N;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int col = n0 + wn * 64 + ni * 16 + (lane & 15);
+      if (col >= G.N) continue;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + i;
+          if (row < p.M) part[(size_t)row * G.N + col] = acc[mi][ni][i];
+        }
+    }
+    return;
+  }
+
   // epilogue: tile (mi, ni) element (row 4*(lane>>4) + i, col lane & 15)
   const int er = 4 * (lane >> 4);
   if constexpr (EPI == EPI_CONV) {
@@ -435,9 +462,44 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6_kernel(const GemmParams p
   }
 }
 
+// Split-K finish: v = sum_s part[s][m][n] (fixed order: deterministic), then the
+// EPI_CONV epilogue (bias, ReLU, BN, residual, plain and transposed stores).
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const GemmParams p) {
+  const GemmGroup &G = p.g[0];
+  const int64_t total = (int64_t)p.M * G.N;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * 256) {
+    const int row = (int)(idx / G.N), col = (int)(idx - (int64_t)row * G.N);
+    float v = p.part[idx];
+    for (int s = 1; s < p.split; ++s) v += p.part[(size_t)s * total + idx];
+    if (G.bias) v += G.bias[col];
+    if (p.relu) v = fmaxf(v, 0.f);
+    if (G.scale) v = v * G.scale[col] + G.shift[col];
+    if (p.residual) v += p.residual[(int64_t)row * p.res_stride + col];
+    if (p.y) p.y[(int64_t)row * p.y_stride + G.ycol0 + col] = v;
+    if (p.yt) {
+      const int b = row / p.To, t = row - b * p.To;
+      p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = v;
+    }
+  }
+}
+
 int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hipStream_t s) {
   if (nblocks <= 0) return FTMI_OK;
   dim3 grid(nblocks), block(256);
+  if (mma == 1 && p.split > 1) {
+    dim3 g2(nblocks, p.split);
+    if (maxpool)
+      hipLaunchKernelGGL((conv_gemm_x6_kernel<EPI_CONV, true>), g2, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_gemm_x6_kernel<EPI_CONV, false>), g2, block, 0, s, p);
+    FTMI_CHECK_LAUNCH();
+    const int64_t total = (int64_t)p.M * p.g[0].N;
+    const int eb = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(eb), block, 0, s, p);
+    FTMI_CHECK_LAUNCH();
+    return FTMI_OK;
+  }
   if (mma == 1) {
     if (epi == EPI_HIGHWAY)
       hipLaunchKernelGGL((conv_gemm_x6_kernel<EPI_HIGHWAY, false>), grid, block, 0, s, p);
@@ -499,6 +561,15 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   g.ntiles = (a->N + BN - 1) / BN;
   g.tile0 = 0;
   const int mtiles = (p.M + BM - 1) / BM;
+  p.split = 1;
+  if (a->split_k > 1) {
+    if (a->mma != 1 || !a->split_ws) return FTMI_E_ARG;
+    const int nkc = (g.Ktot + X6_BK - 1) / X6_BK;
+    const int kc_per = (nkc + a->split_k - 1) / a->split_k;
+    p.split = (nkc + kc_per - 1) / kc_per;  // no empty splits
+    p.kc_per = kc_per;
+    p.part = a->split_ws;
+  }
   return launch(p, EPI_CONV, a->maxpool != 0, mtiles * g.ntiles, a->mma, ftmi_hs(stream));
 }
 

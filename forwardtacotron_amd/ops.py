@@ -24,6 +24,25 @@ _f32 = torch.float32
 MMA = int(os.environ.get('FTMI_MMA', '1'))
 
 
+def _num_cus() -> int:
+    n = getattr(_num_cus, 'v', None)
+    if n is None:
+        n = _num_cus.v = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    return n
+
+
+def _split_k(M: int, N: int, K: int, mma: int) -> int:
+    """Split K when the tile grid cannot fill the chip (x6 kernel: 2 workgroups per CU)
+    and K is long enough for the partial-sum round trip to pay."""
+    if mma != 1 or K < 2048:
+        return 1
+    tiles = -(-M // 128) * -(-N // 128)
+    slots = 2 * _num_cus()
+    if tiles >= slots:
+        return 1
+    return int(min(8, -(-slots // tiles), K // 1024))
+
+
 def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
@@ -100,6 +119,10 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
     a.T_out = To
     a.mma = MMA if mma is None else mma
     M = B * To
+    sk = _split_k(M, N, k * Cin, a.mma)
+    if sk > 1:
+        part = torch.empty(sk * M * N, device=x.device, dtype=_f32)
+        a.split_k, a.split_ws = sk, part.data_ptr()
     label = f'conv1d[M={M},N={N},K={k * Cin}{",maxpool" if maxpool else ""},mma={a.mma}]'
     launch('ftmi_conv1d', label, 2.0 * M * N * k * Cin,
            4.0 * (B * T * Cin + N * k * Cin + M * N * (1 + (residual is not None))),

@@ -88,6 +88,10 @@ typedef struct ftmi_conv_args {
   float *yt; /* (B,N,T_out) or NULL */
   int32_t T_out; /* output frames per sequence, 0 = T (even k in PyTorch gives T+1) */
   int32_t mma;   /* matrix path: FTMI_MMA_F32 or FTMI_MMA_BF16X6 (both fp32-accurate) */
+  int32_t split_k;  /* > 1: split K over that many workgroups (FTMI_MMA_BF16X6 only); partial
+                       sums go to split_ws and a second launch sums them in fixed order
+                       (deterministic) and applies the epilogue */
+  float *split_ws;  /* split_k * B*T_out * N floats of caller-owned workspace, or NULL */
 } ftmi_conv_args;
 
 int ftmi_conv1d(const ftmi_conv_args *args, ftmi_stream_t stream);

@@ -43,6 +43,7 @@ MMAS = pytest.mark.parametrize('mma', [0, 1], ids=['f32', 'bf16x6'])
     (2, 129, 512, 80, 1, False, False, True),   # lin-like (N tail)
     (1, 7, 16, 40, 4, True, True, False),       # even k, tiny
     (2, 300, 80, 256, 8, True, True, False),    # postnet bank k=8
+    (2, 60, 1024, 256, 3, True, True, True),    # long K, few tiles: split-K on the x6 path
 ])
 def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma):
     from forwardtacotron_amd import ops
@@ -64,10 +65,11 @@ def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma):
 
 
 @MMAS
-def test_conv1d_maxpool_residual_transposed(rng, mma):
+@pytest.mark.parametrize('Cin', [128, 1024])
+def test_conv1d_maxpool_residual_transposed(rng, mma, Cin):
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
-    B, T, Cin, N = 2, 45, 128, 80
+    B, T, N = 2, 45, 80
     x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
     res = rng.normal(0, 1, (B, T, N)).astype(np.float32)
     w = rng.normal(0, 0.1, (N, Cin, 3)).astype(np.float32)
