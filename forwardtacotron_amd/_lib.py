@@ -19,7 +19,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 2
+ABI_VERSION = 3
 MMA_F32, MMA_BF16X6 = 0, 1
 
 
@@ -31,7 +31,7 @@ class ConvArgs(ctypes.Structure):
         ('bias', P), ('relu', c_int), ('bn_scale', P), ('bn_shift', P), ('maxpool', c_int),
         ('residual', P), ('res_stride', c_int64),
         ('y', P), ('y_stride', c_int64), ('yt', P), ('T_out', c_int), ('mma', c_int),
-        ('split_k', c_int), ('split_ws', P),
+        ('split_k', c_int), ('split_ws', P), ('w_split', P),
     ]
 
 
@@ -41,9 +41,11 @@ SIGNATURES = {
     'ftmi_strerror': (ctypes.c_char_p, [c_int]),
     'ftmi_embedding': (c_int, [P, c_int64, P, c_int64, c_int64, P, P, P]),
     'ftmi_conv1d': (c_int, [ctypes.POINTER(ConvArgs), P]),
-    'ftmi_conv_bank': (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, c_int, P, P, P, c_int64,
+    'ftmi_conv_bank': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P, c_int64,
                                c_int, P]),
-    'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, c_int64, c_int, P]),
+    'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P]),
+    'ftmi_split_weights_bytes': (c_int64, [c_int64, c_int64]),
+    'ftmi_split_weights': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_rnn_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
     'ftmi_rnn_error_offset': (c_int64, [c_int]),
     'ftmi_rnn_bidir': (c_int, [c_int, c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,

@@ -82,6 +82,11 @@ def pack_conv(w: torch.Tensor) -> torch.Tensor:
     return w.detach().permute(0, 2, 1).contiguous().reshape(w.size(0), -1)
 
 
+def presplit(w: torch.Tensor):
+    """bf16 pieces of a packed weight for the bf16x6 GEMM path (None on the fp32 path)."""
+    return ops.split_weights(w) if ops.MMA == 1 else None
+
+
 # --------------------------------------------------------------------------------------
 # packed-weight cache: rebuilt whenever a parameter / buffer changes (load_state_dict, .to)
 
@@ -134,12 +139,15 @@ class BatchNormConv(Packed):
         self.kernel = kernel
 
     def _pack(self):
-        return pack_conv(self.conv.weight), self.bnorm.folded()
+        w = pack_conv(self.conv.weight)
+        return w, self.bnorm.folded(), presplit(w)
 
     def forward_cl(self, x: torch.Tensor, T_out: int = 0, residual=None, maxpool=False) -> torch.Tensor:
-        w, bn = self.packed_weights()
+        w, bn, w3 = self.packed_weights()
+        # the pre-split path measured slower on the maxpool (CBHG proj1) shapes
         y, _ = ops.conv1d(x, w, self.kernel, self.kernel // 2, relu=self.relu, bn=bn,
-                          residual=residual, maxpool=maxpool, T_out=T_out)
+                          residual=residual, maxpool=maxpool, T_out=T_out,
+                          w_split=None if maxpool else w3)
         return y
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -165,11 +173,12 @@ class HighwayNetwork(Packed):
         w1 = self.W1.weight.detach().reshape(C // 32, 32, C)
         w2 = self.W2.weight.detach().reshape(C // 32, 32, C)
         w12 = torch.stack([w1, w2], 1).reshape(2 * C, C).contiguous()
-        return w12, self.W1.bias.detach().contiguous(), self.W2.bias.detach().contiguous()
+        return (w12, self.W1.bias.detach().contiguous(), self.W2.bias.detach().contiguous(),
+                presplit(w12))
 
     def forward_cl(self, x: torch.Tensor, out=None) -> torch.Tensor:
-        w12, b1, b2 = self.packed_weights()
-        return ops.highway(x, w12, b1, b2, out=out)
+        w12, b1, b2, w3 = self.packed_weights()
+        return ops.highway(x, w12, b1, b2, out=out, w_split=w3)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         shp = x.shape
@@ -202,14 +211,14 @@ class BiRNN(Packed):
         b_hh = torch.cat([self.bias_hh_l0, self.bias_hh_l0_reverse], 0).detach().contiguous()
         w_hh = torch.stack([self.weight_hh_l0, self.weight_hh_l0_reverse], 0).detach().contiguous()
         if self.cell == 1:  # LSTM: both biases folded into the input projection
-            return w_ih, (b_ih + b_hh).contiguous(), None, w_hh
-        return w_ih, b_ih, b_hh, w_hh
+            return w_ih, (b_ih + b_hh).contiguous(), None, w_hh, presplit(w_ih)
+        return w_ih, b_ih, b_hh, w_hh, presplit(w_ih)
 
     def forward_cl(self, x: torch.Tensor, T: Optional[int] = None, index=None, lengths=None,
                    pad_value: float = 0.0) -> torch.Tensor:
         """x: (B, T_src, In) channels-last; with index, frame t reads row index[b, t]."""
-        w_ih, b_in, b_hh, w_hh = self.packed_weights()
-        xp, _ = ops.conv1d(x, w_ih, 1, 0, bias=b_in)
+        w_ih, b_in, b_hh, w_hh, w3 = self.packed_weights()
+        xp, _ = ops.conv1d(x, w_ih, 1, 0, bias=b_in, w_split=w3)
         return ops.rnn_bidir(self.cell, xp, self.hidden, w_hh, b_hh, T=T, index=index,
                              xp_zero=b_in if index is not None else None, lengths=lengths,
                              pad_value=pad_value)
@@ -244,16 +253,19 @@ class CBHG(Packed):
         folds = [c.bnorm.folded() for c in self.conv1d_bank]
         scale = torch.cat([f[0] for f in folds]).contiguous()
         shift = torch.cat([f[1] for f in folds]).contiguous()
-        return bank_w, scale, shift, self.pre_highway.weight.detach().contiguous()
+        w_pre = self.pre_highway.weight.detach().contiguous()
+        bank3 = (ops.split_bank_weights(bank_w, self.K, ws[0].size(1), self.channels)
+                 if ops.MMA == 1 else None)
+        return bank_w, scale, shift, w_pre, bank3, presplit(w_pre)
 
     def forward_cl(self, x: torch.Tensor) -> torch.Tensor:
         """(B, T, Cin) channels-last -> (B, T, 2*channels)."""
-        bank_w, scale, shift, w_pre = self.packed_weights()
-        bank = ops.conv_bank(x, bank_w, self.K, self.channels, scale, shift)
+        bank_w, scale, shift, w_pre, bank3, pre3 = self.packed_weights()
+        bank = ops.conv_bank(x, bank_w, self.K, self.channels, scale, shift, w_split=bank3)
         y = self.conv_project1.forward_cl(bank, maxpool=True)
         del bank
         y = self.conv_project2.forward_cl(y, residual=x)
-        h, _ = ops.conv1d(y, w_pre, 1, 0)
+        h, _ = ops.conv1d(y, w_pre, 1, 0, w_split=pre3)
         h2 = torch.empty_like(h)
         for hw in self.highways:
             hw.forward_cl(h, out=h2)

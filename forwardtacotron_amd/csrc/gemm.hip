@@ -38,6 +38,8 @@ enum { EPI_CONV = 0, EPI_HIGHWAY = 1 };
 
 struct GemmGroup {
   const float *w;  // [N][Ktot]
+  const __bf16 *w3;  // optional pre-split weights [3][N][Kpad], Kpad = roundup(Ktot, 32)
+  int Kpad;
   const float *bias;
   const float *scale;
   const float *shift;
@@ -308,11 +310,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6_kernel(const GemmParams p
     kc0 = blockIdx.y * p.kc_per;
     nk = min(nk - kc0, p.kc_per);
   }
-  f32x4 ra[4], rb[4];
   // this thread's K index k = kc*32 + 4*lc  ->  (tap j, channel c), advanced per chunk
   int kk = kc0 * X6_BK + 4 * lc, tj = kk / p.Cin, tc = kk - tj * p.Cin;
 
-  auto gload = [&]() {
+  auto gload = [&](f32x4 (&ra)[4], f32x4 (&rb)[4]) {
     const bool kok = kk < G.Ktot;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6_kernel(const GemmParams p
       ++tj;
     }
   };
-  auto swrite = [&]() {
+  auto swrite = [&](const f32x4 (&ra)[4], const f32x4 (&rb)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int off = (lr + 32 * q) * X6_STRIDE + 4 * lc;
@@ -385,11 +386,20 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6_kernel(const GemmParams p
       }
   };
 
-  gload();
-  for (int kc = 0; kc < nk; ++kc) {
-    swrite();
+  // two register sets: chunk k+2's loads are in flight while chunk k is computed
+  f32x4 ra0[4], rb0[4], ra1[4], rb1[4];
+  gload(ra0, rb0);
+  if (nk > 1) gload(ra1, rb1);
+  for (int kc = 0; kc < nk; kc += 2) {
+    swrite(ra0, rb0);
     __syncthreads();
-    if (kc + 1 < nk) gload();
+    if (kc + 2 < nk) gload(ra0, rb0);
+    compute();
+    __syncthreads();
+    if (kc + 1 >= nk) break;
+    swrite(ra1, rb1);
+    __syncthreads();
+    if (kc + 3 < nk) gload(ra1, rb1);
     compute();
     __syncthreads();
   }
@@ -462,6 +472,455 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6_kernel(const GemmParams p
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// bf16x6, software-pipelined variant ("x6p"): ONE workgroup per CU (4 waves, one per SIMD),
+// LDS double-buffered (2 x 72 KB).  In iteration k each wave reads chunk k's fragments from
+// buffer k&1, and between its MFMAs splits chunk k+1 (already in registers) into buffer
+// (k+1)&1; chunk k+2's global loads are issued at the top of the iteration into the register
+// set chunk k+1 just vacated (two register sets, loop unrolled by two so every index is
+// static).  One barrier per chunk.
+template <int EPI, bool MAXPOOL>
+__global__ __launch_bounds__(256, 1) void conv_gemm_x6p_kernel(const GemmParams p) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 2 * 3 * X6_PIECE];
+
+  const int tile = blockIdx.x;
+  int gi = 0;
+  while (gi + 1 < p.ngroups && tile >= p.g[gi + 1].tile0) ++gi;
+  const GemmGroup &G = p.g[gi];
+  const int lt = tile - G.tile0;
+  const int mt = lt / G.ntiles;
+  const int nt = lt - mt * G.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int lr = tid >> 3, lc = tid & 7;
+  const float *arow[4];
+  int at[4];
+  bool aok[4], bok[4];
+  const float *wrow[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = m0 + lr + 32 * q;
+    aok[q] = m < p.M;
+    const int mm = aok[q] ? m : 0;
+    const int b = mm / p.To;
+    at[q] = mm - b * p.To;
+    arow[q] = p.x + (int64_t)b * p.T * p.x_stride;
+    const int n = n0 + lr + 32 * q;
+    bok[q] = n < G.N;
+    wrow[q] = G.w + (int64_t)(bok[q] ? n : 0) * G.Ktot;
+  }
+  int nk = (G.Ktot + X6_BK - 1) / X6_BK;
+  int kc0 = 0;
+  if (p.split > 1) {
+    kc0 = blockIdx.y * p.kc_per;
+    nk = min(nk - kc0, p.kc_per);
+  }
+  int kk = kc0 * X6_BK + 4 * lc, tj = kk / p.Cin, tc = kk - tj * p.Cin;
+
+  auto gload = [&](f32x4 (&ra)[4], f32x4 (&rb)[4]) {
+    const bool kok = kk < G.Ktot;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ts = at[q] + tj - G.pad;
+      const bool ok = kok && aok[q] && ts >= 0 && ts < p.T;
+      const float *src = arow[q] + (int64_t)(ok ? ts : 0) * p.x_stride + (ok ? tc : 0);
+      f32x4 v = *(const f32x4 *)src;
+      if (MAXPOOL) {
+        const bool okp = ok && ts > 0;
+        v = fmax4(v, *(const f32x4 *)(src - (okp ? p.x_stride : 0)));
+      }
+      ra[q] = sel4(ok, v);
+      rb[q] = sel4(kok && bok[q], *(const f32x4 *)(wrow[q] + (kok ? kk : 0)));
+    }
+    kk += X6_BK;
+    tc += X6_BK;
+    while (tc >= p.Cin) {
+      tc -= p.Cin;
+      ++tj;
+    }
+  };
+  auto split_store = [&](__bf16 *base, int q, f32x4 va, f32x4 vb) {
+    const int off = (lr + 32 * q) * X6_STRIDE + 4 * lc;
+    bf16x4 h1, h2, h3;
+    split3(va, h1, h2, h3);
+    *(bf16x4 *)(base + 0 * X6_PIECE + off) = h1;
+    *(bf16x4 *)(base + 1 * X6_PIECE + off) = h2;
+    *(bf16x4 *)(base + 2 * X6_PIECE + off) = h3;
+    split3(vb, h1, h2, h3);
+    *(bf16x4 *)(base + 3 * X6_PIECE + off) = h1;
+    *(bf16x4 *)(base + 4 * X6_PIECE + off) = h2;
+    *(bf16x4 *)(base + 5 * X6_PIECE + off) = h3;
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  // MFMAs on buffer `cur`, interleaved with staging the next chunk into `nxt`
+  auto step = [&](const __bf16 *cur, __bf16 *nxt, bool stage, const f32x4 (&ra)[4],
+                  const f32x4 (&rb)[4]) {
+    bf16x8 b[4][3];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+        b[ni][pc] = *(const bf16x8 *)(cur + (3 + pc) * X6_PIECE + (wn * 64 + ni * 16 + fr) * X6_STRIDE + fk);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      bf16x8 a[3];
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+        a[pc] = *(const bf16x8 *)(cur + pc * X6_PIECE + (wm * 64 + mi * 16 + fr) * X6_STRIDE + fk);
+      if (stage) split_store(nxt, mi, ra[mi], rb[mi]);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        f32x4 c = acc[mi][ni];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[ni][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[ni][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[ni][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[ni][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[ni][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[ni][0], c, 0, 0, 0);
+        acc[mi][ni] = c;
+      }
+    }
+  };
+
+  __bf16 *buf0 = lds, *buf1 = lds + 2 * 3 * X6_PIECE;
+  f32x4 ra0[4], rb0[4], ra1[4], rb1[4];
+  // prologue: chunk 0 -> buf0, chunk 1 -> registers set 1
+  gload(ra0, rb0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) split_store(buf0, q, ra0[q], rb0[q]);
+  if (nk > 1) gload(ra1, rb1);
+  __syncthreads();
+  int kc = 0;
+  for (; kc + 1 < nk; kc += 2) {
+    // even iteration: compute buf0 (chunk kc), stage chunk kc+1 (set 1) into buf1
+    if (kc + 2 < nk) gload(ra0, rb0);
+    step(buf0, buf1, true, ra1, rb1);
+    __syncthreads();
+    // odd iteration: compute buf1 (chunk kc+1), stage chunk kc+2 (set 0) into buf0
+    if (kc + 3 < nk) gload(ra1, rb1);
+    step(buf1, buf0, kc + 2 < nk, ra0, rb0);
+    __syncthreads();
+  }
+  if (kc < nk) step(buf0, buf1, false, ra1, rb1);  // odd chunk count: last chunk in buf0
+
+  if (p.split > 1) {  // raw partial sums; the epilogue runs in splitk_epilogue_kernel
+    float *part = p.part + (size_t)blockIdx.y * p.M * G.N;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int col = n0 + wn * 64 + ni * 16 + (lane & 15);
+      if (col >= G.N) continue;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + i;
+          if (row < p.M) part[(size_t)row * G.N + col] = acc[mi][ni][i];
+        }
+    }
+    return;
+  }
+
+  // epilogue: tile (mi, ni) element (row 4*(lane>>4) + i, col lane & 15)
+  const int er = 4 * (lane >> 4);
+  if constexpr (EPI == EPI_CONV) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int col = n0 + wn * 64 + ni * 16 + fr;
+      if (col >= G.N) continue;
+      const float bias = G.bias ? G.bias[col] : 0.f;
+      const float sc = G.scale ? G.scale[col] : 1.f;
+      const float sh = G.scale ? G.shift[col] : 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wm * 64 + mi * 16 + er + i;
+          if (row >= p.M) continue;
+          float v = acc[mi][ni][i];
+          if (G.bias) v += bias;
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (G.scale) v = v * sc + sh;
+          if (p.residual) v += p.residual[(int64_t)row * p.res_stride + col];
+          if (p.y) p.y[(int64_t)row * p.y_stride + G.ycol0 + col] = v;
+          if (p.yt) {
+            const int b = row / p.To, t = row - b * p.To;
+            p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = v;
+          }
+        }
+    }
+  } else {
+    // packed column blocks of 32: tiles ni = 0,1 are W1 columns, ni = 2,3 the matching W2
+    if (n0 + wn * 64 >= G.N) return;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int col = (n0 + wn * 64) / 2 + ni * 16 + fr;
+      const float b1 = p.b1[col], b2 = p.b2[col];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wm * 64 + mi * 16 + er + i;
+          if (row >= p.M) continue;
+          const float x1 = acc[mi][ni][i] + b1;
+          const float x2 = acc[mi][ni + 2][i] + b2;
+          const float g = ftmi_sigmoid(x2);
+          const float xin = p.x[(int64_t)row * p.x_stride + col];
+          p.y[(int64_t)row * p.y_stride + col] = g * fmaxf(x1, 0.f) + (1.f - g) * xin;
+        }
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------
+// bf16x6 with PRE-SPLIT weights ("x6b", used when the caller passes w_split).  The 4 waves
+// tile the 128x128 block along M (each 32 rows x 128 cols = 2 x 8 tiles of 16x16), so each
+// wave loads and splits only ITS OWN activation rows, straight into MFMA A-fragments in
+// registers — the activations never go through LDS.  The weights were split into bf16
+// pieces once (ftmi_split_weights); each 32-deep chunk of them is staged with 16-B loads
+// and ds_write_b128 into a double-buffered LDS image shared by the 4 waves.  Compared with
+// the x6 kernel this halves the split VALU work and the LDS write traffic (the binding
+// resource there) and needs one barrier per chunk.
+template <int EPI, bool MAXPOOL>
+__global__ __launch_bounds__(256, 2) void conv_gemm_x6b_kernel(const GemmParams p) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 3 * X6_PIECE];  // [buf][piece][n][48]
+
+  const int tile = blockIdx.x;
+  int gi = 0;
+  while (gi + 1 < p.ngroups && tile >= p.g[gi + 1].tile0) ++gi;
+  const GemmGroup &G = p.g[gi];
+  const int lt = tile - G.tile0;
+  const int mt = lt / G.ntiles;
+  const int nt = lt - mt * G.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fs = lane >> 4;  // fragment row / k-segment (8 k each)
+
+  // ---- A: this lane's rows (per mi) and K position --------------------------------
+  const float *arow[2];
+  int at[2];
+  bool aok[2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    const int m = m0 + wave * 32 + mi * 16 + fr;
+    aok[mi] = m < p.M;
+    const int mm = aok[mi] ? m : 0;
+    const int b = mm / p.To;
+    at[mi] = mm - b * p.To;
+    arow[mi] = p.x + (int64_t)b * p.T * p.x_stride;
+  }
+  int nk = (G.Ktot + X6_BK - 1) / X6_BK;
+  int kc0 = 0;
+  if (p.split > 1) {
+    kc0 = blockIdx.y * p.kc_per;
+    nk = min(nk - kc0, p.kc_per);
+  }
+  int kk = kc0 * X6_BK + 8 * fs, tj = kk / p.Cin, tc = kk - tj * p.Cin;
+  f32x4 ra[2][2];
+  auto loadA = [&]() {
+    const bool kok = kk < G.Ktot;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int ts = at[mi] + tj - G.pad;
+      const bool ok = kok && aok[mi] && ts >= 0 && ts < p.T;
+      const float *src = arow[mi] + (int64_t)(ok ? ts : 0) * p.x_stride + (ok ? tc : 0);
+      f32x4 v0 = *(const f32x4 *)src, v1 = *(const f32x4 *)(src + 4);
+      if (MAXPOOL) {
+        const float *sp = src - ((ok && ts > 0) ? p.x_stride : 0);
+        v0 = fmax4(v0, *(const f32x4 *)sp);
+        v1 = fmax4(v1, *(const f32x4 *)(sp + 4));
+      }
+      ra[mi][0] = sel4(ok, v0);
+      ra[mi][1] = sel4(ok, v1);
+    }
+    kk += X6_BK;
+    tc += X6_BK;
+    while (tc >= p.Cin) {
+      tc -= p.Cin;
+      ++tj;
+    }
+  };
+
+  // ---- B: 6 x 16 B of pre-split pieces per thread per chunk ------------------------
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 rb[6];
+  const __bf16 *bsrc[6];
+  int boff[6];
+  bool bok[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int idx = tid + 256 * i;
+    const int pc = idx >> 9, rem = idx & 511, nl = rem >> 2, seg = rem & 3;
+    const int n = n0 + nl;
+    bok[i] = n < G.N;
+    bsrc[i] = G.w3 + ((int64_t)pc * G.N + (bok[i] ? n : 0)) * G.Kpad + kc0 * X6_BK + seg * 8;
+    boff[i] = pc * X6_PIECE + nl * X6_STRIDE + seg * 8;
+  }
+  int kb = 0;  // chunk offset (elements) of the next B load
+  auto loadB = [&]() {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      const u32x4 v = *(const u32x4 *)(bsrc[i] + kb);
+      rb[i] = bok[i] ? v : z;
+    }
+    kb += X6_BK;
+  };
+  auto storeB = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) *(u32x4 *)(lds + buf * 3 * X6_PIECE + boff[i]) = rb[i];
+  };
+
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  loadA();
+  loadB();
+  storeB(0);
+  if (nk > 1) loadB();
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    // split this chunk's activations (registers) into bf16 A-fragments
+    bf16x8 a[2][3];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      bf16x4 l1, l2, l3, h1, h2, h3;
+      split3(ra[mi][0], l1, l2, l3);
+      split3(ra[mi][1], h1, h2, h3);
+      a[mi][0] = __builtin_shufflevector(l1, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+      a[mi][1] = __builtin_shufflevector(l2, h2, 0, 1, 2, 3, 4, 5, 6, 7);
+      a[mi][2] = __builtin_shufflevector(l3, h3, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    if (kc + 1 < nk) {
+      loadA();
+      storeB((kc + 1) & 1);
+      if (kc + 2 < nk) loadB();
+    }
+    const __bf16 *cur = lds + (kc & 1) * 3 * X6_PIECE;
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+      bf16x8 b[3];
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+        b[pc] = *(const bf16x8 *)(cur + pc * X6_PIECE + (ni * 16 + fr) * X6_STRIDE + 8 * fs);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        f32x4 c = acc[mi][ni];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][2], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][1], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][0], b[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][1], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][0], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][0], b[0], c, 0, 0, 0);
+        acc[mi][ni] = c;
+      }
+    }
+    __syncthreads();
+  }
+
+  const int er = 4 * fs;
+  if (p.split > 1) {  // raw partial sums; the epilogue runs in splitk_epilogue_kernel
+    float *part = p.part + (size_t)blockIdx.y * p.M * G.N;
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+      const int col = n0 + ni * 16 + fr;
+      if (col >= G.N) continue;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wave * 32 + mi * 16 + er + i;
+          if (row < p.M) part[(size_t)row * G.N + col] = acc[mi][ni][i];
+        }
+    }
+    return;
+  }
+  if constexpr (EPI == EPI_CONV) {
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+      const int col = n0 + ni * 16 + fr;
+      if (col >= G.N) continue;
+      const float bias = G.bias ? G.bias[col] : 0.f;
+      const float sc = G.scale ? G.scale[col] : 1.f;
+      const float sh = G.scale ? G.shift[col] : 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wave * 32 + mi * 16 + er + i;
+          if (row >= p.M) continue;
+          float v = acc[mi][ni][i];
+          if (G.bias) v += bias;
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (G.scale) v = v * sc + sh;
+          if (p.residual) v += p.residual[(int64_t)row * p.res_stride + col];
+          if (p.y) p.y[(int64_t)row * p.y_stride + G.ycol0 + col] = v;
+          if (p.yt) {
+            const int b = row / p.To, t = row - b * p.To;
+            p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = v;
+          }
+        }
+    }
+  } else {
+    // packed 32-row blocks [W1 | W2] per 64 columns: tiles ni = 4q + {0,1} are W1,
+    // ni = 4q + {2,3} the matching W2 columns (q = 0, 1)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (n0 + q * 64 >= G.N) continue;
+        const int ni = 4 * q + h;
+        const int col = n0 / 2 + q * 32 + h * 16 + fr;
+        const float b1 = p.b1[col], b2 = p.b2[col];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = m0 + wave * 32 + mi * 16 + er + i;
+            if (row >= p.M) continue;
+            const float x1 = acc[mi][ni][i] + b1;
+            const float x2 = acc[mi][ni + 2][i] + b2;
+            const float g = ftmi_sigmoid(x2);
+            const float xin = p.x[(int64_t)row * p.x_stride + col];
+            p.y[(int64_t)row * p.y_stride + col] = g * fmaxf(x1, 0.f) + (1.f - g) * xin;
+          }
+      }
+  }
+}
+
+// w [N][K] fp32 -> [3][N][Kpad] bf16 pieces (w = p0 + p1 + p2 exactly), zero K padding
+__global__ void split_weights_kernel(const float *__restrict__ w, int64_t N, int64_t K,
+                                     int64_t Kpad, __bf16 *__restrict__ out) {
+  const int64_t total = N * Kpad;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t n = i / Kpad, k = i - n * Kpad;
+    const float v = k < K ? w[n * K + k] : 0.f;
+    const __bf16 h1 = (__bf16)v;
+    const float r1 = v - (float)h1;
+    const __bf16 h2 = (__bf16)r1;
+    const __bf16 h3 = (__bf16)(r1 - (float)h2);
+    out[i] = h1;
+    out[total + i] = h2;
+    out[2 * total + i] = h3;
+  }
+}
+
 // Split-K finish: v = sum_s part[s][m][n] (fixed order: deterministic), then the
 // EPI_CONV epilogue (bias, ReLU, BN, residual, plain and transposed stores).
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const GemmParams p) {
@@ -484,9 +943,53 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const GemmParams p
   }
 }
 
+static int x6_variant() {
+  static const int v = [] {
+    const char *e = getenv("FTMI_GEMM_X6");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hipStream_t s) {
   if (nblocks <= 0) return FTMI_OK;
   dim3 grid(nblocks), block(256);
+  bool presplit = mma == 1 && x6_variant() != 3;
+  for (int i = 0; i < p.ngroups; ++i) presplit &= p.g[i].w3 != nullptr;
+  if (presplit) {
+    dim3 g2(nblocks, p.split > 1 ? p.split : 1);
+    if (epi == EPI_HIGHWAY)
+      hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_HIGHWAY, false>), g2, block, 0, s, p);
+    else if (maxpool)
+      hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_CONV, true>), g2, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_CONV, false>), g2, block, 0, s, p);
+    FTMI_CHECK_LAUNCH();
+    if (p.split > 1) {
+      const int64_t total = (int64_t)p.M * p.g[0].N;
+      const int eb = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+      hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(eb), block, 0, s, p);
+      FTMI_CHECK_LAUNCH();
+    }
+    return FTMI_OK;
+  }
+  if (mma == 1 && x6_variant() == 2) {  // software-pipelined variant
+    dim3 g2(nblocks, p.split > 1 ? p.split : 1);
+    if (epi == EPI_HIGHWAY)
+      hipLaunchKernelGGL((conv_gemm_x6p_kernel<EPI_HIGHWAY, false>), g2, block, 0, s, p);
+    else if (maxpool)
+      hipLaunchKernelGGL((conv_gemm_x6p_kernel<EPI_CONV, true>), g2, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_gemm_x6p_kernel<EPI_CONV, false>), g2, block, 0, s, p);
+    FTMI_CHECK_LAUNCH();
+    if (p.split > 1) {
+      const int64_t total = (int64_t)p.M * p.g[0].N;
+      const int eb = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+      hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(eb), block, 0, s, p);
+      FTMI_CHECK_LAUNCH();
+    }
+    return FTMI_OK;
+  }
   if (mma == 1 && p.split > 1) {
     dim3 g2(nblocks, p.split);
     if (maxpool)
@@ -530,6 +1033,7 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   if (a->pad < 0 || a->pad >= a->k + a->T) return FTMI_E_SHAPE;
   if ((a->bn_scale == nullptr) != (a->bn_shift == nullptr)) return FTMI_E_ARG;
   if (!ftmi_aligned16(a->x) || !ftmi_aligned16(a->w) || (a->x_stride & 3)) return FTMI_E_ALIGN;
+  if (a->w_split && !ftmi_aligned16(a->w_split)) return FTMI_E_ALIGN;
   const int To = a->T_out > 0 ? a->T_out : a->T;
   if ((int64_t)a->B * To > INT32_MAX) return FTMI_E_SHAPE;
   GemmParams p = {};
@@ -550,6 +1054,8 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   p.yt_channels = a->N;
   GemmGroup &g = p.g[0];
   g.w = a->w;
+  g.w3 = (const __bf16 *)a->w_split;
+  g.Kpad = (a->k * a->Cin + X6_BK - 1) / X6_BK * X6_BK;
   g.bias = a->bias;
   g.scale = a->bn_scale;
   g.shift = a->bn_shift;
@@ -574,14 +1080,15 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
 }
 
 extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T,
-                              int32_t Cin, const float *w, int32_t K, int32_t Cout,
-                              const float *bn_scale, const float *bn_shift, float *y,
-                              int64_t y_stride, int32_t mma, ftmi_stream_t stream) {
+                              int32_t Cin, const float *w, const void *w_split, int32_t K,
+                              int32_t Cout, const float *bn_scale, const float *bn_shift,
+                              float *y, int64_t y_stride, int32_t mma, ftmi_stream_t stream) {
   if (!x || !w || !bn_scale || !bn_shift || !y) return FTMI_E_ARG;
   if (B <= 0 || T <= 0 || Cin <= 0 || Cout <= 0 || K <= 0) return FTMI_E_ARG;
   if (K > MAX_GROUPS) return FTMI_E_UNSUPPORTED;
   if (Cin % 16 != 0) return FTMI_E_SHAPE;
   if (!ftmi_aligned16(x) || !ftmi_aligned16(w) || (x_stride & 3)) return FTMI_E_ALIGN;
+  if (w_split && !ftmi_aligned16(w_split)) return FTMI_E_ALIGN;
   if ((int64_t)B * T > INT32_MAX) return FTMI_E_SHAPE;
   GemmParams p = {};
   p.x = x;
@@ -603,6 +1110,13 @@ extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32
     const int gidx = ks - 1;
     GemmGroup &g = p.g[gi];
     g.w = w + (int64_t)Cout * Cin * gidx * (gidx + 1) / 2;
+    g.w3 = nullptr;
+    g.Kpad = (ks * Cin + X6_BK - 1) / X6_BK * X6_BK;
+    if (w_split) {  // groups back to back, each [3][Cout][Kpad_g]
+      int64_t off = 0;
+      for (int j = 0; j < gidx; ++j) off += 3LL * Cout * (((j + 1) * Cin + X6_BK - 1) / X6_BK * X6_BK);
+      g.w3 = (const __bf16 *)w_split + off;
+    }
     g.bias = nullptr;
     g.scale = bn_scale + (int64_t)gidx * Cout;
     g.shift = bn_shift + (int64_t)gidx * Cout;
@@ -619,13 +1133,15 @@ extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32
 }
 
 extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t C,
-                            const float *w12, const float *b1, const float *b2, float *y,
-                            int64_t y_stride, int32_t mma, ftmi_stream_t stream) {
+                            const float *w12, const void *w12_split, const float *b1,
+                            const float *b2, float *y, int64_t y_stride, int32_t mma,
+                            ftmi_stream_t stream) {
   if (!x || !w12 || !b1 || !b2 || !y) return FTMI_E_ARG;
   if (M <= 0 || C <= 0) return FTMI_E_ARG;
   if (C % 32 != 0 || C % 16 != 0) return FTMI_E_SHAPE;
   if (M > INT32_MAX) return FTMI_E_SHAPE;
   if (!ftmi_aligned16(x) || !ftmi_aligned16(w12) || (x_stride & 3)) return FTMI_E_ALIGN;
+  if (w12_split && !ftmi_aligned16(w12_split)) return FTMI_E_ALIGN;
   if (x == y) return FTMI_E_ARG;
   GemmParams p = {};
   p.x = x;
@@ -642,6 +1158,8 @@ extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t
   p.b2 = b2;
   GemmGroup &g = p.g[0];
   g.w = w12;
+  g.w3 = (const __bf16 *)w12_split;
+  g.Kpad = (C + X6_BK - 1) / X6_BK * X6_BK;
   g.N = 2 * C;
   g.k = 1;
   g.pad = 0;
@@ -650,4 +1168,21 @@ extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t
   g.tile0 = 0;
   const int mtiles = (p.M + BM - 1) / BM;
   return launch(p, EPI_HIGHWAY, false, mtiles * g.ntiles, mma, ftmi_hs(stream));
+}
+
+extern "C" int ftmi_split_weights(const float *w, int64_t N, int64_t K, void *out,
+                                  ftmi_stream_t stream) {
+  if (!w || !out || N <= 0 || K <= 0) return FTMI_E_ARG;
+  if (!ftmi_aligned16(out)) return FTMI_E_ALIGN;
+  const int64_t Kpad = (K + X6_BK - 1) / X6_BK * X6_BK;
+  const int64_t total = N * Kpad;
+  const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(split_weights_kernel, dim3(blocks), dim3(256), 0, ftmi_hs(stream), w, N, K,
+                     Kpad, (__bf16 *)out);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int64_t ftmi_split_weights_bytes(int64_t N, int64_t K) {
+  return 3 * N * ((K + X6_BK - 1) / X6_BK * X6_BK) * 2;
 }

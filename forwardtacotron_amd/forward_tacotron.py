@@ -216,25 +216,29 @@ class ForwardTacotron(nn.Module):
         return cache[device]
 
     def _phoneme_phase(self, x, alpha, pitch_fn, energy_fn):
-        """Duration / pitch / energy predictors and the prenet CBHG are independent: they
-        run concurrently on three side streams next to the caller's stream (the predictor
-        recurrences occupy only 2*ceil(B/16) workgroups each).  Returns
-        (dur_hat, pitch_hat, energy_hat, prenet_out) ready on the caller's stream."""
+        """Duration / pitch / energy predictors and the prenet CBHG are independent: pitch,
+        energy and the prenet run on three side streams while the caller's stream runs the
+        duration predictor and the LengthRegulator bookkeeping (fill-2 rule, counts, T_mel).
+        The one host sync (T_mel) therefore waits only for the duration path and overlaps
+        the prenet.  Returns (dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel) with
+        every tensor ready on the caller's stream."""
         main = torch.cuda.current_stream(x.device)
         s_pitch, s_energy, s_prenet = self._side_streams(x.device)
         for s in (s_pitch, s_energy, s_prenet):
             s.wait_stream(main)
+        with torch.cuda.stream(s_prenet):
+            enc = self.prenet.forward_cl(ops.embedding(x, self.embedding.weight.detach()))
         with torch.cuda.stream(s_pitch):
             pitch_hat = pitch_fn(self.pitch_pred.forward_bt(x).unsqueeze(1))
         with torch.cuda.stream(s_energy):
             energy_hat = energy_fn(self.energy_pred.forward_bt(x).unsqueeze(1))
-        with torch.cuda.stream(s_prenet):
-            enc = self.prenet.forward_cl(ops.embedding(x, self.embedding.weight.detach()))
         dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
+        offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=True)
+        T_mel = int(totals.max().item())  # the one host sync (output size is data dependent)
         for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat), (s_prenet, enc)):
             main.wait_stream(s)
             t.record_stream(main)
-        return dur_hat, pitch_hat, energy_hat, enc
+        return dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel
 
     def generate(self,
                  x: torch.Tensor,
@@ -246,31 +250,37 @@ class ForwardTacotron(nn.Module):
         self.eval()
         self._check_device(x)
         with torch.no_grad():
-            dur_hat, pitch_hat, energy_hat, enc = self._phoneme_phase(
+            dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel = self._phoneme_phase(
                 x, alpha, pitch_function, energy_function)
-            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, apply_fill=True, enc=enc)
+            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
+                                      lr=(offsets, T_mel))
 
     def generate_jit(self, x: torch.Tensor, alpha: float = 1.0, beta: float = 1.0) -> Dict[str, torch.Tensor]:
         """`models/forward_tacotron.py:270-284` (pitch scaled by beta, no callbacks)."""
         self._check_device(x)
         with torch.no_grad():
-            dur_hat, pitch_hat, energy_hat, enc = self._phoneme_phase(
+            dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel = self._phoneme_phase(
                 x, alpha, lambda p: p * beta, lambda e: e)
-            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, apply_fill=True, enc=enc)
+            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
+                                      lr=(offsets, T_mel))
 
     def get_step(self) -> int:
         return self.step.data.item()
 
-    def _generate_mel(self, x, dur_hat, pitch_hat, energy_hat, apply_fill=False, enc=None):
-        """`models/forward_tacotron.py:289-330` (+ the fill-2 rule of :254-255 when apply_fill).
-        enc: the prenet output if already computed (by _phoneme_phase)."""
+    def _generate_mel(self, x, dur_hat, pitch_hat, energy_hat, enc=None, lr=None):
+        """`models/forward_tacotron.py:289-330`.  enc: the prenet output if already computed;
+        lr: (offsets, T_mel) if the LengthRegulator counts were already computed (then
+        dur_hat has already been clipped / filled in place)."""
         if enc is None:
             enc = self.prenet.forward_cl(ops.embedding(x, self.embedding.weight.detach()))
         wp, bp, we, be = self._series_proj_weights()
         ops.series_proj_add(enc, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
                             self.energy_strength)
-        offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=apply_fill)
-        T_mel = int(totals.max().item())  # the one host sync: output size is data dependent
+        if lr is None:
+            offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=False)
+            T_mel = int(totals.max().item())  # the one host sync: output size is data dependent
+        else:
+            offsets, T_mel = lr
         index = ops.lr_index(offsets, T_mel)
         mel, mel_post = self._decode(enc, index)
         return {'mel': mel, 'mel_post': mel_post, 'dur': dur_hat,

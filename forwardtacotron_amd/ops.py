@@ -83,15 +83,41 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, err: Optional[torch.Tensor
     return out
 
 
+def split_weights(w: torch.Tensor) -> torch.Tensor:
+    """fp32 [N][K] -> bf16 [3][N][roundup(K, 32)] pieces (w = p0 + p1 + p2 exactly), the
+    pre-split operand of the bf16x6 GEMM path (`ftmi_split_weights`)."""
+    _dev(w)
+    if w.dim() != 2 or w.dtype != _f32 or not w.is_contiguous():
+        raise ValueError('split_weights: contiguous fp32 [N][K] expected')
+    N, K = w.shape
+    Kp = (K + 31) // 32 * 32
+    out = torch.empty(3, N, Kp, device=w.device, dtype=torch.bfloat16)
+    launch('ftmi_split_weights', f'split_weights[N={N},K={K}]', 0, 4.0 * N * K + 6.0 * N * Kp,
+           w.data_ptr(), N, K, out.data_ptr(), _stream())
+    return out
+
+
+def split_bank_weights(w: torch.Tensor, K: int, Cin: int, Cout: int) -> torch.Tensor:
+    """Pre-split pieces of a packed conv bank: group g's [3][Cout][roundup((g+1)Cin, 32)]
+    back to back (the `w_split` layout of `ftmi_conv_bank`)."""
+    parts, off = [], 0
+    for g in range(K):
+        n = Cout * Cin * (g + 1)
+        parts.append(split_weights(w[off:off + n].view(Cout, (g + 1) * Cin)).reshape(-1))
+        off += n
+    return torch.cat(parts)
+
+
 def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, relu=False,
            bn=None, maxpool=False, residual=None, out=None, out_t=None, want_y=True,
-           T_out: int = 0, mma: Optional[int] = None):
+           T_out: int = 0, mma: Optional[int] = None, w_split: Optional[torch.Tensor] = None):
     """Fused Conv1d (+bias, ReLU, BN, residual) on a channels-last (B, T, Cin) view.
 
     w: packed [N][k*Cin].  Returns (y, yt) where y is (B, T_out, N) (or `out`) and yt is
-    the optional (B, N, T_out) transposed copy (`out_t`).
+    the optional (B, N, T_out) transposed copy (`out_t`).  w_split: optional
+    `split_weights(w)` (bf16x6 path without the per-call weight split).
     """
-    _dev(x, w, bias, residual, out, out_t)
+    _dev(x, w, bias, residual, out, out_t, w_split)
     B, T, Cin, xs = _rows(x)
     N = w.size(0)
     To = T_out or T
@@ -118,6 +144,7 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
     a.yt = _ptr(out_t)
     a.T_out = To
     a.mma = MMA if mma is None else mma
+    a.w_split = _ptr(w_split)
     M = B * To
     sk = _split_k(M, N, k * Cin, a.mma)
     if sk > 1:
@@ -131,9 +158,10 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
 
 
 def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.Tensor,
-              shift: torch.Tensor, mma: Optional[int] = None) -> torch.Tensor:
+              shift: torch.Tensor, mma: Optional[int] = None,
+              w_split: Optional[torch.Tensor] = None) -> torch.Tensor:
     """CBHG conv bank, (B, T, Cin) -> (B, T, K*Cout)."""
-    _dev(x, w, scale, shift)
+    _dev(x, w, scale, shift, w_split)
     B, T, Cin, xs = _rows(x)
     y = torch.empty(B, T, K * Cout, device=x.device, dtype=_f32)
     M = B * T
@@ -141,21 +169,22 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
     mma = MMA if mma is None else mma
     launch('ftmi_conv_bank', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}]', flops,
            4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
-           x.data_ptr(), xs, B, T, Cin, w.data_ptr(), K, Cout, scale.data_ptr(),
+           x.data_ptr(), xs, B, T, Cin, w.data_ptr(), _ptr(w_split), K, Cout, scale.data_ptr(),
            shift.data_ptr(), y.data_ptr(), y.stride(1), mma, _stream())
     return y
 
 
 def highway(x: torch.Tensor, w12: torch.Tensor, b1: torch.Tensor, b2: torch.Tensor,
-            out: Optional[torch.Tensor] = None, mma: Optional[int] = None) -> torch.Tensor:
-    _dev(x, w12, b1, b2, out)
+            out: Optional[torch.Tensor] = None, mma: Optional[int] = None,
+            w_split: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(x, w12, b1, b2, out, w_split)
     B, T, C, xs = _rows(x)
     y = out if out is not None else torch.empty(B, T, C, device=x.device, dtype=_f32)
     M = B * T
     mma = MMA if mma is None else mma
     launch('ftmi_highway', f'highway[M={M},C={C},mma={mma}]', 2.0 * M * 2 * C * C,
            4.0 * (2 * M * C + 2 * C * C),
-           x.data_ptr(), xs, M, C, w12.data_ptr(), b1.data_ptr(), b2.data_ptr(),
+           x.data_ptr(), xs, M, C, w12.data_ptr(), _ptr(w_split), b1.data_ptr(), b2.data_ptr(),
            y.data_ptr(), y.stride(1), mma, _stream())
     return y
 

@@ -92,7 +92,16 @@ typedef struct ftmi_conv_args {
                        sums go to split_ws and a second launch sums them in fixed order
                        (deterministic) and applies the epilogue */
   float *split_ws;  /* split_k * B*T_out * N floats of caller-owned workspace, or NULL */
+  const void *w_split; /* optional bf16 [3][N][roundup(k*Cin, 32)] pieces of w made by
+                          ftmi_split_weights: FTMI_MMA_BF16X6 then skips the per-call
+                          weight split (fastest path) */
 } ftmi_conv_args;
+
+/* Split fp32 weights [N][K] once into three bf16 pieces (w = p0 + p1 + p2 exactly), laid
+ * out [3][N][Kpad], Kpad = roundup(K, 32), zero padded; out must hold
+ * ftmi_split_weights_bytes(N, K) bytes (16-byte aligned). */
+int64_t ftmi_split_weights_bytes(int64_t N, int64_t K);
+int ftmi_split_weights(const float *w, int64_t N, int64_t K, void *out, ftmi_stream_t stream);
 
 int ftmi_conv1d(const ftmi_conv_args *args, ftmi_stream_t stream);
 
@@ -102,9 +111,11 @@ int ftmi_conv1d(const ftmi_conv_args *args, ftmi_stream_t stream);
  *   y[b,t, g*Cout + n] = BN_g(relu(sum_{j<=g} sum_c w_g[n, j*Cin+c] * x[b, t+j-(g+1)/2, c]))
  * w: the K packed weights back to back, group g is [Cout][(g+1)*Cin] starting at float
  * offset Cout*Cin*g*(g+1)/2.  bn_scale / bn_shift: [K*Cout].  y: (B,T,K*Cout) rows.
+ * w_split (optional): each group's ftmi_split_weights pieces back to back.
  * ---------------------------------------------------------------------------------- */
 int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t Cin,
-                   const float *w, int32_t K, int32_t Cout, const float *bn_scale,
+                   const float *w, const void *w_split, int32_t K, int32_t Cout,
+                   const float *bn_scale,
                    const float *bn_shift, float *y, int64_t y_stride, int32_t mma,
                    ftmi_stream_t stream);
 
@@ -113,11 +124,12 @@ int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32
  *   g = sigmoid(x W2^T + b2);  y = g * relu(x W1^T + b1) + (1 - g) * x
  * w12: [2C][C] with rows interleaved in blocks of 32: rows 64q..64q+31 = W1 rows
  * 32q..32q+31, rows 64q+32..64q+63 = W2 rows 32q..32q+31.  Requires C % 32 == 0.
+ * w12_split (optional): ftmi_split_weights pieces of w12.
  * y must not alias x.
  * ---------------------------------------------------------------------------------- */
 int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t C, const float *w12,
-                 const float *b1, const float *b2, float *y, int64_t y_stride, int32_t mma,
-                 ftmi_stream_t stream);
+                 const void *w12_split, const float *b1, const float *b2, float *y,
+                 int64_t y_stride, int32_t mma, ftmi_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Bidirectional single-layer GRU / LSTM recurrence, PyTorch semantics, h0 = c0 = 0,

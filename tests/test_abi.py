@@ -48,8 +48,9 @@ def test_strerror():
 @pytest.mark.parametrize('call,code', [
     (lambda L: L.ftmi_embedding(None, 4, None, 135, 256, None, None, None), 1001),
     (lambda L: L.ftmi_conv1d(None, None), 1001),
-    (lambda L: L.ftmi_conv_bank(None, 0, 1, 1, 16, None, 4, 8, None, None, None, 0, 1, None), 1001),
-    (lambda L: L.ftmi_highway(None, 0, 1, 32, None, None, None, None, 0, 1, None), 1001),
+    (lambda L: L.ftmi_conv_bank(None, 0, 1, 1, 16, None, None, 4, 8, None, None, None, 0, 1, None), 1001),
+    (lambda L: L.ftmi_highway(None, 0, 1, 32, None, None, None, None, None, 0, 1, None), 1001),
+    (lambda L: L.ftmi_split_weights(None, 4, 4, None, None), 1001),
     (lambda L: L.ftmi_rnn_bidir(0, 1, 1, 64, None, 0, 1, None, None, None, None, None, 0.0, None, 0, None, None), 1001),
     (lambda L: L.ftmi_duration_counts(None, 1, 1, 1, 2.0, None, None, None, None), 1001),
     (lambda L: L.ftmi_lr_index(None, 1, 1, 1, None, None), 1001),

@@ -36,7 +36,15 @@ def rng():
 
 
 # ---------------------------------------------------------------- conv / GEMM family
-MMAS = pytest.mark.parametrize('mma', [0, 1], ids=['f32', 'bf16x6'])
+# (mma, pre-split weights): fp32 MFMA, bf16x6 splitting both operands per call, bf16x6
+# with the weights split once by ftmi_split_weights (the model's default path)
+MMAS = pytest.mark.parametrize('mma,pre', [(0, False), (1, False), (1, True)],
+                               ids=['f32', 'bf16x6', 'bf16x6-presplit'])
+
+
+def wsplit(w, pre):
+    from forwardtacotron_amd import ops
+    return ops.split_weights(w) if pre else None
 
 
 @MMAS
@@ -48,7 +56,7 @@ MMAS = pytest.mark.parametrize('mma', [0, 1], ids=['f32', 'bf16x6'])
     (2, 300, 80, 256, 8, True, True, False),    # postnet bank k=8
     (2, 60, 1024, 256, 3, True, True, True),    # long K, few tiles: split-K on the x6 path
 ])
-def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma):
+def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre):
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
@@ -61,15 +69,15 @@ def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma):
         ref = np.maximum(ref, 0)
     if bn:
         ref = ref * sc[None, :, None] + sh[None, :, None]
-    y, _ = ops.conv1d(dev(x), pack_conv(torch.from_numpy(w)).cuda(), k, k // 2,
-                      bias=dev(b) if bias else None, relu=relu,
-                      bn=(dev(sc), dev(sh)) if bn else None, mma=mma)
+    wp = pack_conv(torch.from_numpy(w)).cuda()
+    y, _ = ops.conv1d(dev(x), wp, k, k // 2, bias=dev(b) if bias else None, relu=relu,
+                      bn=(dev(sc), dev(sh)) if bn else None, mma=mma, w_split=wsplit(wp, pre))
     close(host(y), ref.transpose(0, 2, 1))
 
 
 @MMAS
 @pytest.mark.parametrize('Cin', [128, 1024])
-def test_conv1d_maxpool_residual_transposed(rng, mma, Cin):
+def test_conv1d_maxpool_residual_transposed(rng, mma, pre, Cin):
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     B, T, N = 2, 45, 80
@@ -78,26 +86,27 @@ def test_conv1d_maxpool_residual_transposed(rng, mma, Cin):
     w = rng.normal(0, 0.1, (N, Cin, 3)).astype(np.float32)
     ref = O.conv1d(O.maxpool_k2_s1_p1(x.transpose(0, 2, 1)), w, 1) + res.transpose(0, 2, 1)
     yt = torch.empty(B, N, T, device='cuda')
-    y, _ = ops.conv1d(dev(x), pack_conv(torch.from_numpy(w)).cuda(), 3, 1, maxpool=True,
-                      residual=dev(res), out_t=yt, mma=mma)
+    wp = pack_conv(torch.from_numpy(w)).cuda()
+    y, _ = ops.conv1d(dev(x), wp, 3, 1, maxpool=True, residual=dev(res), out_t=yt, mma=mma,
+                      w_split=wsplit(wp, pre))
     close(host(y), ref.transpose(0, 2, 1))
     close(host(yt), ref)
 
 
 @MMAS
-def test_conv1d_strided_input_view(rng, mma):
+def test_conv1d_strided_input_view(rng, mma, pre):
     from forwardtacotron_amd import ops
     B, T, C = 2, 33, 64
     full = rng.normal(0, 1, (B, T, 2 * C)).astype(np.float32)
     w = rng.normal(0, 0.1, (48, C)).astype(np.float32)
     xt = dev(full)[:, :, C:]  # row stride 2C
-    y, _ = ops.conv1d(xt, dev(w), 1, 0, mma=mma)
+    y, _ = ops.conv1d(xt, dev(w), 1, 0, mma=mma, w_split=wsplit(dev(w), pre))
     close(host(y), full[:, :, C:] @ w.T)
 
 
 @MMAS
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 2, 41), (8, 80, 2, 150)])
-def test_conv_bank(K, Cin, B, T, rng, mma):
+def test_conv_bank(K, Cin, B, T, rng, mma, pre):
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     C = 256
@@ -108,12 +117,13 @@ def test_conv_bank(K, Cin, B, T, rng, mma):
     refs = [np.maximum(O.conv1d(x.transpose(0, 2, 1), w, w.shape[2] // 2)[:, :, :T], 0) for w in ws]
     ref = np.concatenate(refs, 1) * sc[None, :, None] + sh[None, :, None]
     wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
-    y = ops.conv_bank(dev(x), wp, K, C, dev(sc), dev(sh), mma=mma)
+    w3 = ops.split_bank_weights(wp, K, Cin, C) if pre else None
+    y = ops.conv_bank(dev(x), wp, K, C, dev(sc), dev(sh), mma=mma, w_split=w3)
     close(host(y), ref.transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
 
 
 @MMAS
-def test_highway(rng, mma):
+def test_highway(rng, mma, pre):
     from forwardtacotron_amd.common_layers import HighwayNetwork
     C = 256
     hw = HighwayNetwork(C)
@@ -123,9 +133,20 @@ def test_highway(rng, mma):
     hw = hw.cuda()
     x = rng.normal(0, 1, (3, 77, C)).astype(np.float32)
     ref = O.highway({'h.' + k: v.astype(np.float32) for k, v in sd.items()}, 'h', x, np.float32)
-    w12, b1, b2 = hw.packed_weights()
+    w12, b1, b2, _ = hw.packed_weights()
     from forwardtacotron_amd import ops
-    close(host(ops.highway(dev(x), w12, b1, b2, mma=mma)), ref)
+    close(host(ops.highway(dev(x), w12, b1, b2, mma=mma, w_split=wsplit(w12, pre))), ref)
+
+
+def test_split_weights_exact(rng):
+    """The three bf16 pieces sum back to the fp32 weights exactly; K padding is zero."""
+    from forwardtacotron_amd import ops
+    w = (rng.normal(0, 1, (70, 1000)) * np.exp(rng.normal(0, 3, (70, 1000)))).astype(np.float32)
+    p = ops.split_weights(dev(w)).double()
+    assert p.shape == (3, 70, 1024)
+    back = host(p[0] + p[1] + p[2])  # exact in float64
+    np.testing.assert_array_equal(back[:, :1000], w.astype(np.float64))
+    assert not back[:, 1000:].any()
 
 
 # ---------------------------------------------------------------- recurrences

@@ -1,0 +1,30 @@
+"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel totals and the timeline of the last
+generate() step (start offset, duration, overlap).  usage: python tools/timeline.py <dir>"""
+import csv, glob, sys
+from collections import defaultdict
+
+path = sorted(glob.glob(f'{sys.argv[1]}/**/*kernel_trace.csv', recursive=True))[-1]
+rows = list(csv.DictReader(open(path)))
+for r in rows:
+    r['s'] = int(r['Start_Timestamp']); r['e'] = int(r['End_Timestamp'])
+rows.sort(key=lambda r: r['s'])
+name = lambda r: r['Kernel_Name'].split('(')[0].replace('(anonymous namespace)::', '')[:60]
+# steps: the LSTM kernel marks each generate(); take the window between the last two
+marks = [i for i, r in enumerate(rows) if 'rnn_bidir_kernel<1' in r['Kernel_Name']]
+if len(marks) >= 2:
+    # the step = from the first kernel after the previous LSTM's postnet to this LSTM's tail
+    lo = marks[-2] + 1
+    # find the start of the last step: first 'embedding' after marks[-2]
+    starts = [i for i in range(lo, len(rows)) if 'embedding' in rows[i]['Kernel_Name']]
+    a = starts[0] if starts else lo
+    b = len(rows)
+    t0 = rows[a]['s']
+    print(f'last step: {len(rows[a:b])} kernels, wall {(max(r["e"] for r in rows[a:b]) - t0) / 1e6:.3f} ms')
+    busy = 0; last = t0
+    for r in rows[a:b]:
+        s, e = max(r['s'], last), r['e']
+        if e > s: busy += e - s
+        last = max(last, e)
+    print(f'   device busy (union) {busy / 1e6:.3f} ms')
+    for r in rows[a:b]:
+        print(f'   {(r["s"] - t0) / 1e3:9.1f} us  +{(r["e"] - r["s"]) / 1e3:8.1f} us  q{r.get("Queue_Id", "?"):>3}  {name(r)}')
