@@ -56,6 +56,16 @@ SIGNATURES = {
     'ftmi_series_proj_add': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, P, c_float, P, P, P,
                                      c_float, P]),
     'ftmi_rowdot': (c_int, [P, c_int64, c_int64, c_int, P, P, c_float, P, P]),
+    'ftmi_stft': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P, P, P]),
+    'ftmi_mel_spectrogram': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P,
+                                     P, P, P, c_int, c_int, P, P]),
+    'ftmi_griffinlim_stft': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P,
+                                     P, P, c_float, c_int, P, P]),
+    'ftmi_spec_mul': (c_int, [P, P, c_int64, P, P]),
+    'ftmi_istft_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
+    'ftmi_istft': (c_int, [P, c_int, c_int, P, c_int, c_int, P, P, P, P, P, c_int64, c_int64, P]),
+    'ftmi_mel_nnls': (c_int, [P, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P,
+                              c_float, c_int, P, P]),
 }
 
 

@@ -1,0 +1,476 @@
+// Audio path of utils/dsp.py on gfx950: STFT / log-mel (wav_to_mel :71-87), ISTFT,
+// fast Griffin-Lim (griffinlim :89-103 -> librosa 0.7.2 core.griffinlim) and the mel
+// pseudo-inversion (feature.inverse.mel_to_stft -> util.nnls).
+//
+// Numerics follow librosa 0.7.2 on numpy 1.x: every FFT runs in float64 (numpy.fft
+// upcasts), spectra are stored as complex64 and audio as float32.  Here each workgroup
+// transforms TWO real frames with one fp64 complex FFT (z = a + i b) held in LDS
+// (Stockham radix-2 autosort, twiddles from a host-built fp64 table), so the
+// float32/complex64 results match the float64 reference up to its final rounding.
+//
+// Layouts (HBM): audio (B, L) rows with a stride; spectra FRAME-major (B, F, n_bins)
+// complex64 (one frame's bins contiguous: coalesced), magnitudes (B, F, n_bins) float32,
+// mel (B, n_mels, F) float32 (the reference's (n_mels, frames) per item).
+#include "common.h"
+
+namespace {
+
+struct FftPlan {
+  int n, log2n, hop;
+  const double *window;  // [n] periodic Hann, pad-centred
+  const double2 *tw;     // [n/2] exp(-2 pi i k / n)
+};
+
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// In-place (ping-pong) fp64 complex FFT of a[0..n) in LDS; returns the buffer holding the
+// result.  Stockham autosort: stage s (= 1, 2, 4, ...) maps butterfly b = p*s + q to
+// y[q + 2sp] = u + v, y[q + 2sp + s] = (u - v) w^(ps), u = a[b], v = a[b + n/2].
+template <bool INV>
+__device__ double2 *fft_lds(double2 *a, double2 *y, const FftPlan &P) {
+  const int n = P.n, h = n >> 1;
+  for (int ls = 0; ls < P.log2n; ++ls) {
+    __syncthreads();
+    const int s = 1 << ls;
+    for (int b = threadIdx.x; b < h; b += blockDim.x) {
+      const int p = b >> ls, q = b & (s - 1);
+      const double2 u = a[b], v = a[b + h];
+      double2 w = P.tw[p << ls];
+      if (INV) w.y = -w.y;
+      y[q + 2 * s * p] = cadd(u, v);
+      y[q + 2 * s * p + s] = cmul(csub(u, v), w);
+    }
+    double2 *t = a;
+    a = y;
+    y = t;
+  }
+  __syncthreads();
+  return a;
+}
+
+// numpy.pad(mode='reflect') index for any pad width (periodic reflection, period 2(L-1))
+__device__ __forceinline__ int64_t reflect_index(int64_t j, int64_t L) {
+  if (L <= 1) return 0;
+  const int64_t per = 2 * (L - 1);
+  j %= per;
+  if (j < 0) j += per;
+  return j >= L ? per - j : j;
+}
+
+// correctly rounded |re + i im| of a complex64 value
+__device__ __forceinline__ float cabs_rn(float re, float im) {
+  return (float)sqrt((double)re * (double)re + (double)im * (double)im);
+}
+
+enum { STFT_COMPLEX = 0, STFT_MEL = 1, STFT_GL = 2 };
+
+struct StftParams {
+  const float *y;
+  int64_t y_stride;
+  int B;
+  int64_t L;
+  const int32_t *lengths;  // samples per item (NULL: L)
+  int F;
+  const int32_t *frames;   // frames per item (NULL: F); frames beyond are skipped
+  FftPlan P;
+  // STFT_COMPLEX
+  float2 *X;
+  // STFT_MEL
+  float *mel;
+  const float *basis;  // [n_mels][n_bins]
+  const int32_t *mlo, *mhi;
+  int n_mels, log_norm;
+  // STFT_GL
+  const float *S;
+  float2 *tprev;
+  float c;
+  int first;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(256) void stft_kernel(const StftParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double2 *buf0 = (double2 *)smem;
+  double2 *buf1 = buf0 + p.P.n;
+  const int b = blockIdx.y;
+  const int f0 = 2 * blockIdx.x;
+  const int Fb = p.frames ? min(p.frames[b], p.F) : p.F;
+  if (f0 >= Fb) return;
+  const bool two = f0 + 1 < Fb;
+  const int64_t Lb = p.lengths ? (int64_t)p.lengths[b] : p.L;
+  const float *yb = p.y + (int64_t)b * p.y_stride;
+  const int n = p.P.n, half = n >> 1, nb = half + 1;
+
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double w = p.P.window[i];
+    const int64_t j0 = (int64_t)f0 * p.P.hop + i - half;
+    const double a = w * (double)yb[reflect_index(j0, Lb)];
+    const double c = two ? w * (double)yb[reflect_index(j0 + p.P.hop, Lb)] : 0.0;
+    buf0[i] = make_double2(a, c);
+  }
+  const double2 *Z = fft_lds<false>(buf0, buf1, p.P);
+  float *mag = (float *)(Z == buf0 ? buf1 : buf0);  // the free buffer
+
+  for (int k = threadIdx.x; k < nb; k += blockDim.x) {
+    const double2 zk = Z[k], zn = Z[(n - k) & (n - 1)];
+    // A = (Z[k] + conj Z[n-k]) / 2,  B = (Z[k] - conj Z[n-k]) / 2i
+    const float2 A = make_float2((float)(0.5 * (zk.x + zn.x)), (float)(0.5 * (zk.y - zn.y)));
+    const float2 Bq = make_float2((float)(0.5 * (zk.y + zn.y)), (float)(-0.5 * (zk.x - zn.x)));
+    for (int fr = 0; fr < 1 + two; ++fr) {
+      const float2 v = fr ? Bq : A;
+      const int64_t o = ((int64_t)b * p.F + f0 + fr) * nb + k;
+      if constexpr (MODE == STFT_COMPLEX) {
+        p.X[o] = v;
+      } else if constexpr (MODE == STFT_MEL) {
+        mag[fr * nb + k] = cabs_rn(v.x, v.y);
+      } else {
+        // fast GL update (librosa 0.7.2 griffinlim loop body, complex64 arithmetic):
+        // angles = rebuilt - c * tprev; angles /= |angles| + 1e-16; X = S * angles
+        float2 an = v;
+        if (!p.first) {
+          const float2 t = p.tprev[o];
+          an.x = __fsub_rn(v.x, __fmul_rn(p.c, t.x));
+          an.y = __fsub_rn(v.y, __fmul_rn(p.c, t.y));
+        }
+        const float d = __fadd_rn(cabs_rn(an.x, an.y), 1e-16f);
+        const float scl = __fdiv_rn(1.0f, d);  // numpy complex / real: (a, b) * (1/d)
+        an.x = __fmul_rn(an.x, scl);
+        an.y = __fmul_rn(an.y, scl);
+        const float s = p.S[o];
+        p.tprev[o] = v;
+        p.X[o] = make_float2(__fmul_rn(s, an.x), __fmul_rn(s, an.y));
+      }
+    }
+  }
+  if constexpr (MODE == STFT_MEL) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < (1 + two) * p.n_mels; t += blockDim.x) {
+      const int fr = t / p.n_mels, i = t - fr * p.n_mels;
+      const float *row = p.basis + (int64_t)i * nb;
+      double acc = 0.0;
+      for (int k = p.mlo[i]; k < p.mhi[i]; ++k) acc += (double)row[k] * (double)mag[fr * nb + k];
+      float v = (float)acc;
+      if (p.log_norm) v = (float)log((double)fmaxf(v, 1e-5f));
+      p.mel[((int64_t)b * p.n_mels + i) * p.F + f0 + fr] = v;
+    }
+  }
+}
+
+// inverse rFFT of two frames per workgroup, times the window; frames written as fp64
+// (B, F, n) so the overlap-add can round exactly like the float32 reference accumulation
+__global__ __launch_bounds__(256) void istft_frames_kernel(const float2 *__restrict__ X, int F,
+                                                           const int32_t *frames, FftPlan P,
+                                                           double *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double2 *buf0 = (double2 *)smem;
+  double2 *buf1 = buf0 + P.n;
+  const int b = blockIdx.y;
+  const int f0 = 2 * blockIdx.x;
+  const int Fb = frames ? min(frames[b], F) : F;
+  if (f0 >= Fb) return;
+  const bool two = f0 + 1 < Fb;
+  const int n = P.n, half = n >> 1, nb = half + 1;
+  const float2 *X0 = X + ((int64_t)b * F + f0) * nb;
+  const float2 *X1 = X0 + nb;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const bool mirror = k > half;
+    const int kk = mirror ? n - k : k;
+    const float2 a32 = X0[kk];
+    const float2 b32 = two ? X1[kk] : make_float2(0.f, 0.f);
+    double ar = a32.x, ai = a32.y, br = b32.x, bi = b32.y;
+    if (kk == 0 || kk == half) ai = bi = 0.0;  // c2r ignores imag of DC / Nyquist
+    if (mirror) {
+      ai = -ai;
+      bi = -bi;
+    }
+    buf0[k] = make_double2(ar - bi, ai + br);  // A_full + i B_full
+  }
+  const double2 *z = fft_lds<true>(buf0, buf1, P);
+  const double scale = 1.0 / n;
+  double *o = out + ((int64_t)b * F + f0) * n;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double2 v = z[i];
+    o[i] = P.window[i] * (v.x * scale);
+    if (two) o[n + i] = P.window[i] * (v.y * scale);
+  }
+}
+
+// overlap-add in frame order with float32 rounding after every add, divide by the float32
+// window sum-square where it exceeds FLT_MIN, crop n/2 on both sides (center=True)
+__global__ void istft_ola_kernel(const double *__restrict__ fr, int F, const int32_t *frames,
+                                 int n, int hop, const double *__restrict__ win_sq,
+                                 float *__restrict__ y, int64_t y_stride, int64_t y_len, int B) {
+  const int b = blockIdx.y;
+  const int Fb = frames ? min(frames[b], F) : F;
+  const int64_t Lb = Fb > 0 ? (int64_t)hop * (Fb - 1) : 0;
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < y_len;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (s < Lb) {
+      const int64_t sf = s + n / 2;
+      const int64_t ihi = min((int64_t)Fb - 1, sf / hop);
+      int64_t ilo = sf - n + 1 > 0 ? (sf - n + 1 + hop - 1) / hop : 0;
+      float w2 = 0.f;
+      for (int64_t i = ilo; i <= ihi; ++i) {
+        const int64_t off = sf - i * hop;
+        v = (float)((double)v + fr[((int64_t)b * F + i) * n + off]);
+        w2 = (float)((double)w2 + win_sq[off]);
+      }
+      if (w2 > 1.17549435e-38f) v = __fdiv_rn(v, w2);
+    }
+    y[(int64_t)b * y_stride + s] = v;
+  }
+}
+
+struct NnlsParams {
+  const float *mel;  // (B, n_mels, F)
+  int B, F, n_mels, nb;
+  const int32_t *frames;
+  int denorm;
+  const float *rowvals;  // packed nonzeros of each mel row (contiguous support)
+  const int32_t *rowptr, *rowlo;  // [n_mels + 1], [n_mels]
+  const int32_t *bi;     // [nb][2] mel rows of each bin (-1: none)
+  const float *bw;       // [nb][2] their weights
+  const float *pinv;     // [nb][n_mels]
+  float inv_L;
+  int iters;
+  float *S;  // (B, F, nb)
+};
+
+constexpr int NNLS_MAX_BINS = 64 * 33;  // n_fft <= 4096
+constexpr int NNLS_MAX_MELS = 512;
+
+// min ||A x - m||, x >= 0 for one frame per workgroup (one wave): FISTA on the sparse
+// filterbank (each bin feeds at most two mel rows), started like librosa's nnls from the
+// clipped minimum-norm least-squares solution pinv(A) m.  Everything stays in LDS /
+// registers across the iterations; HBM sees only m in and x out.
+template <int NJ>
+__global__ __launch_bounds__(64) void nnls_kernel(const NnlsParams p) {
+  extern __shared__ float dyn[];  // m[n_mels] r[n_mels] y[nb] vals[nnz]
+  float *m_s = dyn, *r_s = dyn + p.n_mels, *y_s = r_s + p.n_mels, *v_s = y_s + p.nb;
+  const int frame = blockIdx.x;
+  const int b = frame / p.F, f = frame - b * p.F;
+  const int lane = threadIdx.x;
+  const int Fb = p.frames ? min(p.frames[b], p.F) : p.F;
+  float *Sout = p.S + (int64_t)frame * p.nb;
+  if (f >= Fb) {
+    for (int k = lane; k < p.nb; k += 64) Sout[k] = 0.f;
+    return;
+  }
+  const int nnz = p.rowptr[p.n_mels];
+  for (int i = lane; i < nnz; i += 64) v_s[i] = p.rowvals[i];
+  for (int i = lane; i < p.n_mels; i += 64) {
+    const float v = p.mel[((int64_t)b * p.n_mels + i) * p.F + f];
+    m_s[i] = p.denorm ? (float)exp((double)v) : v;
+  }
+  __syncthreads();
+  float x[NJ], yv[NJ], w0[NJ], w1[NJ];
+  int i0[NJ], i1[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k = lane + 64 * j;
+    x[j] = 0.f;
+    i0[j] = i1[j] = -1;
+    w0[j] = w1[j] = 0.f;
+    if (k < p.nb) {
+      double acc = 0.0;
+      const float *pr = p.pinv + (int64_t)k * p.n_mels;
+      for (int i = 0; i < p.n_mels; ++i) acc += (double)pr[i] * (double)m_s[i];
+      x[j] = fmaxf((float)acc, 0.f);
+      i0[j] = p.bi[2 * k];
+      i1[j] = p.bi[2 * k + 1];
+      w0[j] = p.bw[2 * k];
+      w1[j] = p.bw[2 * k + 1];
+      y_s[k] = x[j];
+    }
+    yv[j] = x[j];
+  }
+  float t = 1.f;
+  for (int it = 0; it < p.iters; ++it) {
+    __syncthreads();
+    for (int i = lane; i < p.n_mels; i += 64) {
+      const int lo = p.rowlo[i], o = p.rowptr[i], cnt = p.rowptr[i + 1] - o;
+      float acc = 0.f;
+      for (int q = 0; q < cnt; ++q) acc = fmaf(v_s[o + q], y_s[lo + q], acc);
+      r_s[i] = acc - m_s[i];
+    }
+    __syncthreads();
+    const float tn = 0.5f * (1.f + sqrtf(1.f + 4.f * t * t));
+    const float beta = (t - 1.f) / tn;
+    t = tn;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int k = lane + 64 * j;
+      if (k < p.nb) {
+        float g = 0.f;
+        if (i0[j] >= 0) g = w0[j] * r_s[i0[j]];
+        if (i1[j] >= 0) g = fmaf(w1[j], r_s[i1[j]], g);
+        const float xn = fmaxf(0.f, yv[j] - g * p.inv_L);
+        yv[j] = xn + beta * (xn - x[j]);
+        x[j] = xn;
+        y_s[k] = yv[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k = lane + 64 * j;
+    if (k < p.nb) Sout[k] = x[j];
+  }
+}
+
+int check_plan(int n, int hop, const double *window, const void *tw) {
+  if (n < 16 || n > 4096 || (n & (n - 1)) || hop <= 0 || !window || !tw) return FTMI_E_ARG;
+  return FTMI_OK;
+}
+
+int log2i(int n) {
+  int l = 0;
+  while ((1 << l) < n) ++l;
+  return l;
+}
+
+size_t fft_smem(int n) { return (size_t)2 * n * sizeof(double2); }
+
+template <int MODE>
+int launch_stft(StftParams &p, hipStream_t s) {
+  const size_t sm = fft_smem(p.P.n);
+  if (sm > 64 * 1024)
+    (void)hipFuncSetAttribute((const void *)stft_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)sm);
+  dim3 grid((p.F + 1) / 2, p.B);
+  hipLaunchKernelGGL(stft_kernel<MODE>, grid, dim3(256), sm, s, p);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+}  // namespace
+
+extern "C" int ftmi_stft(const float *y, int64_t y_stride, int32_t B, int64_t L,
+                         const int32_t *lengths, int32_t n_fft, int32_t hop,
+                         const double *window, const void *twiddle, int32_t F,
+                         const int32_t *frames, void *X, ftmi_stream_t stream) {
+  if (!y || !X || B <= 0 || L <= 0 || F <= 0) return FTMI_E_ARG;
+  if (int rc = check_plan(n_fft, hop, window, twiddle)) return rc;
+  StftParams p = {};
+  p.y = y, p.y_stride = y_stride, p.B = B, p.L = L, p.lengths = lengths, p.F = F, p.frames = frames;
+  p.P = FftPlan{n_fft, log2i(n_fft), hop, window, (const double2 *)twiddle};
+  p.X = (float2 *)X;
+  return launch_stft<STFT_COMPLEX>(p, ftmi_hs(stream));
+}
+
+extern "C" int ftmi_mel_spectrogram(const float *y, int64_t y_stride, int32_t B, int64_t L,
+                                    const int32_t *lengths, int32_t n_fft, int32_t hop,
+                                    const double *window, const void *twiddle, int32_t F,
+                                    const int32_t *frames, const float *basis,
+                                    const int32_t *mel_lo, const int32_t *mel_hi, int32_t n_mels,
+                                    int32_t log_norm, float *mel, ftmi_stream_t stream) {
+  if (!y || !mel || !basis || !mel_lo || !mel_hi || B <= 0 || L <= 0 || F <= 0 || n_mels <= 0)
+    return FTMI_E_ARG;
+  if (int rc = check_plan(n_fft, hop, window, twiddle)) return rc;
+  StftParams p = {};
+  p.y = y, p.y_stride = y_stride, p.B = B, p.L = L, p.lengths = lengths, p.F = F, p.frames = frames;
+  p.P = FftPlan{n_fft, log2i(n_fft), hop, window, (const double2 *)twiddle};
+  p.mel = mel, p.basis = basis, p.mlo = mel_lo, p.mhi = mel_hi, p.n_mels = n_mels;
+  p.log_norm = log_norm;
+  return launch_stft<STFT_MEL>(p, ftmi_hs(stream));
+}
+
+extern "C" int ftmi_griffinlim_stft(const float *y, int64_t y_stride, int32_t B, int64_t L,
+                                    const int32_t *lengths, int32_t n_fft, int32_t hop,
+                                    const double *window, const void *twiddle, int32_t F,
+                                    const int32_t *frames, const float *S, void *tprev,
+                                    float c, int32_t first, void *X, ftmi_stream_t stream) {
+  if (!y || !S || !tprev || !X || B <= 0 || L <= 0 || F <= 0) return FTMI_E_ARG;
+  if (int rc = check_plan(n_fft, hop, window, twiddle)) return rc;
+  StftParams p = {};
+  p.y = y, p.y_stride = y_stride, p.B = B, p.L = L, p.lengths = lengths, p.F = F, p.frames = frames;
+  p.P = FftPlan{n_fft, log2i(n_fft), hop, window, (const double2 *)twiddle};
+  p.S = S, p.tprev = (float2 *)tprev, p.c = c, p.first = first, p.X = (float2 *)X;
+  return launch_stft<STFT_GL>(p, ftmi_hs(stream));
+}
+
+extern "C" int64_t ftmi_istft_workspace_bytes(int32_t B, int32_t F, int32_t n_fft) {
+  return (int64_t)B * F * n_fft * (int64_t)sizeof(double);
+}
+
+extern "C" int ftmi_istft(const void *X, int32_t B, int32_t F, const int32_t *frames,
+                          int32_t n_fft, int32_t hop, const double *window, const double *win_sq,
+                          const void *twiddle, void *work, float *y, int64_t y_stride,
+                          int64_t y_len, ftmi_stream_t stream) {
+  if (!X || !work || !y || !win_sq || B <= 0 || F <= 0 || y_len < 0) return FTMI_E_ARG;
+  if (int rc = check_plan(n_fft, hop, window, twiddle)) return rc;
+  const hipStream_t s = ftmi_hs(stream);
+  FftPlan P{n_fft, log2i(n_fft), hop, window, (const double2 *)twiddle};
+  const size_t sm = fft_smem(n_fft);
+  if (sm > 64 * 1024)
+    (void)hipFuncSetAttribute((const void *)istft_frames_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)sm);
+  hipLaunchKernelGGL(istft_frames_kernel, dim3((F + 1) / 2, B), dim3(256), sm, s, (const float2 *)X,
+                     F, frames, P, (double *)work);
+  FTMI_CHECK_LAUNCH();
+  if (y_len == 0) return FTMI_OK;
+  const int64_t blocks = (y_len + 255) / 256;
+  hipLaunchKernelGGL(istft_ola_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096), B), dim3(256), 0,
+                     s, (const double *)work, F, frames, n_fft, hop, win_sq, y, y_stride, y_len, B);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_mel_nnls(const float *mel, int32_t B, int32_t F, const int32_t *frames,
+                             int32_t n_mels, int32_t n_bins, int32_t denorm, int32_t nnz,
+                             const float *rowvals,
+                             const int32_t *rowptr, const int32_t *rowlo, const int32_t *bin_rows,
+                             const float *bin_w, const float *pinv, float inv_L, int32_t iters,
+                             float *S, ftmi_stream_t stream) {
+  if (!mel || !S || !rowvals || !rowptr || !rowlo || !bin_rows || !bin_w || !pinv) return FTMI_E_ARG;
+  if (B <= 0 || F <= 0 || n_mels <= 0 || n_mels > NNLS_MAX_MELS || n_bins <= 0 ||
+      n_bins > NNLS_MAX_BINS || iters < 0)
+    return FTMI_E_SHAPE;
+  NnlsParams p{mel, B, F, n_mels, n_bins, frames, denorm, rowvals, rowptr, rowlo,
+               bin_rows, bin_w, pinv, inv_L, iters, S};
+  if (nnz <= 0 || nnz > 16384) return FTMI_E_SHAPE;
+  const hipStream_t s = ftmi_hs(stream);
+  const int nj = (n_bins + 63) / 64;
+  const dim3 grid((unsigned)((int64_t)B * F)), block(64);
+  const size_t sm = (size_t)(2 * n_mels + n_bins + nnz) * sizeof(float);
+  if (nj <= 3)
+    hipLaunchKernelGGL(nnls_kernel<3>, grid, block, sm, s, p);
+  else if (nj <= 5)
+    hipLaunchKernelGGL(nnls_kernel<5>, grid, block, sm, s, p);
+  else if (nj <= 9)
+    hipLaunchKernelGGL(nnls_kernel<9>, grid, block, sm, s, p);
+  else if (nj <= 17)
+    hipLaunchKernelGGL(nnls_kernel<17>, grid, block, sm, s, p);
+  else
+    hipLaunchKernelGGL(nnls_kernel<33>, grid, block, sm, s, p);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+namespace {
+__global__ void spec_mul_kernel(const float *__restrict__ S, const float2 *__restrict__ A,
+                                float2 *__restrict__ X, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float s = S[i];
+    const float2 a = A[i];
+    X[i] = make_float2(__fmul_rn(s, a.x), __fmul_rn(s, a.y));
+  }
+}
+}  // namespace
+
+extern "C" int ftmi_spec_mul(const float *S, const void *angles, int64_t n, void *X,
+                             ftmi_stream_t stream) {
+  if (!S || !angles || !X || n < 0) return FTMI_E_ARG;
+  if (n == 0) return FTMI_OK;
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(spec_mul_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                     ftmi_hs(stream), S, (const float2 *)angles, (float2 *)X, n);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}

@@ -1,0 +1,395 @@
+"""`utils/dsp.py` (reference) on libftmi.so: the DSP class with the same constructor,
+``from_config``, ``wav_to_mel``, ``griffinlim``, ``normalize`` / ``denormalize``,
+``save_wav`` and the mu-law / label helpers.
+
+The reference delegates the arithmetic to librosa 0.7.2 (``requirements.txt:2``); here the
+STFT / log-mel, ISTFT, Griffin-Lim and the mel pseudo-inverse run as HIP kernels
+(``csrc/dsp.hip``, entry points in ``include/ftmi.h``).  The host side only builds the
+per-config plan once (window, fp64 twiddles, the Slaney mel filterbank, its sparse form
+and pseudo-inverse) and moves arrays between numpy and the device, so
+``wav_to_mel(np.ndarray) -> np.ndarray`` and ``griffinlim(np.ndarray) -> np.ndarray``
+keep the reference's signatures.  The batched device entry points
+(``mel_spectrogram`` / ``griffinlim_batch``) take and return HIP tensors.
+
+Not carried over (outside the hot path, need absent libraries): ``load_wav`` resampling
+(librosa), ``trim_silence`` (librosa.effects), ``trim_long_silences`` (webrtcvad).
+"""
+from __future__ import annotations
+
+import ctypes
+import wave
+from pathlib import Path
+from typing import Any, Dict, Optional, Tuple, Union
+
+import numpy as np
+import scipy.signal
+import torch
+
+from . import _lib
+from .probe import launch
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+# --- plan (host-built constants; librosa 0.7.2 definitions) ----------------------------------
+
+def _hz_to_mel(f: np.ndarray) -> np.ndarray:
+    """Slaney mel scale (librosa core.hz_to_mel, htk=False)."""
+    f = np.asanyarray(f, dtype=np.float64)
+    f_sp, min_log_hz = 200.0 / 3, 1000.0
+    min_log_mel, logstep = min_log_hz / f_sp, np.log(6.4) / 27.0
+    m = f / f_sp
+    if m.ndim:
+        hi = f >= min_log_hz
+        m[hi] = min_log_mel + np.log(f[hi] / min_log_hz) / logstep
+    elif f >= min_log_hz:
+        m = min_log_mel + np.log(f / min_log_hz) / logstep
+    return m
+
+
+def _mel_to_hz(m: np.ndarray) -> np.ndarray:
+    m = np.asanyarray(m, dtype=np.float64)
+    f_sp, min_log_hz = 200.0 / 3, 1000.0
+    min_log_mel, logstep = min_log_hz / f_sp, np.log(6.4) / 27.0
+    f = f_sp * m
+    hi = m >= min_log_mel
+    f[hi] = min_log_hz * np.exp(logstep * (m[hi] - min_log_mel))
+    return f
+
+
+def mel_basis(sr: int, n_fft: int, n_mels: int, fmin: float, fmax: Optional[float]) -> np.ndarray:
+    """librosa filters.mel(sr, n_fft, n_mels, fmin, fmax) (htk=False, norm=1, float32):
+    triangles in float64 stored to float32, then scaled in place by 2/(f[i+2]-f[i])."""
+    fmax = float(sr) / 2 if fmax is None else fmax
+    nb = 1 + n_fft // 2
+    w = np.zeros((n_mels, nb), dtype=np.float32)
+    fftf = np.linspace(0, float(sr) / 2, nb, endpoint=True)
+    melf = _mel_to_hz(np.linspace(_hz_to_mel(fmin), _hz_to_mel(fmax), n_mels + 2))
+    fd = np.diff(melf)
+    ramps = np.subtract.outer(melf, fftf)
+    for i in range(n_mels):
+        w[i] = np.maximum(0, np.minimum(-ramps[i] / fd[i], ramps[i + 2] / fd[i + 1]))
+    w *= (2.0 / (melf[2:n_mels + 2] - melf[:n_mels]))[:, None]
+    return w
+
+
+class DspPlan:
+    """Device constants of one DSP configuration (built once per device)."""
+
+    def __init__(self, sr: int, n_fft: int, hop: int, win_length: int, n_mels: int,
+                 fmin: float, fmax: float, device) -> None:
+        if n_fft & (n_fft - 1) or not 16 <= n_fft <= 4096:
+            raise ValueError('n_fft must be a power of two in [16, 4096]')
+        self.n_fft, self.hop, self.n_mels, self.nb = n_fft, hop, n_mels, n_fft // 2 + 1
+        dev = torch.device(device)
+        win = scipy.signal.get_window('hann', win_length, fftbins=True)
+        lp = (n_fft - win_length) // 2
+        win = np.pad(win, (lp, n_fft - win_length - lp))
+        tw = np.exp(-2j * np.pi * np.arange(n_fft // 2) / n_fft)
+        A = mel_basis(sr, n_fft, n_mels, fmin, fmax)
+        nz = A > 0
+        lo = np.array([np.argmax(r) if r.any() else 0 for r in nz], dtype=np.int32)
+        hi = np.array([len(r) - np.argmax(r[::-1]) if r.any() else 0 for r in nz], dtype=np.int32)
+        rowptr = np.zeros(n_mels + 1, dtype=np.int32)
+        rowptr[1:] = np.cumsum(hi - lo)
+        vals = np.concatenate([A[i, lo[i]:hi[i]] for i in range(n_mels)]).astype(np.float32)
+        bin_rows = np.full((self.nb, 2), -1, dtype=np.int32)
+        bin_w = np.zeros((self.nb, 2), dtype=np.float32)
+        for k in range(self.nb):
+            rows = [i for i in range(n_mels) if lo[i] <= k < hi[i]]
+            if len(rows) > 2:
+                raise ValueError('mel filterbank with more than two filters per bin')
+            for j, i in enumerate(rows):
+                bin_rows[k, j], bin_w[k, j] = i, A[i, k]
+        A64 = A.astype(np.float64)
+        self.inv_L = float(1.0 / np.linalg.norm(A64, 2) ** 2)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        self.window = t(win.astype(np.float64))
+        self.win_sq = t((win ** 2).astype(np.float64))
+        self.twiddle = t(np.stack([tw.real, tw.imag], -1).astype(np.float64))
+        self.basis_np = A
+        self.basis = t(A)
+        self.mel_lo, self.mel_hi = t(lo), t(hi)
+        self.nnz = int(rowptr[-1])
+        self.rowvals, self.rowptr, self.rowlo = t(vals), t(rowptr), t(lo)
+        self.bin_rows, self.bin_w = t(bin_rows), t(bin_w)
+        self.pinv = t(np.linalg.pinv(A64).astype(np.float32))
+
+    def frames(self, n_samples: int) -> int:
+        return 1 + n_samples // self.hop
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError('forwardtacotron_amd.dsp runs on a HIP device only (got a CPU '
+                               'tensor); there is no CPU fallback')
+
+
+# --- device entry points ---------------------------------------------------------------------
+
+def stft(plan: DspPlan, y: torch.Tensor, lengths: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Complex STFT of audio rows y (B, L): (B, F, n_fft/2+1) complex64, frame-major."""
+    _need_cuda(y, lengths)
+    B, L = y.shape
+    F = plan.frames(L)
+    X = torch.empty(B, F, plan.nb, dtype=torch.complex64, device=y.device)
+    launch('ftmi_stft', f'stft[B={B},F={F},n={plan.n_fft}]', 0, 4.0 * B * L + 8.0 * B * F * plan.nb,
+           y.data_ptr(), y.stride(0), B, L, _p(lengths), plan.n_fft, plan.hop,
+           plan.window.data_ptr(), plan.twiddle.data_ptr(), F, None, X.data_ptr(), _stream())
+    return X
+
+
+def mel_spectrogram(plan: DspPlan, y: torch.Tensor, lengths: Optional[torch.Tensor] = None,
+                    log_norm: bool = True) -> torch.Tensor:
+    """Batched DSP.wav_to_mel: audio rows (B, L) float32 -> (B, n_mels, 1 + L // hop)."""
+    _need_cuda(y, lengths)
+    if y.dtype != torch.float32 or y.dim() != 2 or y.stride(1) != 1:
+        raise ValueError('audio rows (B, L) float32 with unit stride expected')
+    B, L = y.shape
+    F = plan.frames(L)
+    mel = torch.empty(B, plan.n_mels, F, device=y.device)
+    launch('ftmi_mel_spectrogram', f'mel_spectrogram[B={B},F={F},n={plan.n_fft}]', 0,
+           4.0 * B * L + 4.0 * B * F * plan.n_mels,
+           y.data_ptr(), y.stride(0), B, L, _p(lengths), plan.n_fft, plan.hop,
+           plan.window.data_ptr(), plan.twiddle.data_ptr(), F, None, plan.basis.data_ptr(),
+           plan.mel_lo.data_ptr(), plan.mel_hi.data_ptr(), plan.n_mels, int(log_norm),
+           mel.data_ptr(), _stream())
+    return mel
+
+
+def istft(plan: DspPlan, X: torch.Tensor, frames: Optional[torch.Tensor] = None,
+          y_len: Optional[int] = None, work: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(B, F, nb) complex64 frame-major -> audio rows (B, hop*(F-1)) (item b valid for
+    hop*(frames[b]-1) samples, zero after)."""
+    _need_cuda(X, frames)
+    B, F, nb = X.shape
+    if nb != plan.nb or X.dtype != torch.complex64 or not X.is_contiguous():
+        raise ValueError('contiguous (B, F, n_fft/2+1) complex64 expected')
+    y_len = plan.hop * (F - 1) if y_len is None else y_len
+    y = torch.empty(B, max(y_len, 1), device=X.device)
+    if work is None:
+        work = torch.empty(_lib.load().ftmi_istft_workspace_bytes(B, F, plan.n_fft),
+                           dtype=torch.uint8, device=X.device)
+    launch('ftmi_istft', f'istft[B={B},F={F},n={plan.n_fft}]', 0,
+           8.0 * B * F * nb + 16.0 * B * F * plan.n_fft + 4.0 * B * y_len,
+           X.data_ptr(), B, F, _p(frames), plan.n_fft, plan.hop, plan.window.data_ptr(),
+           plan.win_sq.data_ptr(), plan.twiddle.data_ptr(), work.data_ptr(), y.data_ptr(),
+           y.stride(0), y_len, _stream())
+    return y[:, :y_len]
+
+
+def mel_to_stft(plan: DspPlan, mel: torch.Tensor, frames: Optional[torch.Tensor] = None,
+                denorm: bool = True, iters: int = 200) -> torch.Tensor:
+    """librosa feature.inverse.mel_to_stft(power=1) of (B, n_mels, F) (log-)mels:
+    (B, F, nb) float32 non-negative magnitudes, frame-major."""
+    _need_cuda(mel, frames)
+    if mel.dtype != torch.float32 or not mel.is_contiguous() or mel.size(1) != plan.n_mels:
+        raise ValueError('contiguous (B, n_mels, F) float32 expected')
+    B, _, F = mel.shape
+    S = torch.empty(B, F, plan.nb, device=mel.device)
+    launch('ftmi_mel_nnls', f'mel_nnls[B={B},F={F},iters={iters}]', 0,
+           4.0 * B * F * (plan.n_mels + plan.nb),
+           mel.data_ptr(), B, F, _p(frames), plan.n_mels, plan.nb, int(denorm), plan.nnz,
+           plan.rowvals.data_ptr(), plan.rowptr.data_ptr(), plan.rowlo.data_ptr(),
+           plan.bin_rows.data_ptr(), plan.bin_w.data_ptr(), plan.pinv.data_ptr(),
+           ctypes.c_float(plan.inv_L), iters, S.data_ptr(), _stream())
+    return S
+
+
+def griffinlim_from_stft(plan: DspPlan, S: torch.Tensor, angles: torch.Tensor, n_iter: int = 32,
+                         frames: Optional[torch.Tensor] = None, momentum: float = 0.99) -> torch.Tensor:
+    """librosa core.griffinlim (0.7.2 fast GL) of magnitudes S (B, F, nb) from initial unit
+    phases `angles` (B, F, nb) complex64 -> audio rows (B, hop*(F-1))."""
+    _need_cuda(S, angles, frames)
+    B, F, nb = S.shape
+    dev = S.device
+    X = torch.empty(B, F, nb, dtype=torch.complex64, device=dev)
+    launch('ftmi_spec_mul', f'spec_mul[n={S.numel()}]', 0, 20.0 * S.numel(),
+           S.data_ptr(), angles.data_ptr(), S.numel(), X.data_ptr(), _stream())
+    tprev = torch.empty_like(X)
+    work = torch.empty(_lib.load().ftmi_istft_workspace_bytes(B, F, plan.n_fft), dtype=torch.uint8,
+                       device=dev)
+    L = plan.hop * (F - 1)
+    lengths = None if frames is None else (plan.hop * (frames - 1)).to(torch.int32)
+    c = float(np.float32(momentum / (1 + momentum)))
+    for it in range(n_iter):
+        y = istft(plan, X, frames, L, work)
+        launch('ftmi_griffinlim_stft', f'gl_stft[B={B},F={F}]', 0, 4.0 * B * L + 28.0 * S.numel(),
+               y.data_ptr(), y.stride(0), B, max(L, 1), _p(lengths), plan.n_fft, plan.hop,
+               plan.window.data_ptr(), plan.twiddle.data_ptr(), F, _p(frames), S.data_ptr(),
+               tprev.data_ptr(), ctypes.c_float(c), int(it == 0), X.data_ptr(), _stream())
+    return istft(plan, X, frames, L, work)
+
+
+# --- the reference class ---------------------------------------------------------------------
+
+class DSP:
+    """`utils/dsp.py:12-57`: same constructor arguments and attributes."""
+
+    def __init__(self, num_mels: int, sample_rate: int, hop_length: int, win_length: int,
+                 n_fft: int, fmin: float, fmax: float, peak_norm: bool,
+                 trim_start_end_silence: bool, trim_silence_top_db: int, pitch_max_freq: int,
+                 trim_long_silences: bool, vad_sample_rate: int, vad_window_length: float,
+                 vad_moving_average_width: float, vad_max_silence_length: int, bits: int,
+                 mu_law: bool, voc_mode: str) -> None:
+        self.n_mels = num_mels
+        self.sample_rate = sample_rate
+        self.hop_length = hop_length
+        self.win_length = win_length
+        self.n_fft = n_fft
+        self.fmin = fmin
+        self.fmax = fmax
+        self.should_peak_norm = peak_norm
+        self.should_trim_start_end_silence = trim_start_end_silence
+        self.should_trim_long_silences = trim_long_silences
+        self.trim_silence_top_db = trim_silence_top_db
+        self.pitch_max_freq = pitch_max_freq
+        self.vad_sample_rate = vad_sample_rate
+        self.vad_window_length = vad_window_length
+        self.vad_moving_average_width = vad_moving_average_width
+        self.vad_max_silence_length = vad_max_silence_length
+        self.bits = bits
+        self.mu_law = mu_law
+        self.voc_mode = voc_mode
+        self._plans: Dict[Any, DspPlan] = {}
+        self.nnls_iters = 200
+
+    @classmethod
+    def from_config(cls, config: Dict[str, Any]) -> 'DSP':
+        return DSP(**config['dsp'])
+
+    def plan(self, device=None) -> DspPlan:
+        dev = torch.device(device if device is not None else 'cuda')
+        if dev.type != 'cuda':
+            raise RuntimeError('forwardtacotron_amd.dsp runs on a HIP device only')
+        if dev.index is None:
+            dev = torch.device('cuda', torch.cuda.current_device())
+        if dev not in self._plans:
+            self._plans[dev] = DspPlan(self.sample_rate, self.n_fft, self.hop_length,
+                                       self.win_length, self.n_mels, self.fmin, self.fmax, dev)
+        return self._plans[dev]
+
+    # -- I/O (utils/dsp.py:62-69) --
+    def load_wav(self, path: Union[str, Path]) -> np.ndarray:
+        """16-bit / float WAV at `sample_rate` (the reference resamples with librosa,
+        which is absent: other rates raise)."""
+        import scipy.io.wavfile
+        sr, wav = scipy.io.wavfile.read(str(path))
+        if sr != self.sample_rate:
+            raise ValueError(f'{path}: sample rate {sr} != {self.sample_rate} (no resampler)')
+        if wav.dtype == np.int16:
+            wav = wav.astype(np.float32) / 32768.0
+        elif wav.dtype == np.int32:
+            wav = wav.astype(np.float32) / 2147483648.0
+        wav = wav.astype(np.float32)
+        return wav.mean(axis=1) if wav.ndim == 2 else wav
+
+    def save_wav(self, wav: np.ndarray, path: Union[str, Path]) -> None:
+        """16-bit PCM WAV (soundfile's default subtype for .wav)."""
+        wav = np.asarray(wav, dtype=np.float32)
+        pcm = np.clip(np.round(wav * 32767.0), -32768, 32767).astype('<i2')
+        with wave.open(str(path), 'wb') as f:
+            f.setnchannels(1)
+            f.setsampwidth(2)
+            f.setframerate(self.sample_rate)
+            f.writeframes(pcm.tobytes())
+
+    # -- analysis / synthesis (utils/dsp.py:71-103) --
+    def wav_to_mel(self, y, normalize: bool = True):
+        """|STFT| -> mel -> log(clip 1e-5).  numpy (L,) -> numpy (n_mels, 1 + L // hop) like
+        the reference; a HIP tensor (L,) or (B, L) returns a tensor."""
+        if isinstance(y, torch.Tensor):
+            _need_cuda(y)
+            yy = y.float().reshape(-1, y.shape[-1]).contiguous()
+            mel = mel_spectrogram(self.plan(y.device), yy, log_norm=normalize)
+            return mel[0] if y.dim() == 1 else mel
+        y = np.asarray(y)
+        if not np.issubdtype(y.dtype, np.floating) or y.ndim != 1:
+            raise ValueError('mono floating-point audio expected')
+        t = torch.from_numpy(np.ascontiguousarray(y, dtype=np.float32)).cuda()[None]
+        return mel_spectrogram(self.plan(t.device), t, log_norm=normalize)[0].cpu().numpy()
+
+    def griffinlim(self, mel, n_iter: int = 32, angles=None, random_state=None):
+        """exp -> mel_to_stft (NNLS) -> fast Griffin-Lim (32 iterations, momentum 0.99).
+        numpy (n_mels, T) -> numpy wav of hop * (T - 1) samples.  The initial phases are
+        exp(2 pi i U[0,1)) drawn like librosa (np.random, or RandomState(random_state)),
+        shape (n_bins, T); pass `angles` to fix them."""
+        is_t = isinstance(mel, torch.Tensor)
+        m = mel if is_t else torch.from_numpy(np.ascontiguousarray(mel, dtype=np.float32)).cuda()
+        _need_cuda(m)
+        plan = self.plan(m.device)
+        T = m.shape[-1]
+        if angles is None:
+            rng = np.random if random_state is None else np.random.RandomState(random_state)
+            angles = np.exp(2j * np.pi * rng.rand(plan.nb, T)).astype(np.complex64)
+        a = angles if isinstance(angles, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(np.asarray(angles, dtype=np.complex64).T))
+        a = a.to(m.device).reshape(1, T, plan.nb).contiguous()
+        S = mel_to_stft(plan, m.float().reshape(1, plan.n_mels, T).contiguous(), iters=self.nnls_iters)
+        wav = griffinlim_from_stft(plan, S, a, n_iter)[0]
+        return wav if is_t else wav.cpu().numpy()
+
+    def griffinlim_batch(self, mel: torch.Tensor, frames: Optional[torch.Tensor] = None,
+                         n_iter: int = 32, generator: Optional[torch.Generator] = None
+                         ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Batched Griffin-Lim of (B, n_mels, F) device mels (item b uses its first
+        frames[b] frames): returns (wav (B, hop*(F-1)), samples per item).  Initial phases
+        from torch's generator on the device."""
+        _need_cuda(mel, frames)
+        plan = self.plan(mel.device)
+        B, _, F = mel.shape
+        fr = None if frames is None else frames.to(device=mel.device, dtype=torch.int32)
+        u = torch.rand(B, F, plan.nb, dtype=torch.float64, device=mel.device, generator=generator)
+        angles = torch.polar(torch.ones_like(u), 2 * np.pi * u).to(torch.complex64)
+        S = mel_to_stft(plan, mel.float().contiguous(), fr, iters=self.nnls_iters)
+        wav = griffinlim_from_stft(plan, S, angles, n_iter, fr)
+        n = plan.hop * ((fr if fr is not None else torch.full((B,), F, device=mel.device)) - 1)
+        return wav, n
+
+    # -- utils/dsp.py:105-110 --
+    def normalize(self, mel):
+        if isinstance(mel, torch.Tensor):
+            return torch.log(torch.clamp(mel, min=1e-5))
+        return np.log(np.clip(mel, a_min=1.e-5, a_max=None))
+
+    def denormalize(self, mel):
+        return torch.exp(mel) if isinstance(mel, torch.Tensor) else np.exp(mel)
+
+    def trim_silence(self, wav: np.ndarray) -> np.ndarray:
+        raise NotImplementedError('trim_silence needs librosa.effects (absent); preprocessing '
+                                  'is outside the inference path')
+
+    def trim_long_silences(self, wav: np.ndarray) -> np.ndarray:
+        raise NotImplementedError('trim_long_silences needs webrtcvad (absent); preprocessing '
+                                  'is outside the inference path')
+
+    # -- utils/dsp.py:143-165 (vocoder label helpers) --
+    @staticmethod
+    def label_2_float(x: np.ndarray, bits: float) -> np.ndarray:
+        return 2 * x / (2 ** bits - 1.) - 1.
+
+    @staticmethod
+    def float_2_label(x: np.ndarray, bits: float) -> np.ndarray:
+        assert abs(x).max() <= 1.0
+        x = (x + 1.) * (2 ** bits - 1) / 2
+        return x.clip(0, 2 ** bits - 1)
+
+    @staticmethod
+    def encode_mu_law(x: np.ndarray, mu: float) -> np.ndarray:
+        mu = mu - 1
+        fx = np.sign(x) * np.log(1 + mu * np.abs(x)) / np.log(1 + mu)
+        return np.floor((fx + 1) / 2 * mu + 0.5)
+
+    @staticmethod
+    def decode_mu_law(y: np.ndarray, mu: float, from_labels: bool = True) -> np.ndarray:
+        if from_labels:
+            y = DSP.label_2_float(y, np.log2(mu))
+        mu = mu - 1
+        return np.sign(y) / mu * ((1 + mu) ** np.abs(y) - 1)

@@ -204,6 +204,69 @@ int ftmi_series_proj_add(float *x, int64_t x_stride, int32_t B, int32_t T, int32
 int ftmi_rowdot(const float *x, int64_t x_stride, int64_t M, int32_t C, const float *w,
                 const float *bias, float alpha, float *out, ftmi_stream_t stream);
 
+/* ====================================================================================
+ * Audio path: utils/dsp.py (DSP.wav_to_mel :71-87, griffinlim :89-103), whose arithmetic
+ * is librosa 0.7.2 (requirements.txt:2): core.stft / core.istft / filters.mel /
+ * util.nnls / core.griffinlim.  Plans (host-built once per DSP config, device buffers):
+ *   window  double[n_fft]     periodic Hann of win_length, zero-padded to n_fft (centred)
+ *   win_sq  double[n_fft]     window**2 (window_sumsquare's envelope)
+ *   twiddle double[n_fft][2]  exp(-2 pi i k / n_fft), k < n_fft / 2
+ * n_fft: power of two in [16, 4096].  center=True, pad_mode='reflect' throughout.
+ * Spectra are FRAME-major complex64 (B, F, n_fft/2+1) (interleaved re, im floats); mel
+ * is (B, n_mels, F).  `lengths` (samples) / `frames` (frames) are optional device int32
+ * per-item limits (NULL: L / F for every item); frames past an item's count are skipped.
+ * ==================================================================================== */
+
+/* complex STFT (librosa core.stft: rfft(window * frame) in fp64, stored complex64) of
+ * audio rows y (B, L) with row stride y_stride; F = 1 + L // hop frames. */
+int ftmi_stft(const float *y, int64_t y_stride, int32_t B, int64_t L, const int32_t *lengths,
+              int32_t n_fft, int32_t hop, const double *window, const void *twiddle, int32_t F,
+              const int32_t *frames, void *X, ftmi_stream_t stream);
+
+/* DSP.wav_to_mel (utils/dsp.py:71-87): mel[b,i,f] = sum_k basis[i,k] |STFT|[b,f,k]
+ * (fp64 accumulation over the row support [mel_lo[i], mel_hi[i]) of basis [n_mels][nb]),
+ * then log(max(., 1e-5)) when log_norm (DSP.normalize :105-107). */
+int ftmi_mel_spectrogram(const float *y, int64_t y_stride, int32_t B, int64_t L,
+                         const int32_t *lengths, int32_t n_fft, int32_t hop, const double *window,
+                         const void *twiddle, int32_t F, const int32_t *frames, const float *basis,
+                         const int32_t *mel_lo, const int32_t *mel_hi, int32_t n_mels,
+                         int32_t log_norm, float *mel, ftmi_stream_t stream);
+
+/* One fast Griffin-Lim analysis step (librosa core.griffinlim loop body): rebuilt =
+ * STFT(y); angles = rebuilt - c * tprev (first: rebuilt); angles /= |angles| + 1e-16;
+ * X = S * angles (next synthesis input); tprev = rebuilt.  S: (B, F, nb) float32;
+ * tprev, X: (B, F, nb) complex64.  c = momentum / (1 + momentum). */
+int ftmi_griffinlim_stft(const float *y, int64_t y_stride, int32_t B, int64_t L,
+                         const int32_t *lengths, int32_t n_fft, int32_t hop, const double *window,
+                         const void *twiddle, int32_t F, const int32_t *frames, const float *S,
+                         void *tprev, float c, int32_t first, void *X, ftmi_stream_t stream);
+
+/* X = S * angles elementwise (complex64 = float32 * complex64, numpy rounding): the
+ * Griffin-Lim synthesis input for the initial phases.  n = number of bins in total. */
+int ftmi_spec_mul(const float *S, const void *angles, int64_t n, void *X, ftmi_stream_t stream);
+
+/* librosa core.istft (center=True): per-frame fp64 irfft * window, overlap-added in frame
+ * order with float32 rounding, divided by the window sum-square where > FLT_MIN, cropped
+ * by n_fft/2.  Item b yields hop * (frames_b - 1) samples into y[b, :], zero-filled up to
+ * y_len.  work: ftmi_istft_workspace_bytes(B, F, n_fft) bytes. */
+int64_t ftmi_istft_workspace_bytes(int32_t B, int32_t F, int32_t n_fft);
+int ftmi_istft(const void *X, int32_t B, int32_t F, const int32_t *frames, int32_t n_fft,
+               int32_t hop, const double *window, const double *win_sq, const void *twiddle,
+               void *work, float *y, int64_t y_stride, int64_t y_len, ftmi_stream_t stream);
+
+/* mel -> linear magnitude (librosa feature.inverse.mel_to_stft, power=1, via util.nnls):
+ * per frame min ||A x - m||^2, x >= 0, m = exp(mel) when denorm (DSP.denormalize
+ * :109-110).  Solved by FISTA (`iters` steps of 1/L = inv_L) from the clipped
+ * minimum-norm solution pinv(A) m.  A is given sparse: row i holds nonzeros
+ * rowvals[rowptr[i] .. rowptr[i+1]) for bins rowlo[i] ...; bin k feeds mel rows
+ * bin_rows[2k], bin_rows[2k+1] (-1: none) with weights bin_w[2k], bin_w[2k+1]; pinv is
+ * [n_bins][n_mels].  nnz = rowptr[n_mels].  S: (B, F, n_bins) float32. */
+int ftmi_mel_nnls(const float *mel, int32_t B, int32_t F, const int32_t *frames, int32_t n_mels,
+                  int32_t n_bins, int32_t denorm, int32_t nnz, const float *rowvals,
+                  const int32_t *rowptr, const int32_t *rowlo, const int32_t *bin_rows,
+                  const float *bin_w, const float *pinv, float inv_L, int32_t iters, float *S,
+                  ftmi_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

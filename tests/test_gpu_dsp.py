@@ -1,0 +1,142 @@
+"""The audio path on the GPU (csrc/dsp.hip through the C-ABI) against the librosa-0.7.2
+oracle (oracle/dsp_oracle.py) on the same seeded inputs.
+
+Tolerances: the kernels run the FFTs in fp64 like numpy 1.x does for librosa, so the
+complex64 / float32 outputs differ from the oracle only where the final rounding of a
+~1e-16-relative fp64 difference flips, or where numpy's float32 |z| (not correctly
+rounded) differs from the kernel's correctly rounded one: bounded here by 1e-6 of the
+frame scale.  Griffin-Lim runs 32 nonlinear iterations on top: 1e-4 of the signal scale.
+The NNLS (mel_to_stft) system is under-determined (80 equations, 513 unknowns), so its
+parity is the objective (no worse than the reference's L-BFGS-B) and closeness of x."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import dsp_oracle as D
+
+pytestmark = pytest.mark.gpu
+
+CFG = json.loads((GOLDEN / 'dsp_config.json').read_text())
+REF_MEL = np.load(GOLDEN / 'ref_test_mel.npy', allow_pickle=False)
+
+
+@pytest.fixture(scope='module')
+def dsp():
+    from forwardtacotron_amd.dsp import DSP
+    return DSP.from_config(CFG)
+
+
+def audio(n, seed):
+    rng = np.random.RandomState(seed)
+    t = np.arange(n) / 22050.0
+    y = 0.3 * np.sin(2 * np.pi * 220 * t) + 0.05 * rng.randn(n)
+    return y.astype(np.float32)
+
+
+@pytest.mark.parametrize('n', [10000, 3001, 300, 1024 * 40 + 17])
+def test_stft_complex(dsp, n):
+    from forwardtacotron_amd import dsp as G
+    y = audio(n, n)
+    ref = D.stft(y)
+    X = G.stft(dsp.plan(), torch.from_numpy(y).cuda()[None])[0].cpu().numpy().T
+    assert X.shape == ref.shape
+    scale = np.abs(ref).max()
+    assert np.abs(X - ref).max() <= 1e-6 * scale
+    # most bins round to the identical complex64 (fewer on 2-frame inputs, where the
+    # two-frames-per-FFT packing mixes a very different partner frame into the rounding)
+    assert np.mean(X == ref) > (0.9 if n > 1000 else 0.4)
+
+
+@pytest.mark.parametrize('n', [10000, 4444])
+def test_wav_to_mel(dsp, n):
+    y = audio(n, 7)
+    ref = D.wav_to_mel(y)
+    got = dsp.wav_to_mel(y)
+    assert got.shape == ref.shape and got.dtype == np.float32
+    np.testing.assert_allclose(got, ref, rtol=0, atol=2e-5)
+
+
+def test_mel_batch_with_lengths_matches_per_item(dsp):
+    from forwardtacotron_amd import dsp as G
+    ys = [audio(n, n) for n in (9000, 7000, 2000)]
+    L = max(len(y) for y in ys)
+    batch = np.zeros((3, L), np.float32)
+    for i, y in enumerate(ys):
+        batch[i, :len(y)] = y
+    lens = torch.tensor([len(y) for y in ys], dtype=torch.int32, device='cuda')
+    mel = G.mel_spectrogram(dsp.plan(), torch.from_numpy(batch).cuda(), lengths=lens).cpu().numpy()
+    for i, y in enumerate(ys):
+        ref = D.wav_to_mel(y)
+        np.testing.assert_allclose(mel[i, :, :ref.shape[1]], ref, atol=2e-5)
+
+
+def test_istft(dsp):
+    from forwardtacotron_amd import dsp as G
+    rng = np.random.RandomState(3)
+    X = (rng.randn(513, 37) + 1j * rng.randn(513, 37)).astype(np.complex64)
+    ref = D.istft(X)
+    got = G.istft(dsp.plan(), torch.from_numpy(np.ascontiguousarray(X.T)).cuda()[None])[0]
+    got = got.cpu().numpy()
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-6 * np.abs(ref).max())
+
+
+def test_mel_to_stft_objective(dsp):
+    from forwardtacotron_amd import dsp as G
+    M = np.exp(REF_MEL)
+    ref = D.mel_to_stft(M)
+    A = D.mel_filters(22050, 1024, 80, 0, 8000).astype(np.float64)
+    S = G.mel_to_stft(dsp.plan(), torch.from_numpy(REF_MEL).cuda()[None])[0].cpu().numpy().T
+    assert S.shape == ref.shape and (S >= 0).all()
+    obj = lambda x: np.linalg.norm(A @ x - M)
+    assert obj(S) <= obj(ref) * 1.01 + 1e-7 * np.linalg.norm(M)
+    assert np.linalg.norm(S - ref) / np.linalg.norm(ref) < 0.05
+
+
+def test_griffinlim_from_fixed_magnitudes_and_phases(dsp):
+    """The GL iteration itself (istft -> stft -> momentum -> normalise) vs the oracle on
+    identical S and init phases."""
+    from forwardtacotron_amd import dsp as G
+    S = D.mel_to_stft(np.exp(REF_MEL))
+    ang = D.random_angles(S.shape, 5)
+    ref = D.griffinlim_from_stft(S, ang, n_iter=32)
+    got = G.griffinlim_from_stft(dsp.plan(), torch.from_numpy(np.ascontiguousarray(S.T)).cuda()[None],
+                                 torch.from_numpy(np.ascontiguousarray(ang.T)).cuda()[None], 32)
+    got = got[0].cpu().numpy()
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-4 * np.abs(ref).max())
+
+
+def test_griffinlim_api_and_round_trip(dsp):
+    wav = dsp.griffinlim(REF_MEL, random_state=0)
+    assert isinstance(wav, np.ndarray) and wav.shape == (256 * 39,) and wav.dtype == np.float32
+    again = dsp.griffinlim(REF_MEL, random_state=0)
+    np.testing.assert_array_equal(wav, again)
+    m2 = D.wav_to_mel(wav)
+    assert np.abs(m2 - REF_MEL).mean() < 0.2
+
+
+def test_griffinlim_batch_lengths(dsp):
+    """Batched GL with per-item frame counts == each item on its own (same phases)."""
+    from forwardtacotron_amd import dsp as G
+    plan = dsp.plan()
+    mels = np.stack([REF_MEL, REF_MEL[:, ::-1]]).copy()
+    frames = torch.tensor([40, 25], dtype=torch.int32, device='cuda')
+    S = G.mel_to_stft(plan, torch.from_numpy(mels).cuda(), frames)
+    ang = torch.polar(torch.ones(2, 40, plan.nb, dtype=torch.float64, device='cuda'),
+                      torch.rand(2, 40, plan.nb, dtype=torch.float64, device='cuda') * 6.283)
+    ang = ang.to(torch.complex64)
+    wb = G.griffinlim_from_stft(plan, S, ang, 8, frames)
+    for i, f in enumerate((40, 25)):
+        wi = G.griffinlim_from_stft(plan, S[i:i + 1, :f].contiguous(), ang[i:i + 1, :f].contiguous(), 8)
+        np.testing.assert_array_equal(wb[i, :256 * (f - 1)].cpu().numpy(), wi[0].cpu().numpy())
+    assert not wb[1, 256 * 24:].any()
+
+
+def test_cpu_tensor_raises(dsp):
+    from forwardtacotron_amd import dsp as G
+    with pytest.raises(RuntimeError):
+        G.mel_spectrogram(dsp.plan(), torch.zeros(1, 4000))
