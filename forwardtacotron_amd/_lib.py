@@ -56,6 +56,11 @@ SIGNATURES = {
     'ftmi_series_proj_add': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, P, c_float, P, P, P,
                                      c_float, P]),
     'ftmi_rowdot': (c_int, [P, c_int64, c_int64, c_int, P, P, c_float, P, P]),
+    'ftmi_embedding_posenc': (c_int, [P, c_int, c_int, P, c_int64, c_int, P, P, P, P, P]),
+    'ftmi_lr_posenc': (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, P, P, P, c_int64, P]),
+    'ftmi_layernorm': (c_int, [P, c_int64, c_int64, c_int, P, P, c_float, P, c_int64, P]),
+    'ftmi_attention': (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
+                               c_float, P, c_int64, P]),
     'ftmi_stft': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P, P, P]),
     'ftmi_mel_spectrogram': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P,
                                      P, P, P, c_int, c_int, P, P]),

@@ -13,6 +13,11 @@
 // mel (B, n_mels, F) float32 (the reference's (n_mels, frames) per item).
 #include "common.h"
 
+// hipcc contracts a*b+c into FMA by default (-ffp-contract=fast; the __fmul_rn family is
+// header-inlined and contracts too): the reference-order float32 roundings below need
+// every multiply and add rounded on its own.
+#pragma clang fp contract(off)
+
 namespace {
 
 struct FftPlan {
@@ -133,16 +138,16 @@ __global__ __launch_bounds__(256) void stft_kernel(const StftParams p) {
         float2 an = v;
         if (!p.first) {
           const float2 t = p.tprev[o];
-          an.x = __fsub_rn(v.x, __fmul_rn(p.c, t.x));
-          an.y = __fsub_rn(v.y, __fmul_rn(p.c, t.y));
+          an.x = (v.x - (p.c * t.x));
+          an.y = (v.y - (p.c * t.y));
         }
-        const float d = __fadd_rn(cabs_rn(an.x, an.y), 1e-16f);
-        const float scl = __fdiv_rn(1.0f, d);  // numpy complex / real: (a, b) * (1/d)
-        an.x = __fmul_rn(an.x, scl);
-        an.y = __fmul_rn(an.y, scl);
+        const float d = (cabs_rn(an.x, an.y) + 1e-16f);
+        const float scl = (1.0f / d);  // numpy complex / real: (a, b) * (1/d)
+        an.x = (an.x * scl);
+        an.y = (an.y * scl);
         const float s = p.S[o];
         p.tprev[o] = v;
-        p.X[o] = make_float2(__fmul_rn(s, an.x), __fmul_rn(s, an.y));
+        p.X[o] = make_float2((s * an.x), (s * an.y));
       }
     }
   }
@@ -220,7 +225,7 @@ __global__ void istft_ola_kernel(const double *__restrict__ fr, int F, const int
         v = (float)((double)v + fr[((int64_t)b * F + i) * n + off]);
         w2 = (float)((double)w2 + win_sq[off]);
       }
-      if (w2 > 1.17549435e-38f) v = __fdiv_rn(v, w2);
+      if (w2 > 1.17549435e-38f) v = (v / w2);
     }
     y[(int64_t)b * y_stride + s] = v;
   }
@@ -459,7 +464,7 @@ __global__ void spec_mul_kernel(const float *__restrict__ S, const float2 *__res
        i += (int64_t)gridDim.x * blockDim.x) {
     const float s = S[i];
     const float2 a = A[i];
-    X[i] = make_float2(__fmul_rn(s, a.x), __fmul_rn(s, a.y));
+    X[i] = make_float2((s * a.x), (s * a.y));
   }
 }
 }  // namespace

@@ -1,0 +1,305 @@
+// FastPitch transformer pieces (models/fast_pitch.py) on gfx950: token embedding +
+// positional encoding (PositionalEncoding :16-33), LayerNorm (FFTBlock norm1/norm2,
+// ForwardTransformer.norm), and fused multi-head self-attention (FFTBlock.self_attn =
+// nn.MultiheadAttention, math path: softmax(q/sqrt(E) k^T + key_padding_mask) v) as one
+// flash-style kernel on fp32 MFMA (v_mfma_f32_16x16x4_f32: products exact in fp32, only
+// the summation order differs from the reference's bmm).  The projections (in_proj,
+// out_proj, conv1 k9, conv2 k1) run on the GEMM family (gemm.hip).
+#include "common.h"
+
+// hipcc contracts a*b+c into FMA by default (-ffp-contract=fast; the __fmul_rn family is
+// header-inlined and contracts too): the reference-order float32 roundings below need
+// every multiply and add rounded on its own.
+#pragma clang fp contract(off)
+
+namespace {
+
+// ---------------------------------------------------------------- embedding + posenc
+// out[b,t,:] = table[ids[b,t], :] + scale * pe[t, :]   (float32 mul, then add: torch order)
+__global__ void embed_posenc_kernel(const int64_t *__restrict__ ids, int T, int64_t n,
+                                    const float *__restrict__ table, int64_t rows, int dim,
+                                    const float *__restrict__ pe, const float *__restrict__ scale,
+                                    float *__restrict__ out, int32_t *err) {
+  const float s = *scale;
+  const int64_t total = n * dim;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / dim;
+    const int c = (int)(i - r * dim);
+    const int t = (int)(r % T);
+    const int64_t id = ids[r];
+    float v = 0.f;
+    if (id < 0 || id >= rows) {
+      if (err) atomicOr(err, 1);
+    } else {
+      v = table[id * dim + c];
+    }
+    out[i] = v + s * pe[(int64_t)t * dim + c];
+  }
+}
+
+// LengthRegulator expansion fused with the postnet's positional encoding:
+// y[b,t,:] = (index[b,t] >= 0 ? x[b,index[b,t],:] : 0) + scale * pe[t,:]
+__global__ void lr_posenc_kernel(const float *__restrict__ x, int64_t xs, int T, int C,
+                                 const int32_t *__restrict__ index, int T_mel, int64_t n,
+                                 const float *__restrict__ pe, const float *__restrict__ scale,
+                                 float *__restrict__ y, int64_t ys) {
+  const float s = *scale;
+  const int64_t total = n * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / C;
+    const int c = (int)(i - r * C);
+    const int b = (int)(r / T_mel), t = (int)(r - (int64_t)b * T_mel);
+    const int src = index[r];
+    const float v = src >= 0 ? x[((int64_t)b * T + src) * xs + c] : 0.f;
+    y[r * ys + c] = v + s * pe[(int64_t)t * C + c];
+  }
+}
+
+// ---------------------------------------------------------------- LayerNorm
+// one wave per row; mean / variance accumulated in fp64 (biased variance, torch), then
+// y = (x * rstd + (-rstd * mean)) * gamma + beta with the reference kernel's rounding order
+template <int VPL>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict__ x, int64_t xs,
+                                                        int64_t M, int C, const float *__restrict__ g,
+                                                        const float *__restrict__ bt, float eps,
+                                                        float *__restrict__ y, int64_t ys) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float *xr = x + row * xs;
+  float v[VPL];
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < C ? xr[c] : 0.f;
+    s += v[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const double mean = s / C;
+  double q = 0.0;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    const double d = (double)v[j] - mean;
+    if (c < C) q += d * d;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = (float)(1.0 / sqrt(q / C + (double)eps));
+  const float meanf = (float)mean;
+  const float bias = -(rstd * meanf);
+  float *yr = y + row * ys;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < C) yr[c] = (v[j] * rstd + bias) * g[c] + bt[c];
+  }
+}
+
+// ---------------------------------------------------------------- attention
+// grid (ceil(T/64), B*H), 256 threads: wave w owns query rows tile*64 + 16w .. +16.
+// Key / value tiles of 32 keys are staged in LDS (fp32) and shared by the 4 waves;
+// online softmax in registers (MFMA C layout: lane holds rows 4(lane>>4)+i, col lane&15).
+constexpr int AT_KT = 32;
+
+template <int HD>
+__global__ __launch_bounds__(256) void attention_kernel(const float *__restrict__ qkv, int64_t rs,
+                                                        int B, int T, int H, int q_off, int k_off,
+                                                        int v_off, const uint8_t *__restrict__ kpm,
+                                                        float qscale, float *__restrict__ out,
+                                                        int64_t os) {
+  constexpr int KS = HD + 2;   // K row stride (floats): b32 B-operand reads conflict-free
+  constexpr int VS = HD + 16;  // V row stride
+  constexpr int PS = AT_KT + 2;
+  constexpr int NT = HD / 16;  // output column tiles
+  __shared__ float Ks[AT_KT * KS];
+  __shared__ float Vs[AT_KT * VS];
+  __shared__ float Ps[4][16 * PS];
+
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh - b * H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int q0 = blockIdx.x * 64 + wave * 16;
+  const float *base = qkv + (int64_t)b * T * rs;
+
+  // A-operand fragments of this wave's 16 query rows, pre-scaled like the reference
+  float qa[HD / 4];
+  {
+    const int qr = q0 + c16;
+    const float *src = base + (int64_t)(qr < T ? qr : 0) * rs + q_off + h * HD;
+#pragma unroll
+    for (int ks = 0; ks < HD / 4; ++ks) qa[ks] = qr < T ? (src[4 * ks + g] * qscale) : 0.f;
+  }
+  f32x4 o[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    m[i] = -INFINITY;
+    l[i] = 0.f;
+  }
+
+  for (int k0 = 0; k0 < T; k0 += AT_KT) {
+    __syncthreads();
+    // stage K and V rows k0 .. k0+31 (zero past T)
+    for (int e = threadIdx.x; e < AT_KT * HD / 4; e += 256) {
+      const int r = e / (HD / 4), c4 = (e - r * (HD / 4)) * 4;
+      const int key = k0 + r;
+      f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+      if (key < T) {
+        const float *row = base + (int64_t)key * rs + h * HD + c4;
+        kv = *(const f32x4 *)(row + k_off);
+        vv = *(const f32x4 *)(row + v_off);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        Ks[r * KS + c4 + j] = kv[j];
+        Vs[r * VS + c4 + j] = vv[j];
+      }
+    }
+    __syncthreads();
+    // S = (q c) K^T for 16 rows x 32 keys
+    f32x4 s[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < HD / 4; ++ks)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[ks], Ks[(n * 16 + c16) * KS + 4 * ks + g], acc,
+                                                   0, 0, 0);
+      s[n] = acc;
+    }
+    // mask: keys past T or flagged in key_padding_mask -> -inf (baddbmm with the float mask)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int key = k0 + n * 16 + c16;
+      const bool dead = key >= T || (kpm && kpm[(int64_t)b * T + key]);
+      if (dead)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[n][i] = -INFINITY;
+    }
+    // online softmax per row (rows 4g+i; the 16 lanes of group g hold its columns)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float mx = fmaxf(s[0][i], s[1][i]);
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+      const float mn = fmaxf(m[i], mx);
+      const float alpha = mn == -INFINITY ? 1.f : expf(m[i] - mn);
+      float ps = 0.f;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const float pv = mn == -INFINITY ? 0.f : expf(s[n][i] - mn);
+        s[n][i] = pv;
+        ps += pv;
+      }
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) ps += __shfl_xor(ps, off);
+      l[i] = l[i] * alpha + ps;
+      m[i] = mn;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) o[n][i] *= alpha;
+    }
+    // P (C layout) -> LDS -> A layout
+    float *P = Ps[wave];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) P[(4 * g + i) * PS + n * 16 + c16] = s[n][i];
+    __syncthreads();
+    // O += P V
+#pragma unroll
+    for (int ks = 0; ks < AT_KT / 4; ++ks) {
+      const float pa = P[c16 * PS + 4 * ks + g];
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+        o[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa, Vs[(4 * ks + g) * VS + n * 16 + c16], o[n],
+                                                    0, 0, 0);
+    }
+  }
+  // normalise and store
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int qr = q0 + 4 * g + i;
+    if (qr >= T) continue;
+    float *dst = out + ((int64_t)b * T + qr) * os + h * HD;
+    const float inv = l[i];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) dst[n * 16 + c16] = o[n][i] / inv;
+  }
+}
+
+}  // namespace
+
+extern "C" int ftmi_embedding_posenc(const int64_t *ids, int32_t B, int32_t T, const float *table,
+                                     int64_t rows, int32_t dim, const float *pe,
+                                     const float *scale, float *out, int32_t *err,
+                                     ftmi_stream_t stream) {
+  if (!ids || !table || !pe || !scale || !out || B <= 0 || T <= 0 || dim <= 0) return FTMI_E_ARG;
+  const int64_t n = (int64_t)B * T;
+  const int64_t total = n * dim;
+  const int64_t blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(embed_posenc_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                     ftmi_hs(stream), ids, T, n, table, rows, dim, pe, scale, out, err);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_lr_posenc(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t C,
+                              const int32_t *index, int32_t T_mel, const float *pe,
+                              const float *scale, float *y, int64_t y_stride, ftmi_stream_t stream) {
+  if (!x || !index || !pe || !scale || !y || B <= 0 || T <= 0 || C <= 0 || T_mel < 0) return FTMI_E_ARG;
+  const int64_t n = (int64_t)B * T_mel;
+  if (n == 0) return FTMI_OK;
+  const int64_t blocks = (n * C + 255) / 256;
+  hipLaunchKernelGGL(lr_posenc_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                     ftmi_hs(stream), x, x_stride, T, C, index, T_mel, n, pe, scale, y, y_stride);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_layernorm(const float *x, int64_t x_stride, int64_t M, int32_t C,
+                              const float *gamma, const float *beta, float eps, float *y,
+                              int64_t y_stride, ftmi_stream_t stream) {
+  if (!x || !gamma || !beta || !y || M <= 0 || C <= 0) return FTMI_E_ARG;
+  if (C > 64 * 16) return FTMI_E_SHAPE;
+  const dim3 grid((unsigned)((M + 3) / 4)), block(256);
+  const hipStream_t s = ftmi_hs(stream);
+  const int vpl = (C + 63) / 64;
+  if (vpl <= 2)
+    hipLaunchKernelGGL(layernorm_kernel<2>, grid, block, 0, s, x, x_stride, M, C, gamma, beta, eps, y, y_stride);
+  else if (vpl <= 4)
+    hipLaunchKernelGGL(layernorm_kernel<4>, grid, block, 0, s, x, x_stride, M, C, gamma, beta, eps, y, y_stride);
+  else if (vpl <= 8)
+    hipLaunchKernelGGL(layernorm_kernel<8>, grid, block, 0, s, x, x_stride, M, C, gamma, beta, eps, y, y_stride);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<16>, grid, block, 0, s, x, x_stride, M, C, gamma, beta, eps, y, y_stride);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, int32_t T,
+                              int32_t H, int32_t head_dim, int32_t q_off, int32_t k_off,
+                              int32_t v_off, const uint8_t *key_padding_mask, float qscale,
+                              float *out, int64_t out_stride, ftmi_stream_t stream) {
+  if (!qkv || !out || B <= 0 || T <= 0 || H <= 0) return FTMI_E_ARG;
+  if (head_dim != 64 && head_dim != 128) return FTMI_E_UNSUPPORTED;
+  if (!ftmi_aligned16(qkv) || (row_stride & 3) || (q_off & 3) || (k_off & 3) || (v_off & 3))
+    return FTMI_E_ALIGN;
+  const dim3 grid((unsigned)((T + 63) / 64), (unsigned)(B * H)), block(256);
+  const hipStream_t s = ftmi_hs(stream);
+  if (head_dim == 64)
+    hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, s, qkv, row_stride, B, T, H, q_off, k_off,
+                       v_off, key_padding_mask, qscale, out, out_stride);
+  else
+    hipLaunchKernelGGL(attention_kernel<128>, grid, block, 0, s, qkv, row_stride, B, T, H, q_off, k_off,
+                       v_off, key_padding_mask, qscale, out, out_stride);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}

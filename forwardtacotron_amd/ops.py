@@ -11,6 +11,7 @@ import ctypes
 import os
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -290,4 +291,64 @@ def rowdot(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], alpha
     launch('ftmi_rowdot', f'rowdot[M={B * T},C={C}]', 2.0 * B * T * C, 4.0 * (B * T * (C + 1) + C),
            x.data_ptr(), xs, B * T, C, w.data_ptr(), _ptr(bias), float(alpha),
            out.data_ptr(), _stream())
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# FastPitch transformer (csrc/transformer.hip)
+
+def embedding_posenc(ids: torch.Tensor, table: torch.Tensor, pe: torch.Tensor,
+                     scale: torch.Tensor) -> torch.Tensor:
+    """(B, T) ids -> table[ids] + scale * pe[:T]  (B, T, dim)."""
+    _dev(ids, table, pe, scale)
+    B, T = ids.shape
+    dim = table.size(1)
+    ids = ids.contiguous().to(torch.int64)
+    out = torch.empty(B, T, dim, device=ids.device, dtype=_f32)
+    launch('ftmi_embedding_posenc', f'embedding_posenc[n={B * T},d={dim}]', B * T * dim * 2.0,
+           8.0 * B * T + 12.0 * B * T * dim,
+           ids.data_ptr(), B, T, table.data_ptr(), table.size(0), dim, pe.data_ptr(),
+           scale.data_ptr(), out.data_ptr(), None, _stream())
+    return out
+
+
+def lr_posenc(x: torch.Tensor, index: torch.Tensor, pe: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """LengthRegulator expansion (index map) + scale * pe[:T_mel]: (B, T_mel, C)."""
+    _dev(x, index, pe, scale)
+    B, T, C, xs = _rows(x)
+    T_mel = index.size(1)
+    y = torch.empty(B, T_mel, C, device=x.device, dtype=_f32)
+    launch('ftmi_lr_posenc', f'lr_posenc[B={B},T_mel={T_mel},C={C}]', 2.0 * B * T_mel * C,
+           4.0 * (B * T * C + B * T_mel * (2 * C + 1)),
+           x.data_ptr(), xs, B, T, C, index.data_ptr(), T_mel, pe.data_ptr(), scale.data_ptr(),
+           y.data_ptr(), y.stride(1), _stream())
+    return y
+
+
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(x, gamma, beta, out)
+    B, T, C, xs = _rows(x)
+    y = out if out is not None else torch.empty(B, T, C, device=x.device, dtype=_f32)
+    launch('ftmi_layernorm', f'layernorm[M={B * T},C={C}]', 8.0 * B * T * C, 8.0 * B * T * C,
+           x.data_ptr(), xs, B * T, C, gamma.data_ptr(), beta.data_ptr(), float(eps),
+           y.data_ptr(), y.stride(1), _stream())
+    return y
+
+
+def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Self-attention core of nn.MultiheadAttention on packed in_proj rows (B, T, 3d)."""
+    _dev(qkv, key_padding_mask)
+    B, T, C3, rs = _rows(qkv)
+    d = C3 // 3
+    hd = d // heads
+    out = torch.empty(B, T, d, device=qkv.device, dtype=_f32)
+    kpm = None
+    if key_padding_mask is not None:
+        kpm = key_padding_mask.to(torch.uint8).contiguous()
+    qscale = float(np.float32(np.sqrt(1.0 / hd)))
+    launch('ftmi_attention', f'attention[B={B},T={T},H={heads},hd={hd}]', 4.0 * B * heads * T * T * hd,
+           4.0 * (B * T * C3 + B * T * d),
+           qkv.data_ptr(), rs, B, T, heads, hd, 0, d, 2 * d, _ptr(kpm), qscale,
+           out.data_ptr(), out.stride(1), _stream())
     return out

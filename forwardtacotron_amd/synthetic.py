@@ -13,6 +13,11 @@ tests/golden/ only store inputs / outputs, never the weights.
                                LJSpeech; random init would give dur ~0.2 and the fill-2 rule)
   lin / post_proj              weight x MEL_GAIN / POST_GAIN  (mean |mel|, |mel_post| ~ 5,
                                log-mel magnitudes, so the 1e-4 parity bound is meaningful)
+
+FastPitch (model='fast_pitch'): LayerNorm gamma ~ U(0.75, 1.25), beta ~ N(0, 0.1);
+pos_encoder.scale ~ U(0.9, 1.1); pos_encoder.pe is the model's own sinusoid buffer (not
+drawn); dur_pred.lin weight x FP_DUR_GAIN, bias = FP_DUR_BIAS (~6.5 frames / phoneme);
+lin.weight x FP_MEL_GAIN (the transformer output is LayerNorm-ed, O(1) per channel).
 """
 from __future__ import annotations
 
@@ -26,6 +31,9 @@ DUR_BIAS = 9.0
 DUR_GAIN = 5.0
 MEL_GAIN = 30.0
 POST_GAIN = 6.0
+FP_DUR_BIAS = 6.0
+FP_DUR_GAIN = 1.5
+FP_MEL_GAIN = 4.0
 
 # forward_tacotron.model and dsp sections of the reference config.yaml (:9-34, :76-106)
 DEFAULT_CONFIG = {
@@ -51,6 +59,20 @@ DEFAULT_CONFIG = {
 }
 
 
+# fast_pitch.model section of the reference config.yaml (:128-163)
+DEFAULT_CONFIG['fast_pitch'] = {'model': {
+    'durpred_d_model': 128, 'durpred_n_heads': 2, 'durpred_layers': 4, 'durpred_d_fft': 128,
+    'durpred_dropout': 0.5,
+    'pitch_d_model': 128, 'pitch_n_heads': 2, 'pitch_layers': 4, 'pitch_d_fft': 128,
+    'pitch_dropout': 0.5, 'pitch_strength': 1.0,
+    'energy_d_model': 128, 'energy_n_heads': 2, 'energy_layers': 4, 'energy_d_fft': 128,
+    'energy_dropout': 0.5, 'energy_strength': 1.0,
+    'd_model': 256, 'conv1_kernel': 9, 'conv2_kernel': 1,
+    'prenet_layers': 4, 'prenet_heads': 2, 'prenet_fft': 1024, 'prenet_dropout': 0.1,
+    'postnet_layers': 4, 'postnet_heads': 2, 'postnet_fft': 1024, 'postnet_dropout': 0.1,
+}}
+
+
 def default_config() -> dict:
     return copy.deepcopy(DEFAULT_CONFIG)
 
@@ -59,25 +81,36 @@ def _rng(seed: int, key: str) -> np.random.Generator:
     return np.random.Generator(np.random.PCG64([seed, zlib.crc32(key.encode())]))
 
 
-def synthetic_array(key: str, shape, dtype: str, seed: int = 0) -> np.ndarray:
+def synthetic_array(key: str, shape, dtype: str, seed: int = 0,
+                    model: str = 'forward_tacotron') -> np.ndarray:
     """The value of one state_dict entry under the recipe above."""
     rng = _rng(seed, key)
     leaf = key.rsplit('.', 1)[-1]
     shape = tuple(shape)
     if dtype.startswith('int'):
         return np.zeros(shape, dtype=np.int64)
+    if model == 'fast_pitch':
+        parent = key.rsplit('.', 2)[-2] if key.count('.') >= 1 else ''
+        if parent.startswith('norm'):
+            a = rng.uniform(0.75, 1.25, shape) if leaf == 'weight' else rng.normal(0.0, 0.1, shape)
+            return a.astype(np.float32)
+        if leaf == 'scale':
+            return rng.uniform(0.9, 1.1, shape).astype(np.float32)
+        if key == 'dur_pred.lin.bias':
+            return np.full(shape, FP_DUR_BIAS, dtype=np.float32)
+        a = _generic(rng, key, leaf, shape)
+        if key == 'dur_pred.lin.weight':
+            a = a * FP_DUR_GAIN
+        elif key == 'lin.weight':
+            a = a * FP_MEL_GAIN
+        return a.astype(np.float32)
     if '.bnorm.' in key:
         if leaf in ('weight', 'running_var'):
             a = rng.uniform(0.75, 1.25, shape)
         else:
             a = rng.normal(0.0, 0.1, shape)
-    elif 'embedding' in key:
-        a = rng.normal(0.0, 1.0, shape)
-    elif leaf.startswith('bias'):
-        a = rng.normal(0.0, 0.1, shape)
     else:
-        fan_in = int(np.prod(shape[1:])) if len(shape) > 1 else 1
-        a = rng.normal(0.0, 1.0 / np.sqrt(fan_in), shape)
+        a = _generic(rng, key, leaf, shape)
     if key == 'dur_pred.lin.weight':
         a = a * DUR_GAIN
     elif key == 'dur_pred.lin.bias':
@@ -89,20 +122,33 @@ def synthetic_array(key: str, shape, dtype: str, seed: int = 0) -> np.ndarray:
     return a.astype(np.float32)
 
 
-def synthetic_state_dict(template, seed: int = 0) -> Dict[str, np.ndarray]:
-    """template: a model (anything with state_dict()) or {key: tensor/array}."""
+def _generic(rng, key, leaf, shape):
+    if 'embedding' in key:
+        return rng.normal(0.0, 1.0, shape)
+    if leaf.startswith('bias') or leaf.endswith('_bias'):
+        return rng.normal(0.0, 0.1, shape)
+    fan_in = int(np.prod(shape[1:])) if len(shape) > 1 else 1
+    return rng.normal(0.0, 1.0 / np.sqrt(fan_in), shape)
+
+
+def synthetic_state_dict(template, seed: int = 0, model: str = 'forward_tacotron') -> Dict[str, np.ndarray]:
+    """template: a model (anything with state_dict()) or {key: tensor/array}.  Buffers that
+    are deterministic functions of the architecture (FastPitch's `pe`) are kept."""
     sd = template.state_dict() if hasattr(template, 'state_dict') else template
     out = {}
     for k, v in sd.items():
+        if k.endswith('pos_encoder.pe'):
+            out[k] = np.asarray(v.detach().cpu().numpy() if hasattr(v, 'detach') else v)
+            continue
         dt = str(v.dtype).replace('torch.', '')
-        out[k] = synthetic_array(k, tuple(v.shape), dt, seed)
+        out[k] = synthetic_array(k, tuple(v.shape), dt, seed, model)
     return out
 
 
-def load_synthetic(model, seed: int = 0):
+def load_synthetic(model, seed: int = 0, kind: str = 'forward_tacotron'):
     """Fill a (reference-compatible) model with the synthetic recipe in place; returns it."""
     import torch
-    sd = synthetic_state_dict(model, seed)
+    sd = synthetic_state_dict(model, seed, kind)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     return model
 

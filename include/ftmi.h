@@ -267,6 +267,41 @@ int ftmi_mel_nnls(const float *mel, int32_t B, int32_t F, const int32_t *frames,
                   const float *bin_w, const float *pinv, float inv_L, int32_t iters, float *S,
                   ftmi_stream_t stream);
 
+/* ====================================================================================
+ * FastPitch transformer (models/fast_pitch.py).  Activations channels-last (B, T, C).
+ * ==================================================================================== */
+
+/* nn.Embedding + PositionalEncoding (fast_pitch.py:16-33, eval: dropout is identity):
+ * out[b,t,:] = table[ids[b,t],:] + scale[0] * pe[t,:] (float32 multiply, then add).
+ * pe: [T_max][dim] rows (the reference buffer (max_len, 1, dim)); scale: device float[1]. */
+int ftmi_embedding_posenc(const int64_t *ids, int32_t B, int32_t T, const float *table,
+                          int64_t rows, int32_t dim, const float *pe, const float *scale,
+                          float *out, int32_t *err, ftmi_stream_t stream);
+
+/* LengthRegulator (common_layers.py:12-19) fused with the postnet's PositionalEncoding:
+ * y[b,t,:] = (index[b,t] >= 0 ? x[b,index[b,t],:] : 0) + scale[0] * pe[t,:].
+ * x: (B, T, C) rows; index: (B, T_mel) from ftmi_lr_index; y: (B, T_mel, C) rows. */
+int ftmi_lr_posenc(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t C,
+                   const int32_t *index, int32_t T_mel, const float *pe, const float *scale,
+                   float *y, int64_t y_stride, ftmi_stream_t stream);
+
+/* nn.LayerNorm(C) over rows (FFTBlock.norm1/norm2 :64-65, ForwardTransformer.norm :112):
+ * biased variance, y = (x*rstd - rstd*mean)*gamma + beta.  C <= 1024; y may alias x. */
+int ftmi_layernorm(const float *x, int64_t x_stride, int64_t M, int32_t C, const float *gamma,
+                   const float *beta, float eps, float *y, int64_t y_stride, ftmi_stream_t stream);
+
+/* nn.MultiheadAttention self-attention core (FFTBlock.forward :76-79; torch
+ * multi_head_attention_forward math path): per batch b and head h,
+ *   O = softmax((Q * qscale) K^T + mask) V,  Q/K/V = qkv[b, :, off + h*head_dim ...]
+ * from the packed in_proj output rows (row stride row_stride floats; q/k/v column
+ * offsets q_off/k_off/v_off).  key_padding_mask: (B, T) bytes, nonzero = padded key
+ * (-inf), or NULL.  qscale = float32(sqrt(1/head_dim)).  out: (B, T, H*head_dim) rows of
+ * stride out_stride.  head_dim in {64, 128}. */
+int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, int32_t T, int32_t H,
+                   int32_t head_dim, int32_t q_off, int32_t k_off, int32_t v_off,
+                   const uint8_t *key_padding_mask, float qscale, float *out, int64_t out_stride,
+                   ftmi_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
