@@ -3,7 +3,7 @@
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
 
-Workload (BASELINE.json configs[2], "c3"): ForwardTacotron LJSpeech config, batch = 64
+Workload (BASELINE.json configs[2], "c3"; --model fast_pitch: configs[4], "c5"): ForwardTacotron LJSpeech config, batch = 64
 synthetic phoneme sequences per GPU (lengths U{50..200}, ids U{1..134}, pad 0; seed =
 rank), synthetic weights (forwardtacotron_amd.synthetic, no checkpoint download), fp32.
 A step is one full `generate()` call on one batch whose tokens are already resident in HBM
@@ -17,7 +17,9 @@ max elapsed over ranks, value = all frames of all ranks / that time.
 The JSON line also carries
   roofline     the dominant kernel (largest device time inside the timed steps, measured
                with HIP events on the launch stream): algorithmic FLOPs (or bytes) per launch
-               / its average duration, against the fp32 MFMA (or HBM) peak of MI355X;
+               / its average duration, against the peak of the arithmetic that kernel
+               issues: bf16 MFMA / 6 for the fp32-accurate bf16x6 path (labels mma=1),
+               the fp32 MFMA peak otherwise, or HBM bandwidth for byte-bound kernels;
   cpu_baseline rank 0, N = 1: the torch-CPU restatement of the reference (oracle/
                ft_torch_cpu.py, same ATen CPU kernels as the reference) on the same batch;
   parity       mean / max |mel_post GPU - CPU| on that batch, and LR counts equality.
@@ -37,11 +39,16 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from forwardtacotron_amd.fast_pitch import FastPitch  # noqa: E402
 from forwardtacotron_amd.forward_tacotron import ForwardTacotron  # noqa: E402
 from forwardtacotron_amd.probe import KernelProbe  # noqa: E402
 from forwardtacotron_amd.synthetic import default_config, synthetic_state_dict, synthetic_tokens  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA == vector rate), MI355X_MICROARCH.md
+# the fp32-accurate bf16x6 path (labels "mma=1") issues 6 bf16 MFMAs per fp32 product:
+# its ceiling is the dense bf16 MFMA peak / 6
+PEAK_BF16_TFLOPS = 2500.0
+PEAK_X6_TFLOPS = PEAK_BF16_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 
@@ -59,6 +66,8 @@ def main():
     ap.add_argument('--tmin', type=int, default=50)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--kernels', action='store_true', help='print the per-kernel table to stderr')
+    ap.add_argument('--model', choices=['forward_tacotron', 'fast_pitch'], default='forward_tacotron',
+                    help='fast_pitch = BASELINE.json configs[4] (c5)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -69,8 +78,9 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
 
-    model = ForwardTacotron.from_config(default_config())
-    sd = synthetic_state_dict(model, seed=0)
+    cls = FastPitch if args.model == 'fast_pitch' else ForwardTacotron
+    model = cls.from_config(default_config())
+    sd = synthetic_state_dict(model, seed=0, model=args.model)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     model = model.to(dev).eval()
     x_np = synthetic_tokens(args.batch, args.tmax, seed=rank, min_len=args.tmin)
@@ -119,9 +129,13 @@ def main():
         s = dom['avg_ms'] / 1e3
         if dom['flops'] > 0:
             achieved = dom['flops'] / s / 1e12
+            x6 = 'mma=1' in dom_label
+            peak = PEAK_X6_TFLOPS if x6 else PEAK_FP32_TFLOPS
             roof = {'kernel': dom_label, 'bound': 'mfma', 'achieved': round(achieved, 3),
-                    'peak': PEAK_FP32_TFLOPS, 'unit': 'TFLOP/s',
-                    'frac': round(achieved / PEAK_FP32_TFLOPS, 4),
+                    'peak': round(peak, 1), 'unit': 'TFLOP/s',
+                    'peak_basis': ('bf16 dense MFMA 2.5 PF / 6 (fp32-accurate bf16x6 split: 6 bf16 '
+                                   'products per fp32 product)') if x6 else 'fp32 dense MFMA',
+                    'frac': round(achieved / peak, 4),
                     'algorithmic_per_launch': dom['flops'], 'avg_launch_ms': round(dom['avg_ms'], 4),
                     'launches': dom['launches'], 'share_of_device_time': round(dom['total_ms'] / total_dev_ms, 4),
                     'traffic': None}
@@ -133,29 +147,36 @@ def main():
                     'launches': dom['launches'], 'traffic': None}
 
         value = frames / elapsed
+        fp = args.model == 'fast_pitch'
         line = {
-            'metric': 'mel-frames/sec at batch=64 LJSpeech shapes (ForwardTacotron.generate, B*T_mel per s)',
+            'metric': 'mel-frames/sec at batch=64 LJSpeech shapes (%s.generate, B*T_mel per s)'
+                      % ('FastPitch' if fp else 'ForwardTacotron'),
             'value': round(value, 1), 'unit': 'mel-frames/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
             'data': 'synthetic (seeded LJSpeech-shaped phoneme batches, synthetic weights)',
-            'config': {'workload': f'c3: ForwardTacotron generate, batch={args.batch} per GPU, '
+            'config': {'workload': f'{"c5: FastPitch" if fp else "c3: ForwardTacotron"} generate, '
+                                   f'batch={args.batch} per GPU, '
                                    f'phoneme lengths U{{{args.tmin}..{args.tmax}}}',
                        'global_batch': args.batch * world, 'T_phonemes': int(x_np.shape[1]),
                        'T_mel': int(out['mel_post'].size(2)), 'parallelism': f'dp{world}'},
             'roofline': roof,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line['cpu_baseline'], line['parity'] = cpu_baseline(sd, x_np, out)
+            line['cpu_baseline'], line['parity'] = cpu_baseline(sd, x_np, out, args.model)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(sd, x_np, out):
+def cpu_baseline(sd, x_np, out, kind='forward_tacotron'):
     """Time the torch-CPU restatement of the reference on the same batch (bounded: one call)."""
-    from oracle import ft_oracle, ft_torch_cpu
+    from oracle import ft_oracle
+    if kind == 'fast_pitch':
+        from oracle import fp_torch_cpu as ft_torch_cpu
+    else:
+        from oracle import ft_torch_cpu
     sdt = ft_torch_cpu.to_torch(sd)
     xt = torch.from_numpy(x_np)
     ft_torch_cpu.generate(sdt, xt[:1, :20])  # warm the CPU kernels
@@ -172,8 +193,8 @@ def cpu_baseline(sd, x_np, out):
     base = {'value': round(frames / dt, 1), 'unit': 'mel-frames/s', 'cores': torch.get_num_threads(),
             'kind': 'port',
             'sample': f'one generate() of the same batch ({x_np.shape[0]} x {x_np.shape[1]} phonemes, '
-                      f'T_mel {r.shape[2]}) with oracle/ft_torch_cpu.py (the reference\'s ATen CPU '
-                      f'kernels), {dt:.2f} s'}
+                      f'T_mel {r.shape[2]}) with oracle/{ft_torch_cpu.__name__.split(".")[-1]}.py '
+                      f'(the reference\'s ATen CPU kernels), {dt:.2f} s'}
     parity = {'mel_post_mean_abs': float(d.mean()) if same_shape else None,
               'mel_post_max_abs': float(d.max()) if same_shape else None,
               'lr_counts_equal': counts_equal}

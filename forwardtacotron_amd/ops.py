@@ -23,6 +23,8 @@ _f32 = torch.float32
 # Matrix path of the dense contractions (include/ftmi.h FTMI_MMA_*): 1 = bf16x6 split
 # (fp32-accurate, 2.7x the fp32 MFMA rate), 0 = plain fp32 MFMA.  FTMI_MMA=0/1 overrides.
 MMA = int(os.environ.get('FTMI_MMA', '1'))
+# the recurrences' matrix path (read by rnn.hip itself; mirrored here for the labels)
+RNN_MMA = int(os.environ.get('FTMI_RNN_MMA', '1'))
 
 
 def _num_cus() -> int:
@@ -217,7 +219,7 @@ def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Opt
     if index is not None:
         assert index.dtype == torch.int32 and index.is_contiguous() and index.shape == (B, T)
     G = 4 if cell else 3
-    label = f'rnn_bidir[{"lstm" if cell else "gru"},B={B},T={T},H={H}]'
+    label = f'rnn_bidir[{"lstm" if cell else "gru"},B={B},T={T},H={H},mma={RNN_MMA}]'
     # recurrent contraction W_hh h per step and direction; bytes: xp rows read per frame,
     # W_hh once, y written once
     launch('ftmi_rnn_bidir', label, 2.0 * B * T * 2 * G * H * H,

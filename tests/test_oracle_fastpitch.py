@@ -54,3 +54,13 @@ def test_forward(fp_sd):
     assert np.abs(o['mel'] - g['mel']).max() < 2e-4
     np.testing.assert_allclose(o['dur'], g['dur'], atol=2e-5)
     np.testing.assert_allclose(o['pitch'], g['pitch'], atol=2e-5)
+
+
+@pytest.mark.parametrize('name', ['fp_gen_b3', 'fp_gen_alpha', 'fp_gen_fill2'])
+def test_torch_cpu_restatement(name, fp_sd):
+    import torch
+    from oracle import fp_torch_cpu as TC
+    g = load_golden(name)
+    o = TC.generate(TC.to_torch(fp_sd), torch.from_numpy(g['x']), alpha=CASES[name]['alpha'])
+    assert np.abs(o['mel'].numpy() - g['mel']).max() < 2e-4
+    np.testing.assert_array_equal(FP.duration_counts(o['dur'].numpy()), FP.duration_counts(g['dur']))
