@@ -52,6 +52,34 @@ PEAK_X6_TFLOPS = PEAK_BF16_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 
+PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r1_pmc_traffic.json')
+
+
+def rocprof_name(label: str):
+    """rocprof kernel-name prefix of a probe label (for the PMC traffic lookup)."""
+    if label.startswith('rnn_bidir['):
+        cell = 1 if label.startswith('rnn_bidir[lstm') else 0
+        H = int(label.split('H=')[1].split(',')[0].rstrip(']'))
+        return f'rnn_bidir_kernel<{cell}, {H},'
+    return None
+
+
+def pmc_traffic(label: str):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes
+    (tools/profile_round.sh + tools/summarize_prof.py: FETCH_SIZE x 2 + WRITE_SIZE), or None."""
+    pref = rocprof_name(label)
+    if pref is None or not os.path.exists(PMC_PROFILE):
+        return None
+    ks = json.load(open(PMC_PROFILE))['kernels']
+    hit = [v for k, v in ks.items() if k.startswith(pref)]
+    if len(hit) != 1:
+        return None
+    return {'bytes_per_launch': hit[0]['hbm_bytes_per_launch'],
+            'read_bytes_corrected': hit[0]['read_bytes_corrected'],
+            'write_bytes': hit[0]['write_bytes'],
+            'source': os.path.relpath(PMC_PROFILE, ROOT)}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -139,6 +167,10 @@ def main():
                     'algorithmic_per_launch': dom['flops'], 'avg_launch_ms': round(dom['avg_ms'], 4),
                     'launches': dom['launches'], 'share_of_device_time': round(dom['total_ms'] / total_dev_ms, 4),
                     'traffic': None}
+            tr = pmc_traffic(dom_label)
+            if tr is not None:
+                roof['traffic'] = tr['bytes_per_launch']
+                roof['traffic_detail'] = tr
         else:
             achieved = dom['bytes'] / s / 1e9
             roof = {'kernel': dom_label, 'bound': 'hbm', 'achieved': round(achieved, 1),

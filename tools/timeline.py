@@ -8,7 +8,7 @@ rows = list(csv.DictReader(open(path)))
 for r in rows:
     r['s'] = int(r['Start_Timestamp']); r['e'] = int(r['End_Timestamp'])
 rows.sort(key=lambda r: r['s'])
-name = lambda r: r['Kernel_Name'].split('(')[0].replace('(anonymous namespace)::', '')[:60]
+name = lambda r: r['Kernel_Name'].replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0][:70]
 # steps: the LSTM kernel marks each generate(); take the window between the last two
 marks = [i for i, r in enumerate(rows) if 'rnn_bidir_kernel<1' in r['Kernel_Name']]
 if len(marks) >= 2:
