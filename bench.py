@@ -10,9 +10,12 @@ A step is one full `generate()` call on one batch whose tokens are already resid
 (pitch / energy identity callbacks, alpha = 1).  Frames = B * T_mel of the returned
 mel_post (padded frames, as the reference returns them).
 
-Multi-GPU: each rank runs its own batch of 64 utterances (weak scaling, no data-path
-collective: utterances are independent); barrier + synchronize around the K timed steps,
-max elapsed over ranks, value = all frames of all ranks / that time.
+Multi-GPU (c4, BASELINE.json configs[3]): the ranks hold the shards (64 utterances each,
+seed = rank) of ONE global batch and run forwardtacotron_amd.sharded.generate_sharded:
+global phoneme padding, the batch-global fill-2 rule and T_mel by scalar RCCL all-reduces,
+the mel_post all-gathered to every rank — the reference's output for the global batch
+(weak scaling: per-GPU work fixed).  Barrier + synchronize around the K timed steps, max
+elapsed over ranks, value = frames of the global mel_post / that time.
 
 The JSON line also carries
   roofline     the dominant kernel (largest device time inside the timed steps, measured
@@ -42,6 +45,7 @@ sys.path.insert(0, ROOT)
 from forwardtacotron_amd.fast_pitch import FastPitch  # noqa: E402
 from forwardtacotron_amd.forward_tacotron import ForwardTacotron  # noqa: E402
 from forwardtacotron_amd.probe import KernelProbe  # noqa: E402
+from forwardtacotron_amd.sharded import generate_sharded  # noqa: E402
 from forwardtacotron_amd.synthetic import default_config, synthetic_state_dict, synthetic_tokens  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA == vector rate), MI355X_MICROARCH.md
@@ -114,8 +118,12 @@ def main():
     x_np = synthetic_tokens(args.batch, args.tmax, seed=rank, min_len=args.tmin)
     x = torch.from_numpy(x_np).to(dev)
 
+    if world > 1:  # c4: one global batch sharded over the ranks (reference-identical result)
+        gen = lambda: generate_sharded(model, x)
+    else:
+        gen = lambda: model.generate(x)
     for _ in range(args.warmup):
-        model.generate(x)
+        gen()
     torch.cuda.synchronize()
 
     def barrier():
@@ -128,7 +136,7 @@ def main():
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            out = model.generate(x)
+            out = gen()  # N > 1: mel_post is already all-gathered (global batch)
             frames += out['mel_post'].size(0) * out['mel_post'].size(2)
         torch.cuda.synchronize()
         barrier()
@@ -140,9 +148,6 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        f = torch.tensor([frames], device=dev, dtype=torch.float64)
-        dist.all_reduce(f, op=dist.ReduceOp.SUM)
-        frames = int(f.item())
 
     if rank == 0:
         # dominant kernel = largest device time inside the timed region
@@ -188,8 +193,12 @@ def main():
             'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
             'data': 'synthetic (seeded LJSpeech-shaped phoneme batches, synthetic weights)',
-            'config': {'workload': f'{"c5: FastPitch" if fp else "c3: ForwardTacotron"} generate, '
-                                   f'batch={args.batch} per GPU, '
+            'config': {'workload': (f'{"c5: FastPitch" if fp else "c3: ForwardTacotron"} generate, '
+                                    if world == 1 else
+                                    f'c4: {"FastPitch" if fp else "ForwardTacotron"} generate of one '
+                                    f'global batch sharded over {world} GPUs (global padding, '
+                                    f'fill rule and T_mel by RCCL all-reduce, mel all-gather), ')
+                                   + f'batch={args.batch} per GPU, '
                                    f'phoneme lengths U{{{args.tmin}..{args.tmax}}}',
                        'global_batch': args.batch * world, 'T_phonemes': int(x_np.shape[1]),
                        'T_mel': int(out['mel_post'].size(2)), 'parallelism': f'dp{world}'},

@@ -51,6 +51,8 @@ SIGNATURES = {
     'ftmi_rnn_bidir': (c_int, [c_int, c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,
                                c_float, P, c_int64, P, P]),
     'ftmi_duration_counts': (c_int, [P, c_int, c_int, c_int, c_float, P, P, P, P]),
+    'ftmi_duration_trunc_sum': (c_int, [P, c_int, c_int, P, P]),
+    'ftmi_duration_counts_global': (c_int, [P, c_int, c_int, P, c_float, P, P, P, P]),
     'ftmi_lr_index': (c_int, [P, c_int, c_int, c_int, P, P]),
     'ftmi_length_regulate': (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, P, c_int64, P]),
     'ftmi_series_proj_add': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, P, c_float, P, P, P,

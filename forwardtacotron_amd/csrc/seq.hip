@@ -29,12 +29,22 @@ __global__ void embedding_kernel(const int64_t *__restrict__ ids, int64_t n,
 __global__ __launch_bounds__(1024) void duration_counts_kernel(float *dur, int B, int T,
                                                                int apply_fill, float fill,
                                                                int32_t *offsets, int32_t *totals,
-                                                               int32_t *fill_flag) {
+                                                               int32_t *fill_flag,
+                                                               const int64_t *ext_sum) {
   __shared__ long long s_part[16];
   __shared__ int s_fill;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t n = (int64_t)B * T;
-  if (apply_fill) {
+  if (apply_fill && ext_sum) {  // batch-global decision (sharded batch): sum over all shards
+    if (tid == 0) {
+      s_fill = *ext_sum <= 0;
+      if (fill_flag) *fill_flag = s_fill;
+    }
+    __syncthreads();
+    if (s_fill)
+      for (int64_t i = tid; i < n; i += 1024) dur[i] = fill;
+    __syncthreads();
+  } else if (apply_fill) {
     long long acc = 0;
     for (int64_t i = tid; i < n; i += 1024) acc += (long long)dur[i];  // trunc toward 0
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
@@ -185,7 +195,42 @@ extern "C" int ftmi_duration_counts(float *dur, int32_t B, int32_t T, int32_t ap
                                     int32_t *fill_flag, ftmi_stream_t stream) {
   if (!dur || !offsets || !totals || B <= 0 || T <= 0) return FTMI_E_ARG;
   hipLaunchKernelGGL(duration_counts_kernel, dim3(1), dim3(1024), 0, ftmi_hs(stream), dur, B, T,
-                     apply_fill, fill_value, offsets, totals, fill_flag);
+                     apply_fill, fill_value, offsets, totals, fill_flag, (const int64_t *)nullptr);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+namespace {
+__global__ __launch_bounds__(1024) void trunc_sum_kernel(const float *dur, int64_t n, int64_t *out) {
+  __shared__ long long part[16];
+  long long acc = 0;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) acc += (long long)dur[i];
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long s = 0;
+    for (int w = 0; w < 16; ++w) s += part[w];
+    *out = s;
+  }
+}
+}  // namespace
+
+extern "C" int ftmi_duration_trunc_sum(const float *dur, int32_t B, int32_t T, int64_t *out,
+                                       ftmi_stream_t stream) {
+  if (!dur || !out || B <= 0 || T <= 0) return FTMI_E_ARG;
+  hipLaunchKernelGGL(trunc_sum_kernel, dim3(1), dim3(1024), 0, ftmi_hs(stream), dur, (int64_t)B * T, out);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_duration_counts_global(float *dur, int32_t B, int32_t T,
+                                           const int64_t *global_sum, float fill_value,
+                                           int32_t *offsets, int32_t *totals, int32_t *fill_flag,
+                                           ftmi_stream_t stream) {
+  if (!dur || !offsets || !totals || !global_sum || B <= 0 || T <= 0) return FTMI_E_ARG;
+  hipLaunchKernelGGL(duration_counts_kernel, dim3(1), dim3(1024), 0, ftmi_hs(stream), dur, B, T, 1,
+                     fill_value, offsets, totals, fill_flag, global_sum);
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
 }

@@ -262,9 +262,11 @@ class FastPitch(nn.Module):
                  x: torch.Tensor,
                  alpha=1.0,
                  pitch_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x,
-                 energy_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x) -> Dict[str, torch.Tensor]:
+                 energy_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x,
+                 batch=None) -> Dict[str, torch.Tensor]:
         """`models/fast_pitch.py:286-303`: predictors without masks; the prenet on side
-        streams overlaps the duration path and its one host sync (T_mel)."""
+        streams overlaps the duration path and its one host sync (T_mel).  `batch`: a
+        sharded.GlobalBatch when x is one rank's shard of a larger batch."""
         self.eval()
         self._check_device(x)
         with torch.no_grad():
@@ -281,8 +283,12 @@ class FastPitch(nn.Module):
             with torch.cuda.stream(s_energy):
                 energy_hat = energy_function(self.energy_pred.forward_bt(x).unsqueeze(1))
             dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
-            offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=True)
-            T_mel = int(totals.max().item())
+            if batch is None:
+                offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=True)
+                T_mel = int(totals.max().item())
+            else:
+                offsets, totals = batch.duration_counts(dur_hat)
+                T_mel = batch.t_mel(totals)
             for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat), (s_prenet, h),
                          (s_prenet, len_mask)):
                 main.wait_stream(s)

@@ -215,7 +215,7 @@ class ForwardTacotron(nn.Module):
             cache[device] = [torch.cuda.Stream(device=device) for _ in range(3)]
         return cache[device]
 
-    def _phoneme_phase(self, x, alpha, pitch_fn, energy_fn):
+    def _phoneme_phase(self, x, alpha, pitch_fn, energy_fn, batch=None):
         """Duration / pitch / energy predictors and the prenet CBHG are independent: pitch,
         energy and the prenet run on three side streams while the caller's stream runs the
         duration predictor and the LengthRegulator bookkeeping (fill-2 rule, counts, T_mel).
@@ -233,8 +233,12 @@ class ForwardTacotron(nn.Module):
         with torch.cuda.stream(s_energy):
             energy_hat = energy_fn(self.energy_pred.forward_bt(x).unsqueeze(1))
         dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
-        offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=True)
-        T_mel = int(totals.max().item())  # the one host sync (output size is data dependent)
+        if batch is None:
+            offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=True)
+            T_mel = int(totals.max().item())  # the one host sync (output size is data dependent)
+        else:  # a shard of a larger batch (sharded.GlobalBatch): batch-global fill rule / T_mel
+            offsets, totals = batch.duration_counts(dur_hat)
+            T_mel = batch.t_mel(totals)
         for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat), (s_prenet, enc)):
             main.wait_stream(s)
             t.record_stream(main)
@@ -244,14 +248,16 @@ class ForwardTacotron(nn.Module):
                  x: torch.Tensor,
                  alpha=1.0,
                  pitch_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x,
-                 energy_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x) -> Dict[str, torch.Tensor]:
+                 energy_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x,
+                 batch=None) -> Dict[str, torch.Tensor]:
         """`models/forward_tacotron.py:244-268`.  The callbacks run on the stream of their
-        predictor (torch ops issued inside them are ordered after the prediction)."""
+        predictor (torch ops issued inside them are ordered after the prediction).
+        `batch`: a sharded.GlobalBatch when x is one rank's shard of a larger batch."""
         self.eval()
         self._check_device(x)
         with torch.no_grad():
             dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel = self._phoneme_phase(
-                x, alpha, pitch_function, energy_function)
+                x, alpha, pitch_function, energy_function, batch)
             return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
                                       lr=(offsets, T_mel))
 

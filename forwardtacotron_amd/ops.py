@@ -250,6 +250,31 @@ def duration_counts(dur: torch.Tensor, apply_fill: bool, fill_value: float = 2.0
     return offsets, totals, flag
 
 
+def duration_trunc_sum(dur: torch.Tensor) -> torch.Tensor:
+    """sum_{b,t} int64(trunc(dur)) as a device int64[1] (the fill-2 rule's statistic)."""
+    _dev(dur)
+    B, T = dur.shape
+    out = torch.empty(1, device=dur.device, dtype=torch.int64)
+    launch('ftmi_duration_trunc_sum', f'duration_trunc_sum[B={B},T={T}]', 0, 4.0 * B * T,
+           dur.data_ptr(), B, T, out.data_ptr(), _stream())
+    return out
+
+
+def duration_counts_global(dur: torch.Tensor, global_sum: torch.Tensor, fill_value: float = 2.0):
+    """duration_counts with the fill-2 decision taken on a batch-global sum (device int64[1])."""
+    _dev(dur, global_sum)
+    if dur.dtype != _f32 or not dur.is_contiguous() or dur.dim() != 2:
+        raise ValueError('dur must be a contiguous (B, T) fp32 tensor')
+    B, T = dur.shape
+    offsets = torch.empty(B, T + 1, device=dur.device, dtype=torch.int32)
+    totals = torch.empty(B, device=dur.device, dtype=torch.int32)
+    flag = torch.empty(1, device=dur.device, dtype=torch.int32)
+    launch('ftmi_duration_counts_global', f'duration_counts[B={B},T={T}]', 0, B * T * 12,
+           dur.data_ptr(), B, T, global_sum.data_ptr(), float(fill_value), offsets.data_ptr(),
+           totals.data_ptr(), flag.data_ptr(), _stream())
+    return offsets, totals, flag
+
+
 def lr_index(offsets: torch.Tensor, T_mel: int) -> torch.Tensor:
     _dev(offsets)
     B, T1 = offsets.shape

@@ -1,0 +1,127 @@
+"""Batch-sharded generation over one process per GPU.
+
+Utterances are independent in the math but the reference couples a batch through three
+things; reproducing ONE reference call on the concatenation of all shards needs exactly:
+  1. every shard padded to the GLOBAL phoneme length T (pad id 0)       all_reduce(MAX)
+  2. the fill-2 rule (`forward_tacotron.py:254-255`, `fast_pitch.py:293-294`) decided on
+     the WHOLE batch's sum of int64(trunc(dur))                        all_reduce(SUM, int64)
+  3. the LengthRegulator output padded to the GLOBAL T_mel (max over all items)
+                                                                       all_reduce(MAX)
+Everything else is rank-local; the results are all-gathered (mel_post is
+(B_global, 80, T_mel) on every rank, exactly the reference's output).  The collectives
+are a few bytes, except the result gather; with the NCCL (= RCCL over xGMI) backend they
+run on device tensors, with gloo on host copies.  Weights are either built identically on
+every rank or broadcast once from rank 0 (`broadcast_state`).
+
+The collective steps are plain functions of torch tensors so the protocol is testable on
+CPU with gloo (tests/test_sharded.py); `generate_sharded` composes them with the HIP model.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+
+
+def _coll_device(group, like: torch.device) -> torch.device:
+    """Tensors for collectives: the GPU for nccl (RCCL), the host for gloo."""
+    backend = dist.get_backend(group)
+    return like if backend == 'nccl' else torch.device('cpu')
+
+
+def global_max(value: int, group=None, device: torch.device = torch.device('cpu')) -> int:
+    t = torch.tensor([int(value)], dtype=torch.int64, device=_coll_device(group, device))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def global_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place SUM all-reduce of a small tensor (device tensor stays on device for nccl)."""
+    dev = _coll_device(group, t.device)
+    if dev == t.device:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        return t
+    h = t.to(dev)
+    dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+    t.copy_(h)
+    return t
+
+
+def pad_tokens(x: torch.Tensor, T: int) -> torch.Tensor:
+    """Right-pad (B, t) phoneme ids with the pad id 0 to length T."""
+    if x.size(1) == T:
+        return x
+    out = torch.zeros(x.size(0), T, dtype=x.dtype, device=x.device)
+    out[:, :x.size(1)] = x
+    return out
+
+
+def gather_rows(t: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather along dim 0 with per-rank row counts that may differ."""
+    world = dist.get_world_size(group)
+    dev = _coll_device(group, t.device)
+    n = torch.tensor([t.size(0)], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    nmax = max(sizes)
+    src = t.to(dev).contiguous()
+    if src.size(0) < nmax:
+        pad = torch.zeros((nmax - src.size(0),) + tuple(src.shape[1:]), dtype=src.dtype, device=dev)
+        src = torch.cat([src, pad], 0)
+    bufs = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(bufs, src, group=group)
+    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0).to(t.device)
+
+
+class GlobalBatch:
+    """The batch-coupling hooks `generate(..., batch=GlobalBatch(group))` calls."""
+
+    def __init__(self, group=None) -> None:
+        self.group = group
+
+    def duration_counts(self, dur_hat: torch.Tensor):
+        """fill-2 rule on the global sum, then this shard's clip / counts / offsets."""
+        s = ops.duration_trunc_sum(dur_hat)
+        global_sum_(s, self.group)
+        offsets, totals, _ = ops.duration_counts_global(dur_hat, s)
+        return offsets, totals
+
+    def t_mel(self, totals: torch.Tensor) -> int:
+        local = int(totals.max().item()) if totals.numel() else 0
+        return global_max(local, self.group, totals.device)
+
+
+def broadcast_state(model: torch.nn.Module, src: int = 0, group=None) -> None:
+    """Copy rank `src`'s parameters and buffers to every rank (one broadcast per tensor)."""
+    for t in list(model.parameters()) + list(model.buffers()):
+        dev = _coll_device(group, t.device)
+        h = t.data if t.device == dev else t.data.to(dev)
+        dist.broadcast(h, src=src, group=group)
+        if h is not t.data:
+            t.data.copy_(h)
+
+
+def generate_sharded(model, x: torch.Tensor, alpha: float = 1.0,
+                     pitch_function: Callable = lambda p: p,
+                     energy_function: Callable = lambda e: e,
+                     group=None, gather: bool = True) -> Dict[str, torch.Tensor]:
+    """This rank's shard x (B_local, t) of one global batch -> the reference's output for the
+    whole batch (gather=True: every rank holds all rows, in rank order) or this rank's rows
+    of it (gather=False).  ForwardTacotron and FastPitch."""
+    T = global_max(x.size(1), group, x.device)
+    x = pad_tokens(x, T)
+    out = model.generate(x, alpha, pitch_function, energy_function, batch=GlobalBatch(group))
+    if not gather:
+        return out
+    res = {}
+    for k, v in out.items():
+        if k == 'mel_post' and out['mel_post'] is out['mel']:
+            continue
+        res[k] = gather_rows(v, group)
+    if 'mel_post' not in res:
+        res['mel_post'] = res['mel']
+    return res

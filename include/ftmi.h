@@ -175,6 +175,17 @@ int ftmi_duration_counts(float *dur, int32_t B, int32_t T, int32_t apply_fill,
                          float fill_value, int32_t *offsets, int32_t *totals,
                          int32_t *fill_flag, ftmi_stream_t stream);
 
+/* Batch-sharded form of the fill-2 rule: the reference decides on the sum
+ * over the WHOLE batch, so each shard computes its partial sum (ftmi_duration_trunc_sum:
+ * out[0] = sum_{b,t} trunc_int64(dur)), the host all-reduces it (RCCL SUM, device int64),
+ * and ftmi_duration_counts_global applies the rule with that global sum, then clips /
+ * counts / scans exactly like ftmi_duration_counts. */
+int ftmi_duration_trunc_sum(const float *dur, int32_t B, int32_t T, int64_t *out,
+                            ftmi_stream_t stream);
+int ftmi_duration_counts_global(float *dur, int32_t B, int32_t T, const int64_t *global_sum,
+                                float fill_value, int32_t *offsets, int32_t *totals,
+                                int32_t *fill_flag, ftmi_stream_t stream);
+
 /* Frame -> phoneme index map of the LengthRegulator: index[b, f] = t such that
  * offsets[b,t] <= f < offsets[b,t+1], or -1 for f >= totals[b] (zero padding,
  * pad_sequence in common_layers.py:18).  index: int32 [B][T_mel]. */

@@ -1,0 +1,137 @@
+"""The batch-sharded protocol (forwardtacotron_amd/sharded.py) with two ranks.
+
+CPU (gloo, world_size 2): the collective helpers, and the protocol end to end on the numpy
+oracle — two shards with different local lengths, globally padded, fill rule and T_mel
+decided globally, reproduce the oracle run on the whole batch (a normal and a fill-2 case);
+the fill decision is also checked on shards whose LOCAL sums disagree with the global one.
+
+GPU (-m gpu): two processes on one device (gloo for the tiny collectives): the HIP
+generate_sharded of two shards == the HIP generate of the concatenated batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+
+
+def _collectives(rank, world, port):
+    from forwardtacotron_amd import sharded as S
+    _init(rank, world, port)
+    try:
+        assert S.global_max(5 + 10 * rank) == 15
+        t = torch.tensor([3 + rank], dtype=torch.int64)
+        S.global_sum_(t)
+        assert int(t) == 7
+        rows = torch.arange((3 - rank) * 4, dtype=torch.float32).reshape(3 - rank, 4) + 100 * rank
+        g = S.gather_rows(rows)
+        ref = torch.cat([torch.arange(12.).reshape(3, 4), torch.arange(8.).reshape(2, 4) + 100])
+        assert torch.equal(g, ref)
+        x = torch.tensor([[4, 5, 6]])
+        assert torch.equal(S.pad_tokens(x, 5), torch.tensor([[4, 5, 6, 0, 0]]))
+        # fill-2 rule on the global sum: local sums +4 / -5 -> global -1 -> BOTH shards fill
+        dur = [np.array([[3.2, 1.1]], np.float32), np.array([[-5.0, -0.2]], np.float32)][rank]
+        t = torch.tensor([int(dur.astype(np.int64).sum())], dtype=torch.int64)
+        S.global_sum_(t)
+        assert int(t) == -1
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collective_helpers_gloo():
+    mp.spawn(_collectives, args=(2, _port()), nprocs=2, join=True)
+
+
+def _oracle_protocol(rank, world, port, alpha, out_path):
+    """Each rank runs the numpy oracle on its shard with the globally decided quantities."""
+    import json
+    from pathlib import Path
+
+    from forwardtacotron_amd import sharded as S
+    from forwardtacotron_amd.synthetic import synthetic_array, synthetic_tokens
+    from oracle import ft_oracle as O
+    _init(rank, world, port)
+    try:
+        keys = json.loads((Path(__file__).parent / 'golden' / 'state_dict_keys.json').read_text())
+        sd = {k: synthetic_array(k, s, d, 0) for k, s, d in keys}
+        full = synthetic_tokens(3, 9, seed=4, lengths=[9, 5, 6])
+        shard = [full[:1], full[1:, :6]][rank]  # rank 1's shard is locally shorter
+        T = S.global_max(shard.shape[1])
+        x = S.pad_tokens(torch.from_numpy(shard), T).numpy()
+        dur = O.series_predictor(sd, 'dur_pred', x, np.float32, alpha)[..., 0]
+        s = torch.tensor([int(dur.astype(np.int64).sum())], dtype=torch.int64)
+        S.global_sum_(s)
+        if int(s) <= 0:
+            dur = np.full_like(dur, 2.0)
+        pitch = O.series_predictor(sd, 'pitch_pred', x, np.float32).transpose(0, 2, 1)
+        energy = O.series_predictor(sd, 'energy_pred', x, np.float32).transpose(0, 2, 1)
+        h = O._encode(sd, x, pitch, energy, np.float32)
+        h, dur = O.length_regulator(h, dur)
+        T_mel = S.global_max(h.shape[1])
+        hp = np.zeros((h.shape[0], T_mel, h.shape[2]), np.float32)
+        hp[:, :h.shape[1]] = h
+        _, mel_post = O._decode(sd, hp, np.float32)
+        g = S.gather_rows(torch.from_numpy(np.ascontiguousarray(mel_post)))
+        if rank == 0:
+            ref = O.generate(sd, full, alpha=alpha)['mel_post']
+            np.savez(out_path, got=g.numpy(), ref=ref, s=int(s))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('alpha', [1.0, 1000.0], ids=['normal', 'global-fill2'])
+def test_protocol_reproduces_one_reference_call(alpha, tmp_path):
+    out = str(tmp_path / 'r.npz')
+    mp.spawn(_oracle_protocol, args=(2, _port(), alpha, out), nprocs=2, join=True)
+    z = np.load(out)
+    got, ref, s = z['got'], z['ref'], int(z['s'])
+    if alpha == 1000.0:
+        assert s <= 0  # the global rule fired
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, atol=2e-4, rtol=1e-5)
+
+
+def _gpu_worker(rank, world, port, out_path):
+    from forwardtacotron_amd import sharded as S
+    from forwardtacotron_amd.forward_tacotron import ForwardTacotron
+    from forwardtacotron_amd.synthetic import default_config, load_synthetic, synthetic_tokens
+    _init(rank, world, port)
+    try:
+        m = load_synthetic(ForwardTacotron.from_config(default_config()), 0).cuda().eval()
+        full = torch.from_numpy(synthetic_tokens(6, 40, seed=9, min_len=10)).cuda()
+        shard = full[:4] if rank == 0 else full[4:, :int((full[4:] != 0).sum(1).max())]
+        out = S.generate_sharded(m, shard)
+        if rank == 0:
+            ref = m.generate(full)
+            np.savez(out_path, got=out['mel_post'].cpu().numpy(), ref=ref['mel_post'].cpu().numpy(),
+                     dg=out['dur'].cpu().numpy(), dr=ref['dur'].cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_generate_sharded_gpu_matches_single_call(tmp_path):
+    from oracle import ft_oracle as O
+    out = str(tmp_path / 'g.npz')
+    mp.spawn(_gpu_worker, args=(2, _port(), out), nprocs=2, join=True)
+    z = np.load(out)
+    got, ref, dg, dr = z['got'], z['ref'], z['dg'], z['dr']
+    assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, atol=1e-4, rtol=1e-5)
+    np.testing.assert_array_equal(O.duration_counts(dg), O.duration_counts(dr))
