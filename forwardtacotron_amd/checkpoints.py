@@ -39,5 +39,6 @@ def init_tts_model(config: Dict[str, Any]) -> ForwardTacotron:
     if model_type == 'forward_tacotron':
         return ForwardTacotron.from_config(config)
     if model_type == 'fast_pitch':
-        raise NotImplementedError('fast_pitch is not on the MI355X path yet (SURVEY.md §8(f))')
+        from .fast_pitch import FastPitch
+        return FastPitch.from_config(config)
     raise ValueError(f'Model type not supported: {model_type}')
