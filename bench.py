@@ -51,8 +51,10 @@ from forwardtacotron_amd.synthetic import default_config, synthetic_state_dict, 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA == vector rate), MI355X_MICROARCH.md
 # the fp32-accurate bf16x6 path (labels "mma=1") issues 6 bf16 MFMAs per fp32 product:
 # its ceiling is the dense bf16 MFMA peak / 6
-PEAK_BF16_TFLOPS = 2500.0
+PEAK_BF16_TFLOPS = 2500.0  # == the dense f16 MFMA peak (same cycles per MFMA on gfx950)
 PEAK_X6_TFLOPS = PEAK_BF16_TFLOPS / 6
+# the default f16x3 path ("mma=2") issues 3 f16 MFMAs per fp32 product
+PEAK_X3_TFLOPS = PEAK_BF16_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 
@@ -162,12 +164,17 @@ def main():
         s = dom['avg_ms'] / 1e3
         if dom['flops'] > 0:
             achieved = dom['flops'] / s / 1e12
-            x6 = 'mma=1' in dom_label
-            peak = PEAK_X6_TFLOPS if x6 else PEAK_FP32_TFLOPS
+            if 'mma=2' in dom_label:
+                peak, basis = PEAK_X3_TFLOPS, ('f16 dense MFMA 2.5 PF / 3 (fp32-level f16x3 split: 3 '
+                                               'f16 products per fp32 product)')
+            elif 'mma=1' in dom_label:
+                peak, basis = PEAK_X6_TFLOPS, ('bf16 dense MFMA 2.5 PF / 6 (fp32-accurate bf16x6 '
+                                               'split: 6 bf16 products per fp32 product)')
+            else:
+                peak, basis = PEAK_FP32_TFLOPS, 'fp32 dense MFMA'
             roof = {'kernel': dom_label, 'bound': 'mfma', 'achieved': round(achieved, 3),
                     'peak': round(peak, 1), 'unit': 'TFLOP/s',
-                    'peak_basis': ('bf16 dense MFMA 2.5 PF / 6 (fp32-accurate bf16x6 split: 6 bf16 '
-                                   'products per fp32 product)') if x6 else 'fp32 dense MFMA',
+                    'peak_basis': basis,
                     'frac': round(achieved / peak, 4),
                     'algorithmic_per_launch': dom['flops'], 'avg_launch_ms': round(dom['avg_ms'], 4),
                     'launches': dom['launches'], 'share_of_device_time': round(dom['total_ms'] / total_dev_ms, 4),

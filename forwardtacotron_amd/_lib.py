@@ -19,8 +19,8 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 3
-MMA_F32, MMA_BF16X6 = 0, 1
+ABI_VERSION = 4
+MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
 class ConvArgs(ctypes.Structure):
@@ -31,7 +31,7 @@ class ConvArgs(ctypes.Structure):
         ('bias', P), ('relu', c_int), ('bn_scale', P), ('bn_shift', P), ('maxpool', c_int),
         ('residual', P), ('res_stride', c_int64),
         ('y', P), ('y_stride', c_int64), ('yt', P), ('T_out', c_int), ('mma', c_int),
-        ('split_k', c_int), ('split_ws', P), ('w_split', P),
+        ('split_k', c_int), ('split_ws', P), ('w_split', P), ('status', P),
     ]
 
 
@@ -42,14 +42,16 @@ SIGNATURES = {
     'ftmi_embedding': (c_int, [P, c_int64, P, c_int64, c_int64, P, P, P]),
     'ftmi_conv1d': (c_int, [ctypes.POINTER(ConvArgs), P]),
     'ftmi_conv_bank': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P, c_int64,
-                               c_int, P]),
-    'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P]),
+                               c_int, P, P]),
+    'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P, P]),
     'ftmi_split_weights_bytes': (c_int64, [c_int64, c_int64]),
     'ftmi_split_weights': (c_int, [P, c_int64, c_int64, P, P]),
+    'ftmi_split_weights_f16_bytes': (c_int64, [c_int64, c_int64]),
+    'ftmi_split_weights_f16': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_rnn_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
     'ftmi_rnn_error_offset': (c_int64, [c_int]),
     'ftmi_rnn_bidir': (c_int, [c_int, c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,
-                               c_float, P, c_int64, P, P]),
+                               c_float, P, c_int64, c_int, P, P, P]),
     'ftmi_duration_counts': (c_int, [P, c_int, c_int, c_int, c_float, P, P, P, P]),
     'ftmi_duration_trunc_sum': (c_int, [P, c_int, c_int, P, P]),
     'ftmi_duration_counts_global': (c_int, [P, c_int, c_int, P, c_float, P, P, P, P]),

@@ -76,6 +76,19 @@ class LinearParams(nn.Module):
         if self.bias is not None:
             _uniform_(self.bias, b)
 
+    def packed_weights(self):
+        """(weight, bias or None, pre-split weight) for ops.conv1d, cached on the parameter
+        identity / version like Packed."""
+        key = tuple((t.data_ptr(), t._version, t.device) for t in self.parameters())
+        cache = self.__dict__.get('_ftmi_pack')
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                w = self.weight.detach().contiguous()
+                b = None if self.bias is None else self.bias.detach().contiguous()
+                cache = (key, (w, b, presplit(w)))
+            self.__dict__['_ftmi_pack'] = cache
+        return cache[1]
+
 
 def pack_conv(w: torch.Tensor) -> torch.Tensor:
     """nn.Conv1d weight (N, Cin, k) -> kernel layout [N][k*Cin] (tap-major K)."""
@@ -83,8 +96,9 @@ def pack_conv(w: torch.Tensor) -> torch.Tensor:
 
 
 def presplit(w: torch.Tensor):
-    """bf16 pieces of a packed weight for the bf16x6 GEMM path (None on the fp32 path)."""
-    return ops.split_weights(w) if ops.MMA == 1 else None
+    """Pre-split operand of a packed weight for the default matrix path (ops.MMA): f16
+    planes (f16x3), bf16 pieces (bf16x6) or None (fp32)."""
+    return ops.presplit_for(w)
 
 
 # --------------------------------------------------------------------------------------
@@ -144,10 +158,10 @@ class BatchNormConv(Packed):
 
     def forward_cl(self, x: torch.Tensor, T_out: int = 0, residual=None, maxpool=False) -> torch.Tensor:
         w, bn, w3 = self.packed_weights()
-        # the pre-split path measured slower on the maxpool (CBHG proj1) shapes
+        # bf16x6: the pre-split kernel measured slower on the maxpool (CBHG proj1) shapes
         y, _ = ops.conv1d(x, w, self.kernel, self.kernel // 2, relu=self.relu, bn=bn,
                           residual=residual, maxpool=maxpool, T_out=T_out,
-                          w_split=None if maxpool else w3)
+                          w_split=None if (maxpool and ops.MMA == 1) else w3)
         return y
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -254,8 +268,7 @@ class CBHG(Packed):
         scale = torch.cat([f[0] for f in folds]).contiguous()
         shift = torch.cat([f[1] for f in folds]).contiguous()
         w_pre = self.pre_highway.weight.detach().contiguous()
-        bank3 = (ops.split_bank_weights(bank_w, self.K, ws[0].size(1), self.channels)
-                 if ops.MMA == 1 else None)
+        bank3 = ops.split_bank_weights(bank_w, self.K, ws[0].size(1), self.channels)
         return bank_w, scale, shift, w_pre, bank3, presplit(w_pre)
 
     def forward_cl(self, x: torch.Tensor) -> torch.Tensor:

@@ -24,6 +24,20 @@
 // (a1b1, a1b2, a2b1, a1b3, a2b2, a3b1) in fp32 — the dropped terms are < 2^-24 relative,
 // so the result is fp32-accurate (emulated: max err 5-7e-7 vs 2e-6 for a plain fp32 GEMM
 // at K = 256..6144) at 16/6 = 2.7x the fp32 MFMA rate.
+//
+// Third path, "h3" (mma = 2, the default): the same contraction in THREE f16 MFMAs per
+// fp32 product (16/3 = 5.3x the fp32 MFMA rate).  Both operands are split into an f16 head
+// and a SCALED f16 tail (Ootomo & Yokota, arXiv:2203.03341):
+//   a = a_h + 2^-11 a_t,   a_h = f16(a), a_t = f16((a - a_h) * 2^11)
+// The weights (pre-split once by ftmi_split_weights_f16, per output column n pre-scaled by
+// a power of two s_n so that |w| s_n < 16) are stored as three f16 planes
+//   B0 = 2^11 w_h,  B1 = w_t,  B2 = w_h            (w = w_h + 2^-11 w_t after scaling)
+// and one fp32 accumulator collects   a_h B0 + a_h B1 + a_t B2 = 2^11 (a w - 2^-22 a_t w_t),
+// multiplied back by colscale[n] = 2^-11 / s_n (exact) in the epilogue.  The scaled tails
+// keep 11 significant bits down to |a| ~ 2^-24 (no subnormal tail loss); the dropped term is
+// < 2^-22 relative.  The only range limit is |a| < 65504 for the activations: an overflow
+// makes the accumulator non-finite, which the epilogue reports through *status (bit 0);
+// the model layer then recomputes the call on the fp32 path.
 #include "common.h"
 
 namespace {
@@ -39,6 +53,8 @@ enum { EPI_CONV = 0, EPI_HIGHWAY = 1 };
 struct GemmGroup {
   const float *w;  // [N][Ktot]
   const __bf16 *w3;  // optional pre-split weights [3][N][Kpad], Kpad = roundup(Ktot, 32)
+                     // (bf16 pieces for mma = 1, f16 planes B0/B1/B2 for mma = 2)
+  const float *colscale;  // mma = 2: per-column 2^-11 / s_n after the f16 planes
   int Kpad;
   const float *bias;
   const float *scale;
@@ -69,11 +85,38 @@ struct GemmParams {
   int split;
   int kc_per;
   float *part;
+  unsigned *status;  // mma = 2: bit 0 set when an accumulator became non-finite
   GemmGroup g[MAX_GROUPS];
 };
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// matrix-fragment type and MFMA of the pre-split kernels: bf16 pieces (x6) or f16 (h3)
+template <bool H3>
+struct Frag {
+  typedef bf16x8 T;
+};
+template <>
+struct Frag<true> {
+  typedef f16x8 T;
+};
+__device__ __forceinline__ f32x4 mma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+constexpr float H3_SCALE = 2048.f;  // 2^11: the tail scale of the f16 split
+
+// a = a_h + 2^-11 a_t  (f16 head, scaled f16 tail)
+__device__ __forceinline__ void split2h(f32x4 v, f16x4 &h, f16x4 &t) {
+  h = __builtin_convertvector(v, f16x4);
+  t = __builtin_convertvector((v - __builtin_convertvector(h, f32x4)) * H3_SCALE, f16x4);
+}
 
 constexpr int X6_BK = 32;
 constexpr int X6_STRIDE = 48;  // bf16 per staged row (32 + 16 pad): 96-B rows make the
@@ -692,8 +735,11 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_x6p_kernel(const GemmParams 
 // and ds_write_b128 into a double-buffered LDS image shared by the 4 waves.  Compared with
 // the x6 kernel this halves the split VALU work and the LDS write traffic (the binding
 // resource there) and needs one barrier per chunk.
-template <int EPI, bool MAXPOOL>
+// H3 = true is the f16 path (mma = 2): the same staging of three weight planes, the
+// activations split into two f16 fragments (head, scaled tail) and three MFMAs per tile.
+template <int EPI, bool MAXPOOL, bool H3>
 __global__ __launch_bounds__(256, 2) void conv_gemm_x6b_kernel(const GemmParams p) {
+  typedef typename Frag<H3>::T frag;
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 3 * X6_PIECE];  // [buf][piece][n][48]
 
   const int tile = blockIdx.x;
@@ -729,57 +775,96 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6b_kernel(const GemmParams 
     nk = min(nk - kc0, p.kc_per);
   }
   int kk = kc0 * X6_BK + 8 * fs, tj = kk / p.Cin, tc = kk - tj * p.Cin;
-  f32x4 ra[2][2];
-  auto loadA = [&]() {
+  // Loads go to registers RAW: the zero-padding select and the maxpool max are applied
+  // when the chunk is split (two iterations later), so no s_waitcnt is forced at the load.
+  // Every load is unconditional (addresses clamped in range): static wait counters.
+  struct ARaw {
+    f32x4 v[2][2];
+    f32x4 u[MAXPOOL ? 2 : 1][2];  // maxpool: the previous frame's row
+    unsigned okm;
+  };
+  auto loadA = [&](ARaw &r) {
     const bool kok = kk < G.Ktot;
+    unsigned okm = 0;
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
       const int ts = at[mi] + tj - G.pad;
       const bool ok = kok && aok[mi] && ts >= 0 && ts < p.T;
       const float *src = arow[mi] + (int64_t)(ok ? ts : 0) * p.x_stride + (ok ? tc : 0);
-      f32x4 v0 = *(const f32x4 *)src, v1 = *(const f32x4 *)(src + 4);
-      if (MAXPOOL) {
+      r.v[mi][0] = *(const f32x4 *)src;
+      r.v[mi][1] = *(const f32x4 *)(src + 4);
+      if constexpr (MAXPOOL) {
         const float *sp = src - ((ok && ts > 0) ? p.x_stride : 0);
-        v0 = fmax4(v0, *(const f32x4 *)sp);
-        v1 = fmax4(v1, *(const f32x4 *)(sp + 4));
+        r.u[mi][0] = *(const f32x4 *)sp;
+        r.u[mi][1] = *(const f32x4 *)(sp + 4);
       }
-      ra[mi][0] = sel4(ok, v0);
-      ra[mi][1] = sel4(ok, v1);
+      okm |= (unsigned)ok << mi;
     }
+    r.okm = okm;
     kk += X6_BK;
     tc += X6_BK;
-    while (tc >= p.Cin) {
-      tc -= p.Cin;
-      ++tj;
+    // Cin >= 16 (checked on the host): at most two wraps per 32-wide chunk
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const bool wrap = tc >= p.Cin;
+      tc -= wrap ? p.Cin : 0;
+      tj += wrap;
+    }
+  };
+  float amax = 0.f;  // H3: largest |activation| fed to the f16 split (range guard)
+  auto splitA = [&](const ARaw &r, frag (&a)[2][H3 ? 2 : 3]) {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      f32x4 v0 = r.v[mi][0], v1 = r.v[mi][1];
+      if constexpr (MAXPOOL) {
+        v0 = fmax4(v0, r.u[mi][0]);
+        v1 = fmax4(v1, r.u[mi][1]);
+      }
+      const bool ok = (r.okm >> mi) & 1u;
+      v0 = sel4(ok, v0);
+      v1 = sel4(ok, v1);
+      if constexpr (H3) {
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w))));
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w))));
+        f16x4 l1, l2, h1, h2;
+        split2h(v0, l1, l2);
+        split2h(v1, h1, h2);
+        a[mi][0] = __builtin_shufflevector(l1, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        a[mi][1] = __builtin_shufflevector(l2, h2, 0, 1, 2, 3, 4, 5, 6, 7);
+      } else {
+        bf16x4 l1, l2, l3, h1, h2, h3;
+        split3(v0, l1, l2, l3);
+        split3(v1, h1, h2, h3);
+        a[mi][0] = __builtin_shufflevector(l1, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        a[mi][1] = __builtin_shufflevector(l2, h2, 0, 1, 2, 3, 4, 5, 6, 7);
+        a[mi][2] = __builtin_shufflevector(l3, h3, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
     }
   };
 
   // ---- B: 6 x 16 B of pre-split pieces per thread per chunk ------------------------
+  // Rows n >= N read row N-1 (clamped, no select): they only feed output columns that
+  // are never stored.  Chunks past the end re-read the last chunk (clamped).
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 rb[6];
   const __bf16 *bsrc[6];
   int boff[6];
-  bool bok[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const int idx = tid + 256 * i;
     const int pc = idx >> 9, rem = idx & 511, nl = rem >> 2, seg = rem & 3;
-    const int n = n0 + nl;
-    bok[i] = n < G.N;
-    bsrc[i] = G.w3 + ((int64_t)pc * G.N + (bok[i] ? n : 0)) * G.Kpad + kc0 * X6_BK + seg * 8;
+    const int n = n0 + nl < G.N ? n0 + nl : G.N - 1;
+    bsrc[i] = G.w3 + ((int64_t)pc * G.N + n) * G.Kpad + kc0 * X6_BK + seg * 8;
     boff[i] = pc * X6_PIECE + nl * X6_STRIDE + seg * 8;
   }
+  const int kb_last = (nk - 1) * X6_BK;
   int kb = 0;  // chunk offset (elements) of the next B load
-  auto loadB = [&]() {
+  auto loadB = [&](u32x4 (&rb)[6]) {
+    const int o = kb < kb_last ? kb : kb_last;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const u32x4 z = {0u, 0u, 0u, 0u};
-      const u32x4 v = *(const u32x4 *)(bsrc[i] + kb);
-      rb[i] = bok[i] ? v : z;
-    }
+    for (int i = 0; i < 6; ++i) rb[i] = *(const u32x4 *)(bsrc[i] + o);
     kb += X6_BK;
   };
-  auto storeB = [&](int buf) {
+  auto storeB = [&](const u32x4 (&rb)[6], int buf) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) *(u32x4 *)(lds + buf * 3 * X6_PIECE + boff[i]) = rb[i];
   };
@@ -790,48 +875,79 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6b_kernel(const GemmParams 
 #pragma unroll
     for (int ni = 0; ni < 8; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  loadA();
-  loadB();
-  storeB(0);
-  if (nk > 1) loadB();
-  __syncthreads();
-  for (int kc = 0; kc < nk; ++kc) {
-    // split this chunk's activations (registers) into bf16 A-fragments
-    bf16x8 a[2][3];
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      bf16x4 l1, l2, l3, h1, h2, h3;
-      split3(ra[mi][0], l1, l2, l3);
-      split3(ra[mi][1], h1, h2, h3);
-      a[mi][0] = __builtin_shufflevector(l1, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-      a[mi][1] = __builtin_shufflevector(l2, h2, 0, 1, 2, 3, 4, 5, 6, 7);
-      a[mi][2] = __builtin_shufflevector(l3, h3, 0, 1, 2, 3, 4, 5, 6, 7);
-    }
-    if (kc + 1 < nk) {
-      loadA();
-      storeB((kc + 1) & 1);
-      if (kc + 2 < nk) loadB();
-    }
-    const __bf16 *cur = lds + (kc & 1) * 3 * X6_PIECE;
+  auto mfma_chunk = [&](const frag (&a)[2][H3 ? 2 : 3], int buf) {
+    const __bf16 *cur = lds + buf * 3 * X6_PIECE;
 #pragma unroll
     for (int ni = 0; ni < 8; ++ni) {
-      bf16x8 b[3];
+      frag b[3];
 #pragma unroll
       for (int pc = 0; pc < 3; ++pc)
-        b[pc] = *(const bf16x8 *)(cur + pc * X6_PIECE + (ni * 16 + fr) * X6_STRIDE + 8 * fs);
+        b[pc] = *(const frag *)(cur + pc * X6_PIECE + (ni * 16 + fr) * X6_STRIDE + 8 * fs);
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi) {
         f32x4 c = acc[mi][ni];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][2], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][1], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][0], b[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][1], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][0], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi][0], b[0], c, 0, 0, 0);
+        if constexpr (H3) {  // small terms first: a_t w_h, a_h w_t, then a_h 2^11 w_h
+          c = mma16(a[mi][1], b[2], c);
+          c = mma16(a[mi][0], b[1], c);
+          c = mma16(a[mi][0], b[0], c);
+        } else {
+          c = mma16(a[mi][2], b[0], c);
+          c = mma16(a[mi][1], b[1], c);
+          c = mma16(a[mi][0], b[2], c);
+          c = mma16(a[mi][1], b[0], c);
+          c = mma16(a[mi][0], b[1], c);
+          c = mma16(a[mi][0], b[0], c);
+        }
         acc[mi][ni] = c;
       }
     }
+  };
+
+  // chunk c lives in LDS buffer c & 1 and (H3) A register set c & 1; the B registers hold
+  // the next chunk to stage.  Prefetch distance: A two chunks on the f16 path, one on the
+  // bf16 path (its three-piece fragments leave no room for a second set), B one.
+  constexpr bool DEEP = H3;
+  ARaw ra0, ra1;
+  u32x4 rb[6];
+  loadA(ra0);
+  loadB(rb);  // chunk 0
+  if constexpr (DEEP) loadA(ra1);
+  storeB(rb, 0);
+  loadB(rb);  // chunk 1
+  __syncthreads();
+  // one step: split chunk kc, prefetch the A chunk DEEP ? kc+2 : kc+1 into the freed set,
+  // stage B kc+1 into LDS and prefetch B kc+2, MFMAs on chunk kc, barrier
+  auto step = [&](int kc, ARaw &ras) {
+    frag a[2][H3 ? 2 : 3];
+    splitA(ras, a);
+    loadA(ras);
+    if (kc + 1 < nk) storeB(rb, (kc + 1) & 1);
+    loadB(rb);
+    mfma_chunk(a, kc & 1);
     __syncthreads();
+  };
+  for (int kc = 0; kc < nk; kc += 2) {
+    step(kc, ra0);
+    if (kc + 1 >= nk) break;
+    step(kc + 1, DEEP ? ra1 : ra0);
+  }
+
+  if constexpr (H3) {  // undo the 2^11 / column pre-scaling; report f16 range overflow
+    bool bad = !(amax <= 65504.f);
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+      const int col = n0 + ni * 16 + fr;
+      const float cs = G.colscale[col < G.N ? col : G.N - 1];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wave * 32 + mi * 16 + 4 * fs + i;
+          bad |= col < G.N && row < p.M && !__builtin_isfinite(acc[mi][ni][i]);
+          acc[mi][ni][i] *= cs;
+        }
+    }
+    if (bad && p.status) atomicOr(p.status, 1u);
   }
 
   const int er = 4 * fs;
@@ -921,6 +1037,38 @@ __global__ void split_weights_kernel(const float *__restrict__ w, int64_t N, int
   }
 }
 
+// w [N][K] fp32 -> f16 planes [3][N][Kpad] (B0 = 2^11 w_h, B1 = w_t, B2 = w_h of the
+// column-scaled row w s_n) followed by colscale[N] = 2^-11 / s_n.  One workgroup per row:
+// s_n = 2^-e with the smallest e >= 0 such that max|w[n]| s_n < 16 (so 2^11 w_h stays
+// inside the f16 range).
+__global__ __launch_bounds__(256) void split_weights_f16_kernel(const float *__restrict__ w,
+                                                                int64_t N, int64_t K, int64_t Kpad,
+                                                                _Float16 *__restrict__ out,
+                                                                float *__restrict__ colscale) {
+  __shared__ float red[4];
+  const int64_t n = blockIdx.x;
+  const float *row = w + n * K;
+  float m = 0.f;
+  for (int64_t k = threadIdx.x; k < K; k += 256) m = fmaxf(m, fabsf(row[k]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  int ex = 0;
+  if (__builtin_isfinite(m) && m > 0.f) frexpf(m, &ex);  // m = f * 2^ex, f in [0.5, 1)
+  const int e = ex > 4 ? ex - 4 : 0;                     // m * 2^-e < 2^4
+  const int64_t plane = N * Kpad;
+  for (int64_t k = threadIdx.x; k < Kpad; k += 256) {
+    const float v = k < K ? ldexpf(row[k], -e) : 0.f;
+    const _Float16 h = (_Float16)v;
+    const _Float16 t = (_Float16)((v - (float)h) * H3_SCALE);
+    out[n * Kpad + k] = (_Float16)((float)h * H3_SCALE);
+    out[plane + n * Kpad + k] = t;
+    out[2 * plane + n * Kpad + k] = h;
+  }
+  if (threadIdx.x == 0) colscale[n] = ldexpf(1.f, e - 11);
+}
+
 // Split-K finish: v = sum_s part[s][m][n] (fixed order: deterministic), then the
 // EPI_CONV epilogue (bias, ReLU, BN, residual, plain and transposed stores).
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const GemmParams p) {
@@ -954,16 +1102,26 @@ static int x6_variant() {
 int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hipStream_t s) {
   if (nblocks <= 0) return FTMI_OK;
   dim3 grid(nblocks), block(256);
-  bool presplit = mma == 1 && x6_variant() != 3;
+  bool presplit = (mma == 1 && x6_variant() != 3) || mma == 2;
   for (int i = 0; i < p.ngroups; ++i) presplit &= p.g[i].w3 != nullptr;
+  if (mma == 2 && !presplit) return FTMI_E_ARG;  // the f16 path needs the split planes
   if (presplit) {
     dim3 g2(nblocks, p.split > 1 ? p.split : 1);
-    if (epi == EPI_HIGHWAY)
-      hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_HIGHWAY, false>), g2, block, 0, s, p);
-    else if (maxpool)
-      hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_CONV, true>), g2, block, 0, s, p);
-    else
-      hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_CONV, false>), g2, block, 0, s, p);
+    if (mma == 2) {
+      if (epi == EPI_HIGHWAY)
+        hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_HIGHWAY, false, true>), g2, block, 0, s, p);
+      else if (maxpool)
+        hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_CONV, true, true>), g2, block, 0, s, p);
+      else
+        hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_CONV, false, true>), g2, block, 0, s, p);
+    } else {
+      if (epi == EPI_HIGHWAY)
+        hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_HIGHWAY, false, false>), g2, block, 0, s, p);
+      else if (maxpool)
+        hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_CONV, true, false>), g2, block, 0, s, p);
+      else
+        hipLaunchKernelGGL((conv_gemm_x6b_kernel<EPI_CONV, false, false>), g2, block, 0, s, p);
+    }
     FTMI_CHECK_LAUNCH();
     if (p.split > 1) {
       const int64_t total = (int64_t)p.M * p.g[0].N;
@@ -1023,13 +1181,26 @@ int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hip
   return FTMI_OK;
 }
 
+// bytes of one weight's pre-split block: bf16 pieces (mma = 1) or f16 planes + colscale
+int64_t split_block_bytes(int64_t N, int64_t K, int mma) {
+  const int64_t planes = 3 * N * ((K + X6_BK - 1) / X6_BK * X6_BK) * 2;
+  return mma == 2 ? planes + (4 * N + 15) / 16 * 16 : planes;
+}
+
+void set_split(GemmGroup &g, const void *block, int mma) {
+  g.w3 = (const __bf16 *)block;
+  g.colscale = (block && mma == 2) ? (const float *)((const char *)block + 3LL * g.N * g.Kpad * 2)
+                                   : nullptr;
+}
+
 }  // namespace
 
 extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   if (!a || !a->x || !a->w || (!a->y && !a->yt)) return FTMI_E_ARG;
   if (a->B <= 0 || a->T <= 0 || a->Cin <= 0 || a->N <= 0 || a->k <= 0) return FTMI_E_ARG;
   if (a->Cin % 16 != 0) return FTMI_E_SHAPE;
-  if (a->mma != 0 && a->mma != 1) return FTMI_E_ARG;
+  if (a->mma < 0 || a->mma > 2) return FTMI_E_ARG;
+  if (a->mma == 2 && !a->w_split) return FTMI_E_ARG;
   if (a->pad < 0 || a->pad >= a->k + a->T) return FTMI_E_SHAPE;
   if ((a->bn_scale == nullptr) != (a->bn_shift == nullptr)) return FTMI_E_ARG;
   if (!ftmi_aligned16(a->x) || !ftmi_aligned16(a->w) || (a->x_stride & 3)) return FTMI_E_ALIGN;
@@ -1052,9 +1223,9 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   p.y_stride = a->y_stride;
   p.yt = a->yt;
   p.yt_channels = a->N;
+  p.status = a->status;
   GemmGroup &g = p.g[0];
   g.w = a->w;
-  g.w3 = (const __bf16 *)a->w_split;
   g.Kpad = (a->k * a->Cin + X6_BK - 1) / X6_BK * X6_BK;
   g.bias = a->bias;
   g.scale = a->bn_scale;
@@ -1066,10 +1237,11 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   g.ycol0 = 0;
   g.ntiles = (a->N + BN - 1) / BN;
   g.tile0 = 0;
+  set_split(g, a->w_split, a->mma);
   const int mtiles = (p.M + BM - 1) / BM;
   p.split = 1;
   if (a->split_k > 1) {
-    if (a->mma != 1 || !a->split_ws) return FTMI_E_ARG;
+    if (a->mma == 0 || !a->split_ws) return FTMI_E_ARG;
     const int nkc = (g.Ktot + X6_BK - 1) / X6_BK;
     const int kc_per = (nkc + a->split_k - 1) / a->split_k;
     p.split = (nkc + kc_per - 1) / kc_per;  // no empty splits
@@ -1082,9 +1254,11 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
 extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T,
                               int32_t Cin, const float *w, const void *w_split, int32_t K,
                               int32_t Cout, const float *bn_scale, const float *bn_shift,
-                              float *y, int64_t y_stride, int32_t mma, ftmi_stream_t stream) {
+                              float *y, int64_t y_stride, int32_t mma, uint32_t *status,
+                              ftmi_stream_t stream) {
   if (!x || !w || !bn_scale || !bn_shift || !y) return FTMI_E_ARG;
   if (B <= 0 || T <= 0 || Cin <= 0 || Cout <= 0 || K <= 0) return FTMI_E_ARG;
+  if (mma < 0 || mma > 2 || (mma == 2 && !w_split)) return FTMI_E_ARG;
   if (K > MAX_GROUPS) return FTMI_E_UNSUPPORTED;
   if (Cin % 16 != 0) return FTMI_E_SHAPE;
   if (!ftmi_aligned16(x) || !ftmi_aligned16(w) || (x_stride & 3)) return FTMI_E_ALIGN;
@@ -1102,6 +1276,7 @@ extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32
   p.ngroups = K;
   p.y = y;
   p.y_stride = y_stride;
+  p.status = status;
   const int mtiles = (p.M + BM - 1) / BM;
   const int ntiles = (Cout + BN - 1) / BN;
   int tile0 = 0;
@@ -1110,13 +1285,15 @@ extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32
     const int gidx = ks - 1;
     GemmGroup &g = p.g[gi];
     g.w = w + (int64_t)Cout * Cin * gidx * (gidx + 1) / 2;
-    g.w3 = nullptr;
     g.Kpad = (ks * Cin + X6_BK - 1) / X6_BK * X6_BK;
-    if (w_split) {  // groups back to back, each [3][Cout][Kpad_g]
+    g.N = Cout;
+    const void *blk = nullptr;
+    if (w_split) {  // per-group split blocks back to back (ftmi_split_weights[_f16] layout)
       int64_t off = 0;
-      for (int j = 0; j < gidx; ++j) off += 3LL * Cout * (((j + 1) * Cin + X6_BK - 1) / X6_BK * X6_BK);
-      g.w3 = (const __bf16 *)w_split + off;
+      for (int j = 0; j < gidx; ++j) off += split_block_bytes(Cout, (int64_t)(j + 1) * Cin, mma);
+      blk = (const char *)w_split + off;
     }
+    set_split(g, blk, mma);
     g.bias = nullptr;
     g.scale = bn_scale + (int64_t)gidx * Cout;
     g.shift = bn_shift + (int64_t)gidx * Cout;
@@ -1135,9 +1312,10 @@ extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32
 extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t C,
                             const float *w12, const void *w12_split, const float *b1,
                             const float *b2, float *y, int64_t y_stride, int32_t mma,
-                            ftmi_stream_t stream) {
+                            uint32_t *status, ftmi_stream_t stream) {
   if (!x || !w12 || !b1 || !b2 || !y) return FTMI_E_ARG;
   if (M <= 0 || C <= 0) return FTMI_E_ARG;
+  if (mma < 0 || mma > 2 || (mma == 2 && !w12_split)) return FTMI_E_ARG;
   if (C % 32 != 0 || C % 16 != 0) return FTMI_E_SHAPE;
   if (M > INT32_MAX) return FTMI_E_SHAPE;
   if (!ftmi_aligned16(x) || !ftmi_aligned16(w12) || (x_stride & 3)) return FTMI_E_ALIGN;
@@ -1156,9 +1334,9 @@ extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t
   p.y_stride = y_stride;
   p.b1 = b1;
   p.b2 = b2;
+  p.status = status;
   GemmGroup &g = p.g[0];
   g.w = w12;
-  g.w3 = (const __bf16 *)w12_split;
   g.Kpad = (C + X6_BK - 1) / X6_BK * X6_BK;
   g.N = 2 * C;
   g.k = 1;
@@ -1166,8 +1344,26 @@ extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t
   g.Ktot = C;
   g.ntiles = (2 * C + BN - 1) / BN;
   g.tile0 = 0;
+  set_split(g, w12_split, mma);
   const int mtiles = (p.M + BM - 1) / BM;
   return launch(p, EPI_HIGHWAY, false, mtiles * g.ntiles, mma, ftmi_hs(stream));
+}
+
+extern "C" int64_t ftmi_split_weights_f16_bytes(int64_t N, int64_t K) {
+  return split_block_bytes(N, K, 2);
+}
+
+extern "C" int ftmi_split_weights_f16(const float *w, int64_t N, int64_t K, void *out,
+                                      ftmi_stream_t stream) {
+  if (!w || !out || N <= 0 || K <= 0) return FTMI_E_ARG;
+  if (N > INT32_MAX) return FTMI_E_SHAPE;
+  if (!ftmi_aligned16(out)) return FTMI_E_ALIGN;
+  const int64_t Kpad = (K + X6_BK - 1) / X6_BK * X6_BK;
+  hipLaunchKernelGGL(split_weights_f16_kernel, dim3((unsigned)N), dim3(256), 0, ftmi_hs(stream), w,
+                     N, K, Kpad, (_Float16 *)out,
+                     (float *)((char *)out + 3 * N * Kpad * 2));
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
 }
 
 extern "C" int ftmi_split_weights(const float *w, int64_t N, int64_t K, void *out,

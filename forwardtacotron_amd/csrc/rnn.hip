@@ -16,10 +16,16 @@
 // its K range with MFMA, the WK partials are summed through LDS, and 256 threads apply the
 // cell update to the U x 16 (unit, sequence) cells they own (c / h state in registers).
 //
-// Matrix path (X6 = true, default): W and h are split into three bf16 pieces each and the
-// six cross products with i + j <= 4 run on v_mfma_f32_16x16x32_bf16 with fp32
-// accumulation — fp32-accurate (see gemm.hip) at 16/6 of the fp32 MFMA rate.  X6 = false
-// keeps v_mfma_f32_16x16x4_f32.
+// Matrix path (MODE):
+//   2 (FTMI_MMA_F16X3, default): W = W_h + 2^-11 W_t (f16 head + scaled f16 tail, kept in
+//     VGPRs: 4 B per weight) and h = h_h + 2^-11 h_t; three v_mfma_f32_16x16x32_f16 per
+//     tile accumulate  W_t h_h + W_h h_t + W_h (2^11 h_h) = 2^11 W h  (dropped term
+//     < 2^-22 relative), scaled back by 2^-11 (exact) before the K-split reduction.  h is a
+//     tanh / sigmoid*tanh output, |h| < 1, so 2^11 h_h never leaves the f16 range; a W_hh
+//     entry beyond the f16 range sets bit 1 of *status (the caller then reruns on mode 1).
+//   1 (FTMI_MMA_BF16X6): W and h split into three bf16 pieces each, the six cross products
+//     with i + j <= 4 on v_mfma_f32_16x16x32_bf16 — fp32-accurate (see gemm.hip).
+//   0 (FTMI_MMA_F32): v_mfma_f32_16x16x4_f32.
 //
 // h hand-off between the BPG workgroups of a group.  New h values go to an exchange buffer
 // hx[t & 1][group][16*H] in MFMA-fragment order (every consumer wave-instruction reads
@@ -71,6 +77,10 @@ __device__ unsigned long long ftmi_rnn_stamps[2048 * 8];
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+constexpr float H3_SCALE = 2048.f;      // 2^11: tail scale of the f16 split
+constexpr float H3_UNSCALE = 1.f / 2048.f;
 
 constexpr int NB = 16;              // sequences per group (MFMA 16x16 columns)
 constexpr int RED_STRIDE = NB + 1;  // LDS partial-sum row stride (floats)
@@ -103,6 +113,10 @@ struct RnnParams {
   int ngroups;    // groups in this launch
   int xcd_local;  // 1: try the census-based XCD-local mode
   unsigned *ws;   // control words (see WS_*)
+  unsigned *status;  // optional: bit 1 = a W_hh entry overflowed f16 (mode 2)
+  int diag;  // timing experiments only (FTMI_RNN_DIAG, results invalid when set): bit 0 =
+             // input projections from one L2-hot row, bit 1 = no hand-off waits,
+             // bit 2 = no drain
 };
 
 __device__ __forceinline__ float fast_sigmoid(float x) {
@@ -122,6 +136,16 @@ __device__ __forceinline__ void split3x8(const float (&v)[8], bf16x8 &h1, bf16x8
   h3 = __builtin_convertvector(r2, bf16x8);
 }
 
+// x = h + 2^-11 t (f16 head, scaled f16 tail); s = 2^11 h (exact for |x| < 32)
+__device__ __forceinline__ void split2h8(const float (&v)[8], f16x8 &h, f16x8 &t) {
+  typedef float f32x8 __attribute__((ext_vector_type(8)));
+  f32x8 x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[i] = v[i];
+  h = __builtin_convertvector(x, f16x8);
+  t = __builtin_convertvector((x - __builtin_convertvector(h, f32x8)) * H3_SCALE, f16x8);
+}
+
 __device__ __forceinline__ unsigned xcc_id() {
   unsigned x;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
@@ -138,8 +162,10 @@ __device__ __forceinline__ bool poll_ge(unsigned *w, unsigned target) {
   return true;
 }
 
-template <int CELL, int H, int U, int WK, bool X6>
-__global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
+template <int CELL, int H, int U, int WK, int MODE>
+__global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(const RnnParams p) {
+  constexpr bool X6 = MODE != 0;  // 16x16x32 fragment layout (bf16x6 and f16x3)
+  constexpr bool H3 = MODE == 2;
   constexpr int G = CELL ? 4 : 3;
   constexpr int R = G * U;
   constexpr int RB = R / 16;
@@ -158,6 +184,10 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
 
   __shared__ __attribute__((aligned(16))) float red[WK * R * RED_STRIDE];
   __shared__ __attribute__((aligned(16))) float hloc[LOCAL ? 2 * 16 * H : 4];
+  // multi-workgroup groups: the new h slice and y values of this workgroup, handed from the
+  // compute waves to the comm wave (cell c = seq * U + unit; float4 f = 4 units)
+  __shared__ __attribute__((aligned(16))) float hstage[LOCAL ? 4 : CELLS];
+  __shared__ __attribute__((aligned(16))) float ystage[LOCAL ? 4 : CELLS];
   __shared__ int s_abort, s_group, s_bi, s_mode;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -205,12 +235,113 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
   unsigned *flags = p.ws + WS_FLAGS + gglob * FLAGS_PER_GROUP;
   static_assert(BPG <= FLAGS_PER_GROUP, "flags");
 
+  // ---- comm wave (wave 4, multi-workgroup groups only) ---------------------------------
+  // Owns every global store of the step and the hand-off, so the compute waves issue only
+  // loads: their input-projection prefetch is never drained by a store wait (vmcnt counts
+  // loads and stores together, in issue order).  Per step: poll the group's flags -> barrier
+  // A -> (compute: h load, MFMA) barrier B -> (compute: cells -> LDS stage) barrier C ->
+  // store this workgroup's h slice (one float4 per lane per 256 cells), drain, arrive, then
+  // store the y rows.
+  if constexpr (!LOCAL) {
+    if (wave == 4) {
+      constexpr int F4 = CELLS / 4;  // float4s of the slice
+      constexpr int FPL = F4 / 64;   // per lane
+      static_assert(F4 % 64 == 0, "comm wave tiling");
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.hx, (short)0, 0x7FFFFFF0, 0x00020000);
+      const int hxp = p.ngroups_total * 16 * H * 4;  // bytes between the parity halves
+      unsigned hofs[FPL];
+      int yb[FPL], k0s[FPL];
+      bool ok[FPL];
+#pragma unroll
+      for (int i = 0; i < FPL; ++i) {
+        const int f = lane + 64 * i;
+        const int bl = f / (U / 4);
+        const int k0 = u0 + (f % (U / 4)) * 4;
+        const int kwv = k0 / KW, r = k0 % KW;
+        int ln, idx4;
+        if constexpr (X6) {
+          const int q = r % 32;
+          ln = (q >> 3) * 16 + bl;
+          idx4 = (r / 32) * 2 + ((q & 7) >> 2);
+        } else {
+          ln = (r / KB) * 16 + bl;
+          idx4 = (r % KB) >> 2;
+        }
+        hofs[i] = (unsigned)((gglob * 16 * H + ((kwv * NL + idx4) * 64 + ln) * 4) * 4);
+        yb[i] = chunk * NB + bl;
+        k0s[i] = k0;
+        ok[i] = yb[i] < p.B;
+      }
+      __syncthreads();  // the compute waves' set-up barrier
+      for (int t = 0; t < p.T; ++t) {
+        const int tt = dir ? (p.T - 1 - t) : t;
+        if (t > 0) {
+          if (!(p.diag & 2)) {
+            if (xcd_mode) {  // lane i watches workgroup i's flag (L2-served sc1 loads)
+              unsigned spins = 0;
+              for (;;) {
+                const unsigned f = lane < BPG ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT)
+                                              : (unsigned)t;
+                if (__all(f >= (unsigned)t)) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > SPIN_LIMIT) {
+                  if (lane == 0) {
+                    s_abort = 1;
+                    __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  }
+                  break;
+                }
+              }
+            } else if (lane == 0 && !poll_ge(cnt, (unsigned)t * BPG)) {
+              s_abort = 1;
+              __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+          __syncthreads();  // A
+          if (s_abort) break;
+        }
+        __syncthreads();  // B
+        __syncthreads();  // C: the stage holds h_t and y_t
+        const int soff = (t & 1) * hxp;
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int i = 0; i < FPL; ++i) {
+          const u32x4 v = *(const u32x4 *)&hstage[(lane + 64 * i) * 4];
+          if (ok[i]) {
+            if (xcd_mode)  // stays in this XCD's L2, read back by same-XCD sc1 loads
+              __builtin_amdgcn_raw_buffer_store_b128(v, rs, hofs[i], soff, 0);
+            else  // write-through (sc1)
+              __builtin_amdgcn_raw_buffer_store_b128(v, rs, hofs[i], soff, 16);
+          }
+        }
+        if (!(p.diag & 4)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+          if (xcd_mode)
+            __hip_atomic_store(flags + bi, (unsigned)(t + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);  // plain store, stays in L2
+          else
+            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // layer output after the hand-off: nothing in this launch reads y
+#pragma unroll
+        for (int i = 0; i < FPL; ++i) {
+          const f32x4 v = *(const f32x4 *)&ystage[(lane + 64 * i) * 4];
+          if (ok[i]) *(f32x4 *)(p.y + ((size_t)yb[i] * p.T + tt) * p.y_stride + dir * H + k0s[i]) = v;
+        }
+      }
+      return;
+    }
+  }
+
   // ---- W_hh slice -> VGPR A-fragments (loaded once) ---------------------------------
   // row block rb = wr*RBW + i, lane row lc; X6: k = wk*KW + ks*32 + 8*ls + j (j < 8)
   //                                        f32: k = wk*KW + ls*KB + kb
   const float *wdir = p.w_hh + (size_t)dir * (G * H) * H;
-  bf16x8 wa[X6 ? RBW : 1][X6 ? KS : 1][3];
+  bf16x8 wa[(X6 && !H3) ? RBW : 1][(X6 && !H3) ? KS : 1][3];
+  f16x8 wh[H3 ? RBW : 1][H3 ? KS : 1][2];  // [head, scaled tail]
   float wf[X6 ? 1 : RBW][X6 ? 1 : KB];
+  bool wbad = false;
 #pragma unroll
   for (int i = 0; i < RBW; ++i) {
     const int lrow = (wr * RBW + i) * 16 + lc;
@@ -224,7 +355,13 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
         const f32x4 b = *(const f32x4 *)(src + ks * 32 + 8 * ls + 4);
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
         v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        split3x8(v, wa[i][ks][0], wa[i][ks][1], wa[i][ks][2]);
+        if constexpr (H3) {
+          split2h8(v, wh[i][ks][0], wh[i][ks][1]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) wbad |= !(__builtin_fabsf(v[e]) <= 65504.f);
+        } else {
+          split3x8(v, wa[i][ks][0], wa[i][ks][1], wa[i][ks][2]);
+        }
       }
     } else {
 #pragma unroll
@@ -237,6 +374,8 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
       }
     }
   }
+
+  if (wbad && p.status) atomicOr(p.status, 2u);
 
   // ---- per-thread cells: cell c = tid + 256*j -> (unit u = c % U, seq b = c / U) ------
   int cu[CPT], cb[CPT], len[CPT], hxo[CPT];
@@ -278,21 +417,45 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
   const unsigned hoff = (unsigned)((gglob * slab + wk * NL * 256 + lane * 4) * 4);
   const int hx_par = p.ngroups_total * slab * 4;  // bytes between the two parity halves
 
-  // input projections (independent of h): step t+1's rows are fetched during step t
-  auto load_gx = [&](int t, float (&g)[CPT][G]) {
-    const int tt = dir ? (p.T - 1 - t) : t;
+  // input projections (independent of h), fetched two steps ahead through register rings
+  // of three sets; with the LengthRegulator map the frame's source row index is fetched a
+  // step before its projection row.  Every load is unconditional (clamped, valid address)
+  // so no value is ever selected or copied before its use: the compiler's vmcnt waits stay
+  // counted instead of draining (vector memory completes in issue order).
+  const int32_t *iptr[CPT];
+  size_t brow[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int b = cvalid[j] ? cb[j] : 0;
+    iptr[j] = p.index ? p.index + (size_t)b * p.T : (const int32_t *)p.ws;
+    brow[j] = (size_t)b * p.T_src;
+  }
+  const float *xcol = p.xp + dir * G * H + u0;   // + src row * stride + gate * H + unit
+  const float *zcol = (p.index ? p.xp_zero : p.xp) + dir * G * H + u0;
+  auto frame = [&](int t) { return dir ? (p.T - 1 - t) : t; };
+  auto load_idx = [&](int t, int (&ir)[CPT]) {
+    const int tt = frame(t < p.T ? t : p.T - 1);
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) ir[j] = iptr[j][p.index ? tt : 0];
+  };
+  auto load_gx = [&](int t, const int (&ir)[CPT], float (&g)[CPT][G]) {
+    const int tt = frame(t < p.T ? t : p.T - 1);
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
-      const int b = cvalid[j] ? cb[j] : 0;
-      int src = tt;
-      if (p.index) src = p.index[(size_t)b * p.T + tt];
-      const float *row = src >= 0 ? p.xp + ((size_t)b * p.T_src + src) * p.xp_stride : p.xp_zero;
+      const int src = p.index ? ir[j] : tt;
+      const float *row = src >= 0 ? xcol + (brow[j] + src) * p.xp_stride : zcol;
+      if (p.diag & 1) row = zcol;  // timing experiment: L2-hot rows
 #pragma unroll
-      for (int gi = 0; gi < G; ++gi) g[j][gi] = row[dir * G * H + gi * H + u0 + cu[j]];
+      for (int gi = 0; gi < G; ++gi) g[j][gi] = row[gi * H + cu[j]];
     }
   };
-  float gx[CPT][G], gxn[CPT][G], yo[CPT];
-  load_gx(0, gx);
+  float g0[CPT][G], g1[CPT][G], g2[CPT][G];
+  int i0[CPT], i1[CPT], i2[CPT];
+  load_idx(0, i0);
+  load_idx(1, i1);
+  load_gx(0, i0, g0);
+  load_gx(1, i1, g1);
+  load_idx(2, i2);
   if (LOCAL)
     for (int i = tid; i < 16 * H; i += 256) hloc[i] = 0.f;
   __syncthreads();
@@ -302,35 +465,15 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
   if (tid == 0) st_last = __builtin_amdgcn_s_memtime();
 #endif
 
-  for (int t = 0; t < p.T; ++t) {
-    const int tt = dir ? (p.T - 1 - t) : t;
+  // one time step; returns false when the launch must stop (hand-off timeout)
+  auto step = [&](int t, const float (&gx)[CPT][G], float (&gnext)[CPT][G],
+                  const int (&inext)[CPT], int (&iload)[CPT]) -> bool {
+    const int tt = frame(t);
     STAMP(0);
-    // wait until every workgroup of the group has published h_{t-1}
+    // the comm wave has seen every workgroup of the group publish h_{t-1}
     if (!LOCAL && t > 0) {
-      if (xcd_mode) {
-        if (wave == 0) {  // lane i watches workgroup i's flag (L2-served sc1 loads)
-          unsigned spins = 0;
-          for (;;) {
-            const unsigned f = lane < BPG ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT)
-                                          : (unsigned)t;
-            if (__all(f >= (unsigned)t)) break;
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > SPIN_LIMIT) {
-              if (lane == 0) {
-                s_abort = 1;
-                __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              }
-              break;
-            }
-          }
-        }
-      } else if (tid == 0 && !poll_ge(cnt, (unsigned)t * BPG)) {
-        s_abort = 1;
-        __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
       __syncthreads();
-      if (s_abort) break;
+      if (s_abort) return false;
     }
     STAMP(1);
 
@@ -363,14 +506,35 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
         hv[4 * i + 3] = v.w;
       }
     }
-    if (t + 1 < p.T) load_gx(t + 1, gxn);
+    load_gx(t + 2, inext, gnext);
+    load_idx(t + 3, iload);
     STAMP(2);
 
     // partial gates over this wave's K range
     f32x4 acc[RBW];
 #pragma unroll
     for (int i = 0; i < RBW; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if constexpr (X6) {
+    if constexpr (H3) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = hv[ks * 8 + e];
+        f16x8 hh, ht;
+        split2h8(v, hh, ht);
+        const f16x8 hs = hh * (_Float16)H3_SCALE;  // 2^11 h_h: exact, |h| < 1
+#pragma unroll
+        for (int i = 0; i < RBW; ++i) {
+          f32x4 c = acc[i];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i][ks][1], hh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i][ks][0], ht, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i][ks][0], hs, c, 0, 0, 0);
+          acc[i] = c;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < RBW; ++i) acc[i] *= H3_UNSCALE;
+    } else if constexpr (X6) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         float v[8];
@@ -441,40 +605,27 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
         yout = p.pad_value;
       }
       hstate[j] = hn;
-      if (cvalid[j]) {
-        if constexpr (LOCAL) {
+      if constexpr (LOCAL) {
+        if (cvalid[j]) {
           hloc[(t & 1) * slab + hxo[j]] = hn;
-        } else {
-          float *dst = p.hx + (size_t)(t & 1) * p.ngroups_total * slab + gglob * slab + hxo[j];
-          if (xcd_mode)
-            *dst = hn;  // stays in this XCD's L2, read back by same-XCD sc1 loads
-          else
-            __hip_atomic_store(dst, hn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          p.y[((size_t)cb[j] * p.T + tt) * p.y_stride + dir * H + u0 + cu[j]] = yout;
         }
+      } else {  // to the comm wave: cell c = bl * U + unit is also its float4 order
+        const int c = bl * U + cu[j];
+        hstage[c] = hn;
+        ystage[c] = yout;
       }
-      yo[j] = yout;
     }
-#pragma unroll
-    for (int j = 0; j < CPT; ++j)
-#pragma unroll
-      for (int gi = 0; gi < G; ++gi) gx[j][gi] = gxn[j][gi];
     STAMP(4);
-
-    // publish: every storing wave drains, barrier, one lane arrives
-    if constexpr (!LOCAL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (!LOCAL && tid == 0) {
-      if (xcd_mode)
-        __hip_atomic_store(flags + bi, (unsigned)(t + 1), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);  // plain store, stays in L2
-      else
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // layer output after the hand-off: nothing in this launch reads y
-#pragma unroll
-    for (int j = 0; j < CPT; ++j)
-      if (cvalid[j]) p.y[((size_t)cb[j] * p.T + tt) * p.y_stride + dir * H + u0 + cu[j]] = yo[j];
+    __syncthreads();  // LOCAL: h_t visible in LDS; else: staged for the comm wave
     STAMP(5);
+    return true;
+  };
+
+  for (int t = 0; t < p.T; t += 3) {
+    if (!step(t, g0, g2, i2, i0)) break;
+    if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1)) break;
+    if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2)) break;
   }
 #ifdef FTMI_RNN_STAMPS
   if (tid == 0)
@@ -482,7 +633,7 @@ __global__ __launch_bounds__(256, 1) void rnn_bidir_kernel(const RnnParams p) {
 #endif
 }
 
-template <int CELL, int H, int U, int WK, bool X6>
+template <int CELL, int H, int U, int WK, int MODE>
 int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
   constexpr int BPG = H / U;
   int max_groups = (max_blocks / BPG) & ~1;
@@ -495,8 +646,8 @@ int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
       hipError_t e = hipMemsetAsync(p.ws + WS_CENSUS, 0, (WS_FLAGS - WS_CENSUS) * 4, s);
       if (e != hipSuccess) return (int)e;
     }
-    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, X6>), dim3(p.ngroups * BPG), dim3(256),
-                       0, s, p);
+    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE>), dim3(p.ngroups * BPG),
+                       dim3(BPG == 1 ? 256 : 320), 0, s, p);
     FTMI_CHECK_LAUNCH();
   }
   return FTMI_OK;
@@ -537,13 +688,16 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
                               int64_t xp_stride, int32_t T_src, const int32_t *index,
                               const float *xp_zero, const float *w_hh, const float *b_hh,
                               const int32_t *lengths, float pad_value, float *y,
-                              int64_t y_stride, void *sync, ftmi_stream_t stream) {
+                              int64_t y_stride, int32_t mma, uint32_t *status, void *sync,
+                              ftmi_stream_t stream) {
   if (!xp || !w_hh || !y || !sync) return FTMI_E_ARG;
   if (B <= 0 || T <= 0 || H <= 0 || T_src <= 0) return FTMI_E_ARG;
+  if (mma < 0 || mma > 2) return FTMI_E_ARG;
   if (cell == 0 && !b_hh) return FTMI_E_ARG;
   if (index && !xp_zero) return FTMI_E_ARG;
   if (!index && T_src != T) return FTMI_E_SHAPE;
   if (!ftmi_aligned16(w_hh) || !ftmi_aligned16(sync)) return FTMI_E_ALIGN;
+  if (!ftmi_aligned16(y) || (y_stride & 3)) return FTMI_E_ALIGN;  // float4 row stores
   hipStream_t s = ftmi_hs(stream);
   const int nchunks = (B + NB - 1) / NB;
   const int64_t ctl = ctl_bytes(nchunks);
@@ -552,10 +706,6 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   if (e != hipSuccess) return (int)e;
   static const int xcd_env = [] {
     const char *v = getenv("FTMI_RNN_XCD_LOCAL");
-    return v ? atoi(v) : 1;
-  }();
-  static const int x6_env = [] {
-    const char *v = getenv("FTMI_RNN_MMA");
     return v ? atoi(v) : 1;
   }();
   RnnParams p = {};
@@ -576,20 +726,24 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   p.xcd_local = xcd_env;
   p.ws = (unsigned *)sync;
   p.hx = (float *)((char *)sync + ctl);
+  p.status = status;
+  static const int diag_env = [] {
+    const char *v = getenv("FTMI_RNN_DIAG");
+    return v ? atoi(v) : 0;
+  }();
+  p.diag = diag_env;
   const int maxb = device_cu_count();
-  const bool x6 = x6_env != 0;
-  if (cell == 0 && H == 64)
-    return x6 ? launch_rnn<0, 64, 64, 2, true>(p, nchunks, maxb, s)
-              : launch_rnn<0, 64, 64, 4, false>(p, nchunks, maxb, s);
-  if (cell == 0 && H == 128)
-    return x6 ? launch_rnn<0, 128, 64, 4, true>(p, nchunks, maxb, s)
-              : launch_rnn<0, 128, 64, 4, false>(p, nchunks, maxb, s);
-  if (cell == 0 && H == 256)
-    return x6 ? launch_rnn<0, 256, 16, 4, true>(p, nchunks, maxb, s)
-              : launch_rnn<0, 256, 16, 4, false>(p, nchunks, maxb, s);
-  if (cell == 1 && H == 512)
-    return x6 ? launch_rnn<1, 512, 16, 4, true>(p, nchunks, maxb, s)
-              : launch_rnn<1, 512, 16, 4, false>(p, nchunks, maxb, s);
+#define FTMI_RNN_MODES(CELL_, H_, U_, WKX_, WKF_)                                   \
+  switch (mma) {                                                                    \
+    case 2: return launch_rnn<CELL_, H_, U_, WKX_, 2>(p, nchunks, maxb, s);          \
+    case 1: return launch_rnn<CELL_, H_, U_, WKX_, 1>(p, nchunks, maxb, s);          \
+    default: return launch_rnn<CELL_, H_, U_, WKF_, 0>(p, nchunks, maxb, s);         \
+  }
+  if (cell == 0 && H == 64) FTMI_RNN_MODES(0, 64, 64, 2, 4)
+  if (cell == 0 && H == 128) FTMI_RNN_MODES(0, 128, 64, 4, 4)
+  if (cell == 0 && H == 256) FTMI_RNN_MODES(0, 256, 16, 4, 4)
+  if (cell == 1 && H == 512) FTMI_RNN_MODES(1, 512, 16, 4, 4)
+#undef FTMI_RNN_MODES
   return FTMI_E_UNSUPPORTED;
 }
 

@@ -248,8 +248,8 @@ class FastPitch(nn.Module):
         h = self.postnet.layers_cl(h, kpm)
         B, T_mel = index.shape
         mel = torch.empty(B, self.n_mels, T_mel, device=enc.device)
-        ops.conv1d(h, self.lin.weight.detach(), 1, 0, bias=self.lin.bias.detach(), out_t=mel,
-                   want_y=False)
+        w, b, w3 = self.lin.packed_weights()
+        ops.conv1d(h, w, 1, 0, bias=b, out_t=mel, want_y=False, w_split=w3)
         return mel
 
     def _side_streams(self, device):
@@ -266,9 +266,15 @@ class FastPitch(nn.Module):
                  batch=None) -> Dict[str, torch.Tensor]:
         """`models/fast_pitch.py:286-303`: predictors without masks; the prenet on side
         streams overlaps the duration path and its one host sync (T_mel).  `batch`: a
-        sharded.GlobalBatch when x is one rank's shard of a larger batch."""
+        sharded.GlobalBatch when x is one rank's shard of a larger batch.  Runs under the
+        f16x3 range guard (ops.run_checked)."""
         self.eval()
         self._check_device(x)
+        return ops.run_checked(
+            lambda: self._generate(x, alpha, pitch_function, energy_function, batch), x.device,
+            reduce=None if batch is None else batch.status)
+
+    def _generate(self, x, alpha, pitch_function, energy_function, batch):
         with torch.no_grad():
             main = torch.cuda.current_stream(x.device)
             s_pitch, s_energy, s_prenet = self._side_streams(x.device)
@@ -315,13 +321,17 @@ class FastPitch(nn.Module):
         """Teacher-forced pass (`models/fast_pitch.py:233-283`), inference numerics."""
         x = batch['x']
         self._check_device(x)
+        if self.training:
+            self.step += 1
+        return ops.run_checked(lambda: self._forward(batch), x.device)
+
+    def _forward(self, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        x = batch['x']
         mel = batch['mel']
         dur = batch['dur']
         mel_lens = batch['mel_len']
         pitch = batch['pitch'].unsqueeze(1)
         energy = batch['energy'].unsqueeze(1)
-        if self.training:
-            self.step += 1
         with torch.no_grad():
             len_mask = x == 0
             dur_hat = self.dur_pred.forward_bt(x, len_mask)

@@ -169,12 +169,13 @@ class ForwardTacotron(nn.Module):
                                         pad_value=self.padding_value)
         mel_cl = torch.empty(B, T_mel, self.n_mels, device=enc.device)
         mel = torch.empty(B, self.n_mels, T_mel, device=enc.device)
-        ops.conv1d(lstm_out, self.lin.weight.detach(), 1, 0, bias=self.lin.bias.detach(),
-                   out=mel_cl, out_t=mel)
+        w, b, w3 = self.lin.packed_weights()
+        ops.conv1d(lstm_out, w, 1, 0, bias=b, out=mel_cl, out_t=mel, w_split=w3)
         del lstm_out
         post = self.postnet.forward_cl(mel_cl)
         mel_post = torch.empty(B, self.n_mels, T_mel, device=enc.device)
-        ops.conv1d(post, self.post_proj.weight.detach(), 1, 0, out_t=mel_post, want_y=False)
+        w, _, w3 = self.post_proj.packed_weights()
+        ops.conv1d(post, w, 1, 0, out_t=mel_post, want_y=False, w_split=w3)
         return mel, mel_post
 
     # ---------------------------------------------------------------------------------
@@ -182,13 +183,17 @@ class ForwardTacotron(nn.Module):
         """Teacher-forced pass (`models/forward_tacotron.py:184-242`), inference numerics."""
         x = batch['x']
         self._check_device(x)
+        if self.training:
+            self.step += 1
+        return ops.run_checked(lambda: self._forward(batch), x.device)
+
+    def _forward(self, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        x = batch['x']
         mel = batch['mel']
         mel_lens = batch['mel_len']
         dur = batch['dur']
         pitch = batch['pitch'].unsqueeze(1)
         energy = batch['energy'].unsqueeze(1)
-        if self.training:
-            self.step += 1
         with torch.no_grad():
             dur_hat = self.dur_pred.forward_bt(x)
             pitch_hat = self.pitch_pred.forward_bt(x).unsqueeze(1)
@@ -252,23 +257,30 @@ class ForwardTacotron(nn.Module):
                  batch=None) -> Dict[str, torch.Tensor]:
         """`models/forward_tacotron.py:244-268`.  The callbacks run on the stream of their
         predictor (torch ops issued inside them are ordered after the prediction).
-        `batch`: a sharded.GlobalBatch when x is one rank's shard of a larger batch."""
+        `batch`: a sharded.GlobalBatch when x is one rank's shard of a larger batch.
+        Runs under the f16x3 range guard (ops.run_checked): one status read at the end."""
         self.eval()
         self._check_device(x)
-        with torch.no_grad():
-            dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel = self._phoneme_phase(
-                x, alpha, pitch_function, energy_function, batch)
-            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
-                                      lr=(offsets, T_mel))
+
+        def run():
+            with torch.no_grad():
+                dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel = self._phoneme_phase(
+                    x, alpha, pitch_function, energy_function, batch)
+                return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
+                                          lr=(offsets, T_mel))
+        return ops.run_checked(run, x.device, reduce=None if batch is None else batch.status)
 
     def generate_jit(self, x: torch.Tensor, alpha: float = 1.0, beta: float = 1.0) -> Dict[str, torch.Tensor]:
         """`models/forward_tacotron.py:270-284` (pitch scaled by beta, no callbacks)."""
         self._check_device(x)
-        with torch.no_grad():
-            dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel = self._phoneme_phase(
-                x, alpha, lambda p: p * beta, lambda e: e)
-            return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
-                                      lr=(offsets, T_mel))
+
+        def run():
+            with torch.no_grad():
+                dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel = self._phoneme_phase(
+                    x, alpha, lambda p: p * beta, lambda e: e)
+                return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
+                                          lr=(offsets, T_mel))
+        return ops.run_checked(run, x.device)
 
     def get_step(self) -> int:
         return self.step.data.item()

@@ -7,6 +7,7 @@ a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from typing import Optional, Tuple
@@ -20,11 +21,73 @@ from .probe import launch
 
 _f32 = torch.float32
 
-# Matrix path of the dense contractions (include/ftmi.h FTMI_MMA_*): 1 = bf16x6 split
-# (fp32-accurate, 2.7x the fp32 MFMA rate), 0 = plain fp32 MFMA.  FTMI_MMA=0/1 overrides.
-MMA = int(os.environ.get('FTMI_MMA', '1'))
-# the recurrences' matrix path (read by rnn.hip itself; mirrored here for the labels)
-RNN_MMA = int(os.environ.get('FTMI_RNN_MMA', '1'))
+# Matrix path of the dense contractions (include/ftmi.h FTMI_MMA_*): 2 = f16x3 split
+# (default; fp32-level accuracy at 5.3x the fp32 MFMA rate, activations < 65504),
+# 1 = bf16x6 split (fp32-accurate, 2.7x), 0 = plain fp32 MFMA.  FTMI_MMA overrides.
+MMA = int(os.environ.get('FTMI_MMA', '2'))
+# the recurrences' W_hh h path (same codes; FTMI_RNN_MMA overrides)
+RNN_MMA = int(os.environ.get('FTMI_RNN_MMA', '2'))
+
+# f16x3 range guard.  Every GEMM / recurrence launch ORs into a per-device status word:
+# bit 0 = an f16x3 accumulator became non-finite (an activation beyond the f16 range),
+# bit 1 = a W_hh entry beyond the f16 range.  The model entry points zero it, run, read it
+# once at the end, and on a non-zero word run the call again under `exact_paths()` (fp32
+# MFMA everywhere), which has no range limit.
+_STATUS = {}
+_FORCED = []  # stack of (gemm mma, rnn mma) overrides
+
+
+def status_word(device) -> torch.Tensor:
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device(dev.type, torch.cuda.current_device())
+    t = _STATUS.get(dev)
+    if t is None:
+        t = _STATUS[dev] = torch.zeros(1, device=dev, dtype=torch.int32)
+    return t
+
+
+@contextlib.contextmanager
+def exact_paths():
+    """Run the enclosed calls on the range-unlimited fp32 MFMA paths (GEMMs and
+    recurrences)."""
+    _FORCED.append((0, 0))
+    try:
+        yield
+    finally:
+        _FORCED.pop()
+
+
+def _gemm_mma(mma: Optional[int], w_split):
+    """(matrix path, w_split pointer) of one GEMM launch.  f16x3 needs the f16 planes
+    (uint8 block of split_weights_f16); without them the launch uses bf16x6, which takes
+    its bf16 pieces (split_weights) or splits the weights in-kernel."""
+    m = _FORCED[-1][0] if _FORCED else (MMA if mma is None else mma)
+    has16 = w_split is not None and w_split.dtype == torch.uint8
+    hasbf = w_split is not None and w_split.dtype == torch.bfloat16
+    if m == 2 and not has16:
+        m = 1
+    ptr = w_split.data_ptr() if (m == 2 and has16) or (m == 1 and hasbf) else None
+    return m, ptr
+
+
+def _rnn_mma() -> int:
+    return _FORCED[-1][1] if _FORCED else RNN_MMA
+
+
+def run_checked(fn, device, reduce=None):
+    """fn() with the f16x3 range guard: zero the status word, run, read it (one host sync)
+    and, if any bit is set, run fn() again under exact_paths().  reduce(word) -> word
+    combines the status over ranks (sharded generation) before the decision."""
+    st = status_word(device)
+    st.zero_()
+    out = fn()
+    if not _FORCED:
+        s = st if reduce is None else reduce(st)
+        if int(s.item()) != 0:
+            with exact_paths():
+                out = fn()
+    return out
 
 
 def _num_cus() -> int:
@@ -35,9 +98,9 @@ def _num_cus() -> int:
 
 
 def _split_k(M: int, N: int, K: int, mma: int) -> int:
-    """Split K when the tile grid cannot fill the chip (x6 kernel: 2 workgroups per CU)
-    and K is long enough for the partial-sum round trip to pay."""
-    if mma != 1 or K < 2048:
+    """Split K when the tile grid cannot fill the chip (x6 / h3 kernels: 2 workgroups per
+    CU) and K is long enough for the partial-sum round trip to pay."""
+    if mma == 0 or K < 2048:
         return 1
     tiles = -(-M // 128) * -(-N // 128)
     slots = 2 * _num_cus()
@@ -100,13 +163,41 @@ def split_weights(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def split_bank_weights(w: torch.Tensor, K: int, Cin: int, Cout: int) -> torch.Tensor:
-    """Pre-split pieces of a packed conv bank: group g's [3][Cout][roundup((g+1)Cin, 32)]
-    back to back (the `w_split` layout of `ftmi_conv_bank`)."""
+def split_weights_f16(w: torch.Tensor) -> torch.Tensor:
+    """fp32 [N][K] -> the f16x3 operand of `ftmi_split_weights_f16` (uint8 bytes: f16 planes
+    [3][N][roundup(K, 32)] = (2^11 h, t, h) of the power-of-two column-scaled rows, then
+    float colscale[N])."""
+    _dev(w)
+    if w.dim() != 2 or w.dtype != _f32 or not w.is_contiguous():
+        raise ValueError('split_weights_f16: contiguous fp32 [N][K] expected')
+    N, K = w.shape
+    nbytes = int(_lib.load().ftmi_split_weights_f16_bytes(N, K))
+    out = torch.empty(nbytes, device=w.device, dtype=torch.uint8)
+    launch('ftmi_split_weights_f16', f'split_weights_f16[N={N},K={K}]', 0, 4.0 * N * K + nbytes,
+           w.data_ptr(), N, K, out.data_ptr(), _stream())
+    return out
+
+
+def presplit_for(w: torch.Tensor, mma: Optional[int] = None) -> Optional[torch.Tensor]:
+    """The pre-split operand of a packed weight for the matrix path `mma` (default MMA):
+    f16 planes (2), bf16 pieces (1), None (0)."""
+    m = MMA if mma is None else mma
+    if m == 2:
+        return split_weights_f16(w)
+    return split_weights(w) if m == 1 else None
+
+
+def split_bank_weights(w: torch.Tensor, K: int, Cin: int, Cout: int,
+                       mma: Optional[int] = None) -> Optional[torch.Tensor]:
+    """Pre-split blocks of a packed conv bank: group g's `presplit_for` block of the
+    [Cout][(g+1) Cin] weight, back to back (the `w_split` layout of `ftmi_conv_bank`)."""
     parts, off = [], 0
     for g in range(K):
         n = Cout * Cin * (g + 1)
-        parts.append(split_weights(w[off:off + n].view(Cout, (g + 1) * Cin)).reshape(-1))
+        blk = presplit_for(w[off:off + n].view(Cout, (g + 1) * Cin), mma)
+        if blk is None:
+            return None
+        parts.append(blk.reshape(-1).view(torch.uint8))
         off += n
     return torch.cat(parts)
 
@@ -146,8 +237,8 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
         a.y, a.y_stride = y.data_ptr(), y.stride(1)
     a.yt = _ptr(out_t)
     a.T_out = To
-    a.mma = MMA if mma is None else mma
-    a.w_split = _ptr(w_split)
+    a.mma, a.w_split = _gemm_mma(mma, w_split)
+    a.status = status_word(x.device).data_ptr()
     M = B * To
     sk = _split_k(M, N, k * Cin, a.mma)
     if sk > 1:
@@ -169,11 +260,12 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
     y = torch.empty(B, T, K * Cout, device=x.device, dtype=_f32)
     M = B * T
     flops = 2.0 * M * Cout * Cin * K * (K + 1) / 2
-    mma = MMA if mma is None else mma
+    mma, wsp = _gemm_mma(mma, w_split)
     launch('ftmi_conv_bank', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}]', flops,
            4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
-           x.data_ptr(), xs, B, T, Cin, w.data_ptr(), _ptr(w_split), K, Cout, scale.data_ptr(),
-           shift.data_ptr(), y.data_ptr(), y.stride(1), mma, _stream())
+           x.data_ptr(), xs, B, T, Cin, w.data_ptr(), wsp, K, Cout,
+           scale.data_ptr(), shift.data_ptr(), y.data_ptr(), y.stride(1), mma,
+           status_word(x.device).data_ptr(), _stream())
     return y
 
 
@@ -184,11 +276,12 @@ def highway(x: torch.Tensor, w12: torch.Tensor, b1: torch.Tensor, b2: torch.Tens
     B, T, C, xs = _rows(x)
     y = out if out is not None else torch.empty(B, T, C, device=x.device, dtype=_f32)
     M = B * T
-    mma = MMA if mma is None else mma
+    mma, wsp = _gemm_mma(mma, w_split)
     launch('ftmi_highway', f'highway[M={M},C={C},mma={mma}]', 2.0 * M * 2 * C * C,
            4.0 * (2 * M * C + 2 * C * C),
-           x.data_ptr(), xs, M, C, w12.data_ptr(), _ptr(w_split), b1.data_ptr(), b2.data_ptr(),
-           y.data_ptr(), y.stride(1), mma, _stream())
+           x.data_ptr(), xs, M, C, w12.data_ptr(), wsp, b1.data_ptr(),
+           b2.data_ptr(), y.data_ptr(), y.stride(1), mma, status_word(x.device).data_ptr(),
+           _stream())
     return y
 
 
@@ -200,12 +293,14 @@ def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Opt
               T: Optional[int] = None, index: Optional[torch.Tensor] = None,
               xp_zero: Optional[torch.Tensor] = None, lengths: Optional[torch.Tensor] = None,
               pad_value: float = 0.0, check: bool = False,
-              ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+              ws: Optional[torch.Tensor] = None, mma: Optional[int] = None) -> torch.Tensor:
     """Bidirectional GRU (cell=0) / LSTM (cell=1) recurrence -> (B, T, 2H).
 
     xp: (B, T_src, 2*G*H) input projections; index: (B, T) int32 frame -> row map.
     check=True synchronises and raises RnnTimeout if a workgroup gave up waiting.
+    mma: matrix path of W_hh h (default RNN_MMA; exact_paths() forces fp32).
     """
+    mma = (_rnn_mma() if mma is None or _FORCED else mma)
     if lengths is not None:  # host-side lengths (as pack_padded_sequence takes) are fine
         lengths = lengths.to(device=xp.device, dtype=torch.int32).contiguous()
     _dev(xp, w_hh, b_hh, index, xp_zero, lengths)
@@ -219,14 +314,14 @@ def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Opt
     if index is not None:
         assert index.dtype == torch.int32 and index.is_contiguous() and index.shape == (B, T)
     G = 4 if cell else 3
-    label = f'rnn_bidir[{"lstm" if cell else "gru"},B={B},T={T},H={H},mma={RNN_MMA}]'
+    label = f'rnn_bidir[{"lstm" if cell else "gru"},B={B},T={T},H={H},mma={mma}]'
     # recurrent contraction W_hh h per step and direction; bytes: xp rows read per frame,
     # W_hh once, y written once
     launch('ftmi_rnn_bidir', label, 2.0 * B * T * 2 * G * H * H,
            4.0 * (B * T * 2 * G * H + 2 * G * H * H + B * T * 2 * H),
            cell, B, T, H, xp.data_ptr(), xs, T_src, _ptr(index), _ptr(xp_zero),
            w_hh.data_ptr(), _ptr(b_hh), _ptr(lengths), float(pad_value), y.data_ptr(), y.stride(1),
-           ws.data_ptr(), _stream())
+           int(mma), status_word(xp.device).data_ptr(), ws.data_ptr(), _stream())
     if check:
         torch.cuda.current_stream().synchronize()
         off = int(lib.ftmi_rnn_error_offset(B)) // 4

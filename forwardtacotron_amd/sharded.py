@@ -94,6 +94,14 @@ class GlobalBatch:
         local = int(totals.max().item()) if totals.numel() else 0
         return global_max(local, self.group, totals.device)
 
+    def status(self, word: torch.Tensor) -> torch.Tensor:
+        """The f16x3 range-guard word (ops.run_checked) combined over ranks (MAX: non-zero
+        anywhere -> non-zero everywhere), so every rank takes the same rerun decision."""
+        dev = _coll_device(self.group, word.device)
+        h = word.clone() if dev == word.device else word.to(dev)
+        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=self.group)
+        return h
+
 
 def broadcast_state(model: torch.nn.Module, src: int = 0, group=None) -> None:
     """Copy rank `src`'s parameters and buffers to every rank (one broadcast per tensor)."""

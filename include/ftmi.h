@@ -39,8 +39,15 @@ enum {
  *   FTMI_MMA_BF16X6  each fp32 operand split into three bf16 pieces (a = a1+a2+a3, exact),
  *                    the six cross products with i+j <= 4 on v_mfma_f32_16x16x32_bf16 with
  *                    fp32 accumulation: fp32-accurate (dropped terms < 2^-24 relative) at
- *                    16/6 of the fp32 MFMA rate. */
-enum { FTMI_MMA_F32 = 0, FTMI_MMA_BF16X6 = 1 };
+ *                    16/6 of the fp32 MFMA rate.
+ *   FTMI_MMA_F16X3   (default) each operand split into an f16 head and a 2^11-scaled f16
+ *                    tail; weights pre-split by ftmi_split_weights_f16 (three f16 planes
+ *                    + a power-of-two column scale); three v_mfma_f32_16x16x32_f16 per
+ *                    product, fp32 accumulation: fp32-level accuracy (dropped terms
+ *                    < 2^-22 relative) at 16/3 of the fp32 MFMA rate.  Activations must
+ *                    stay below 65504 in magnitude: otherwise the output is invalid and
+ *                    bit 0 of *status (optional) is set — recompute on FTMI_MMA_F32. */
+enum { FTMI_MMA_F32 = 0, FTMI_MMA_BF16X6 = 1, FTMI_MMA_F16X3 = 2 };
 
 /* ABI version; bumped on any signature change. */
 int ftmi_abi_version(void);
@@ -87,14 +94,15 @@ typedef struct ftmi_conv_args {
   int64_t y_stride;
   float *yt; /* (B,N,T_out) or NULL */
   int32_t T_out; /* output frames per sequence, 0 = T (even k in PyTorch gives T+1) */
-  int32_t mma;   /* matrix path: FTMI_MMA_F32 or FTMI_MMA_BF16X6 (both fp32-accurate) */
-  int32_t split_k;  /* > 1: split K over that many workgroups (FTMI_MMA_BF16X6 only); partial
-                       sums go to split_ws and a second launch sums them in fixed order
-                       (deterministic) and applies the epilogue */
+  int32_t mma;   /* matrix path: FTMI_MMA_F32, FTMI_MMA_BF16X6 or FTMI_MMA_F16X3 */
+  int32_t split_k;  /* > 1: split K over that many workgroups (FTMI_MMA_BF16X6 / F16X3);
+                       partial sums go to split_ws and a second launch sums them in fixed
+                       order (deterministic) and applies the epilogue */
   float *split_ws;  /* split_k * B*T_out * N floats of caller-owned workspace, or NULL */
-  const void *w_split; /* optional bf16 [3][N][roundup(k*Cin, 32)] pieces of w made by
-                          ftmi_split_weights: FTMI_MMA_BF16X6 then skips the per-call
-                          weight split (fastest path) */
+  const void *w_split; /* FTMI_MMA_BF16X6: optional ftmi_split_weights pieces (skips the
+                          per-call weight split); FTMI_MMA_F16X3: REQUIRED
+                          ftmi_split_weights_f16 planes */
+  uint32_t *status;    /* optional device word: bit 0 set on f16 range overflow (F16X3) */
 } ftmi_conv_args;
 
 /* Split fp32 weights [N][K] once into three bf16 pieces (w = p0 + p1 + p2 exactly), laid
@@ -102,6 +110,16 @@ typedef struct ftmi_conv_args {
  * ftmi_split_weights_bytes(N, K) bytes (16-byte aligned). */
 int64_t ftmi_split_weights_bytes(int64_t N, int64_t K);
 int ftmi_split_weights(const float *w, int64_t N, int64_t K, void *out, ftmi_stream_t stream);
+
+/* Split fp32 weights [N][K] once for FTMI_MMA_F16X3: per row n a power-of-two scale
+ * s_n = 2^-e (smallest e >= 0 with max|w[n]| s_n < 16), h = f16(w s_n),
+ * t = f16((w s_n - h) * 2^11); layout: f16 planes [3][N][Kpad] = (2^11 h, t, h), Kpad =
+ * roundup(K, 32), zero padded, then float colscale[N] = 2^-11 / s_n.  out must hold
+ * ftmi_split_weights_f16_bytes(N, K) bytes (16-byte aligned).  The conv bank's w_split
+ * is each group's block back to back. */
+int64_t ftmi_split_weights_f16_bytes(int64_t N, int64_t K);
+int ftmi_split_weights_f16(const float *w, int64_t N, int64_t K, void *out,
+                           ftmi_stream_t stream);
 
 int ftmi_conv1d(const ftmi_conv_args *args, ftmi_stream_t stream);
 
@@ -111,25 +129,26 @@ int ftmi_conv1d(const ftmi_conv_args *args, ftmi_stream_t stream);
  *   y[b,t, g*Cout + n] = BN_g(relu(sum_{j<=g} sum_c w_g[n, j*Cin+c] * x[b, t+j-(g+1)/2, c]))
  * w: the K packed weights back to back, group g is [Cout][(g+1)*Cin] starting at float
  * offset Cout*Cin*g*(g+1)/2.  bn_scale / bn_shift: [K*Cout].  y: (B,T,K*Cout) rows.
- * w_split (optional): each group's ftmi_split_weights pieces back to back.
+ * w_split: each group's ftmi_split_weights (BF16X6, optional) or ftmi_split_weights_f16
+ * (F16X3, required) block back to back.  status: as in ftmi_conv_args.
  * ---------------------------------------------------------------------------------- */
 int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t Cin,
                    const float *w, const void *w_split, int32_t K, int32_t Cout,
                    const float *bn_scale,
                    const float *bn_shift, float *y, int64_t y_stride, int32_t mma,
-                   ftmi_stream_t stream);
+                   uint32_t *status, ftmi_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * One highway layer (common_layers.py:22-35):
  *   g = sigmoid(x W2^T + b2);  y = g * relu(x W1^T + b1) + (1 - g) * x
  * w12: [2C][C] with rows interleaved in blocks of 32: rows 64q..64q+31 = W1 rows
  * 32q..32q+31, rows 64q+32..64q+63 = W2 rows 32q..32q+31.  Requires C % 32 == 0.
- * w12_split (optional): ftmi_split_weights pieces of w12.
- * y must not alias x.
+ * w12_split: ftmi_split_weights (BF16X6, optional) / ftmi_split_weights_f16 (F16X3,
+ * required) of w12.  status: as in ftmi_conv_args.  y must not alias x.
  * ---------------------------------------------------------------------------------- */
 int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t C, const float *w12,
                  const void *w12_split, const float *b1, const float *b2, float *y,
-                 int64_t y_stride, int32_t mma, ftmi_stream_t stream);
+                 int64_t y_stride, int32_t mma, uint32_t *status, ftmi_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Bidirectional single-layer GRU / LSTM recurrence, PyTorch semantics, h0 = c0 = 0,
@@ -147,6 +166,9 @@ int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t C, const f
  *     pad_packed_sequence, forward_tacotron.py:224-230): frames t >= lengths[b] output
  *     pad_value and the reverse direction starts from h = c = 0 at t = lengths[b]-1.
  * y:    (B, T, 2H) rows with y_stride.
+ * mma:  matrix path of W_hh h: FTMI_MMA_F16X3 (default; W_hh split in-kernel, bit 1 of
+ *     *status set if an entry exceeds the f16 range — rerun with FTMI_MMA_BF16X6),
+ *     FTMI_MMA_BF16X6 or FTMI_MMA_F32.  status: optional device word.
  * sync: 16-byte aligned device workspace of ftmi_rnn_workspace_bytes() bytes (zeroed by
  *     the call; holds the arrival counters and the h exchange buffer).  After the stream
  *     has completed, the 32-bit word at byte offset ftmi_rnn_error_offset() is non-zero if
@@ -159,7 +181,7 @@ int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, const float *x
                    int64_t xp_stride, int32_t T_src, const int32_t *index,
                    const float *xp_zero, const float *w_hh, const float *b_hh,
                    const int32_t *lengths, float pad_value, float *y, int64_t y_stride,
-                   void *sync, ftmi_stream_t stream);
+                   int32_t mma, uint32_t *status, void *sync, ftmi_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Duration post-processing of ForwardTacotron.generate + LengthRegulator counts:

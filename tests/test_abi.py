@@ -48,10 +48,11 @@ def test_strerror():
 @pytest.mark.parametrize('call,code', [
     (lambda L: L.ftmi_embedding(None, 4, None, 135, 256, None, None, None), 1001),
     (lambda L: L.ftmi_conv1d(None, None), 1001),
-    (lambda L: L.ftmi_conv_bank(None, 0, 1, 1, 16, None, None, 4, 8, None, None, None, 0, 1, None), 1001),
-    (lambda L: L.ftmi_highway(None, 0, 1, 32, None, None, None, None, None, 0, 1, None), 1001),
+    (lambda L: L.ftmi_conv_bank(None, 0, 1, 1, 16, None, None, 4, 8, None, None, None, 0, 1, None, None), 1001),
+    (lambda L: L.ftmi_highway(None, 0, 1, 32, None, None, None, None, None, 0, 1, None, None), 1001),
     (lambda L: L.ftmi_split_weights(None, 4, 4, None, None), 1001),
-    (lambda L: L.ftmi_rnn_bidir(0, 1, 1, 64, None, 0, 1, None, None, None, None, None, 0.0, None, 0, None, None), 1001),
+    (lambda L: L.ftmi_split_weights_f16(None, 4, 4, None, None), 1001),
+    (lambda L: L.ftmi_rnn_bidir(0, 1, 1, 64, None, 0, 1, None, None, None, None, None, 0.0, None, 0, 2, None, None, None), 1001),
     (lambda L: L.ftmi_duration_counts(None, 1, 1, 1, 2.0, None, None, None, None), 1001),
     (lambda L: L.ftmi_lr_index(None, 1, 1, 1, None, None), 1001),
     (lambda L: L.ftmi_length_regulate(None, 0, 1, 1, 4, None, 1, None, 0, None), 1001),
@@ -73,13 +74,15 @@ def test_conv_shape_errors():
     assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1004
     a.x_stride, a.mma = 16, 7  # unknown matrix path
     assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1001
+    a.mma = 2  # the f16x3 path needs the pre-split planes
+    assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1001
 
 
 def test_rnn_unsupported_hidden():
     lib = _lib.load()
     fake = ctypes.c_void_p(256)
     rc = lib.ftmi_rnn_bidir(0, 2, 4, 96, fake, 576, 4, None, None, fake, fake, None, 0.0, fake,
-                            192, fake, None)
+                            192, 2, None, fake, None)
     assert rc in (1003, ) or rc < 1000  # 1003 before any launch
     assert rc == 1003 or rc != 0
 

@@ -37,14 +37,15 @@ def rng():
 
 # ---------------------------------------------------------------- conv / GEMM family
 # (mma, pre-split weights): fp32 MFMA, bf16x6 splitting both operands per call, bf16x6
-# with the weights split once by ftmi_split_weights (the model's default path)
-MMAS = pytest.mark.parametrize('mma,pre', [(0, False), (1, False), (1, True)],
-                               ids=['f32', 'bf16x6', 'bf16x6-presplit'])
+# with the weights split once by ftmi_split_weights, f16x3 on ftmi_split_weights_f16
+# planes (the model's default path)
+MMAS = pytest.mark.parametrize('mma,pre', [(0, False), (1, False), (1, True), (2, True)],
+                               ids=['f32', 'bf16x6', 'bf16x6-presplit', 'f16x3'])
 
 
-def wsplit(w, pre):
+def wsplit(w, pre, mma=1):
     from forwardtacotron_amd import ops
-    return ops.split_weights(w) if pre else None
+    return ops.presplit_for(w, mma) if pre else None
 
 
 @MMAS
@@ -71,7 +72,7 @@ def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre):
         ref = ref * sc[None, :, None] + sh[None, :, None]
     wp = pack_conv(torch.from_numpy(w)).cuda()
     y, _ = ops.conv1d(dev(x), wp, k, k // 2, bias=dev(b) if bias else None, relu=relu,
-                      bn=(dev(sc), dev(sh)) if bn else None, mma=mma, w_split=wsplit(wp, pre))
+                      bn=(dev(sc), dev(sh)) if bn else None, mma=mma, w_split=wsplit(wp, pre, mma))
     close(host(y), ref.transpose(0, 2, 1))
 
 
@@ -88,7 +89,7 @@ def test_conv1d_maxpool_residual_transposed(rng, mma, pre, Cin):
     yt = torch.empty(B, N, T, device='cuda')
     wp = pack_conv(torch.from_numpy(w)).cuda()
     y, _ = ops.conv1d(dev(x), wp, 3, 1, maxpool=True, residual=dev(res), out_t=yt, mma=mma,
-                      w_split=wsplit(wp, pre))
+                      w_split=wsplit(wp, pre, mma))
     close(host(y), ref.transpose(0, 2, 1))
     close(host(yt), ref)
 
@@ -100,7 +101,7 @@ def test_conv1d_strided_input_view(rng, mma, pre):
     full = rng.normal(0, 1, (B, T, 2 * C)).astype(np.float32)
     w = rng.normal(0, 0.1, (48, C)).astype(np.float32)
     xt = dev(full)[:, :, C:]  # row stride 2C
-    y, _ = ops.conv1d(xt, dev(w), 1, 0, mma=mma, w_split=wsplit(dev(w), pre))
+    y, _ = ops.conv1d(xt, dev(w), 1, 0, mma=mma, w_split=wsplit(dev(w), pre, mma))
     close(host(y), full[:, :, C:] @ w.T)
 
 
@@ -117,7 +118,7 @@ def test_conv_bank(K, Cin, B, T, rng, mma, pre):
     refs = [np.maximum(O.conv1d(x.transpose(0, 2, 1), w, w.shape[2] // 2)[:, :, :T], 0) for w in ws]
     ref = np.concatenate(refs, 1) * sc[None, :, None] + sh[None, :, None]
     wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
-    w3 = ops.split_bank_weights(wp, K, Cin, C) if pre else None
+    w3 = ops.split_bank_weights(wp, K, Cin, C, mma) if pre else None
     y = ops.conv_bank(dev(x), wp, K, C, dev(sc), dev(sh), mma=mma, w_split=w3)
     close(host(y), ref.transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
 
@@ -135,7 +136,7 @@ def test_highway(rng, mma, pre):
     ref = O.highway({'h.' + k: v.astype(np.float32) for k, v in sd.items()}, 'h', x, np.float32)
     w12, b1, b2, _ = hw.packed_weights()
     from forwardtacotron_amd import ops
-    close(host(ops.highway(dev(x), w12, b1, b2, mma=mma, w_split=wsplit(w12, pre))), ref)
+    close(host(ops.highway(dev(x), w12, b1, b2, mma=mma, w_split=wsplit(w12, pre, mma))), ref)
 
 
 def test_split_weights_exact(rng):
@@ -147,6 +148,48 @@ def test_split_weights_exact(rng):
     back = host(p[0] + p[1] + p[2])  # exact in float64
     np.testing.assert_array_equal(back[:, :1000], w.astype(np.float64))
     assert not back[:, 1000:].any()
+
+
+def test_split_weights_f16_layout(rng):
+    """f16x3 planes: B0 = 2^11 h, B2 = h, w s_n ~= h + 2^-11 B1 to 2^-22 relative; the
+    column scale is a power of two with max|w| s_n < 16; K padding is zero."""
+    from forwardtacotron_amd import ops
+    N, K = 40, 300
+    w = rng.normal(0, 1, (N, K)).astype(np.float32)
+    w[3] *= 1000.0  # a row that needs s_n < 1
+    w[5] = 0.0
+    blk = host(ops.split_weights_f16(dev(w)))
+    Kp = 320
+    planes = blk[:3 * N * Kp * 2].view(np.float16).reshape(3, N, Kp).astype(np.float64)
+    cs = blk[3 * N * Kp * 2:3 * N * Kp * 2 + 4 * N].view(np.float32).astype(np.float64)
+    s = 2.0 ** -11 / cs
+    assert np.all(np.log2(s) == np.round(np.log2(s))) and np.all(s <= 1.0)
+    assert np.all(np.abs(w).max(1) * s < 16) and s[3] < 1.0 and s[0] == 1.0
+    np.testing.assert_array_equal(planes[0], planes[2] * 2048.0)
+    back = (planes[2] + planes[1] / 2048.0) / s[:, None]
+    ws = w.astype(np.float64)
+    assert np.all(np.abs(back[:, :K] - ws) <= 2.0 ** -22 * np.abs(ws) + 1e-30)
+    assert not planes[:, :, K:].any()
+
+
+def test_f16x3_range_guard(rng):
+    """An activation beyond the f16 range sets status bit 0 (the output is then invalid);
+    in range it stays clear."""
+    from forwardtacotron_amd import ops
+    x = rng.normal(0, 1, (1, 40, 64)).astype(np.float32)
+    w = dev(rng.normal(0, 0.1, (32, 64)).astype(np.float32))
+    st = ops.status_word('cuda')
+    st.zero_()
+    ops.conv1d(dev(x), w, 1, 0, mma=2, w_split=ops.split_weights_f16(w))
+    assert int(st.item()) == 0
+    x[0, 7, 3] = 1e5
+    ops.conv1d(dev(x), w, 1, 0, mma=2, w_split=ops.split_weights_f16(w))
+    assert int(st.item()) & 1
+    st.zero_()
+    with ops.exact_paths():  # fp32 MFMA: no range limit, no status
+        y, _ = ops.conv1d(dev(x), w, 1, 0, w_split=ops.split_weights_f16(w))
+    assert int(st.item()) == 0
+    close(host(y)[0], x[0] @ host(w).T)
 
 
 # ---------------------------------------------------------------- recurrences
@@ -165,19 +208,40 @@ def _rnn_module(cell, fin, H, rng):
     return m.cuda(), {'r.' + k: v for k, v in sd.items()}
 
 
+RNN_MMAS = pytest.mark.parametrize('rnn_mma', [2, 1, 0], ids=['f16x3', 'bf16x6', 'f32'])
+
+
+@RNN_MMAS
 @pytest.mark.parametrize('H,B,T', [(64, 3, 40), (128, 2, 33), (256, 5, 60), (256, 17, 9)])
-def test_gru_bidir(H, B, T, rng):
+def test_gru_bidir(H, B, T, rng, rnn_mma, monkeypatch):
+    from forwardtacotron_amd import ops
+    monkeypatch.setattr(ops, 'RNN_MMA', rnn_mma)
     m, sd = _rnn_module('gru', 256, H, rng)
     x = rng.normal(0, 1, (B, T, 256)).astype(np.float32)
     ref = O.gru_bidir(sd, 'r', x, np.float32)
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
 
 
-def test_lstm_bidir(rng):
+@RNN_MMAS
+def test_lstm_bidir(rng, rnn_mma, monkeypatch):
+    from forwardtacotron_amd import ops
+    monkeypatch.setattr(ops, 'RNN_MMA', rnn_mma)
     m, sd = _rnn_module('lstm', 512, 512, rng)
     x = rng.normal(0, 1, (3, 70, 512)).astype(np.float32)
     ref = O.lstm_bidir(sd, 'r', x, np.float32)
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
+
+
+def test_rnn_f16_weight_range_guard(rng):
+    """A W_hh entry beyond the f16 range sets status bit 1 on the f16x3 recurrence."""
+    from forwardtacotron_amd import ops
+    m, sd = _rnn_module('gru', 256, 64, rng)
+    with torch.no_grad():
+        m.weight_hh_l0[5, 7] = 1e6
+    st = ops.status_word('cuda')
+    st.zero_()
+    m.forward_cl(dev(rng.normal(0, 1, (2, 5, 256)).astype(np.float32)))
+    assert int(st.item()) & 2
 
 
 def test_lstm_through_lr_index_and_lengths(rng):

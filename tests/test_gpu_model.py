@@ -88,6 +88,23 @@ def test_length_regulator_layer_api(gpu_model):
     assert np.array_equal(d.cpu().numpy(), g['dur_out'])
 
 
+def test_f16_range_guard_reruns_exact(gpu_model):
+    """A pitch callback that drives the encoder beyond the f16 range: the f16x3 GEMMs flag
+    it, generate() reruns on the exact paths, and the result equals an exact-path run."""
+    from forwardtacotron_amd import ops
+    g = load_golden('gen_b3')
+    x = torch.from_numpy(g['x']).cuda()
+    big = dict(pitch_function=lambda p: p * 0 + 1e7)
+    out = gpu_model.generate(x, **big)
+    assert int(ops.status_word(x.device).item()) != 0
+    with ops.exact_paths():
+        ref = gpu_model.generate(x, **big)
+    for k in ('mel', 'mel_post', 'dur'):
+        assert torch.equal(out[k], ref[k]), k
+    out = gpu_model.generate(x)  # in range: the word is cleared and stays clear
+    assert int(ops.status_word(x.device).item()) == 0
+
+
 def test_repeated_calls_deterministic(gpu_model):
     g = load_golden('gen_b3')
     x = torch.from_numpy(g['x']).cuda()
