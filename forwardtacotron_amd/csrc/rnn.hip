@@ -27,24 +27,25 @@
 //     with i + j <= 4 on v_mfma_f32_16x16x32_bf16 — fp32-accurate (see gemm.hip).
 //   0 (FTMI_MMA_F32): v_mfma_f32_16x16x4_f32.
 //
-// h hand-off between the BPG workgroups of a group.  New h values go to an exchange buffer
-// hx[t & 1][group][16*H] in MFMA-fragment order (every consumer wave-instruction reads
-// 1 KB of consecutive bytes); parity double buffering is race-free because a workgroup can
-// only start step t+1 after every workgroup of its group finished step t.  Every storing
-// wave drains vmcnt(0), a workgroup barrier, then ONE lane adds 1 to the group's arrival
-// counter (agent-scope atomic); before step t ONE lane polls that counter (relaxed sc1
-// loads) until it reaches t*BPG, a workgroup barrier releases the other waves, and every
-// load of handed-off h is an sc1 load (L1 bypassed).  Two modes, chosen per launch:
+// h hand-off between the BPG workgroups of a group: the data is the flag.  Each exchanged
+// h value carries a step tag in its mantissa LSB (h_tag: a <= 1 ulp change; the tagged value
+// is used everywhere: state, exchange and layer output).  A fifth "comm" wave per workgroup
+// writes the workgroup's new h slice (one 16-B store per lane) into an exchange buffer
+// hx[t & 1][group][16*H] kept in MFMA-fragment order; consumer waves sc1-load their K range
+// of it (1 KB of consecutive bytes per wave-instruction) and re-load until every value
+// carries the tag of the step they need.  4-byte accesses are single-copy atomic, so torn
+// 16-byte stores only delay a read; no flag, counter, drain or barrier is on the path
+// (MI355X_MICROARCH.md "Valid forms", R2).  Parity double buffering is race-free because a
+// workgroup can only produce h_{t+1} after it read every workgroup's h_t.  The compute waves
+// never store to global memory, so their loads (input-projection prefetch, h) are never held
+// behind a store in the in-order vmcnt.  Two store modes, chosen per launch:
 //   XCD-local: a start-of-launch census reads each workgroup's XCC_ID (s_getreg) and, when
 //     every XCD received exactly the workgroups of whole groups, forms the groups from
-//     co-located workgroups.  h is then stored with PLAIN stores (kept in that XCD's L2)
-//     and read by sc1 loads served from the same L2, and the arrival counter is replaced by
-//     one flag word per workgroup (plain store of the step number after the drain + barrier,
-//     polled by one wave with a single sc1 load of all BPG flags) — no fabric round trip.
-//     Correct by construction because group membership comes from the measured XCD, never
-//     from an assumed dispatch order.
+//     co-located workgroups; h is then stored with PLAIN stores (kept in that XCD's L2) and
+//     read by sc1 loads served from the same L2.  Correct by construction because group
+//     membership comes from the measured XCD, never from an assumed dispatch order.
 //   global (fallback when the census is unbalanced, or disabled): sc1 write-through
-//     stores, groups by blockIdx (MI355X_MICROARCH.md "Valid forms", row 1).
+//     stores, groups by blockIdx.
 // BPG == 1 groups never leave the workgroup: h goes through LDS.  Every spin is bounded;
 // on timeout the call's error word is set and the workgroup leaves the time loop.
 //
@@ -146,6 +147,11 @@ __device__ __forceinline__ void split2h8(const float (&v)[8], f16x8 &h, f16x8 &t
   t = __builtin_convertvector((x - __builtin_convertvector(h, f32x8)) * H3_SCALE, f16x8);
 }
 
+// Step tag carried in the mantissa LSB of every exchanged h value.  Buffer half t & 1 holds
+// h_t over h_{t-2} (or the zeroed workspace before step 2): the tags of t and t - 2 differ,
+// and step 0/1's tag (1) differs from the zero fill.
+__device__ __forceinline__ unsigned h_tag(int t) { return (((unsigned)t >> 1) & 1u) ^ 1u; }
+
 __device__ __forceinline__ unsigned xcc_id() {
   unsigned x;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
@@ -236,12 +242,12 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   static_assert(BPG <= FLAGS_PER_GROUP, "flags");
 
   // ---- comm wave (wave 4, multi-workgroup groups only) ---------------------------------
-  // Owns every global store of the step and the hand-off, so the compute waves issue only
-  // loads: their input-projection prefetch is never drained by a store wait (vmcnt counts
-  // loads and stores together, in issue order).  Per step: poll the group's flags -> barrier
-  // A -> (compute: h load, MFMA) barrier B -> (compute: cells -> LDS stage) barrier C ->
-  // store this workgroup's h slice (one float4 per lane per 256 cells), drain, arrive, then
-  // store the y rows.
+  // Owns every global store of the step, so the compute waves issue only loads (vmcnt
+  // counts loads and stores together, in issue order: a store would hold back the loads
+  // issued after it).  Per step: (compute: h acquire, MFMA) barrier B -> (compute: cells ->
+  // LDS stage) barrier C -> store this workgroup's tagged h slice (one float4 per lane per
+  // 256 cells) and the y rows.  No flag, counter or drain: readiness travels IN the data
+  // (MI355X_MICROARCH.md "Valid forms", R2: the data is the flag).
   if constexpr (!LOCAL) {
     if (wave == 4) {
       constexpr int F4 = CELLS / 4;  // float4s of the slice
@@ -275,55 +281,21 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       __syncthreads();  // the compute waves' set-up barrier
       for (int t = 0; t < p.T; ++t) {
         const int tt = dir ? (p.T - 1 - t) : t;
-        if (t > 0) {
-          if (!(p.diag & 2)) {
-            if (xcd_mode) {  // lane i watches workgroup i's flag (L2-served sc1 loads)
-              unsigned spins = 0;
-              for (;;) {
-                const unsigned f = lane < BPG ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
-                                                                  __HIP_MEMORY_SCOPE_AGENT)
-                                              : (unsigned)t;
-                if (__all(f >= (unsigned)t)) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > SPIN_LIMIT) {
-                  if (lane == 0) {
-                    s_abort = 1;
-                    __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  }
-                  break;
-                }
-              }
-            } else if (lane == 0 && !poll_ge(cnt, (unsigned)t * BPG)) {
-              s_abort = 1;
-              __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-          }
-          __syncthreads();  // A
-          if (s_abort) break;
-        }
         __syncthreads();  // B
-        __syncthreads();  // C: the stage holds h_t and y_t
+        if (s_abort) break;
+        __syncthreads();  // C: the stage holds the tagged h_t and y_t
         const int soff = (t & 1) * hxp;
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int i = 0; i < FPL; ++i) {
+          // every sequence slot of the chunk, the batch tail's too: consumers check the tags
+          // of all 16 columns of their fragments
           const u32x4 v = *(const u32x4 *)&hstage[(lane + 64 * i) * 4];
-          if (ok[i]) {
-            if (xcd_mode)  // stays in this XCD's L2, read back by same-XCD sc1 loads
-              __builtin_amdgcn_raw_buffer_store_b128(v, rs, hofs[i], soff, 0);
-            else  // write-through (sc1)
-              __builtin_amdgcn_raw_buffer_store_b128(v, rs, hofs[i], soff, 16);
-          }
+          if (xcd_mode)  // stays in this XCD's L2, read back by same-XCD sc1 loads
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, hofs[i], soff, 0);
+          else  // write-through (sc1)
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, hofs[i], soff, 16);
         }
-        if (!(p.diag & 4)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) {
-          if (xcd_mode)
-            __hip_atomic_store(flags + bi, (unsigned)(t + 1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);  // plain store, stays in L2
-          else
-            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // layer output after the hand-off: nothing in this launch reads y
 #pragma unroll
         for (int i = 0; i < FPL; ++i) {
           const f32x4 v = *(const f32x4 *)&ystage[(lane + 64 * i) * 4];
@@ -470,13 +442,6 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
                   const int (&inext)[CPT], int (&iload)[CPT]) -> bool {
     const int tt = frame(t);
     STAMP(0);
-    // the comm wave has seen every workgroup of the group publish h_{t-1}
-    if (!LOCAL && t > 0) {
-      __syncthreads();
-      if (s_abort) return false;
-    }
-    STAMP(1);
-
     // h_{t-1} operand: NL float4 per lane (fragment order), zero at t = 0
     float hv[NL * 4];
     if (t == 0) {
@@ -493,19 +458,44 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         hv[4 * i + 3] = v.w;
       }
     } else {
+      // Tagged acquire: every exchanged h value carries h_tag(step) in its mantissa LSB;
+      // re-load until this wave's whole K range carries the tag of h_{t-1}.  4-byte
+      // accesses are single-copy atomic, so a torn 16-byte store only delays the read;
+      // every load of the exchange buffer is sc1 (L2-served).
       const int soff = ((t - 1) & 1) * hx_par;
+      const unsigned want = h_tag(t - 1);
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 hr[NL];
+      for (unsigned spins = 0;; ++spins) {
+        bool fresh = true;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          hr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + i * 1024, soff, 16);
+          const u32x4 d = (hr[i] & 1u) ^ want;
+          fresh &= (d.x | d.y | d.z | d.w) == 0u;
+        }
+        if (__all(fresh) || (p.diag & 2)) break;
+        if (spins > SPIN_LIMIT) {
+          if (lane == 0) {
+            s_abort = 1;
+            __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
         // NB: bit_cast the whole vector; extracting u32 lanes one by one and bit-casting
         // each is miscompiled by ROCm 7.2 (every lane reads element 0).
-        const f32x4 v = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + i * 1024, soff, 16));
+        const f32x4 v = __builtin_bit_cast(f32x4, hr[i]);
         hv[4 * i] = v.x;
         hv[4 * i + 1] = v.y;
         hv[4 * i + 2] = v.z;
         hv[4 * i + 3] = v.w;
       }
     }
+    STAMP(1);
     load_gx(t + 2, inext, gnext);
     load_idx(t + 3, iload);
     STAMP(2);
@@ -567,6 +557,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       for (int e = 0; e < 4; ++e)
         red[(wk * R + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] = acc[i][e];
     __syncthreads();
+    if (!LOCAL && s_abort) return false;  // a wave timed out acquiring h_{t-1}
     STAMP(3);
 
     // cell update
@@ -598,12 +589,14 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         cstate[j] = fg * cstate[j] + ig * gg;
         hn = og * fast_tanh(cstate[j]);
       }
-      float yout = hn;
       if (tt >= len[j]) {  // packed-sequence padding: reverse direction restarts from zero
         hn = 0.f;
         cstate[j] = 0.f;
-        yout = p.pad_value;
       }
+      // multi-workgroup groups: h_t carries the step tag in its mantissa LSB (a <= 1 ulp
+      // change); the same tagged value is the state, the exchange and the layer output
+      if constexpr (!LOCAL) hn = __uint_as_float((__float_as_uint(hn) & ~1u) | h_tag(t));
+      const float yout = tt >= len[j] ? p.pad_value : hn;
       hstate[j] = hn;
       if constexpr (LOCAL) {
         if (cvalid[j]) {
