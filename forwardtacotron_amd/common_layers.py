@@ -108,8 +108,16 @@ class Packed(nn.Module):
     """Base class: caches kernel-layout weights, keyed by the identity/version of params."""
 
     def _pack_key(self):
-        return tuple((t.data_ptr(), t._version, t.device) for t in
-                     list(self.parameters()) + list(self.buffers()))
+        # The (owner dict, name, tensor) list is cached: walking the module tree costs ~10 us
+        # per call, which is host time on the launch path.  A parameter / buffer REPLACED in
+        # any submodule (owner dict no longer holds the same object) rebuilds the list; an
+        # in-place change (load_state_dict, .to, .copy_) changes data_ptr or _version.
+        refs = self.__dict__.get('_ftmi_refs')
+        if refs is None or any(d.get(n) is not t for d, n, t in refs):
+            refs = [(d, n, t) for m in self.modules() for d in (m._parameters, m._buffers)
+                    for n, t in d.items() if t is not None]
+            self.__dict__['_ftmi_refs'] = refs
+        return tuple((t.data_ptr(), t._version) for _, _, t in refs)
 
     def packed_weights(self):
         key = self._pack_key()
@@ -231,8 +239,19 @@ class BiRNN(Packed):
     def forward_cl(self, x: torch.Tensor, T: Optional[int] = None, index=None, lengths=None,
                    pad_value: float = 0.0) -> torch.Tensor:
         """x: (B, T_src, In) channels-last; with index, frame t reads row index[b, t]."""
-        w_ih, b_in, b_hh, w_hh, w3 = self.packed_weights()
+        return self.recur(self.project(x), T=T, index=index, lengths=lengths,
+                          pad_value=pad_value)
+
+    def project(self, x: torch.Tensor) -> torch.Tensor:
+        """Input projections of both directions, x W_ih^T + b: (B, T_src, 2*G*H)."""
+        w_ih, b_in, _, _, w3 = self.packed_weights()
         xp, _ = ops.conv1d(x, w_ih, 1, 0, bias=b_in, w_split=w3)
+        return xp
+
+    def recur(self, xp: torch.Tensor, T: Optional[int] = None, index=None, lengths=None,
+              pad_value: float = 0.0) -> torch.Tensor:
+        """The recurrence over `project`'s output (frame t reads row index[b, t])."""
+        _, b_in, b_hh, w_hh, _ = self.packed_weights()
         return ops.rnn_bidir(self.cell, xp, self.hidden, w_hh, b_hh, T=T, index=index,
                              xp_zero=b_in if index is not None else None, lengths=lengths,
                              pad_value=pad_value)

@@ -161,12 +161,16 @@ class ForwardTacotron(nn.Module):
                             self.energy_strength)
         return h
 
-    def _decode(self, enc: torch.Tensor, index: torch.Tensor, lengths=None, T_out=None):
-        """LSTM over LR(enc) (through the index map) -> lin -> postnet -> post_proj."""
+    def _decode(self, enc: torch.Tensor, index: torch.Tensor, lengths=None, T_out=None, xp=None):
+        """LSTM over LR(enc) (through the index map) -> lin -> postnet -> post_proj.
+        xp: the LSTM input projection of enc if already queued (self.lstm.project)."""
         B = enc.size(0)
         T_mel = index.size(1)
-        lstm_out = self.lstm.forward_cl(enc, T=T_mel, index=index, lengths=lengths,
-                                        pad_value=self.padding_value)
+        if xp is None:
+            xp = self.lstm.project(enc)
+        lstm_out = self.lstm.recur(xp, T=T_mel, index=index, lengths=lengths,
+                                   pad_value=self.padding_value)
+        del xp
         mel_cl = torch.empty(B, T_mel, self.n_mels, device=enc.device)
         mel = torch.empty(B, self.n_mels, T_mel, device=enc.device)
         w, b, w3 = self.lin.packed_weights()
@@ -225,8 +229,11 @@ class ForwardTacotron(nn.Module):
         energy and the prenet run on three side streams while the caller's stream runs the
         duration predictor and the LengthRegulator bookkeeping (fill-2 rule, counts, T_mel).
         The one host sync (T_mel) therefore waits only for the duration path and overlaps
-        the prenet.  Returns (dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel) with
-        every tensor ready on the caller's stream."""
+        the prenet.  The encoder tail (pitch / energy projections) and the LSTM input
+        projection do not depend on T_mel: they are queued BEFORE the host waits for it, so
+        the device keeps working through the sync.  Returns (dur_hat, pitch_hat, energy_hat,
+        enc, offsets, T_mel, xp) with every tensor ready on the caller's stream (xp: the
+        LSTM input projection of enc)."""
         main = torch.cuda.current_stream(x.device)
         s_pitch, s_energy, s_prenet = self._side_streams(x.device)
         for s in (s_pitch, s_energy, s_prenet):
@@ -238,16 +245,29 @@ class ForwardTacotron(nn.Module):
         with torch.cuda.stream(s_energy):
             energy_hat = energy_fn(self.energy_pred.forward_bt(x).unsqueeze(1))
         dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
+        t_host = t_ready = None
         if batch is None:
             offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=True)
-            T_mel = int(totals.max().item())  # the one host sync (output size is data dependent)
+            # the one host sync (output size is data dependent): max(totals) goes to pinned
+            # host memory now and is read after the T_mel-independent work is queued
+            t_host = torch.empty((), dtype=totals.dtype, pin_memory=True)
+            t_host.copy_(totals.max(), non_blocking=True)
+            t_ready = torch.cuda.Event()
+            t_ready.record(main)
         else:  # a shard of a larger batch (sharded.GlobalBatch): batch-global fill rule / T_mel
             offsets, totals = batch.duration_counts(dur_hat)
             T_mel = batch.t_mel(totals)
         for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat), (s_prenet, enc)):
             main.wait_stream(s)
             t.record_stream(main)
-        return dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel
+        wp, bp, we, be = self._series_proj_weights()
+        ops.series_proj_add(enc, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
+                            self.energy_strength)
+        xp = self.lstm.project(enc)
+        if t_ready is not None:
+            t_ready.synchronize()
+            T_mel = int(t_host)
+        return dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel, xp
 
     def generate(self,
                  x: torch.Tensor,
@@ -259,15 +279,16 @@ class ForwardTacotron(nn.Module):
         predictor (torch ops issued inside them are ordered after the prediction).
         `batch`: a sharded.GlobalBatch when x is one rank's shard of a larger batch.
         Runs under the f16x3 range guard (ops.run_checked): one status read at the end."""
-        self.eval()
+        if self.training:  # the module-tree walk of eval() is host time on every call
+            self.eval()
         self._check_device(x)
 
         def run():
             with torch.no_grad():
-                dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel = self._phoneme_phase(
+                dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel, xp = self._phoneme_phase(
                     x, alpha, pitch_function, energy_function, batch)
                 return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
-                                          lr=(offsets, T_mel))
+                                          lr=(offsets, T_mel), xp=xp)
         return ops.run_checked(run, x.device, reduce=None if batch is None else batch.status)
 
     def generate_jit(self, x: torch.Tensor, alpha: float = 1.0, beta: float = 1.0) -> Dict[str, torch.Tensor]:
@@ -276,31 +297,33 @@ class ForwardTacotron(nn.Module):
 
         def run():
             with torch.no_grad():
-                dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel = self._phoneme_phase(
+                dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel, xp = self._phoneme_phase(
                     x, alpha, lambda p: p * beta, lambda e: e)
                 return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
-                                          lr=(offsets, T_mel))
+                                          lr=(offsets, T_mel), xp=xp)
         return ops.run_checked(run, x.device)
 
     def get_step(self) -> int:
         return self.step.data.item()
 
-    def _generate_mel(self, x, dur_hat, pitch_hat, energy_hat, enc=None, lr=None):
+    def _generate_mel(self, x, dur_hat, pitch_hat, energy_hat, enc=None, lr=None, xp=None):
         """`models/forward_tacotron.py:289-330`.  enc: the prenet output if already computed;
         lr: (offsets, T_mel) if the LengthRegulator counts were already computed (then
-        dur_hat has already been clipped / filled in place)."""
+        dur_hat has already been clipped / filled in place); xp: the LSTM input projection
+        if already queued (then enc already carries the pitch / energy projections)."""
         if enc is None:
             enc = self.prenet.forward_cl(ops.embedding(x, self.embedding.weight.detach()))
-        wp, bp, we, be = self._series_proj_weights()
-        ops.series_proj_add(enc, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
-                            self.energy_strength)
+        if xp is None:
+            wp, bp, we, be = self._series_proj_weights()
+            ops.series_proj_add(enc, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
+                                self.energy_strength)
         if lr is None:
             offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=False)
             T_mel = int(totals.max().item())  # the one host sync: output size is data dependent
         else:
             offsets, T_mel = lr
         index = ops.lr_index(offsets, T_mel)
-        mel, mel_post = self._decode(enc, index)
+        mel, mel_post = self._decode(enc, index, xp=xp)
         return {'mel': mel, 'mel_post': mel_post, 'dur': dur_hat,
                 'pitch': pitch_hat, 'energy': energy_hat}
 

@@ -38,6 +38,9 @@ _FORCED = []  # stack of (gemm mma, rnn mma) overrides
 
 
 def status_word(device) -> torch.Tensor:
+    t = _STATUS.get(device)  # fast path: an indexed torch.device seen before
+    if t is not None:
+        return t
     dev = torch.device(device)
     if dev.index is None:
         dev = torch.device(dev.type, torch.cuda.current_device())
@@ -109,8 +112,14 @@ def _split_k(M: int, N: int, K: int, mma: int) -> int:
     return int(min(8, -(-slots // tiles), K // 1024))
 
 
-def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+if hasattr(torch._C, '_cuda_getCurrentRawStream'):
+    def _stream() -> int:
+        """hipStream_t of torch's current stream (the raw-handle query skips the Stream
+        object torch.cuda.current_stream() builds: host time on every launch)."""
+        return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
+else:  # pragma: no cover
+    def _stream() -> int:
+        return torch.cuda.current_stream().cuda_stream
 
 
 def _ptr(t: Optional[torch.Tensor]):
