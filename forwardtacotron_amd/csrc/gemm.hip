@@ -84,6 +84,8 @@ struct GemmParams {
   // store raw partial sums to part[s][M][N]; splitk_epilogue_kernel finishes the tile
   int split;
   int kc_per;
+  int split_req;  // the caller's split_k (the slab kernel re-derives split / kc_per from it)
+  int diag;       // slab kernel timing experiments (FTMI_SLAB_DIAG; results invalid when set)
   float *part;
   unsigned *status;  // mma = 2: bit 0 set when an accumulator became non-finite
   GemmGroup g[MAX_GROUPS];
@@ -1020,6 +1022,288 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6b_kernel(const GemmParams 
   }
 }
 
+// ---- slab kernel: k-tap convolutions on the f16x3 path (mma = 2, To == T, one group) ----
+// A 256 x 128 output tile per workgroup, 8 waves as 4 (rows) x 2 (columns) of 64 x 64.
+// Per 32-channel chunk the input rows [m0 - pad, m0 + 256 + k - 1 - pad) are read ONCE,
+// split into f16 head / scaled tail while staged into LDS (the "slab"), and serve all k taps:
+// tap j reads slab row r + j for output row r; a row whose frame t + j - pad falls outside
+// its sequence takes zero (per-row tap masks).  The x6b kernel re-reads every input row k
+// times through L2 with a 128 x 128 tile; here the operand bytes per MFMA drop ~3x for
+// k = 3.  B moves two f16 planes per tap (B0 = 2^11 w_h, B1 = w_t); the third, w_h, is B0 *
+// 2^-11 in registers (exact: a power-of-two rescale of an f16 value back to itself).
+// Steps are (chunk, tap): B double buffered per step, the slab double buffered per chunk.
+constexpr int SL_BM = 256;
+constexpr int SL_BN = 128;
+constexpr int SL_MAXK = 16;
+constexpr int SL_SR = SL_BM + SL_MAXK - 1;          // slab rows
+constexpr int SL_P = 48;                            // halves per LDS row: 96-B pitch keeps
+                                                    // the ds_read_b128 fragments conflict free
+constexpr int SL_ZROW = SL_SR;                       // an all-zero row after the slab rows:
+                                                    // masked taps read it (no selects)
+constexpr int SL_AIMG = (SL_SR + 1) * SL_P;         // halves per (buffer, plane) slab image
+constexpr int SL_BIMG = SL_BN * SL_P;               // halves per (buffer, plane) B image
+constexpr int SL_ASLOTS = (SL_SR * 8 + 511) / 512;  // float4 slab loads per thread per chunk
+
+template <bool MAXPOOL>
+__global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams p) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds_a[2 * 2 * SL_AIMG];  // [buf][h|t][row][48]
+  __shared__ __attribute__((aligned(16))) _Float16 lds_b[2 * 2 * SL_BIMG];  // [buf][B0|B1][n][48]
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const GemmGroup &G = p.g[0];
+  // XCD-aware order: blocks b and b + 8 run on the same XCD, and the NT column tiles of one
+  // row tile are consecutive in that XCD's order, so its slab rows are shared through L2
+  const int MT = (p.M + SL_BM - 1) / SL_BM, NT = G.ntiles;
+  const int bid = blockIdx.x, s8 = bid >> 3, q8 = s8 / NT;
+  const int mt = q8 * 8 + (bid & 7), nt = s8 - q8 * NT;
+  if (mt >= MT) return;  // the grid is padded to whole XCD rounds
+  const int m0 = mt * SL_BM, n0 = nt * SL_BN;
+  const int k = G.k, pad = G.pad, Cin = p.Cin;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int fr = lane & 15, fs = lane >> 4;  // fragment row / k-segment (8 k each)
+
+  int nch = Cin / 32, c_begin = 0;
+  if (p.split > 1) {  // split over channel chunks: blockIdx.y = s takes [s kc_per, ...)
+    c_begin = blockIdx.y * p.kc_per;
+    nch = min(nch - c_begin, p.kc_per);
+  }
+  const int nsteps = nch * k;
+
+  // ---- slab loads: slot i = slab row sr (input row m0 - pad + sr), channels seg*4..+3 ----
+  // Every load is unconditional with a clamped address (static wait counters); clamped
+  // rows only feed taps that the row masks zero.
+  const int SR = SL_BM + k - 1;
+  unsigned aoff[SL_ASLOTS];
+  unsigned poff[MAXPOOL ? SL_ASLOTS : 1];
+  int adst[SL_ASLOTS];
+#pragma unroll
+  for (int i = 0; i < SL_ASLOTS; ++i) {
+    // the 16 lanes of one ds_write_b64 group write slab rows sr and sr + 2 (conflict free)
+    const int idx = tid + 512 * i, seg = idx & 7, pr = idx >> 4;
+    const int sr = 4 * (pr >> 1) + (pr & 1) + 2 * ((idx >> 3) & 1);
+    int mp = m0 - pad + sr;
+    mp = mp < 0 ? 0 : (mp >= p.M ? p.M - 1 : mp);
+    aoff[i] = (unsigned)mp * (unsigned)p.x_stride + (unsigned)(c_begin * 32 + seg * 4);
+    if constexpr (MAXPOOL) {  // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
+      const int tp = mp % p.T;
+      poff[i] = aoff[i] - (tp > 0 ? (unsigned)p.x_stride : 0u);
+    }
+    adst[i] = sr < SR ? sr * SL_P + seg * 4 : -1;
+  }
+  struct ARaw {
+    f32x4 v[SL_ASLOTS];
+    f32x4 u[MAXPOOL ? SL_ASLOTS : 1];
+  };
+  const unsigned a_last = (unsigned)(nch - 1) * 32u;
+  unsigned ach = 0;  // channel offset (within this split) of the next slab load
+  auto loadA = [&](ARaw &r) {
+    const unsigned o = ach < a_last ? ach : a_last;
+#pragma unroll
+    for (int i = 0; i < SL_ASLOTS; ++i) {
+      r.v[i] = *(const f32x4 *)(p.x + aoff[i] + o);
+      if constexpr (MAXPOOL) r.u[i] = *(const f32x4 *)(p.x + poff[i] + o);
+    }
+    ach += 32;
+  };
+  float amax = 0.f;  // range guard: largest |activation| fed to the f16 split
+  auto storeA = [&](const ARaw &r, int buf) {
+    _Float16 *dst = lds_a + buf * 2 * SL_AIMG;
+#pragma unroll
+    for (int i = 0; i < SL_ASLOTS; ++i) {
+      if (adst[i] < 0) continue;
+      f32x4 v = r.v[i];
+      if constexpr (MAXPOOL) v = fmax4(v, r.u[i]);
+      amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      f16x4 h, t;
+      split2h(v, h, t);
+      *(f16x4 *)(dst + adst[i]) = h;
+      *(f16x4 *)(dst + SL_AIMG + adst[i]) = t;
+    }
+  };
+
+  // ---- B: planes B0 / B1 of tap j, channels of the chunk; 2 x 16 B per thread per step ---
+  // Rows n >= N read row N-1 (their output columns are never stored); steps past the end
+  // re-read the last step (clamped).
+  const _Float16 *w16 = (const _Float16 *)G.w3;
+  const _Float16 *bsrc[2];
+  int bdst[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    // the 8 lanes of one ds_write_b128 group write rows nl and nl + 2 (bank offset 16 of 32:
+    // conflict free); rows 4g + {0, 1, 2, 3} come from lane pairs (2g, 2g + 1)
+    const int idx = tid + 512 * i, pl = idx >> 9, rem = idx & 511, seg = rem & 3;
+    const int pr = rem >> 3, nl = 4 * (pr >> 1) + (pr & 1) + 2 * ((rem >> 2) & 1);
+    const int n = n0 + nl < G.N ? n0 + nl : G.N - 1;
+    bsrc[i] = w16 + ((int64_t)pl * G.N + n) * G.Kpad + c_begin * 32 + seg * 8;
+    bdst[i] = pl * SL_BIMG + nl * SL_P + seg * 8;
+  }
+  int bj = 0, bc = 0;  // tap / chunk of the next B load
+  auto loadB = [&](u32x4 (&rb)[2]) {
+    const bool in = bc < nch;
+    const int off = (in ? bj : k - 1) * Cin + (in ? bc : nch - 1) * 32;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) rb[i] = *(const u32x4 *)(bsrc[i] + off);
+    if (++bj == k) {
+      bj = 0;
+      ++bc;
+    }
+  };
+  auto storeB = [&](const u32x4 (&rb)[2], int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *(u32x4 *)(lds_b + buf * 2 * SL_BIMG + bdst[i]) = rb[i];
+  };
+
+  // ---- per-row tap masks: bit j set iff frame t + j - pad lies inside the sequence -------
+  unsigned vmask[4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + wm * 64 + mi * 16 + fr;
+    unsigned msk = 0;
+    if (m < p.M) {
+      const int t = m % p.T;
+      const int lo = max(pad - t, 0), hi = min(p.T - 1 + pad - t, k - 1);
+      if (lo <= hi) msk = (2u << hi) - (1u << lo);
+    }
+    vmask[mi] = msk;
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto mfma_step = [&](int abuf, int bbuf, int j) {
+    const _Float16 *Ab = lds_a + abuf * 2 * SL_AIMG;
+    const _Float16 *Bb = lds_b + bbuf * 2 * SL_BIMG;
+    f16x8 ah[4], at[4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const bool ok = (vmask[mi] >> j) & 1u;
+      const int o = (ok ? wm * 64 + mi * 16 + fr + j : SL_ZROW) * SL_P + fs * 8;
+      ah[mi] = *(const f16x8 *)(Ab + o);
+      at[mi] = *(const f16x8 *)(Ab + SL_AIMG + o);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int o = (wn * 64 + ni * 16 + fr) * SL_P + fs * 8;
+      const f16x8 b0 = *(const f16x8 *)(Bb + o);
+      const f16x8 b1 = *(const f16x8 *)(Bb + SL_BIMG + o);
+      const f16x8 bh = b0 * (_Float16)(1.0f / H3_SCALE);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {  // small terms first, as in x6b
+        f32x4 c = acc[mi][ni];
+        c = mma16(at[mi], bh, c);
+        c = mma16(ah[mi], b1, c);
+        c = mma16(ah[mi], b0, c);
+        acc[mi][ni] = c;
+      }
+    }
+  };
+
+  // ---- pipeline: step s = (chunk c, tap j) uses slab buffer c & 1 and B buffer s & 1 ------
+  // At step s: stage B s+1 (register set (s+1) & 1, loaded two steps ago) and, on a chunk's
+  // last tap, slab c+1; reload that B set with step s+3 and the slab registers with chunk
+  // c+2; MFMAs; barrier.
+  if (tid < 2 * 2 * SL_P / 8) {  // the zero rows of both buffers and planes
+    const int img = tid / (SL_P / 8), part = tid % (SL_P / 8);
+    *(u32x4 *)(lds_a + img * SL_AIMG + SL_ZROW * SL_P + part * 8) = (u32x4){0u, 0u, 0u, 0u};
+  }
+  ARaw ra;
+  u32x4 rb0[2], rb1[2];
+  loadA(ra);
+  loadB(rb0);  // step 0
+  storeA(ra, 0);
+  storeB(rb0, 0);
+  loadB(rb1);  // step 1
+  loadB(rb0);  // step 2
+  if (nch > 1) loadA(ra);  // chunk 1
+  __syncthreads();
+  int c = 0, j = 0;
+  auto step = [&](int s, u32x4 (&rbs)[2]) {
+    const bool last_tap = j == k - 1 && c + 1 < nch;
+    // MFMAs first: the staging below (LDS stores of the next B / slab, the slab's f16 split,
+    // the next loads) is independent of them and fills the matrix pipe's shadow
+    if (!(p.diag & 2)) mfma_step(c & 1, s & 1, j);
+    if (s + 1 < nsteps) storeB(rbs, (s + 1) & 1);
+    if (last_tap) storeA(ra, (c + 1) & 1);
+    if (!(p.diag & 4)) {
+      loadB(rbs);
+      if (last_tap) loadA(ra);
+    }
+    if (!(p.diag & 1)) __syncthreads();
+    if (++j == k) {
+      j = 0;
+      ++c;
+    }
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, rb1);
+    if (s + 1 >= nsteps) break;
+    step(s + 1, rb0);
+  }
+
+  // ---- epilogue: undo the 2^11 / column scaling, range guard, stores ---------------------
+  bool bad = !(amax <= 65504.f);
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int col = n0 + wn * 64 + ni * 16 + fr;
+    const float cs = G.colscale[col < G.N ? col : G.N - 1];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wm * 64 + mi * 16 + 4 * fs + i;
+        bad |= col < G.N && row < p.M && !__builtin_isfinite(acc[mi][ni][i]);
+        acc[mi][ni][i] *= cs;
+      }
+  }
+  if (bad && p.status) atomicOr(p.status, 1u);
+
+  if (p.split > 1) {  // raw partial sums; splitk_epilogue_kernel finishes
+    float *part = p.part + (size_t)blockIdx.y * p.M * G.N;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int col = n0 + wn * 64 + ni * 16 + fr;
+      if (col >= G.N) continue;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wm * 64 + mi * 16 + 4 * fs + i;
+          if (row < p.M) part[(size_t)row * G.N + col] = acc[mi][ni][i];
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int col = n0 + wn * 64 + ni * 16 + fr;
+    if (col >= G.N) continue;
+    const float bias = G.bias ? G.bias[col] : 0.f;
+    const float sc = G.scale ? G.scale[col] : 1.f;
+    const float sh = G.scale ? G.shift[col] : 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wm * 64 + mi * 16 + 4 * fs + i;
+        if (row >= p.M) continue;
+        float v = acc[mi][ni][i];
+        if (G.bias) v += bias;
+        if (p.relu) v = fmaxf(v, 0.f);
+        if (G.scale) v = v * sc + sh;
+        if (p.residual) v += p.residual[(int64_t)row * p.res_stride + col];
+        if (p.y) p.y[(int64_t)row * p.y_stride + G.ycol0 + col] = v;
+        if (p.yt) {
+          const int b = row / p.To, t = row - b * p.To;
+          p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = v;
+        }
+      }
+  }
+}
+
 // w [N][K] fp32 -> [3][N][Kpad] bf16 pieces (w = p0 + p1 + p2 exactly), zero K padding
 __global__ void split_weights_kernel(const float *__restrict__ w, int64_t N, int64_t K,
                                      int64_t Kpad, __bf16 *__restrict__ out) {
@@ -1099,12 +1383,72 @@ static int x6_variant() {
   return v;
 }
 
+// FTMI_GEMM_SLAB=0 routes the slab-eligible convolutions to the x6b kernel (A/B timing)
+static bool slab_enabled() {
+  static const bool v = [] {
+    const char *e = getenv("FTMI_GEMM_SLAB");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
+// slab kernel eligibility: one group, same-length output, whole 32-channel chunks, k taps
+// within the slab halo, 32-bit activation offsets; a k = 1 GEMM only when it has more than
+// one column tile (narrow Linear layers run faster on the 128 x 128 x6b tiles).
+// FTMI_GEMM_SLAB_MIN (MACs, read per call; default 0) keeps smaller contractions on the
+// x6b kernel: tests use it to cover both kernels, A/B runs to size the choice (taking
+// the slab for every eligible shape measured fastest on c3: 10.01 vs 10.19 ms/step with
+// an 8 GMAC bar)
+constexpr int64_t SL_MIN_MACS = 0;
+static int64_t slab_min_macs() {
+  const char *e = getenv("FTMI_GEMM_SLAB_MIN");
+  return e ? atoll(e) : SL_MIN_MACS;
+}
+static bool slab_ok(const GemmParams &p) {
+  return slab_enabled() && p.ngroups == 1 && p.To == p.T && p.Cin % 32 == 0 &&
+         p.g[0].k <= SL_MAXK && (p.g[0].k > 1 || p.g[0].N > SL_BN) &&
+         (int64_t)p.M * p.g[0].N * p.g[0].Ktot >= slab_min_macs() &&
+         (int64_t)p.M * p.x_stride < ((int64_t)1 << 31);
+}
+
+static int launch_slab(const GemmParams &p, bool maxpool, hipStream_t s) {
+  GemmParams q = p;
+  const int nch = q.Cin / 32;
+  q.split = 1;
+  static const int diag = [] {
+    const char *e = getenv("FTMI_SLAB_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  q.diag = diag;
+  q.kc_per = nch;
+  if (p.split_req > 1 && p.part) {  // split over channel chunks, no empty splits
+    q.kc_per = (nch + p.split_req - 1) / p.split_req;
+    q.split = (nch + q.kc_per - 1) / q.kc_per;
+  }
+  const int MT = (q.M + SL_BM - 1) / SL_BM;
+  const int nblk = (MT + 7) / 8 * 8 * q.g[0].ntiles;  // whole XCD rounds (see the kernel)
+  dim3 grid(nblk, q.split), block(512);
+  if (maxpool)
+    hipLaunchKernelGGL((conv_gemm_slab_kernel<true>), grid, block, 0, s, q);
+  else
+    hipLaunchKernelGGL((conv_gemm_slab_kernel<false>), grid, block, 0, s, q);
+  FTMI_CHECK_LAUNCH();
+  if (q.split > 1) {
+    const int64_t total = (int64_t)q.M * q.g[0].N;
+    const int eb = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(eb), dim3(256), 0, s, q);
+    FTMI_CHECK_LAUNCH();
+  }
+  return FTMI_OK;
+}
+
 int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hipStream_t s) {
   if (nblocks <= 0) return FTMI_OK;
   dim3 grid(nblocks), block(256);
   bool presplit = (mma == 1 && x6_variant() != 3) || mma == 2;
   for (int i = 0; i < p.ngroups; ++i) presplit &= p.g[i].w3 != nullptr;
   if (mma == 2 && !presplit) return FTMI_E_ARG;  // the f16 path needs the split planes
+  if (mma == 2 && epi == EPI_CONV && slab_ok(p)) return launch_slab(p, maxpool, s);
   if (presplit) {
     dim3 g2(nblocks, p.split > 1 ? p.split : 1);
     if (mma == 2) {
@@ -1246,6 +1590,7 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
     const int kc_per = (nkc + a->split_k - 1) / a->split_k;
     p.split = (nkc + kc_per - 1) / kc_per;  // no empty splits
     p.kc_per = kc_per;
+    p.split_req = a->split_k;
     p.part = a->split_ws;
   }
   return launch(p, EPI_CONV, a->maxpool != 0, mtiles * g.ntiles, a->mma, ftmi_hs(stream));

@@ -100,9 +100,25 @@ def _num_cus() -> int:
     return n
 
 
-def _split_k(M: int, N: int, K: int, mma: int) -> int:
+SLAB = os.environ.get('FTMI_GEMM_SLAB', '1') != '0'
+
+
+def _slab(mma: int, T: int, To: int, Cin: int, k: int, N: int, M: int) -> bool:
+    """Whether ftmi_conv1d takes the slab kernel (gemm.hip slab_ok)."""
+    return (SLAB and mma == 2 and To == T and Cin % 32 == 0 and k <= 16 and (k > 1 or N > 128)
+            and M * N * k * Cin >= int(os.environ.get('FTMI_GEMM_SLAB_MIN', 0)))
+
+
+def _split_k(M: int, N: int, K: int, mma: int, slab: bool = False, Cin: int = 0) -> int:
     """Split K when the tile grid cannot fill the chip (x6 / h3 kernels: 2 workgroups per
-    CU) and K is long enough for the partial-sum round trip to pay."""
+    CU; slab kernel: 256 x 128 tiles, 1 per CU, split over 32-channel chunks) and K is long
+    enough for the partial-sum round trip to pay."""
+    if slab:
+        tiles = -(-M // 256) * -(-N // 128)
+        cus = _num_cus()
+        if K < 1024 or tiles * 4 >= cus * 3:
+            return 1
+        return int(max(1, min(8, -(-cus // tiles), Cin // 32)))
     if mma == 0 or K < 2048:
         return 1
     tiles = -(-M // 128) * -(-N // 128)
@@ -249,7 +265,7 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
     a.mma, a.w_split = _gemm_mma(mma, w_split)
     a.status = status_word(x.device).data_ptr()
     M = B * To
-    sk = _split_k(M, N, k * Cin, a.mma)
+    sk = _split_k(M, N, k * Cin, a.mma, _slab(a.mma, T, To, Cin, k, N, M), Cin)
     if sk > 1:
         part = torch.empty(sk * M * N, device=x.device, dtype=_f32)
         a.split_k, a.split_ws = sk, part.data_ptr()

@@ -43,6 +43,16 @@ MMAS = pytest.mark.parametrize('mma,pre', [(0, False), (1, False), (1, True), (2
                                ids=['f32', 'bf16x6', 'bf16x6-presplit', 'f16x3'])
 
 
+def slab_or_skip(kernel, mma, monkeypatch):
+    """'slab': the default choice (the f16x3 slab kernel for every eligible shape);
+    'tiled': the 128 x 128 tiled kernels only (FTMI_GEMM_SLAB_MIN above any shape here)."""
+    if kernel == 'slab':
+        if mma != 2:
+            pytest.skip('the slab kernel is an f16x3 kernel')
+    else:
+        monkeypatch.setenv('FTMI_GEMM_SLAB_MIN', str(1 << 62))
+
+
 def wsplit(w, pre, mma=1):
     from forwardtacotron_amd import ops
     return ops.presplit_for(w, mma) if pre else None
@@ -56,8 +66,13 @@ def wsplit(w, pre, mma=1):
     (1, 7, 16, 40, 4, True, True, False),       # even k, tiny
     (2, 300, 80, 256, 8, True, True, False),    # postnet bank k=8
     (2, 60, 1024, 256, 3, True, True, True),    # long K, few tiles: split-K on the x6 path
+    (3, 301, 96, 200, 7, True, True, True),     # slab kernel: ragged rows / columns, k = 7
+    (2, 9, 32, 64, 16, True, False, False),     # slab kernel: k = 16 > T, every tap masked
+    (4, 70, 64, 1536, 1, False, False, True),   # slab kernel, k = 1, many column tiles
 ])
-def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre):
+@pytest.mark.parametrize('kernel', ['tiled', 'slab'])
+def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre, kernel, monkeypatch):
+    slab_or_skip(kernel, mma, monkeypatch)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
@@ -78,7 +93,9 @@ def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre):
 
 @MMAS
 @pytest.mark.parametrize('Cin', [128, 1024])
-def test_conv1d_maxpool_residual_transposed(rng, mma, pre, Cin):
+@pytest.mark.parametrize('kernel', ['tiled', 'slab'])
+def test_conv1d_maxpool_residual_transposed(rng, mma, pre, Cin, kernel, monkeypatch):
+    slab_or_skip(kernel, mma, monkeypatch)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     B, T, N = 2, 45, 80

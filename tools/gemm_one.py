@@ -10,6 +10,8 @@ SHAPES = {  # name: (kind, B, T, Cin, N, k, maxpool)
     'post.gru_in': ('conv', 64, 1368, 256, 1536, 1, False),
     'lstm_in': ('conv', 64, 200, 512, 4096, 1, False),
     'post.bank': ('bank', 64, 1368, 80, 8),
+    'pre.proj1': ('conv', 64, 200, 4096, 256, 3, True),
+    'pred.conv': ('conv', 64, 200, 256, 256, 5, False),
     'pre.bank': ('bank', 64, 200, 256, 16),
 }
 ap = argparse.ArgumentParser()
@@ -23,7 +25,7 @@ if s[0] == 'conv':
     _, B, T, Cin, N, k, mp = s
     x = torch.randn(B, T, Cin, device='cuda')
     w = torch.randn(N, k * Cin, device='cuda') * 0.05
-    w3 = ops.split_weights(w) if a.pre else None
+    w3 = ops.presplit_for(w) if a.pre else None
     fn = lambda: ops.conv1d(x, w, k, k // 2, relu=True, maxpool=mp, w_split=w3)
 else:
     _, B, T, Cin, K = s
