@@ -1043,11 +1043,16 @@ constexpr int SL_ZROW = SL_SR;                       // an all-zero row after th
 constexpr int SL_AIMG = (SL_SR + 1) * SL_P;         // halves per (buffer, plane) slab image
 constexpr int SL_BIMG = SL_BN * SL_P;               // halves per (buffer, plane) B image
 constexpr int SL_ASLOTS = (SL_SR * 8 + 511) / 512;  // float4 slab loads per thread per chunk
+constexpr int SL_TP = SL_BN + 4;                    // floats per row of the epilogue tile
 
-template <bool MAXPOOL>
+template <int EPI, bool MAXPOOL>
 __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams p) {
-  __shared__ __attribute__((aligned(16))) _Float16 lds_a[2 * 2 * SL_AIMG];  // [buf][h|t][row][48]
-  __shared__ __attribute__((aligned(16))) _Float16 lds_b[2 * 2 * SL_BIMG];  // [buf][B0|B1][n][48]
+  // slab images [buf][h|t][row][48], then B images [buf][B0|B1][n][48]; the epilogue reuses
+  // the whole array as the fp32 output tile
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 2 * SL_AIMG + 2 * 2 * SL_BIMG];
+  static_assert(SL_BM * SL_TP * 4 <= sizeof(lds), "epilogue tile");
+  _Float16 *const lds_a = lds;
+  _Float16 *const lds_b = lds + 2 * 2 * SL_AIMG;
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const GemmGroup &G = p.g[0];
   // XCD-aware order: blocks b and b + 8 run on the same XCD, and the NT column tiles of one
@@ -1244,7 +1249,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
     step(s + 1, rb0);
   }
 
-  // ---- epilogue: undo the 2^11 / column scaling, range guard, stores ---------------------
+  // ---- epilogue: undo the 2^11 / column scaling, range guard ----------------------------
   bool bad = !(amax <= 65504.f);
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni) {
@@ -1261,46 +1266,70 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
   }
   if (bad && p.status) atomicOr(p.status, 1u);
 
-  if (p.split > 1) {  // raw partial sums; splitk_epilogue_kernel finishes
-    float *part = p.part + (size_t)blockIdx.y * p.M * G.N;
+  // ---- the tile goes through LDS (the pipeline buffers are free now) so that every store
+  // moves whole rows, 16 B per lane: the fragment layout would write 64-B pieces of 4 rows
+  float *tile = (float *)lds;  // [SL_BM][SL_TP]
+  __syncthreads();             // every wave is past its last fragment read
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int col = n0 + wn * 64 + ni * 16 + fr;
-      if (col >= G.N) continue;
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = m0 + wm * 64 + mi * 16 + 4 * fs + i;
-          if (row < p.M) part[(size_t)row * G.N + col] = acc[mi][ni][i];
-        }
-    }
-    return;
-  }
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int col = n0 + wn * 64 + ni * 16 + fr;
-    if (col >= G.N) continue;
-    const float bias = G.bias ? G.bias[col] : 0.f;
-    const float sc = G.scale ? G.scale[col] : 1.f;
-    const float sh = G.scale ? G.shift[col] : 0.f;
+  for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = m0 + wm * 64 + mi * 16 + 4 * fs + i;
-        if (row >= p.M) continue;
-        float v = acc[mi][ni][i];
-        if (G.bias) v += bias;
-        if (p.relu) v = fmaxf(v, 0.f);
-        if (G.scale) v = v * sc + sh;
-        if (p.residual) v += p.residual[(int64_t)row * p.res_stride + col];
-        if (p.y) p.y[(int64_t)row * p.y_stride + G.ycol0 + col] = v;
-        if (p.yt) {
-          const int b = row / p.To, t = row - b * p.To;
-          p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = v;
-        }
+      for (int i = 0; i < 4; ++i)
+        tile[(wm * 64 + mi * 16 + 4 * fs + i) * SL_TP + wn * 64 + ni * 16 + fr] = acc[mi][ni][i];
+  __syncthreads();
+  const int rows = min(SL_BM, p.M - m0);
+  const int ncols = min(SL_BN, G.N - n0);  // a multiple of 4 (slab_ok)
+
+  if (p.split > 1) {  // raw partial sums; splitk_epilogue_kernel finishes
+    float *part = p.part + (size_t)blockIdx.y * p.M * G.N;
+    for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += 512) {
+      const int r = idx >> 5, c = (idx & 31) * 4;
+      if (r < rows && c < ncols)
+        *(f32x4 *)(part + (size_t)(m0 + r) * G.N + n0 + c) = *(const f32x4 *)(tile + r * SL_TP + c);
+    }
+    return;
+  }
+  if constexpr (EPI == EPI_CONV) {
+    for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += 512) {
+      const int r = idx >> 5, c = (idx & 31) * 4;
+      if (r >= rows || c >= ncols) continue;
+      const int row = m0 + r, col = n0 + c;
+      f32x4 v = *(const f32x4 *)(tile + r * SL_TP + c);
+      if (G.bias) v += *(const f32x4 *)(G.bias + col);
+      if (p.relu) v = fmax4(v, (f32x4){0.f, 0.f, 0.f, 0.f});
+      if (G.scale) v = v * *(const f32x4 *)(G.scale + col) + *(const f32x4 *)(G.shift + col);
+      if (p.residual) v += *(const f32x4 *)(p.residual + (int64_t)row * p.res_stride + col);
+      if (p.y) *(f32x4 *)(p.y + (int64_t)row * p.y_stride + G.ycol0 + col) = v;
+      if (p.yt) *(f32x4 *)(tile + r * SL_TP + c) = v;  // finished values for the yt pass
+    }
+    if (p.yt) {  // (B, N, To) copy: consecutive lanes take consecutive frames
+      __syncthreads();
+      for (int idx = tid; idx < SL_BM * SL_BN; idx += 512) {
+        const int r = idx & (SL_BM - 1), c = idx / SL_BM;
+        if (r >= rows || c >= ncols) continue;
+        const int row = m0 + r, b = row / p.To, t = row - b * p.To;
+        p.yt[((int64_t)b * p.yt_channels + G.ycol0 + n0 + c) * p.To + t] = tile[r * SL_TP + c];
       }
+    }
+  } else {
+    // highway: packed 32-column blocks [W1 | W2] per 64 GEMM columns; GEMM columns
+    // q*64 + h (W1) and q*64 + 32 + h (W2) of the tile give output column n0/2 + q*32 + h
+    for (int idx = tid; idx < SL_BM * (SL_BN / 8); idx += 512) {
+      const int r = idx >> 4, o = (idx & 15) * 4, q = o >> 5, h = o & 31;
+      if (r >= rows || q * 64 >= ncols) continue;
+      const int row = m0 + r, col = n0 / 2 + o;
+      const f32x4 x1 = *(const f32x4 *)(tile + r * SL_TP + q * 64 + h) + *(const f32x4 *)(p.b1 + col);
+      const f32x4 x2 = *(const f32x4 *)(tile + r * SL_TP + q * 64 + 32 + h) + *(const f32x4 *)(p.b2 + col);
+      const f32x4 xin = *(const f32x4 *)(p.x + (int64_t)row * p.x_stride + col);
+      f32x4 out;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g = ftmi_sigmoid(x2[e]);
+        out[e] = g * fmaxf(x1[e], 0.f) + (1.f - g) * xin[e];
+      }
+      *(f32x4 *)(p.y + (int64_t)row * p.y_stride + col) = out;
+    }
   }
 }
 
@@ -1404,14 +1433,22 @@ static int64_t slab_min_macs() {
   const char *e = getenv("FTMI_GEMM_SLAB_MIN");
   return e ? atoll(e) : SL_MIN_MACS;
 }
-static bool slab_ok(const GemmParams &p) {
-  return slab_enabled() && p.ngroups == 1 && p.To == p.T && p.Cin % 32 == 0 &&
-         p.g[0].k <= SL_MAXK && (p.g[0].k > 1 || p.g[0].N > SL_BN) &&
-         (int64_t)p.M * p.g[0].N * p.g[0].Ktot >= slab_min_macs() &&
-         (int64_t)p.M * p.x_stride < ((int64_t)1 << 31);
+static bool al16(const void *q) { return ((uintptr_t)q & 15u) == 0; }
+static bool slab_ok(const GemmParams &p, int epi) {
+  const GemmGroup &g = p.g[0];
+  if (!(slab_enabled() && p.ngroups == 1 && p.To == p.T && p.Cin % 32 == 0 && g.k <= SL_MAXK &&
+        (g.k > 1 || g.N > SL_BN) && (int64_t)p.M * g.N * g.Ktot >= slab_min_macs() &&
+        (int64_t)p.M * p.x_stride < ((int64_t)1 << 31)))
+    return false;
+  // the epilogue moves float4s: 16-B aligned rows and per-column vectors
+  if (g.N % 4 || (p.y && (!al16(p.y + g.ycol0) || p.y_stride % 4))) return false;
+  if (p.residual && (!al16(p.residual) || p.res_stride % 4)) return false;
+  if (!al16(g.bias) || !al16(g.scale) || !al16(g.shift)) return false;
+  if (epi == EPI_HIGHWAY && (p.split_req > 1 || !al16(p.b1) || !al16(p.b2))) return false;
+  return true;
 }
 
-static int launch_slab(const GemmParams &p, bool maxpool, hipStream_t s) {
+static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s) {
   GemmParams q = p;
   const int nch = q.Cin / 32;
   q.split = 1;
@@ -1428,10 +1465,12 @@ static int launch_slab(const GemmParams &p, bool maxpool, hipStream_t s) {
   const int MT = (q.M + SL_BM - 1) / SL_BM;
   const int nblk = (MT + 7) / 8 * 8 * q.g[0].ntiles;  // whole XCD rounds (see the kernel)
   dim3 grid(nblk, q.split), block(512);
-  if (maxpool)
-    hipLaunchKernelGGL((conv_gemm_slab_kernel<true>), grid, block, 0, s, q);
+  if (epi == EPI_HIGHWAY)
+    hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_HIGHWAY, false>), grid, block, 0, s, q);
+  else if (maxpool)
+    hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_CONV, true>), grid, block, 0, s, q);
   else
-    hipLaunchKernelGGL((conv_gemm_slab_kernel<false>), grid, block, 0, s, q);
+    hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_CONV, false>), grid, block, 0, s, q);
   FTMI_CHECK_LAUNCH();
   if (q.split > 1) {
     const int64_t total = (int64_t)q.M * q.g[0].N;
@@ -1448,7 +1487,7 @@ int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hip
   bool presplit = (mma == 1 && x6_variant() != 3) || mma == 2;
   for (int i = 0; i < p.ngroups; ++i) presplit &= p.g[i].w3 != nullptr;
   if (mma == 2 && !presplit) return FTMI_E_ARG;  // the f16 path needs the split planes
-  if (mma == 2 && epi == EPI_CONV && slab_ok(p)) return launch_slab(p, maxpool, s);
+  if (mma == 2 && slab_ok(p, epi)) return launch_slab(p, epi, maxpool, s);
   if (presplit) {
     dim3 g2(nblocks, p.split > 1 ? p.split : 1);
     if (mma == 2) {

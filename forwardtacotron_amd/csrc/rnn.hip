@@ -511,7 +511,16 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = hv[ks * 8 + e];
         f16x8 hh, ht;
-        split2h8(v, hh, ht);
+        if (p.diag & 8) {  // timing experiment: head only (no tail split)
+          typedef float f32x8 __attribute__((ext_vector_type(8)));
+          f32x8 x;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = v[e];
+          hh = __builtin_convertvector(x, f16x8);
+          ht = hh;
+        } else {
+          split2h8(v, hh, ht);
+        }
         const f16x8 hs = hh * (_Float16)H3_SCALE;  // 2^11 h_h: exact, |h| < 1
 #pragma unroll
         for (int i = 0; i < RBW; ++i) {

@@ -141,15 +141,17 @@ def test_conv_bank(K, Cin, B, T, rng, mma, pre):
 
 
 @MMAS
-def test_highway(rng, mma, pre):
+@pytest.mark.parametrize('kernel', ['tiled', 'slab'])
+@pytest.mark.parametrize('C,B,T', [(256, 3, 77), (128, 2, 300)])
+def test_highway(rng, mma, pre, kernel, C, B, T, monkeypatch):
     from forwardtacotron_amd.common_layers import HighwayNetwork
-    C = 256
+    slab_or_skip(kernel, mma, monkeypatch)
     hw = HighwayNetwork(C)
     sd = {'W1.weight': rng.normal(0, 1 / 16, (C, C)), 'W1.bias': rng.normal(0, .1, C),
           'W2.weight': rng.normal(0, 1 / 16, (C, C)), 'W2.bias': rng.normal(0, .1, C)}
     hw.load_state_dict({k: torch.from_numpy(v.astype(np.float32)) for k, v in sd.items()})
     hw = hw.cuda()
-    x = rng.normal(0, 1, (3, 77, C)).astype(np.float32)
+    x = rng.normal(0, 1, (B, T, C)).astype(np.float32)
     ref = O.highway({'h.' + k: v.astype(np.float32) for k, v in sd.items()}, 'h', x, np.float32)
     w12, b1, b2, _ = hw.packed_weights()
     from forwardtacotron_amd import ops
