@@ -1054,13 +1054,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
   _Float16 *const lds_a = lds;
   _Float16 *const lds_b = lds + 2 * 2 * SL_AIMG;
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const GemmGroup &G = p.g[0];
-  // XCD-aware order: blocks b and b + 8 run on the same XCD, and the NT column tiles of one
-  // row tile are consecutive in that XCD's order, so its slab rows are shared through L2
-  const int MT = (p.M + SL_BM - 1) / SL_BM, NT = G.ntiles;
-  const int bid = blockIdx.x, s8 = bid >> 3, q8 = s8 / NT;
-  const int mt = q8 * 8 + (bid & 7), nt = s8 - q8 * NT;
+  // XCD-aware order: blocks b and b + 8 run on the same XCD, and the tiles of one row tile
+  // (every column tile of every group: a conv bank's groups all read the same input rows)
+  // are consecutive in that XCD's order, so its slab rows are shared through L2.  Groups
+  // (conv bank: one per kernel size, heaviest first) all have NT column tiles.
+  const int MT = (p.M + SL_BM - 1) / SL_BM, NT = p.g[0].ntiles, VT = p.ngroups * NT;
+  const int bid = blockIdx.x, s8 = bid >> 3, q8 = s8 / VT;
+  const int mt = q8 * 8 + (bid & 7), v8 = s8 - q8 * VT, gi = v8 / NT, nt = v8 - gi * NT;
   if (mt >= MT) return;  // the grid is padded to whole XCD rounds
+  const GemmGroup &G = p.g[gi];
   const int m0 = mt * SL_BM, n0 = nt * SL_BN;
   const int k = G.k, pad = G.pad, Cin = p.Cin;
 
@@ -1068,7 +1070,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
   const int wm = wave & 3, wn = wave >> 2;
   const int fr = lane & 15, fs = lane >> 4;  // fragment row / k-segment (8 k each)
 
-  int nch = Cin / 32, c_begin = 0;
+  // 32-channel chunks; with Cin % 32 != 0 the last chunk is partial: its missing channels
+  // are zero in the slab and in the staged B (cbase + chunk offset + lane channel >= Cin)
+  int nch = (Cin + 31) / 32, c_begin = 0;
   if (p.split > 1) {  // split over channel chunks: blockIdx.y = s takes [s kc_per, ...)
     c_begin = blockIdx.y * p.kc_per;
     nch = min(nch - c_begin, p.kc_per);
@@ -1089,7 +1093,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
     const int sr = 4 * (pr >> 1) + (pr & 1) + 2 * ((idx >> 3) & 1);
     int mp = m0 - pad + sr;
     mp = mp < 0 ? 0 : (mp >= p.M ? p.M - 1 : mp);
-    aoff[i] = (unsigned)mp * (unsigned)p.x_stride + (unsigned)(c_begin * 32 + seg * 4);
+    aoff[i] = (unsigned)mp * (unsigned)p.x_stride;  // row start; + channel at the load
     if constexpr (MAXPOOL) {  // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
       const int tp = mp % p.T;
       poff[i] = aoff[i] - (tp > 0 ? (unsigned)p.x_stride : 0u);
@@ -1099,11 +1103,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
   struct ARaw {
     f32x4 v[SL_ASLOTS];
     f32x4 u[MAXPOOL ? SL_ASLOTS : 1];
+    bool ok;  // this lane's 4 channels exist (all slots of a lane share them)
   };
+  const unsigned cbase = (unsigned)c_begin * 32u, aseg = (unsigned)(tid & 7) * 4u;
   const unsigned a_last = (unsigned)(nch - 1) * 32u;
   unsigned ach = 0;  // channel offset (within this split) of the next slab load
   auto loadA = [&](ARaw &r) {
-    const unsigned o = ach < a_last ? ach : a_last;
+    const unsigned ch = cbase + (ach < a_last ? ach : a_last) + aseg;
+    r.ok = ch < (unsigned)Cin;
+    const unsigned o = r.ok ? ch : 0u;
 #pragma unroll
     for (int i = 0; i < SL_ASLOTS; ++i) {
       r.v[i] = *(const f32x4 *)(p.x + aoff[i] + o);
@@ -1119,6 +1127,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
       if (adst[i] < 0) continue;
       f32x4 v = r.v[i];
       if constexpr (MAXPOOL) v = fmax4(v, r.u[i]);
+      v = sel4(r.ok, v);
       amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
       f16x4 h, t;
       split2h(v, h, t);
@@ -1140,23 +1149,31 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
     const int idx = tid + 512 * i, pl = idx >> 9, rem = idx & 511, seg = rem & 3;
     const int pr = rem >> 3, nl = 4 * (pr >> 1) + (pr & 1) + 2 * ((rem >> 2) & 1);
     const int n = n0 + nl < G.N ? n0 + nl : G.N - 1;
-    bsrc[i] = w16 + ((int64_t)pl * G.N + n) * G.Kpad + c_begin * 32 + seg * 8;
+    bsrc[i] = w16 + ((int64_t)pl * G.N + n) * G.Kpad;  // row start; + tap / channel at the load
     bdst[i] = pl * SL_BIMG + nl * SL_P + seg * 8;
   }
+  struct BRaw {
+    u32x4 v[2];
+    bool ok;  // this lane's 8 channels exist
+  };
+  const int bseg = (tid & 3) * 8;
   int bj = 0, bc = 0;  // tap / chunk of the next B load
-  auto loadB = [&](u32x4 (&rb)[2]) {
+  auto loadB = [&](BRaw &rb) {
     const bool in = bc < nch;
-    const int off = (in ? bj : k - 1) * Cin + (in ? bc : nch - 1) * 32;
+    const int ch = (int)cbase + (in ? bc : nch - 1) * 32 + bseg;
+    rb.ok = ch < Cin;
+    const int off = (in ? bj : k - 1) * Cin + (rb.ok ? ch : 0);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) rb[i] = *(const u32x4 *)(bsrc[i] + off);
+    for (int i = 0; i < 2; ++i) rb.v[i] = *(const u32x4 *)(bsrc[i] + off);
     if (++bj == k) {
       bj = 0;
       ++bc;
     }
   };
-  auto storeB = [&](const u32x4 (&rb)[2], int buf) {
+  auto storeB = [&](const BRaw &rb, int buf) {
+    const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *(u32x4 *)(lds_b + buf * 2 * SL_BIMG + bdst[i]) = rb[i];
+    for (int i = 0; i < 2; ++i) *(u32x4 *)(lds_b + buf * 2 * SL_BIMG + bdst[i]) = rb.ok ? rb.v[i] : z;
   };
 
   // ---- per-row tap masks: bit j set iff frame t + j - pad lies inside the sequence -------
@@ -1216,7 +1233,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
     *(u32x4 *)(lds_a + img * SL_AIMG + SL_ZROW * SL_P + part * 8) = (u32x4){0u, 0u, 0u, 0u};
   }
   ARaw ra;
-  u32x4 rb0[2], rb1[2];
+  BRaw rb0, rb1;
   loadA(ra);
   loadB(rb0);  // step 0
   storeA(ra, 0);
@@ -1226,7 +1243,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
   if (nch > 1) loadA(ra);  // chunk 1
   __syncthreads();
   int c = 0, j = 0;
-  auto step = [&](int s, u32x4 (&rbs)[2]) {
+  auto step = [&](int s, BRaw &rbs) {
     const bool last_tap = j == k - 1 && c + 1 < nch;
     // MFMAs first: the staging below (LDS stores of the next B / slab, the slab's f16 split,
     // the next loads) is independent of them and fills the matrix pipe's shadow
@@ -1421,8 +1438,9 @@ static bool slab_enabled() {
   return v;
 }
 
-// slab kernel eligibility: one group, same-length output, whole 32-channel chunks, k taps
-// within the slab halo, 32-bit activation offsets; a k = 1 GEMM only when it has more than
+// slab kernel eligibility: same-length output, Cin % 16 == 0, k taps within the slab halo,
+// groups of equal width (conv bank), 32-bit activation offsets; a k = 1 GEMM only when it
+// has more than
 // one column tile (narrow Linear layers run faster on the 128 x 128 x6b tiles).
 // FTMI_GEMM_SLAB_MIN (MACs, read per call; default 0) keeps smaller contractions on the
 // x6b kernel: tests use it to cover both kernels, A/B runs to size the choice (taking
@@ -1436,21 +1454,27 @@ static int64_t slab_min_macs() {
 static bool al16(const void *q) { return ((uintptr_t)q & 15u) == 0; }
 static bool slab_ok(const GemmParams &p, int epi) {
   const GemmGroup &g = p.g[0];
-  if (!(slab_enabled() && p.ngroups == 1 && p.To == p.T && p.Cin % 32 == 0 && g.k <= SL_MAXK &&
-        (g.k > 1 || g.N > SL_BN) && (int64_t)p.M * g.N * g.Ktot >= slab_min_macs() &&
-        (int64_t)p.M * p.x_stride < ((int64_t)1 << 31)))
+  int64_t macs = 0;
+  for (int i = 0; i < p.ngroups; ++i) macs += (int64_t)p.M * p.g[i].N * p.g[i].Ktot;
+  if (!(slab_enabled() && p.To == p.T && p.Cin % 16 == 0 && (g.k > 1 || g.N > SL_BN) &&
+        macs >= slab_min_macs() && (int64_t)p.M * p.x_stride < ((int64_t)1 << 31)))
     return false;
-  // the epilogue moves float4s: 16-B aligned rows and per-column vectors
-  if (g.N % 4 || (p.y && (!al16(p.y + g.ycol0) || p.y_stride % 4))) return false;
+  if (p.ngroups > 1 && p.split_req > 1) return false;  // the split-K finish is single-group
+  for (int i = 0; i < p.ngroups; ++i) {
+    const GemmGroup &gi = p.g[i];
+    if (gi.k > SL_MAXK || gi.ntiles != g.ntiles || gi.N % 4) return false;
+    // the epilogue moves float4s: 16-B aligned rows and per-column vectors
+    if (p.y && (!al16(p.y + gi.ycol0) || p.y_stride % 4)) return false;
+    if (!al16(gi.bias) || !al16(gi.scale) || !al16(gi.shift)) return false;
+  }
   if (p.residual && (!al16(p.residual) || p.res_stride % 4)) return false;
-  if (!al16(g.bias) || !al16(g.scale) || !al16(g.shift)) return false;
   if (epi == EPI_HIGHWAY && (p.split_req > 1 || !al16(p.b1) || !al16(p.b2))) return false;
   return true;
 }
 
 static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s) {
   GemmParams q = p;
-  const int nch = q.Cin / 32;
+  const int nch = (q.Cin + 31) / 32;
   q.split = 1;
   static const int diag = [] {
     const char *e = getenv("FTMI_SLAB_DIAG");
@@ -1463,7 +1487,7 @@ static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s
     q.split = (nch + q.kc_per - 1) / q.kc_per;
   }
   const int MT = (q.M + SL_BM - 1) / SL_BM;
-  const int nblk = (MT + 7) / 8 * 8 * q.g[0].ntiles;  // whole XCD rounds (see the kernel)
+  const int nblk = (MT + 7) / 8 * 8 * q.ngroups * q.g[0].ntiles;  // whole XCD rounds
   dim3 grid(nblk, q.split), block(512);
   if (epi == EPI_HIGHWAY)
     hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_HIGHWAY, false>), grid, block, 0, s, q);

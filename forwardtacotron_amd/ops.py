@@ -105,7 +105,7 @@ SLAB = os.environ.get('FTMI_GEMM_SLAB', '1') != '0'
 
 def _slab(mma: int, T: int, To: int, Cin: int, k: int, N: int, M: int) -> bool:
     """Whether ftmi_conv1d takes the slab kernel (gemm.hip slab_ok)."""
-    return (SLAB and mma == 2 and To == T and Cin % 32 == 0 and k <= 16 and (k > 1 or N > 128)
+    return (SLAB and mma == 2 and To == T and Cin % 16 == 0 and k <= 16 and (k > 1 or N > 128)
             and M * N * k * Cin >= int(os.environ.get('FTMI_GEMM_SLAB_MIN', 0)))
 
 
@@ -118,7 +118,7 @@ def _split_k(M: int, N: int, K: int, mma: int, slab: bool = False, Cin: int = 0)
         cus = _num_cus()
         if K < 1024 or tiles * 4 >= cus * 3:
             return 1
-        return int(max(1, min(8, -(-cus // tiles), Cin // 32)))
+        return int(max(1, min(8, -(-cus // tiles), -(-Cin // 32))))
     if mma == 0 or K < 2048:
         return 1
     tiles = -(-M // 128) * -(-N // 128)

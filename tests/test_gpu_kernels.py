@@ -123,8 +123,10 @@ def test_conv1d_strided_input_view(rng, mma, pre):
 
 
 @MMAS
-@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 2, 41), (8, 80, 2, 150)])
-def test_conv_bank(K, Cin, B, T, rng, mma, pre):
+@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 2, 41), (8, 80, 2, 150), (5, 48, 3, 270)])
+@pytest.mark.parametrize('kernel', ['tiled', 'slab'])
+def test_conv_bank(K, Cin, B, T, rng, mma, pre, kernel, monkeypatch):
+    slab_or_skip(kernel, mma, monkeypatch)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     C = 256
