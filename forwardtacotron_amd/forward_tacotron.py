@@ -19,6 +19,7 @@ Pipeline of ``generate`` (channels-last activations, one HIP stream):
 """
 from __future__ import annotations
 
+import os
 from pathlib import Path
 from typing import Any, Callable, Dict, Union
 
@@ -219,9 +220,15 @@ class ForwardTacotron(nn.Module):
                 'dur': dur_hat, 'pitch': pitch_hat, 'energy': energy_hat}
 
     def _side_streams(self, device):
+        """(pitch, energy, prenet) streams.  The prenet CBHG -> LSTM input projection is the
+        phoneme phase's critical chain: its stream gets the higher priority
+        (FTMI_PRENET_PRIORITY, default -1 = high; 0 = same as the others), so the
+        predictors fill the CUs it leaves idle instead of delaying it."""
         cache = self.__dict__.setdefault('_ftmi_streams', {})
         if device not in cache:
-            cache[device] = [torch.cuda.Stream(device=device) for _ in range(3)]
+            prio = int(os.environ.get('FTMI_PRENET_PRIORITY', '-1'))
+            cache[device] = [torch.cuda.Stream(device=device), torch.cuda.Stream(device=device),
+                             torch.cuda.Stream(device=device, priority=prio)]
         return cache[device]
 
     def _phoneme_phase(self, x, alpha, pitch_fn, energy_fn, batch=None):
