@@ -1042,11 +1042,17 @@ constexpr int SL_ZROW = SL_SR;                       // an all-zero row after th
                                                     // masked taps read it (no selects)
 constexpr int SL_AIMG = (SL_SR + 1) * SL_P;         // halves per (buffer, plane) slab image
 constexpr int SL_BIMG = SL_BN * SL_P;               // halves per (buffer, plane) B image
-constexpr int SL_ASLOTS = (SL_SR * 8 + 511) / 512;  // float4 slab loads per thread per chunk
 constexpr int SL_TP = SL_BN + 4;                    // floats per row of the epilogue tile
 
-template <int EPI, bool MAXPOOL>
-__global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams p) {
+// WS (warp-specialised, 768 threads): waves 0-7 only read fragments and issue MFMAs; waves
+// 8-11 do all staging (global loads, the slab's f16 split, LDS stores), so the staging VALU
+// and load waits never sit in the MFMA waves' instruction streams.  !WS: all 8 waves do both.
+template <int EPI, bool MAXPOOL, bool WS>
+__global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const GemmParams p) {
+  constexpr int NTHR = WS ? 768 : 512;              // threads per workgroup
+  constexpr int NSTG = WS ? 256 : 512;              // staging threads
+  constexpr int SL_ASLOTS = (SL_SR * 8 + NSTG - 1) / NSTG;  // float4 slab loads per thread
+  constexpr int SL_BSLOTS = 1024 / NSTG;            // 16-B B loads per thread per step
   // slab images [buf][h|t][row][48], then B images [buf][B0|B1][n][48]; the epilogue reuses
   // the whole array as the fp32 output tile
   __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 2 * SL_AIMG + 2 * 2 * SL_BIMG];
@@ -1067,8 +1073,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
   const int k = G.k, pad = G.pad, Cin = p.Cin;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 3, wn = wave >> 2;
+  const int wm = wave & 3, wn = (wave >> 2) & 1;
   const int fr = lane & 15, fs = lane >> 4;  // fragment row / k-segment (8 k each)
+  const bool is_mma = !WS || wave < 8;       // wave-uniform roles
+  const bool is_stg = !WS || wave >= 8;
+  const int stid = WS ? tid - 512 : tid;     // staging thread index (valid when is_stg)
 
   // 32-channel chunks; with Cin % 32 != 0 the last chunk is partial: its missing channels
   // are zero in the slab and in the staged B (cbase + chunk offset + lane channel >= Cin)
@@ -1083,29 +1092,25 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
   // Every load is unconditional with a clamped address (static wait counters); clamped
   // rows only feed taps that the row masks zero.
   const int SR = SL_BM + k - 1;
+  // the 16 lanes of one ds_write_b64 group write slab rows sr and sr + 2 (conflict free);
+  // slot i of a staging lane is slab row sr0 + (NSTG / 8) i
+  const int sr0 = 4 * (stid >> 5) + ((stid >> 4) & 1) + 2 * ((stid >> 3) & 1);
+  const int adst0 = sr0 * SL_P + (stid & 7) * 4;
   unsigned aoff[SL_ASLOTS];
-  unsigned poff[MAXPOOL ? SL_ASLOTS : 1];
-  int adst[SL_ASLOTS];
+  unsigned prev = 0;  // maxpool: bit i = slot i's frame has a predecessor in its sequence
 #pragma unroll
   for (int i = 0; i < SL_ASLOTS; ++i) {
-    // the 16 lanes of one ds_write_b64 group write slab rows sr and sr + 2 (conflict free)
-    const int idx = tid + 512 * i, seg = idx & 7, pr = idx >> 4;
-    const int sr = 4 * (pr >> 1) + (pr & 1) + 2 * ((idx >> 3) & 1);
-    int mp = m0 - pad + sr;
+    int mp = m0 - pad + sr0 + (NSTG / 8) * i;
     mp = mp < 0 ? 0 : (mp >= p.M ? p.M - 1 : mp);
     aoff[i] = (unsigned)mp * (unsigned)p.x_stride;  // row start; + channel at the load
-    if constexpr (MAXPOOL) {  // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
-      const int tp = mp % p.T;
-      poff[i] = aoff[i] - (tp > 0 ? (unsigned)p.x_stride : 0u);
-    }
-    adst[i] = sr < SR ? sr * SL_P + seg * 4 : -1;
+    if constexpr (MAXPOOL) prev |= (unsigned)(mp % p.T > 0) << i;
   }
   struct ARaw {
     f32x4 v[SL_ASLOTS];
     f32x4 u[MAXPOOL ? SL_ASLOTS : 1];
     bool ok;  // this lane's 4 channels exist (all slots of a lane share them)
   };
-  const unsigned cbase = (unsigned)c_begin * 32u, aseg = (unsigned)(tid & 7) * 4u;
+  const unsigned cbase = (unsigned)c_begin * 32u, aseg = (unsigned)(stid & 7) * 4u;
   const unsigned a_last = (unsigned)(nch - 1) * 32u;
   unsigned ach = 0;  // channel offset (within this split) of the next slab load
   auto loadA = [&](ARaw &r) {
@@ -1115,7 +1120,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
 #pragma unroll
     for (int i = 0; i < SL_ASLOTS; ++i) {
       r.v[i] = *(const f32x4 *)(p.x + aoff[i] + o);
-      if constexpr (MAXPOOL) r.u[i] = *(const f32x4 *)(p.x + poff[i] + o);
+      // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
+      if constexpr (MAXPOOL)
+        r.u[i] = *(const f32x4 *)(p.x + aoff[i] - ((prev >> i) & 1u ? (unsigned)p.x_stride : 0u) + o);
     }
     ach += 32;
   };
@@ -1124,15 +1131,16 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
     _Float16 *dst = lds_a + buf * 2 * SL_AIMG;
 #pragma unroll
     for (int i = 0; i < SL_ASLOTS; ++i) {
-      if (adst[i] < 0) continue;
+      if (sr0 + (NSTG / 8) * i >= SR) continue;
+      const int adst = adst0 + (NSTG / 8) * i * SL_P;
       f32x4 v = r.v[i];
       if constexpr (MAXPOOL) v = fmax4(v, r.u[i]);
       v = sel4(r.ok, v);
       amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
       f16x4 h, t;
       split2h(v, h, t);
-      *(f16x4 *)(dst + adst[i]) = h;
-      *(f16x4 *)(dst + SL_AIMG + adst[i]) = t;
+      *(f16x4 *)(dst + adst) = h;
+      *(f16x4 *)(dst + SL_AIMG + adst) = t;
     }
   };
 
@@ -1140,23 +1148,23 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
   // Rows n >= N read row N-1 (their output columns are never stored); steps past the end
   // re-read the last step (clamped).
   const _Float16 *w16 = (const _Float16 *)G.w3;
-  const _Float16 *bsrc[2];
-  int bdst[2];
+  const _Float16 *bsrc[SL_BSLOTS];
+  int bdst[SL_BSLOTS];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < SL_BSLOTS; ++i) {
     // the 8 lanes of one ds_write_b128 group write rows nl and nl + 2 (bank offset 16 of 32:
     // conflict free); rows 4g + {0, 1, 2, 3} come from lane pairs (2g, 2g + 1)
-    const int idx = tid + 512 * i, pl = idx >> 9, rem = idx & 511, seg = rem & 3;
+    const int idx = stid + NSTG * i, pl = idx >> 9, rem = idx & 511, seg = rem & 3;
     const int pr = rem >> 3, nl = 4 * (pr >> 1) + (pr & 1) + 2 * ((rem >> 2) & 1);
     const int n = n0 + nl < G.N ? n0 + nl : G.N - 1;
     bsrc[i] = w16 + ((int64_t)pl * G.N + n) * G.Kpad;  // row start; + tap / channel at the load
     bdst[i] = pl * SL_BIMG + nl * SL_P + seg * 8;
   }
   struct BRaw {
-    u32x4 v[2];
+    u32x4 v[SL_BSLOTS];
     bool ok;  // this lane's 8 channels exist
   };
-  const int bseg = (tid & 3) * 8;
+  const int bseg = (stid & 3) * 8;
   int bj = 0, bc = 0;  // tap / chunk of the next B load
   auto loadB = [&](BRaw &rb) {
     const bool in = bc < nch;
@@ -1164,7 +1172,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
     rb.ok = ch < Cin;
     const int off = (in ? bj : k - 1) * Cin + (rb.ok ? ch : 0);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) rb.v[i] = *(const u32x4 *)(bsrc[i] + off);
+    for (int i = 0; i < SL_BSLOTS; ++i) rb.v[i] = *(const u32x4 *)(bsrc[i] + off);
     if (++bj == k) {
       bj = 0;
       ++bc;
@@ -1173,7 +1181,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
   auto storeB = [&](const BRaw &rb, int buf) {
     const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *(u32x4 *)(lds_b + buf * 2 * SL_BIMG + bdst[i]) = rb.ok ? rb.v[i] : z;
+    for (int i = 0; i < SL_BSLOTS; ++i)
+      *(u32x4 *)(lds_b + buf * 2 * SL_BIMG + bdst[i]) = rb.ok ? rb.v[i] : z;
   };
 
   // ---- per-row tap masks: bit j set iff frame t + j - pad lies inside the sequence -------
@@ -1190,13 +1199,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
     vmask[mi] = msk;
   }
 
-  f32x4 acc[4][4];
+  auto zero_acc = [](f32x4 (&acc)[4][4]) {
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  auto mfma_step = [&](int abuf, int bbuf, int j) {
+      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  };
+  auto mfma_step = [&](f32x4 (&acc)[4][4], int abuf, int bbuf, int j) {
     const _Float16 *Ab = lds_a + abuf * 2 * SL_AIMG;
     const _Float16 *Bb = lds_b + bbuf * 2 * SL_BIMG;
     f16x8 ah[4], at[4];
@@ -1223,6 +1232,37 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
       }
     }
   };
+  // undo the 2^11 / column scaling; true when an accumulator of a stored element is not
+  // finite (range guard)
+  auto finish_acc = [&](f32x4 (&acc)[4][4]) -> bool {
+    bool bad = false;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int col = n0 + wn * 64 + ni * 16 + fr;
+      const float cs = G.colscale[col < G.N ? col : G.N - 1];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wm * 64 + mi * 16 + 4 * fs + i;
+          bad |= col < G.N && row < p.M && !__builtin_isfinite(acc[mi][ni][i]);
+          acc[mi][ni][i] *= cs;
+        }
+    }
+    return bad;
+  };
+  // the tile goes through LDS (the pipeline buffers are free by then) so that every store
+  // moves whole rows, 16 B per lane: the fragment layout would write 64-B pieces of 4 rows
+  float *tile = (float *)lds;  // [SL_BM][SL_TP]
+  auto write_tile = [&](const f32x4 (&acc)[4][4]) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          tile[(wm * 64 + mi * 16 + 4 * fs + i) * SL_TP + wn * 64 + ni * 16 + fr] = acc[mi][ni][i];
+  };
 
   // ---- pipeline: step s = (chunk c, tap j) uses slab buffer c & 1 and B buffer s & 1 ------
   // At step s: stage B s+1 (register set (s+1) & 1, loaded two steps ago) and, on a chunk's
@@ -1232,75 +1272,107 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
     const int img = tid / (SL_P / 8), part = tid % (SL_P / 8);
     *(u32x4 *)(lds_a + img * SL_AIMG + SL_ZROW * SL_P + part * 8) = (u32x4){0u, 0u, 0u, 0u};
   }
-  ARaw ra;
-  BRaw rb0, rb1;
-  loadA(ra);
-  loadB(rb0);  // step 0
-  storeA(ra, 0);
-  storeB(rb0, 0);
-  loadB(rb1);  // step 1
-  loadB(rb0);  // step 2
-  if (nch > 1) loadA(ra);  // chunk 1
-  __syncthreads();
-  int c = 0, j = 0;
-  auto step = [&](int s, BRaw &rbs) {
-    const bool last_tap = j == k - 1 && c + 1 < nch;
-    // MFMAs first: the staging below (LDS stores of the next B / slab, the slab's f16 split,
-    // the next loads) is independent of them and fills the matrix pipe's shadow
-    if (!(p.diag & 2)) mfma_step(c & 1, s & 1, j);
-    if (s + 1 < nsteps) storeB(rbs, (s + 1) & 1);
-    if (last_tap) storeA(ra, (c + 1) & 1);
-    if (!(p.diag & 4)) {
-      loadB(rbs);
-      if (last_tap) loadA(ra);
-    }
-    if (!(p.diag & 1)) __syncthreads();
-    if (++j == k) {
-      j = 0;
-      ++c;
-    }
-  };
-  for (int s = 0; s < nsteps; s += 2) {
-    step(s, rb1);
-    if (s + 1 >= nsteps) break;
-    step(s + 1, rb0);
-  }
-
-  // ---- epilogue: undo the 2^11 / column scaling, range guard ----------------------------
-  bool bad = !(amax <= 65504.f);
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int col = n0 + wn * 64 + ni * 16 + fr;
-    const float cs = G.colscale[col < G.N ? col : G.N - 1];
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = m0 + wm * 64 + mi * 16 + 4 * fs + i;
-        bad |= col < G.N && row < p.M && !__builtin_isfinite(acc[mi][ni][i]);
-        acc[mi][ni][i] *= cs;
+  bool bad;
+  if constexpr (WS) {
+    // Two loops with the same barrier count (1 + nsteps + 1): the staging waves never hold
+    // accumulators and the MFMA waves never hold staging registers.
+    if (is_stg) {
+      ARaw ra;
+      BRaw rb0, rb1;
+      loadA(ra);
+      loadB(rb0);  // step 0
+      storeA(ra, 0);
+      storeB(rb0, 0);
+      loadB(rb1);  // step 1
+      loadB(rb0);  // step 2
+      if (nch > 1) loadA(ra);  // chunk 1
+      __syncthreads();
+      int c = 0, j = 0;
+      auto sstep = [&](int s, BRaw &rbs) {
+        const bool last_tap = j == k - 1 && c + 1 < nch;
+        if (s + 1 < nsteps) storeB(rbs, (s + 1) & 1);
+        if (last_tap) storeA(ra, (c + 1) & 1);
+        loadB(rbs);
+        if (last_tap) loadA(ra);
+        __syncthreads();
+        if (++j == k) {
+          j = 0;
+          ++c;
+        }
+      };
+      for (int s = 0; s < nsteps; s += 2) {
+        sstep(s, rb1);
+        if (s + 1 >= nsteps) break;
+        sstep(s + 1, rb0);
       }
+      bad = !(amax <= 65504.f);
+      __syncthreads();  // the MFMA waves write the tile
+    } else {
+      f32x4 acc[4][4];
+      zero_acc(acc);
+      __syncthreads();
+      int c = 0, j = 0;
+      for (int s = 0; s < nsteps; ++s) {
+        mfma_step(acc, c & 1, s & 1, j);
+        __syncthreads();
+        if (++j == k) {
+          j = 0;
+          ++c;
+        }
+      }
+      bad = finish_acc(acc);
+      write_tile(acc);  // every wave is past its last fragment read (the loop's barrier)
+      __syncthreads();
+    }
+  } else {
+    f32x4 acc[4][4];
+    zero_acc(acc);
+    ARaw ra;
+    BRaw rb0, rb1;
+    loadA(ra);
+    loadB(rb0);  // step 0
+    storeA(ra, 0);
+    storeB(rb0, 0);
+    loadB(rb1);  // step 1
+    loadB(rb0);  // step 2
+    if (nch > 1) loadA(ra);  // chunk 1
+    __syncthreads();
+    int c = 0, j = 0;
+    auto step = [&](int s, BRaw &rbs) {
+      const bool last_tap = j == k - 1 && c + 1 < nch;
+      // MFMAs first: the staging below (LDS stores of the next B / slab, the slab's f16
+      // split, the next loads) is independent of them and fills the matrix pipe's shadow
+      if (!(p.diag & 2)) mfma_step(acc, c & 1, s & 1, j);
+      if (s + 1 < nsteps) storeB(rbs, (s + 1) & 1);
+      if (last_tap) storeA(ra, (c + 1) & 1);
+      if (!(p.diag & 4)) {
+        loadB(rbs);
+        if (last_tap) loadA(ra);
+      }
+      if (!(p.diag & 1)) __syncthreads();
+      if (++j == k) {
+        j = 0;
+        ++c;
+      }
+    };
+    for (int s = 0; s < nsteps; s += 2) {
+      step(s, rb1);
+      if (s + 1 >= nsteps) break;
+      step(s + 1, rb0);
+    }
+    bad = !(amax <= 65504.f);
+    bad |= finish_acc(acc);
+    __syncthreads();  // every wave is past its last fragment read
+    write_tile(acc);
+    __syncthreads();
   }
   if (bad && p.status) atomicOr(p.status, 1u);
-
-  // ---- the tile goes through LDS (the pipeline buffers are free now) so that every store
-  // moves whole rows, 16 B per lane: the fragment layout would write 64-B pieces of 4 rows
-  float *tile = (float *)lds;  // [SL_BM][SL_TP]
-  __syncthreads();             // every wave is past its last fragment read
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        tile[(wm * 64 + mi * 16 + 4 * fs + i) * SL_TP + wn * 64 + ni * 16 + fr] = acc[mi][ni][i];
-  __syncthreads();
   const int rows = min(SL_BM, p.M - m0);
   const int ncols = min(SL_BN, G.N - n0);  // a multiple of 4 (slab_ok)
 
   if (p.split > 1) {  // raw partial sums; splitk_epilogue_kernel finishes
     float *part = p.part + (size_t)blockIdx.y * p.M * G.N;
-    for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += 512) {
+    for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
       const int r = idx >> 5, c = (idx & 31) * 4;
       if (r < rows && c < ncols)
         *(f32x4 *)(part + (size_t)(m0 + r) * G.N + n0 + c) = *(const f32x4 *)(tile + r * SL_TP + c);
@@ -1308,7 +1380,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
     return;
   }
   if constexpr (EPI == EPI_CONV) {
-    for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += 512) {
+    for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
       const int r = idx >> 5, c = (idx & 31) * 4;
       if (r >= rows || c >= ncols) continue;
       const int row = m0 + r, col = n0 + c;
@@ -1322,7 +1394,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
     }
     if (p.yt) {  // (B, N, To) copy: consecutive lanes take consecutive frames
       __syncthreads();
-      for (int idx = tid; idx < SL_BM * SL_BN; idx += 512) {
+      for (int idx = tid; idx < SL_BM * SL_BN; idx += NTHR) {
         const int r = idx & (SL_BM - 1), c = idx / SL_BM;
         if (r >= rows || c >= ncols) continue;
         const int row = m0 + r, b = row / p.To, t = row - b * p.To;
@@ -1332,7 +1404,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slab_kernel(const GemmParams
   } else {
     // highway: packed 32-column blocks [W1 | W2] per 64 GEMM columns; GEMM columns
     // q*64 + h (W1) and q*64 + 32 + h (W2) of the tile give output column n0/2 + q*32 + h
-    for (int idx = tid; idx < SL_BM * (SL_BN / 8); idx += 512) {
+    for (int idx = tid; idx < SL_BM * (SL_BN / 8); idx += NTHR) {
       const int r = idx >> 4, o = (idx & 15) * 4, q = o >> 5, h = o & 31;
       if (r >= rows || q * 64 >= ncols) continue;
       const int row = m0 + r, col = n0 / 2 + o;
@@ -1472,6 +1544,17 @@ static bool slab_ok(const GemmParams &p, int epi) {
   return true;
 }
 
+// The warp-specialised slab kernel (768 threads) for multi-tap convolutions and banks,
+// where the slab split is most of the staging work (measured 7-14 % faster at c3 shapes);
+// the 512-thread form for k = 1 (equal or faster there).  FTMI_GEMM_SLAB_WS=0/1 forces one.
+static bool slab_ws(const GemmParams &p) {
+  static const int v = [] {
+    const char *e = getenv("FTMI_GEMM_SLAB_WS");
+    return e ? atoi(e) : -1;
+  }();
+  return v < 0 ? (p.g[0].k > 1 || p.ngroups > 1) : v != 0;
+}
+
 static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s) {
   GemmParams q = p;
   const int nch = (q.Cin + 31) / 32;
@@ -1489,12 +1572,22 @@ static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s
   const int MT = (q.M + SL_BM - 1) / SL_BM;
   const int nblk = (MT + 7) / 8 * 8 * q.ngroups * q.g[0].ntiles;  // whole XCD rounds
   dim3 grid(nblk, q.split), block(512);
-  if (epi == EPI_HIGHWAY)
-    hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_HIGHWAY, false>), grid, block, 0, s, q);
-  else if (maxpool)
-    hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_CONV, true>), grid, block, 0, s, q);
-  else
-    hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_CONV, false>), grid, block, 0, s, q);
+  if (slab_ws(q)) {
+    block = dim3(768);
+    if (epi == EPI_HIGHWAY)
+      hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_HIGHWAY, false, true>), grid, block, 0, s, q);
+    else if (maxpool)
+      hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_CONV, true, true>), grid, block, 0, s, q);
+    else
+      hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_CONV, false, true>), grid, block, 0, s, q);
+  } else {
+    if (epi == EPI_HIGHWAY)
+      hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_HIGHWAY, false, false>), grid, block, 0, s, q);
+    else if (maxpool)
+      hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_CONV, true, false>), grid, block, 0, s, q);
+    else
+      hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_CONV, false, false>), grid, block, 0, s, q);
+  }
   FTMI_CHECK_LAUNCH();
   if (q.split > 1) {
     const int64_t total = (int64_t)q.M * q.g[0].N;

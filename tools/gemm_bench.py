@@ -61,7 +61,8 @@ print(json.dumps(res))
 VARIANTS = {'f32': {'FTMI_MMA': '0'},
             'x6b': {'FTMI_MMA': '1', 'FTMI_GEMM_X6': '1', 'PRE': '1'},
             'h3': {'FTMI_MMA': '2', 'PRE': '1', 'FTMI_GEMM_SLAB': '0'},
-            'slab': {'FTMI_MMA': '2', 'PRE': '1', 'FTMI_GEMM_SLAB': '1'}}
+            'slab': {'FTMI_MMA': '2', 'PRE': '1', 'FTMI_GEMM_SLAB': '1', 'FTMI_GEMM_SLAB_WS': '0'},
+            'slabws': {'FTMI_MMA': '2', 'PRE': '1', 'FTMI_GEMM_SLAB': '1', 'FTMI_GEMM_SLAB_WS': '1'}}
 names = sys.argv[1:] or ['h3', 'slab']
 out = {}
 for name in names:
