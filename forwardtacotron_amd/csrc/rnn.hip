@@ -261,22 +261,34 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 #pragma unroll
       for (int i = 0; i < FPL; ++i) {
         const int f = lane + 64 * i;
-        const int bl = f / (U / 4);
-        const int k0 = u0 + (f % (U / 4)) * 4;
-        const int kwv = k0 / KW, r = k0 % KW;
-        int ln, idx4;
-        if constexpr (X6) {
-          const int q = r % 32;
-          ln = (q >> 3) * 16 + bl;
-          idx4 = (r / 32) * 2 + ((q & 7) >> 2);
-        } else {
-          ln = (r / KB) * 16 + bl;
-          idx4 = (r % KB) >> 2;
+        {  // y: float4 f = 4 units of one sequence
+          const int bl = f / (U / 4);
+          yb[i] = chunk * NB + bl;
+          k0s[i] = u0 + (f % (U / 4)) * 4;
+          ok[i] = yb[i] < p.B;
         }
-        hofs[i] = (unsigned)((gglob * 16 * H + ((kwv * NL + idx4) * 64 + ln) * 4) * 4);
-        yb[i] = chunk * NB + bl;
-        k0s[i] = k0;
-        ok[i] = yb[i] < p.B;
+        if constexpr (H3) {  // h: 16-B chunk f = (seq, 8 units, plane) of f16 halves
+          const int bl = f / (U / 4), rem = f % (U / 4), plane = rem & 1;
+          const int k0 = u0 + (rem >> 1) * 8;
+          const int kwv = k0 / KW, r = k0 % KW, q = r % 32;
+          const int ln = (q >> 3) * 16 + bl;
+          hofs[i] = (unsigned)((gglob * 16 * H * 2 +
+                                ((kwv * NL + (r / 32) * 2 + plane) * 64 + ln) * 8) * 2);
+        } else {  // h: float4 f = 4 units of one sequence, fp32
+          const int bl = f / (U / 4);
+          const int k0 = u0 + (f % (U / 4)) * 4;
+          const int kwv = k0 / KW, r = k0 % KW;
+          int ln, idx4;
+          if constexpr (X6) {
+            const int q = r % 32;
+            ln = (q >> 3) * 16 + bl;
+            idx4 = (r / 32) * 2 + ((q & 7) >> 2);
+          } else {
+            ln = (r / KB) * 16 + bl;
+            idx4 = (r % KB) >> 2;
+          }
+          hofs[i] = (unsigned)((gglob * 16 * H + ((kwv * NL + idx4) * 64 + ln) * 4) * 4);
+        }
       }
       __syncthreads();  // the compute waves' set-up barrier
       for (int t = 0; t < p.T; ++t) {
@@ -442,11 +454,18 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
                   const int (&inext)[CPT], int (&iload)[CPT]) -> bool {
     const int tt = frame(t);
     STAMP(0);
-    // h_{t-1} operand: NL float4 per lane (fragment order), zero at t = 0
-    float hv[NL * 4];
+    // h_{t-1} operand: NL float4 per lane (fragment order), zero at t = 0.  f16x3 groups of
+    // several workgroups exchange h pre-split: hr[2 ks] = 8 heads, hr[2 ks + 1] = 8 scaled
+    // tails (f16), used as MFMA operands directly.
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    constexpr bool HSPLIT = H3 && !LOCAL;
+    float hv[HSPLIT ? 1 : NL * 4];
+    u32x4 hr[NL];
     if (t == 0) {
 #pragma unroll
-      for (int i = 0; i < NL * 4; ++i) hv[i] = 0.f;
+      for (int i = 0; i < (HSPLIT ? 1 : NL * 4); ++i) hv[i] = 0.f;
+#pragma unroll
+      for (int i = 0; i < NL; ++i) hr[i] = (u32x4){0u, 0u, 0u, 0u};
     } else if constexpr (LOCAL) {
       const float *hb = hloc + ((t - 1) & 1) * slab + wk * NL * 256 + lane * 4;
 #pragma unroll
@@ -463,15 +482,15 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       // accesses are single-copy atomic, so a torn 16-byte store only delays the read;
       // every load of the exchange buffer is sc1 (L2-served).
       const int soff = ((t - 1) & 1) * hx_par;
-      const unsigned want = h_tag(t - 1);
-      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-      u32x4 hr[NL];
+      // fp32 words carry the tag in bit 0; f16 pairs in bits 0 and 16 (both halves)
+      const unsigned tmask = HSPLIT ? 0x00010001u : 1u;
+      const unsigned want = h_tag(t - 1) * tmask;
       for (unsigned spins = 0;; ++spins) {
         bool fresh = true;
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
           hr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + i * 1024, soff, 16);
-          const u32x4 d = (hr[i] & 1u) ^ want;
+          const u32x4 d = (hr[i] & tmask) ^ want;
           fresh &= (d.x | d.y | d.z | d.w) == 0u;
         }
         if (__all(fresh) || (p.diag & 2)) break;
@@ -485,7 +504,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         __builtin_amdgcn_s_sleep(1);
       }
 #pragma unroll
-      for (int i = 0; i < NL; ++i) {
+      for (int i = 0; i < (HSPLIT ? 0 : NL); ++i) {
         // NB: bit_cast the whole vector; extracting u32 lanes one by one and bit-casting
         // each is miscompiled by ROCm 7.2 (every lane reads element 0).
         const f32x4 v = __builtin_bit_cast(f32x4, hr[i]);
@@ -509,15 +528,11 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       for (int ks = 0; ks < KS; ++ks) {
         float v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = hv[ks * 8 + e];
+        for (int e = 0; e < 8; ++e) v[e] = HSPLIT ? 0.f : hv[HSPLIT ? 0 : ks * 8 + e];
         f16x8 hh, ht;
-        if (p.diag & 8) {  // timing experiment: head only (no tail split)
-          typedef float f32x8 __attribute__((ext_vector_type(8)));
-          f32x8 x;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) x[e] = v[e];
-          hh = __builtin_convertvector(x, f16x8);
-          ht = hh;
+        if constexpr (HSPLIT) {  // pre-split by the producer
+          hh = __builtin_bit_cast(f16x8, hr[2 * ks]);
+          ht = __builtin_bit_cast(f16x8, hr[2 * ks + 1]);
         } else {
           split2h8(v, hh, ht);
         }
@@ -602,9 +617,28 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         hn = 0.f;
         cstate[j] = 0.f;
       }
-      // multi-workgroup groups: h_t carries the step tag in its mantissa LSB (a <= 1 ulp
-      // change); the same tagged value is the state, the exchange and the layer output
-      if constexpr (!LOCAL) hn = __uint_as_float((__float_as_uint(hn) & ~1u) | h_tag(t));
+      if constexpr (HSPLIT) {
+        // exchanged pre-split: head h_h = f16(h) and scaled tail f16((h - h_h) 2^11), each
+        // carrying the step tag in its mantissa LSB; the tail is taken AFTER the head's tag
+        // bit is set, so the pair still represents h to ~2^-21 (the head's tag error is
+        // absorbed by the tail).  The state and the output stay exact fp32.
+        const unsigned short tg = (unsigned short)h_tag(t);
+        const _Float16 h16 = __builtin_bit_cast(
+            _Float16, (unsigned short)((__builtin_bit_cast(unsigned short, (_Float16)hn) & 0xFFFEu) | tg));
+        const _Float16 t16 = __builtin_bit_cast(
+            _Float16, (unsigned short)((__builtin_bit_cast(unsigned short,
+                                                           (_Float16)((hn - (float)h16) * H3_SCALE)) &
+                                        0xFFFEu) | tg));
+        // chunk (seq, 8 units, plane) of halves: the comm wave's 16-B order
+        _Float16 *hs16 = (_Float16 *)hstage;
+        const int base = ((bl * (U / 8) + cu[j] / 8) * 2) * 8 + (cu[j] % 8);
+        hs16[base] = h16;
+        hs16[base + 8] = t16;
+      } else if constexpr (!LOCAL) {
+        // multi-workgroup groups: h_t carries the step tag in its mantissa LSB (a <= 1 ulp
+        // change); the same tagged value is the state, the exchange and the layer output
+        hn = __uint_as_float((__float_as_uint(hn) & ~1u) | h_tag(t));
+      }
       const float yout = tt >= len[j] ? p.pad_value : hn;
       hstate[j] = hn;
       if constexpr (LOCAL) {
@@ -614,7 +648,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         }
       } else {  // to the comm wave: cell c = bl * U + unit is also its float4 order
         const int c = bl * U + cu[j];
-        hstage[c] = hn;
+        if constexpr (!HSPLIT) hstage[c] = hn;
         ystage[c] = yout;
       }
     }
