@@ -235,22 +235,19 @@ class ForwardTacotron(nn.Module):
         """Duration / pitch / energy predictors and the prenet CBHG are independent: pitch,
         energy and the prenet run on three side streams while the caller's stream runs the
         duration predictor and the LengthRegulator bookkeeping (fill-2 rule, counts, T_mel).
-        The one host sync (T_mel) therefore waits only for the duration path and overlaps
-        the prenet.  The encoder tail (pitch / energy projections) and the LSTM input
-        projection do not depend on T_mel: they are queued BEFORE the host waits for it, so
-        the device keeps working through the sync.  Returns (dur_hat, pitch_hat, energy_hat,
-        enc, offsets, T_mel, xp) with every tensor ready on the caller's stream (xp: the
-        LSTM input projection of enc)."""
+        The prenet stream (high priority: its chain is the phase's critical path) continues
+        with the encoder tail (pitch / energy projections, after those streams) and the
+        LSTM input projection: neither depends on T_mel, so they run while the duration path
+        finishes and the host waits for T_mel (the one host sync, a pinned copy queued right
+        after the duration kernel).  Issue order = priority order: prenet, durations, pitch,
+        energy.  Returns (dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel, xp) with every
+        tensor ready on the caller's stream (xp: the LSTM input projection of enc)."""
         main = torch.cuda.current_stream(x.device)
         s_pitch, s_energy, s_prenet = self._side_streams(x.device)
         for s in (s_pitch, s_energy, s_prenet):
             s.wait_stream(main)
         with torch.cuda.stream(s_prenet):
             enc = self.prenet.forward_cl(ops.embedding(x, self.embedding.weight.detach()))
-        with torch.cuda.stream(s_pitch):
-            pitch_hat = pitch_fn(self.pitch_pred.forward_bt(x).unsqueeze(1))
-        with torch.cuda.stream(s_energy):
-            energy_hat = energy_fn(self.energy_pred.forward_bt(x).unsqueeze(1))
         dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
         t_host = t_ready = None
         if batch is None:
@@ -261,16 +258,26 @@ class ForwardTacotron(nn.Module):
             t_host.copy_(totals.max(), non_blocking=True)
             t_ready = torch.cuda.Event()
             t_ready.record(main)
-        else:  # a shard of a larger batch (sharded.GlobalBatch): batch-global fill rule / T_mel
-            offsets, totals = batch.duration_counts(dur_hat)
+        with torch.cuda.stream(s_pitch):
+            pitch_hat = pitch_fn(self.pitch_pred.forward_bt(x).unsqueeze(1))
+        with torch.cuda.stream(s_energy):
+            energy_hat = energy_fn(self.energy_pred.forward_bt(x).unsqueeze(1))
+        with torch.cuda.stream(s_prenet):
+            for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat)):
+                s_prenet.wait_stream(s)
+                t.record_stream(s_prenet)
+            wp, bp, we, be = self._series_proj_weights()
+            ops.series_proj_add(enc, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we,
+                                be, self.energy_strength)
+            xp = self.lstm.project(enc)
+        if batch is not None:  # a shard of a larger batch (sharded.GlobalBatch): batch-global
+            offsets, totals = batch.duration_counts(dur_hat)  # fill rule / T_mel
             T_mel = batch.t_mel(totals)
-        for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat), (s_prenet, enc)):
+        for s, ts in ((s_pitch, (pitch_hat,)), (s_energy, (energy_hat,)),
+                      (s_prenet, (enc, xp))):
             main.wait_stream(s)
-            t.record_stream(main)
-        wp, bp, we, be = self._series_proj_weights()
-        ops.series_proj_add(enc, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
-                            self.energy_strength)
-        xp = self.lstm.project(enc)
+            for t in ts:
+                t.record_stream(main)
         if t_ready is not None:
             t_ready.synchronize()
             T_mel = int(t_host)
