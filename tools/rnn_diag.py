@@ -1,6 +1,7 @@
 """Timing experiments on the persistent recurrence: what each part of a step costs.
 FTMI_RNN_DIAG bits (results are invalid when set; timing only): 1 = L2-hot input-projection
-rows, 2 = no hand-off waits, 8 = no f16 tail split of h (head only).  Run on the GPU box."""
+rows, 2 = no hand-off waits, 8 = no f16 tail split of h (head only); 16 = s_sleep between
+polls (valid results).  Run on the GPU box."""
 import json
 import os
 import subprocess
@@ -31,7 +32,7 @@ for cell, H, B, T in [(1, 512, 64, 1368), (0, 256, 64, 1368), (0, 128, 64, 200),
 print(json.dumps(res))
 '''
 rows = {}
-for diag in (0, 1, 2, 8, 10):
+for diag in (0, 16, 0, 16):
     env = {**os.environ, 'FTMI_RNN_DIAG': str(diag)}
     r = subprocess.run([sys.executable, '-c', CHILD], env=env, capture_output=True, text=True,
                        timeout=300)
