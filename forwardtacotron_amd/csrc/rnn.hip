@@ -777,8 +777,21 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
     case 1: return launch_rnn<CELL_, H_, U_, WKX_, 1>(p, nchunks, maxb, s);          \
     default: return launch_rnn<CELL_, H_, U_, WKF_, 0>(p, nchunks, maxb, s);         \
   }
-  if (cell == 0 && H == 64) FTMI_RNN_MODES(0, 64, 64, 2, 4)
-  if (cell == 0 && H == 128) FTMI_RNN_MODES(0, 128, 64, 4, 4)
+  // H = 64 on the f16x3 path: 32 units per workgroup (2 per group, h exchanged through L2)
+  // 1.19 us/step against 1.45 for one workgroup per group (h in LDS) at B = 64;
+  // FTMI_RNN_U64=64 selects the single-workgroup form
+  if (cell == 0 && H == 64) {
+    static const int u64 = [] {
+      const char *v = getenv("FTMI_RNN_U64");
+      return v ? atoi(v) : 32;
+    }();
+    if (mma == 2 && u64 == 32) return launch_rnn<0, 64, 32, 2, 2>(p, nchunks, maxb, s);
+    FTMI_RNN_MODES(0, 64, 64, 2, 4)
+  }
+  // H = 128: 16 units per workgroup (8 workgroups per group): 1.04 us/step against 2.33 with
+  // 64 units (2 workgroups) at B = 64 — the per-step cell and MFMA work of a workgroup
+  // shrinks 4x for one more hop in the exchange
+  if (cell == 0 && H == 128) FTMI_RNN_MODES(0, 128, 16, 4, 4)
   if (cell == 0 && H == 256) FTMI_RNN_MODES(0, 256, 16, 4, 4)
   if (cell == 1 && H == 512) FTMI_RNN_MODES(1, 512, 16, 4, 4)
 #undef FTMI_RNN_MODES

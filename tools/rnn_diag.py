@@ -32,13 +32,15 @@ for cell, H, B, T in [(1, 512, 64, 1368), (0, 256, 64, 1368), (0, 128, 64, 200),
 print(json.dumps(res))
 '''
 rows = {}
-for diag in (0, 16, 0, 16):
-    env = {**os.environ, 'FTMI_RNN_DIAG': str(diag)}
+VAR = os.environ.get('DIAG_VAR', 'FTMI_RNN_DIAG')
+VALS = os.environ.get('DIAG_VALS', '0 16 0 16').split()
+for diag in VALS:
+    env = {**os.environ, VAR: str(diag)}
     r = subprocess.run([sys.executable, '-c', CHILD], env=env, capture_output=True, text=True,
                        timeout=300)
     if r.returncode != 0:
         print('diag', diag, 'FAILED', r.stderr[-2000:])
         sys.exit(1)
     rows[diag] = json.loads(r.stdout.strip().splitlines()[-1])
-    print(f'diag={diag}: ' + '  '.join(f'{k} {v:6.2f} us/step' for k, v in rows[diag].items()),
+    print(f'{VAR}={diag}: ' + '  '.join(f'{k} {v:6.2f} us/step' for k, v in rows[diag].items()),
           flush=True)
