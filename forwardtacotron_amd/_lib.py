@@ -19,7 +19,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 4
+ABI_VERSION = 5
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -52,6 +52,8 @@ SIGNATURES = {
     'ftmi_rnn_error_offset': (c_int64, [c_int]),
     'ftmi_rnn_bidir': (c_int, [c_int, c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,
                                c_float, P, c_int64, c_int, P, P, P]),
+    'ftmi_gru_bidir_fused': (c_int, [c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,
+                                     c_float, P, c_int64, P, P, P]),
     'ftmi_duration_counts': (c_int, [P, c_int, c_int, c_int, c_float, P, P, P, P]),
     'ftmi_duration_trunc_sum': (c_int, [P, c_int, c_int, P, P]),
     'ftmi_duration_counts_global': (c_int, [P, c_int, c_int, P, c_float, P, P, P, P]),

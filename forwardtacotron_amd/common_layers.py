@@ -239,6 +239,11 @@ class BiRNN(Packed):
     def forward_cl(self, x: torch.Tensor, T: Optional[int] = None, index=None, lengths=None,
                    pad_value: float = 0.0) -> torch.Tensor:
         """x: (B, T_src, In) channels-last; with index, frame t reads row index[b, t]."""
+        if self.cell == 0 and index is None and ops.gru_fused_ok(self.hidden, x.size(2)):
+            # the input projection inside the recurrence (no (B, T, 6H) intermediate)
+            w_ih, b_in, b_hh, w_hh, _ = self.packed_weights()
+            return ops.gru_bidir_fused(x, self.hidden, w_ih, b_in, w_hh, b_hh, lengths=lengths,
+                                       pad_value=pad_value)
         return self.recur(self.project(x), T=T, index=index, lengths=lengths,
                           pad_value=pad_value)
 

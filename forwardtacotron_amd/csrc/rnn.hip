@@ -115,6 +115,12 @@ struct RnnParams {
   int xcd_local;  // 1: try the census-based XCD-local mode
   unsigned *ws;   // control words (see WS_*)
   unsigned *status;  // optional: bit 1 = a W_hh entry overflowed f16 (mode 2)
+  // fused input projection (FUSE instances): x (B, T, FUSE_CIN) rows, W_ih [2][G*H][Cin],
+  // b_ih [2*G*H]; the gate inputs x_t W_ih^T + b_ih are computed in the recurrence
+  const float *x;
+  int64_t x_stride;
+  const float *w_ih;
+  const float *b_ih;
   int diag;  // timing experiments only (FTMI_RNN_DIAG, results invalid when set): bit 0 =
              // input projections from one L2-hot row, bit 1 = no hand-off waits,
              // bit 2 = no drain
@@ -168,7 +174,9 @@ __device__ __forceinline__ bool poll_ge(unsigned *w, unsigned target) {
   return true;
 }
 
-template <int CELL, int H, int U, int WK, int MODE>
+constexpr int FUSE_CIN = 256;  // input width of the fused-projection instances
+
+template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false>
 __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(const RnnParams p) {
   constexpr bool X6 = MODE != 0;  // 16x16x32 fragment layout (bf16x6 and f16x3)
   constexpr bool H3 = MODE == 2;
@@ -187,8 +195,14 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   constexpr int CPT = CELLS / 256;
   static_assert(U % 16 == 0 && H % U == 0 && RB % WR == 0 && CELLS % 256 == 0, "shape");
   static_assert(X6 ? (KW % 32 == 0) : (KB % 4 == 0), "K split");
+  // FUSE (f16x3 GRU, several workgroups per group): each wave also multiplies its quarter of
+  // the input channels by W_ih; the partial gate inputs go through the same LDS reduction
+  static_assert(!FUSE || (H3 && CELL == 0 && !LOCAL), "fused input projection: f16x3 GRU");
+  constexpr int KWI = FUSE ? FUSE_CIN / WK : 32;  // input channels per wave
+  constexpr int KSI = KWI / 32;                   // their 32-deep k-steps
+  constexpr int RR = FUSE ? 2 * R : R;            // reduction rows: W_hh h [+ W_ih x]
 
-  __shared__ __attribute__((aligned(16))) float red[WK * R * RED_STRIDE];
+  __shared__ __attribute__((aligned(16))) float red[WK * RR * RED_STRIDE];
   __shared__ __attribute__((aligned(16))) float hloc[LOCAL ? 2 * 16 * H : 4];
   // multi-workgroup groups: the new h slice and y values of this workgroup, handed from the
   // compute waves to the comm wave (cell c = seq * U + unit; float4 f = 4 units)
@@ -359,12 +373,35 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
     }
   }
 
+  // ---- FUSE: W_ih slice (this wave's input-channel quarter) -> f16 head / scaled tail ----
+  f16x8 wi[FUSE ? RBW : 1][FUSE ? KSI : 1][2];
+  if constexpr (FUSE) {
+    const float *widir = p.w_ih + (size_t)dir * (G * H) * FUSE_CIN;
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) {
+      const int lrow = (wr * RBW + i) * 16 + lc;
+      const int grow = (lrow / U) * H + u0 + (lrow % U);
+      const float *src = widir + (size_t)grow * FUSE_CIN + wk * KWI;
+#pragma unroll
+      for (int ks = 0; ks < KSI; ++ks) {
+        float v[8];
+        const f32x4 a = *(const f32x4 *)(src + ks * 32 + 8 * ls);
+        const f32x4 b = *(const f32x4 *)(src + ks * 32 + 8 * ls + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        split2h8(v, wi[i][ks][0], wi[i][ks][1]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wbad |= !(__builtin_fabsf(v[e]) <= 65504.f);
+      }
+    }
+  }
+
   if (wbad && p.status) atomicOr(p.status, 2u);
 
   // ---- per-thread cells: cell c = tid + 256*j -> (unit u = c % U, seq b = c / U) ------
   int cu[CPT], cb[CPT], len[CPT], hxo[CPT];
   bool cvalid[CPT];
-  float hstate[CPT], cstate[CPT], bhh[CPT][G];
+  float hstate[CPT], cstate[CPT], bhh[CPT][G], bih[FUSE ? CPT : 1][G];
 #pragma unroll
   for (int j = 0; j < CPT; ++j) {
     const int c = tid + 256 * j;
@@ -376,8 +413,10 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
     cstate[j] = 0.f;
     len[j] = (p.lengths && cvalid[j]) ? p.lengths[cb[j]] : p.T;
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+    for (int g = 0; g < G; ++g) {
       bhh[j][g] = (CELL == 0) ? p.b_hh[dir * G * H + g * H + u0 + cu[j]] : 0.f;
+      if constexpr (FUSE) bih[j][g] = p.b_ih[dir * G * H + g * H + u0 + cu[j]];
+    }
     // fragment-order position of (seq bl, unit k) in the group's 16*H slab
     const int k = u0 + cu[j];
     const int kwv = k / KW, r = k % KW;
@@ -435,11 +474,33 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   };
   float g0[CPT][G], g1[CPT][G], g2[CPT][G];
   int i0[CPT], i1[CPT], i2[CPT];
-  load_idx(0, i0);
-  load_idx(1, i1);
-  load_gx(0, i0, g0);
-  load_gx(1, i1, g1);
-  load_idx(2, i2);
+  // FUSE: x rows of the chunk's 16 sequences (lane column lc), this wave's channel quarter,
+  // 8 consecutive channels per k-step (the MFMA B layout), two steps ahead in three sets
+  constexpr int NXR = FUSE ? 2 * KSI : 1;
+  f32x4 x0[NXR], x1[NXR], x2[NXR];
+  const int xb = chunk * NB + lc < p.B ? chunk * NB + lc : p.B - 1;
+  auto load_x = [&](int t, f32x4 (&xr)[NXR]) {
+    if constexpr (FUSE) {
+      const int tt = frame(t < p.T ? t : p.T - 1);
+      const float *row = p.x + ((size_t)xb * p.T + tt) * p.x_stride + wk * KWI + 8 * ls;
+#pragma unroll
+      for (int ks = 0; ks < KSI; ++ks) {
+        xr[2 * ks] = *(const f32x4 *)(row + ks * 32);
+        xr[2 * ks + 1] = *(const f32x4 *)(row + ks * 32 + 4);
+      }
+    }
+  };
+  float xamax = 0.f;  // FUSE range guard: largest |x| fed to the f16 split
+  if constexpr (FUSE) {
+    load_x(0, x0);
+    load_x(1, x1);
+  } else {
+    load_idx(0, i0);
+    load_idx(1, i1);
+    load_gx(0, i0, g0);
+    load_gx(1, i1, g1);
+    load_idx(2, i2);
+  }
   if (LOCAL)
     for (int i = tid; i < 16 * H; i += 256) hloc[i] = 0.f;
   __syncthreads();
@@ -451,9 +512,35 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 
   // one time step; returns false when the launch must stop (hand-off timeout)
   auto step = [&](int t, const float (&gx)[CPT][G], float (&gnext)[CPT][G],
-                  const int (&inext)[CPT], int (&iload)[CPT]) -> bool {
+                  const int (&inext)[CPT], int (&iload)[CPT], const f32x4 (&xc)[NXR],
+                  f32x4 (&xl)[NXR]) -> bool {
     const int tt = frame(t);
     STAMP(0);
+    // FUSE: the gate inputs W_ih x_t, computed before the h hand-off wait (x_t was loaded
+    // two steps ago), as a sum of the f16 products w_h x_h + 2^-11 (w_t x_h + w_h x_t)
+    f32x4 axb[FUSE ? RBW : 1], axs[FUSE ? RBW : 1];
+    if constexpr (FUSE) {
+#pragma unroll
+      for (int i = 0; i < RBW; ++i) axb[i] = axs[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KSI; ++ks) {
+        float v[8];
+        v[0] = xc[2 * ks].x; v[1] = xc[2 * ks].y; v[2] = xc[2 * ks].z; v[3] = xc[2 * ks].w;
+        v[4] = xc[2 * ks + 1].x; v[5] = xc[2 * ks + 1].y;
+        v[6] = xc[2 * ks + 1].z; v[7] = xc[2 * ks + 1].w;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xamax = fmaxf(xamax, __builtin_fabsf(v[e]));
+        f16x8 xh, xt;
+        split2h8(v, xh, xt);
+#pragma unroll
+        for (int i = 0; i < RBW; ++i) {
+          axs[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wi[i][ks][1], xh, axs[i], 0, 0, 0);
+          axs[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wi[i][ks][0], xt, axs[i], 0, 0, 0);
+          axb[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wi[i][ks][0], xh, axb[i], 0, 0, 0);
+        }
+      }
+      load_x(t + 2, xl);
+    }
     // h_{t-1} operand: NL float4 per lane (fragment order), zero at t = 0.  f16x3 groups of
     // several workgroups exchange h pre-split: hr[2 ks] = 8 heads, hr[2 ks + 1] = 8 scaled
     // tails (f16), used as MFMA operands directly.
@@ -517,8 +604,10 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       }
     }
     STAMP(1);
-    load_gx(t + 2, inext, gnext);
-    load_idx(t + 3, iload);
+    if constexpr (!FUSE) {
+      load_gx(t + 2, inext, gnext);
+      load_idx(t + 3, iload);
+    }
     STAMP(2);
 
     // partial gates over this wave's K range
@@ -581,7 +670,15 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
     for (int i = 0; i < RBW; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        red[(wk * R + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] = acc[i][e];
+        red[(wk * RR + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] = acc[i][e];
+    if constexpr (FUSE) {
+#pragma unroll
+      for (int i = 0; i < RBW; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          red[(wk * RR + R + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] =
+              axb[i][e] + axs[i][e] * H3_UNSCALE;
+    }
     __syncthreads();
     if (!LOCAL && s_abort) return false;  // a wave timed out acquiring h_{t-1}
     STAMP(3);
@@ -590,28 +687,36 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
       const int bl = cb[j] - chunk * NB;
-      float gs[G];
+      float gs[G], gi[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int row = g * U + cu[j];
         float sum = red[row * RED_STRIDE + bl];
 #pragma unroll
-        for (int w = 1; w < WK; ++w) sum += red[(w * R + row) * RED_STRIDE + bl];
+        for (int w = 1; w < WK; ++w) sum += red[(w * RR + row) * RED_STRIDE + bl];
         gs[g] = sum;
+        if constexpr (FUSE) {  // x_t W_ih^T + b_ih (the unfused path adds b_ih in its GEMM)
+          float sx = red[(R + row) * RED_STRIDE + bl];
+#pragma unroll
+          for (int w = 1; w < WK; ++w) sx += red[(w * RR + R + row) * RED_STRIDE + bl];
+          gi[g] = sx + bih[j][g];
+        } else {
+          gi[g] = gx[j][g];
+        }
       }
       float hn;
       if (CELL == 0) {
         // ATen GRU cell: r, z, n ; h' = n + z * (h - n)
-        const float r = fast_sigmoid(gx[j][0] + (gs[0] + bhh[j][0]));
-        const float z = fast_sigmoid(gx[j][1] + (gs[1] + bhh[j][1]));
-        const float n = fast_tanh(gx[j][2] + r * (gs[2] + bhh[j][2]));
+        const float r = fast_sigmoid(gi[0] + (gs[0] + bhh[j][0]));
+        const float z = fast_sigmoid(gi[1] + (gs[1] + bhh[j][1]));
+        const float n = fast_tanh(gi[2] + r * (gs[2] + bhh[j][2]));
         hn = n + z * (hstate[j] - n);
       } else {
         // LSTM cell: i, f, g, o
-        const float ig = fast_sigmoid(gx[j][0] + gs[0]);
-        const float fg = fast_sigmoid(gx[j][1] + gs[1]);
-        const float gg = fast_tanh(gx[j][2] + gs[2]);
-        const float og = fast_sigmoid(gx[j][3] + gs[3]);
+        const float ig = fast_sigmoid(gi[0] + gs[0]);
+        const float fg = fast_sigmoid(gi[1] + gs[1]);
+        const float gg = fast_tanh(gi[2] + gs[2]);
+        const float og = fast_sigmoid(gi[3] + gs[3]);
         cstate[j] = fg * cstate[j] + ig * gg;
         hn = og * fast_tanh(cstate[j]);
       }
@@ -661,17 +766,18 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   };
 
   for (int t = 0; t < p.T; t += 3) {
-    if (!step(t, g0, g2, i2, i0)) break;
-    if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1)) break;
-    if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2)) break;
+    if (!step(t, g0, g2, i2, i0, x0, x2)) break;
+    if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1, x1, x0)) break;
+    if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2, x2, x1)) break;
   }
+  if (FUSE && !(xamax <= 65504.f) && p.status) atomicOr(p.status, 1u);
 #ifdef FTMI_RNN_STAMPS
   if (tid == 0)
     for (int i = 0; i < 6; ++i) ftmi_rnn_stamps[blockIdx.x * 8 + i] = st_acc[i];
 #endif
 }
 
-template <int CELL, int H, int U, int WK, int MODE>
+template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false>
 int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
   constexpr int BPG = H / U;
   int max_groups = (max_blocks / BPG) & ~1;
@@ -684,7 +790,7 @@ int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
       hipError_t e = hipMemsetAsync(p.ws + WS_CENSUS, 0, (WS_FLAGS - WS_CENSUS) * 4, s);
       if (e != hipSuccess) return (int)e;
     }
-    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE>), dim3(p.ngroups * BPG),
+    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, FUSE>), dim3(p.ngroups * BPG),
                        dim3(BPG == 1 ? 256 : 320), 0, s, p);
     FTMI_CHECK_LAUNCH();
   }
@@ -722,22 +828,13 @@ extern "C" int64_t ftmi_rnn_error_offset(int32_t B) {
   return WS_ERR * (int64_t)sizeof(unsigned);
 }
 
-extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, const float *xp,
-                              int64_t xp_stride, int32_t T_src, const int32_t *index,
-                              const float *xp_zero, const float *w_hh, const float *b_hh,
-                              const int32_t *lengths, float pad_value, float *y,
-                              int64_t y_stride, int32_t mma, uint32_t *status, void *sync,
-                              ftmi_stream_t stream) {
-  if (!xp || !w_hh || !y || !sync) return FTMI_E_ARG;
-  if (B <= 0 || T <= 0 || H <= 0 || T_src <= 0) return FTMI_E_ARG;
-  if (mma < 0 || mma > 2) return FTMI_E_ARG;
-  if (cell == 0 && !b_hh) return FTMI_E_ARG;
-  if (index && !xp_zero) return FTMI_E_ARG;
-  if (!index && T_src != T) return FTMI_E_SHAPE;
-  if (!ftmi_aligned16(w_hh) || !ftmi_aligned16(sync)) return FTMI_E_ALIGN;
-  if (!ftmi_aligned16(y) || (y_stride & 3)) return FTMI_E_ALIGN;  // float4 row stores
-  hipStream_t s = ftmi_hs(stream);
-  const int nchunks = (B + NB - 1) / NB;
+// the launch set-up shared by ftmi_rnn_bidir and ftmi_gru_bidir_fused: clears the
+// workspace (control words and the exchange buffer) and fills the common parameters
+static int rnn_setup(RnnParams &p, int B, int T, int H, int cell, const float *w_hh,
+                     const float *b_hh, const int32_t *lengths, float pad_value, float *y,
+                     int64_t y_stride, uint32_t *status, void *sync, hipStream_t s,
+                     int &nchunks) {
+  nchunks = (B + NB - 1) / NB;
   const int64_t ctl = ctl_bytes(nchunks);
   const int64_t wsb = ftmi_rnn_workspace_bytes(B, H, cell);
   hipError_t e = hipMemsetAsync(sync, 0, (size_t)wsb, s);
@@ -746,12 +843,6 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
     const char *v = getenv("FTMI_RNN_XCD_LOCAL");
     return v ? atoi(v) : 1;
   }();
-  RnnParams p = {};
-  p.xp = xp;
-  p.xp_stride = xp_stride;
-  p.T_src = T_src;
-  p.index = index;
-  p.xp_zero = xp_zero;
   p.w_hh = w_hh;
   p.b_hh = b_hh;
   p.y = y;
@@ -770,6 +861,34 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
     return v ? atoi(v) : 0;
   }();
   p.diag = diag_env;
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, const float *xp,
+                              int64_t xp_stride, int32_t T_src, const int32_t *index,
+                              const float *xp_zero, const float *w_hh, const float *b_hh,
+                              const int32_t *lengths, float pad_value, float *y,
+                              int64_t y_stride, int32_t mma, uint32_t *status, void *sync,
+                              ftmi_stream_t stream) {
+  if (!xp || !w_hh || !y || !sync) return FTMI_E_ARG;
+  if (B <= 0 || T <= 0 || H <= 0 || T_src <= 0) return FTMI_E_ARG;
+  if (mma < 0 || mma > 2) return FTMI_E_ARG;
+  if (cell == 0 && !b_hh) return FTMI_E_ARG;
+  if (index && !xp_zero) return FTMI_E_ARG;
+  if (!index && T_src != T) return FTMI_E_SHAPE;
+  if (!ftmi_aligned16(w_hh) || !ftmi_aligned16(sync)) return FTMI_E_ALIGN;
+  if (!ftmi_aligned16(y) || (y_stride & 3)) return FTMI_E_ALIGN;  // float4 row stores
+  hipStream_t s = ftmi_hs(stream);
+  RnnParams p = {};
+  int nchunks = 0;
+  const int rc = rnn_setup(p, B, T, H, cell, w_hh, b_hh, lengths, pad_value, y, y_stride,
+                           status, sync, s, nchunks);
+  if (rc != FTMI_OK) return rc;
+  p.xp = xp;
+  p.xp_stride = xp_stride;
+  p.T_src = T_src;
+  p.index = index;
+  p.xp_zero = xp_zero;
   const int maxb = device_cu_count();
 #define FTMI_RNN_MODES(CELL_, H_, U_, WKX_, WKF_)                                   \
   switch (mma) {                                                                    \
@@ -798,6 +917,34 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   if (cell == 1 && H == 512) FTMI_RNN_MODES(1, 512, 16, 4, 4)
 #undef FTMI_RNN_MODES
   return FTMI_E_UNSUPPORTED;
+}
+
+extern "C" int ftmi_gru_bidir_fused(int32_t B, int32_t T, int32_t H, const float *x,
+                                    int64_t x_stride, int32_t Cin, const float *w_ih,
+                                    const float *b_ih, const float *w_hh, const float *b_hh,
+                                    const int32_t *lengths, float pad_value, float *y,
+                                    int64_t y_stride, uint32_t *status, void *sync,
+                                    ftmi_stream_t stream) {
+  if (!x || !w_ih || !b_ih || !w_hh || !b_hh || !y || !sync) return FTMI_E_ARG;
+  if (B <= 0 || T <= 0 || H <= 0 || Cin <= 0) return FTMI_E_ARG;
+  if (Cin != FUSE_CIN || (H != 128 && H != 256)) return FTMI_E_UNSUPPORTED;
+  if (!ftmi_aligned16(x) || (x_stride & 3) || !ftmi_aligned16(w_ih)) return FTMI_E_ALIGN;
+  if (!ftmi_aligned16(w_hh) || !ftmi_aligned16(sync)) return FTMI_E_ALIGN;
+  if (!ftmi_aligned16(y) || (y_stride & 3)) return FTMI_E_ALIGN;
+  hipStream_t s = ftmi_hs(stream);
+  RnnParams p = {};
+  int nchunks = 0;
+  const int rc = rnn_setup(p, B, T, H, 0, w_hh, b_hh, lengths, pad_value, y, y_stride, status,
+                           sync, s, nchunks);
+  if (rc != FTMI_OK) return rc;
+  p.T_src = T;
+  p.x = x;
+  p.x_stride = x_stride;
+  p.w_ih = w_ih;
+  p.b_ih = b_ih;
+  const int maxb = device_cu_count();
+  if (H == 128) return launch_rnn<0, 128, 16, 4, 2, true>(p, nchunks, maxb, s);
+  return launch_rnn<0, 256, 16, 4, 2, true>(p, nchunks, maxb, s);
 }
 
 #ifdef FTMI_RNN_STAMPS

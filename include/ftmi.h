@@ -183,6 +183,19 @@ int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, const float *x
                    const int32_t *lengths, float pad_value, float *y, int64_t y_stride,
                    int32_t mma, uint32_t *status, void *sync, ftmi_stream_t stream);
 
+/* Bidirectional GRU with the input projection fused into the recurrence (f16x3 only):
+ * the same result as ftmi_conv1d(x, W_ih, k=1, bias=b_ih) followed by ftmi_rnn_bidir, with
+ * x (B, T, Cin) fp32 rows read directly (the (B, T, 6H) projection is never materialised;
+ * each step's W_ih x_t is computed while the workgroup waits for the h hand-off).
+ * w_ih [2][3H][Cin] (forward, reverse), b_ih [2*3H]; other arguments as ftmi_rnn_bidir.
+ * Supported: Cin == 256, H in {128, 256} (FTMI_E_UNSUPPORTED otherwise: use the two-call
+ * form).  Replaces nn.GRU's input GEMM + recurrence, models/common_layers.py:84,118
+ * (CBHG) and models/forward_tacotron.py:39,53 (SeriesPredictor). */
+int ftmi_gru_bidir_fused(int32_t B, int32_t T, int32_t H, const float *x, int64_t x_stride,
+                         int32_t Cin, const float *w_ih, const float *b_ih, const float *w_hh,
+                         const float *b_hh, const int32_t *lengths, float pad_value, float *y,
+                         int64_t y_stride, uint32_t *status, void *sync, ftmi_stream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * Duration post-processing of ForwardTacotron.generate + LengthRegulator counts:
  *   if sum_{b,t} trunc_int64(dur) <= 0: dur[:] = fill_value   (forward_tacotron.py:254-255,

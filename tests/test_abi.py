@@ -53,6 +53,8 @@ def test_strerror():
     (lambda L: L.ftmi_split_weights(None, 4, 4, None, None), 1001),
     (lambda L: L.ftmi_split_weights_f16(None, 4, 4, None, None), 1001),
     (lambda L: L.ftmi_rnn_bidir(0, 1, 1, 64, None, 0, 1, None, None, None, None, None, 0.0, None, 0, 2, None, None, None), 1001),
+    (lambda L: L.ftmi_gru_bidir_fused(1, 1, 128, None, 0, 256, None, None, None, None, None, 0.0, None, 0, None, None, None), 1001),
+    (lambda L: L.ftmi_gru_bidir_fused(1, 1, 96, ctypes.c_void_p(256), 256, 256, ctypes.c_void_p(256), ctypes.c_void_p(256), ctypes.c_void_p(256), ctypes.c_void_p(256), None, 0.0, ctypes.c_void_p(256), 192, None, ctypes.c_void_p(256), None), 1003),
     (lambda L: L.ftmi_duration_counts(None, 1, 1, 1, 2.0, None, None, None, None), 1001),
     (lambda L: L.ftmi_lr_index(None, 1, 1, 1, None, None), 1001),
     (lambda L: L.ftmi_length_regulate(None, 0, 1, 1, 4, None, 1, None, 0, None), 1001),

@@ -234,9 +234,15 @@ RNN_MMAS = pytest.mark.parametrize('rnn_mma', [2, 1, 0], ids=['f16x3', 'bf16x6',
 
 @RNN_MMAS
 @pytest.mark.parametrize('H,B,T', [(64, 3, 40), (128, 2, 33), (256, 5, 60), (256, 17, 9)])
-def test_gru_bidir(H, B, T, rng, rnn_mma, monkeypatch):
+@pytest.mark.parametrize('fused', [True, False], ids=['fused', 'two-call'])
+def test_gru_bidir(H, B, T, rng, rnn_mma, fused, monkeypatch):
+    """fused: the input projection inside the recurrence (ftmi_gru_bidir_fused, f16x3,
+    H 128 / 256); two-call: ftmi_conv1d + ftmi_rnn_bidir."""
     from forwardtacotron_amd import ops
     monkeypatch.setattr(ops, 'RNN_MMA', rnn_mma)
+    monkeypatch.setattr(ops, 'FUSED_GRU', fused)
+    if fused and not ops.gru_fused_ok(H, 256):
+        pytest.skip('no fused form for this shape / path')
     m, sd = _rnn_module('gru', 256, H, rng)
     x = rng.normal(0, 1, (B, T, 256)).astype(np.float32)
     ref = O.gru_bidir(sd, 'r', x, np.float32)
