@@ -114,11 +114,18 @@ def _split_k(M: int, N: int, K: int, mma: int, slab: bool = False, Cin: int = 0)
     CU; slab kernel: 256 x 128 tiles, 1 per CU, split over 32-channel chunks) and K is long
     enough for the partial-sum round trip to pay."""
     if slab:
+        # one workgroup per CU: model the time as (rounds of workgroups) x (steps per
+        # workgroup, ~1.8 us each) + the partial-sum round trip of a split (sp x M x N fp32
+        # written and read back at ~5 TB/s, plus the finishing launch)
         tiles = -(-M // 256) * -(-N // 128)
         cus = _num_cus()
-        if K < 1024 or tiles * 4 >= cus * 3:
-            return 1
-        return int(max(1, min(8, -(-cus // tiles), -(-Cin // 32))))
+        nch = -(-Cin // 32)
+        k = K // Cin if Cin else 1
+
+        def t_us(sp):
+            run = -(-tiles * sp // cus) * -(-nch // sp) * k * 1.8
+            return run + (sp * M * N * 8 / 5e6 + 5.0 if sp > 1 else 0.0)
+        return int(min(range(1, min(8, nch) + 1), key=t_us))
     if mma == 0 or K < 2048:
         return 1
     tiles = -(-M // 128) * -(-N // 128)
