@@ -102,7 +102,12 @@ def main():
     ap.add_argument('--kernels', action='store_true', help='print the per-kernel table to stderr')
     ap.add_argument('--model', choices=['forward_tacotron', 'fast_pitch'], default='forward_tacotron',
                     help='fast_pitch = BASELINE.json configs[4] (c5)')
+    ap.add_argument('--config', choices=['c2', 'c3'], default=None,
+                    help='c2 = BASELINE.json configs[1] (batch 1, 120 phonemes); c3 = the default')
     args = ap.parse_args()
+    if args.config == 'c2':
+        args.batch, args.tmin, args.tmax = 1, 120, 120
+    c3_shape = (args.batch, args.tmin, args.tmax) == (64, 50, 200)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -179,7 +184,7 @@ def main():
                     'algorithmic_per_launch': dom['flops'], 'avg_launch_ms': round(dom['avg_ms'], 4),
                     'launches': dom['launches'], 'share_of_device_time': round(dom['total_ms'] / total_dev_ms, 4),
                     'traffic': None}
-            tr = pmc_traffic(dom_label)
+            tr = pmc_traffic(dom_label) if c3_shape and args.model == 'forward_tacotron' else None
             if tr is not None:
                 roof['traffic'] = tr['bytes_per_launch']
                 roof['traffic_detail'] = tr
@@ -190,6 +195,19 @@ def main():
                     'algorithmic_per_launch': dom['bytes'], 'avg_launch_ms': round(dom['avg_ms'], 4),
                     'launches': dom['launches'], 'traffic': None}
 
+        # north-star kernel: the fused Conv1d+ReLU+BN prenet bank (K = 16), against HBM
+        # (weight planes + input + output, once) and against the f16x3 MFMA ceiling
+        pre = [(lab, v) for lab, v in kern.items() if lab.startswith('conv_bank[') and ',K=16,' in lab]
+        prenet = None
+        if pre:
+            lab, v = pre[0]
+            s_ = v['avg_ms'] / 1e3
+            prenet = {'kernel': lab, 'avg_launch_ms': round(v['avg_ms'], 4),
+                      'hbm_achieved_GBs': round(v['bytes'] / s_ / 1e9, 1), 'hbm_peak_GBs': PEAK_HBM_GBS,
+                      'hbm_frac': round(v['bytes'] / s_ / 1e9 / PEAK_HBM_GBS, 4),
+                      'algorithmic_bytes': v['bytes'],
+                      'mfma_achieved_TFLOPs': round(v['flops'] / s_ / 1e12, 2),
+                      'mfma_frac': round(v['flops'] / s_ / 1e12 / PEAK_X3_TFLOPS, 4)}
         value = frames / elapsed
         fp = args.model == 'fast_pitch'
         line = {
@@ -200,7 +218,7 @@ def main():
             'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
             'data': 'synthetic (seeded LJSpeech-shaped phoneme batches, synthetic weights)',
-            'config': {'workload': (f'{"c5: FastPitch" if fp else "c3: ForwardTacotron"} generate, '
+            'config': {'workload': (f'{"c5: FastPitch" if fp else ("c2" if args.batch == 1 else "c3") + ": ForwardTacotron"} generate, '
                                     if world == 1 else
                                     f'c4: {"FastPitch" if fp else "ForwardTacotron"} generate of one '
                                     f'global batch sharded over {world} GPUs (global padding, '
@@ -211,6 +229,8 @@ def main():
                        'T_mel': int(out['mel_post'].size(2)), 'parallelism': f'dp{world}'},
             'roofline': roof,
         }
+        if prenet is not None:
+            line['prenet_bank'] = prenet
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'], line['parity'] = cpu_baseline(sd, x_np, out, args.model)
         print(json.dumps(line), flush=True)

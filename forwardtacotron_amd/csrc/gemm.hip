@@ -87,6 +87,7 @@ struct GemmParams {
   int split_req;  // the caller's split_k (the slab kernel re-derives split / kc_per from it)
   int diag;       // slab kernel timing experiments (FTMI_SLAB_DIAG; results invalid when set)
   float *part;
+  int ldp;  // skinny kernel: columns of a partial-sum row (all groups, output order)
   unsigned *status;  // mma = 2: bit 0 set when an accumulator became non-finite
   GemmGroup g[MAX_GROUPS];
 };
@@ -1065,8 +1066,15 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
   // are consecutive in that XCD's order, so its slab rows are shared through L2.  Groups
   // (conv bank: one per kernel size, heaviest first) all have NT column tiles.
   const int MT = (p.M + SL_BM - 1) / SL_BM, NT = p.g[0].ntiles, VT = p.ngroups * NT;
+  // With fewer than 8 row tiles (small batches) that order would put every working block on
+  // one XCD: the grid is then compact, row tile fastest, and consecutive blocks spread.
   const int bid = blockIdx.x, s8 = bid >> 3, q8 = s8 / VT;
-  const int mt = q8 * 8 + (bid & 7), v8 = s8 - q8 * VT, gi = v8 / NT, nt = v8 - gi * NT;
+  int mt = q8 * 8 + (bid & 7), v8 = s8 - q8 * VT;
+  if (MT < 8) {
+    mt = bid % MT;
+    v8 = bid / MT;
+  }
+  const int gi = v8 / NT, nt = v8 - gi * NT;
   if (mt >= MT) return;  // the grid is padded to whole XCD rounds
   const GemmGroup &G = p.g[gi];
   const int m0 = mt * SL_BM, n0 = nt * SL_BN;
@@ -1422,6 +1430,199 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
   }
 }
 
+// ---- skinny kernel: few output rows (M <= SK_MMAX, e.g. batch 1), the weight stream binds --
+// At B = 1 (BASELINE config c2: T = 120 phonemes) a conv moves its whole weight block for a
+// handful of rows: the prenet bank reads 35.65 MB of weight planes for 120 x 4096 outputs, so
+// the bound is HBM, not MFMA.  Work unit = (128-row tile, group, 64 output columns, two
+// 32-channel chunks): the block stages the rows of its chunks ONCE into an f16 head / scaled
+// tail slab (the slab kernel's layout, taps read shifted rows, masked taps a zero row), then
+// every wave streams the f16 weight planes of ITS 16 columns straight from HBM into
+// registers (no LDS, no barrier after the prologue, 4 steps of prefetch) and multiplies them
+// against the slab: 3 f16 MFMAs per fp32 product (f16x3, as the slab kernel).  Channel
+// chunks beyond the block's two go to other blocks (blockIdx.y): their raw partial sums land
+// in part[s][M][ldp] (output-column order) and skinny_finish_kernel adds them in split order
+// (deterministic) and applies the epilogue; with one split the wave finishes its columns.
+constexpr int SK_BM = 128;
+constexpr int SK_BN = 64;   // 4 waves x 16 columns
+constexpr int SK_CPB = 2;   // 32-channel chunks per block
+constexpr int SK_SR = SK_BM + SL_MAXK - 1;
+constexpr int SK_ZROW = SK_SR;
+constexpr int SK_AIMG = (SK_SR + 1) * SL_P;  // halves per (chunk, plane) slab image
+constexpr int SK_MMAX = 256;
+constexpr int SK_PF = 4;    // weight-fragment prefetch depth (steps)
+
+template <bool MAXPOOL>
+__global__ __launch_bounds__(256, 2) void conv_gemm_skinny_kernel(const GemmParams p) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[SK_CPB * 2 * SK_AIMG];
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const int MT = (p.M + SK_BM - 1) / SK_BM, NT = p.g[0].ntiles;
+  // consecutive blocks: row tiles, then column blocks of the heaviest group first; a
+  // compact grid, so consecutive blocks land on different XCDs
+  const int bid = blockIdx.x, mt = bid % MT, v = bid / MT, gi = v / NT, nt = v - gi * NT;
+  const GemmGroup &G = p.g[gi];
+  const int m0 = mt * SK_BM, k = G.k, pad = G.pad, Cin = p.Cin;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fs = lane >> 4;
+  const int nch_all = (Cin + 31) / 32;
+  const int c_begin = blockIdx.y * p.kc_per;
+  const int nch = min(nch_all - c_begin, p.kc_per);  // >= 1 (no empty splits)
+  const int SR = SK_BM + k - 1;
+
+  // ---- prologue: the slab of this block's chunks (one float4 of 4 channels per item) ----
+  float amax = 0.f;
+  for (int idx = tid; idx < nch * SR * 8; idx += 256) {
+    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
+    int m = m0 - pad + sr;
+    m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
+    const int ch = (c_begin + c) * 32 + seg * 4;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (ch < Cin) {
+      const float *src = p.x + (int64_t)m * p.x_stride + ch;
+      x = *(const f32x4 *)src;
+      // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
+      if constexpr (MAXPOOL)
+        if (m % p.T > 0) x = fmax4(x, *(const f32x4 *)(src - p.x_stride));
+    }
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+    f16x4 h, t;
+    split2h(x, h, t);
+    _Float16 *dst = lds + c * 2 * SK_AIMG + sr * SL_P + seg * 4;
+    *(f16x4 *)dst = h;
+    *(f16x4 *)(dst + SK_AIMG) = t;
+  }
+  if (tid < SK_CPB * 2 * (SL_P / 8)) {  // the zero row of every (chunk, plane) image
+    const int img = tid / (SL_P / 8), part = tid % (SL_P / 8);
+    *(u32x4 *)(lds + img * SK_AIMG + SK_ZROW * SL_P + part * 8) = (u32x4){0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+  bool bad = !(amax <= 65504.f);
+
+  const int col0 = nt * SK_BN + wave * 16;  // this wave's 16 columns of group gi
+  if (col0 < G.N) {  // wave-uniform; nothing below synchronises
+    // per-row tap masks: bit j set iff frame t + j - pad lies inside the sequence
+    unsigned vmask[8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int m = m0 + mi * 16 + fr;
+      unsigned msk = 0;
+      if (m < p.M) {
+        const int t = m % p.T;
+        const int lo = max(pad - t, 0), hi = min(p.T - 1 + pad - t, k - 1);
+        if (lo <= hi) msk = (2u << hi) - (1u << lo);
+      }
+      vmask[mi] = msk;
+    }
+    // weight planes B0 = 2^11 w_h, B1 = w_t of column n, taps j, channels of step s
+    const int n = col0 + fr < G.N ? col0 + fr : G.N - 1;
+    const _Float16 *w0 = (const _Float16 *)G.w3 + (int64_t)n * G.Kpad;
+    const int64_t plane = (int64_t)G.N * G.Kpad;
+    const int nsteps = nch * k;
+    auto loadB = [&](int s, f16x8 &b0, f16x8 &b1) {
+      const int c = s / k, j = s - c * k;
+      const int ch = (c_begin + c) * 32 + fs * 8;
+      const bool ok = ch < Cin;  // Cin % 16 == 0: a segment is wholly in or out
+      const int off = j * Cin + (ok ? ch : 0);
+      const f16x8 z = {};
+      b0 = ok ? *(const f16x8 *)(w0 + off) : z;
+      b1 = ok ? *(const f16x8 *)(w0 + plane + off) : z;
+    };
+    f32x4 acc[8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) acc[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    f16x8 rb0[SK_PF], rb1[SK_PF];
+#pragma unroll
+    for (int u = 0; u < SK_PF; ++u)
+      if (u < nsteps) loadB(u, rb0[u], rb1[u]);
+    for (int s0 = 0; s0 < nsteps; s0 += SK_PF) {
+#pragma unroll
+      for (int u = 0; u < SK_PF; ++u) {
+        const int s = s0 + u;
+        if (s >= nsteps) break;
+        const f16x8 b0 = rb0[u], b1 = rb1[u];
+        if (s + SK_PF < nsteps) loadB(s + SK_PF, rb0[u], rb1[u]);
+        const int c = s / k, j = s - c * k;
+        const _Float16 *Ab = lds + c * 2 * SK_AIMG;
+        const f16x8 bh = b0 * (_Float16)(1.0f / H3_SCALE);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+          const bool ok = (vmask[mi] >> j) & 1u;
+          const int o = (ok ? mi * 16 + fr + j : SK_ZROW) * SL_P + fs * 8;
+          const f16x8 ah = *(const f16x8 *)(Ab + o);
+          const f16x8 at = *(const f16x8 *)(Ab + SK_AIMG + o);
+          f32x4 cc = acc[mi];
+          cc = mma16(at, bh, cc);  // small terms first
+          cc = mma16(ah, b1, cc);
+          cc = mma16(ah, b0, cc);
+          acc[mi] = cc;
+        }
+      }
+    }
+    // lane (fr, fs) holds rows mi*16 + 4 fs + i of column col0 + fr
+    const int col = col0 + fr;
+    const bool cok = col < G.N;
+    const float cs = G.colscale[cok ? col : G.N - 1];
+    if (p.split > 1) {
+      float *part = p.part + (size_t)blockIdx.y * p.M * p.ldp + G.ycol0;
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + mi * 16 + 4 * fs + i;
+          if (cok && row < p.M) {
+            bad |= !__builtin_isfinite(acc[mi][i]);
+            part[(size_t)row * p.ldp + col] = acc[mi][i] * cs;
+          }
+        }
+    } else {
+      const float bias = G.bias && cok ? G.bias[col] : 0.f;
+      const float sc = G.scale && cok ? G.scale[col] : 1.f;
+      const float sh = G.scale && cok ? G.shift[col] : 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + mi * 16 + 4 * fs + i;
+          if (!cok || row >= p.M) continue;
+          bad |= !__builtin_isfinite(acc[mi][i]);
+          float y = acc[mi][i] * cs + bias;
+          if (p.relu) y = fmaxf(y, 0.f);
+          if (G.scale) y = y * sc + sh;
+          if (p.residual) y += p.residual[(int64_t)row * p.res_stride + col];
+          if (p.y) p.y[(int64_t)row * p.y_stride + G.ycol0 + col] = y;
+          if (p.yt) {
+            const int b = row / p.To, t = row - b * p.To;
+            p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = y;
+          }
+        }
+    }
+  }
+  if (bad && p.status) atomicOr(p.status, 1u);
+}
+
+// sum of the skinny kernel's split partials (split order) + the conv epilogue, every group
+__global__ __launch_bounds__(256) void skinny_finish_kernel(const GemmParams p) {
+  const int64_t total = (int64_t)p.M * p.ldp;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * 256) {
+    const int row = (int)(idx / p.ldp), pc = (int)(idx - (int64_t)row * p.ldp);
+    int gi = 0;
+    while (gi + 1 < p.ngroups && !(pc >= p.g[gi].ycol0 && pc < p.g[gi].ycol0 + p.g[gi].N)) ++gi;
+    const GemmGroup &G = p.g[gi];
+    const int col = pc - G.ycol0;
+    float v = p.part[idx];
+    for (int s = 1; s < p.split; ++s) v += p.part[(size_t)s * total + idx];
+    if (G.bias) v += G.bias[col];
+    if (p.relu) v = fmaxf(v, 0.f);
+    if (G.scale) v = v * G.scale[col] + G.shift[col];
+    if (p.residual) v += p.residual[(int64_t)row * p.res_stride + col];
+    if (p.y) p.y[(int64_t)row * p.y_stride + pc] = v;
+    if (p.yt) {
+      const int b = row / p.To, t = row - b * p.To;
+      p.yt[((int64_t)b * p.yt_channels + pc) * p.To + t] = v;
+    }
+  }
+}
+
 // w [N][K] fp32 -> [3][N][Kpad] bf16 pieces (w = p0 + p1 + p2 exactly), zero K padding
 __global__ void split_weights_kernel(const float *__restrict__ w, int64_t N, int64_t K,
                                      int64_t Kpad, __bf16 *__restrict__ out) {
@@ -1570,7 +1771,7 @@ static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s
     q.split = (nch + q.kc_per - 1) / q.kc_per;
   }
   const int MT = (q.M + SL_BM - 1) / SL_BM;
-  const int nblk = (MT + 7) / 8 * 8 * q.ngroups * q.g[0].ntiles;  // whole XCD rounds
+  const int nblk = (MT < 8 ? MT : (MT + 7) / 8 * 8) * q.ngroups * q.g[0].ntiles;  // whole XCD rounds
   dim3 grid(nblk, q.split), block(512);
   if (slab_ws(q)) {
     block = dim3(768);
@@ -1598,12 +1799,60 @@ static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s
   return FTMI_OK;
 }
 
+// skinny kernel eligibility (FTMI_GEMM_SKINNY=0, read per call, turns it off): few rows,
+// same-length output, conv epilogue, groups of equal width, and at most SK_CPB chunks per
+// block for the caller's split (partials in p.part when it splits)
+static bool skinny_ok(const GemmParams &p, int epi) {
+  const char *e = getenv("FTMI_GEMM_SKINNY");
+  if (e && atoi(e) == 0) return false;
+  if (epi != EPI_CONV || p.To != p.T || p.Cin % 16 || p.M > SK_MMAX || p.M <= 0) return false;
+  for (int i = 0; i < p.ngroups; ++i)
+    if (p.g[i].k > SL_MAXK || p.g[i].N != p.g[0].N || !p.g[i].w3 || !p.g[i].colscale) return false;
+  const int nch = (p.Cin + 31) / 32, S = p.split_req > 1 ? p.split_req : 1;
+  const int kc_per = (nch + S - 1) / S;
+  if (kc_per > SK_CPB) return false;
+  return (nch + kc_per - 1) / kc_per == 1 || p.part != nullptr;
+}
+
+static int launch_skinny(const GemmParams &p, bool maxpool, hipStream_t s) {
+  GemmParams q = p;
+  const int nch = (q.Cin + 31) / 32, S = q.split_req > 1 ? q.split_req : 1;
+  q.kc_per = (nch + S - 1) / S;
+  q.split = (nch + q.kc_per - 1) / q.kc_per;  // no empty splits
+  const int NT = (q.g[0].N + SK_BN - 1) / SK_BN, MT = (q.M + SK_BM - 1) / SK_BM;
+  q.ldp = 0;
+  for (int i = 0; i < q.ngroups; ++i) {
+    q.g[i].ntiles = NT;
+    q.ldp = max(q.ldp, q.g[i].ycol0 + q.g[i].N);
+  }
+  dim3 grid(MT * q.ngroups * NT, q.split), block(256);
+  if (maxpool)
+    hipLaunchKernelGGL(conv_gemm_skinny_kernel<true>, grid, block, 0, s, q);
+  else
+    hipLaunchKernelGGL(conv_gemm_skinny_kernel<false>, grid, block, 0, s, q);
+  FTMI_CHECK_LAUNCH();
+  if (q.split > 1) {
+    const int64_t total = (int64_t)q.M * q.ldp;
+    const int eb = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+    hipLaunchKernelGGL(skinny_finish_kernel, dim3(eb), dim3(256), 0, s, q);
+    FTMI_CHECK_LAUNCH();
+  }
+  return FTMI_OK;
+}
+
 int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hipStream_t s) {
   if (nblocks <= 0) return FTMI_OK;
   dim3 grid(nblocks), block(256);
   bool presplit = (mma == 1 && x6_variant() != 3) || mma == 2;
   for (int i = 0; i < p.ngroups; ++i) presplit &= p.g[i].w3 != nullptr;
   if (mma == 2 && !presplit) return FTMI_E_ARG;  // the f16 path needs the split planes
+  if (mma == 2 && presplit && skinny_ok(p, epi)) return launch_skinny(p, maxpool, s);
+  if (p.ngroups > 1 && p.split_req > 1) {  // a bank split only serves the skinny kernel
+    GemmParams q = p;
+    q.split_req = 0;
+    q.part = nullptr;
+    return launch(q, epi, maxpool, nblocks, mma, s);
+  }
   if (mma == 2 && slab_ok(p, epi)) return launch_slab(p, epi, maxpool, s);
   if (presplit) {
     dim3 g2(nblocks, p.split > 1 ? p.split : 1);
@@ -1757,6 +2006,16 @@ extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32
                               int32_t Cout, const float *bn_scale, const float *bn_shift,
                               float *y, int64_t y_stride, int32_t mma, uint32_t *status,
                               ftmi_stream_t stream) {
+  return ftmi_conv_bank_split(x, x_stride, B, T, Cin, w, w_split, K, Cout, bn_scale, bn_shift,
+                              y, y_stride, mma, status, 0, nullptr, stream);
+}
+
+extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B, int32_t T,
+                                    int32_t Cin, const float *w, const void *w_split, int32_t K,
+                                    int32_t Cout, const float *bn_scale, const float *bn_shift,
+                                    float *y, int64_t y_stride, int32_t mma, uint32_t *status,
+                                    int32_t split_k, float *split_ws, ftmi_stream_t stream) {
+  if (split_k > 1 && !split_ws) return FTMI_E_ARG;
   if (!x || !w || !bn_scale || !bn_shift || !y) return FTMI_E_ARG;
   if (B <= 0 || T <= 0 || Cin <= 0 || Cout <= 0 || K <= 0) return FTMI_E_ARG;
   if (mma < 0 || mma > 2 || (mma == 2 && !w_split)) return FTMI_E_ARG;
@@ -1806,6 +2065,10 @@ extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32
     g.ntiles = ntiles;
     g.tile0 = tile0;
     tile0 += mtiles * ntiles;
+  }
+  if (split_k > 1) {
+    p.split_req = split_k;
+    p.part = split_ws;
   }
   return launch(p, EPI_CONV, false, tile0, mma, ftmi_hs(stream));
 }

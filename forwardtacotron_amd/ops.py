@@ -109,6 +109,22 @@ def _slab(mma: int, T: int, To: int, Cin: int, k: int, N: int, M: int) -> bool:
             and M * N * k * Cin >= int(os.environ.get('FTMI_GEMM_SLAB_MIN', 0)))
 
 
+SKINNY_MMAX = 256  # gemm.hip SK_MMAX
+
+
+def _skinny(mma: int, T: int, To: int, Cin: int, k: int, M: int) -> bool:
+    """Whether a conv takes the weight-streaming skinny kernel (gemm.hip skinny_ok): few
+    rows (B = 1 generation), f16x3, same-length output."""
+    return (os.environ.get('FTMI_GEMM_SKINNY', '1') != '0' and mma == 2 and To == T
+            and Cin % 16 == 0 and k <= 16 and 0 < M <= SKINNY_MMAX)
+
+
+def _skinny_split(Cin: int) -> int:
+    """Channel split of the skinny kernel: two 32-channel chunks per block."""
+    nch = -(-Cin // 32)
+    return -(-nch // 2)
+
+
 def _split_k(M: int, N: int, K: int, mma: int, slab: bool = False, Cin: int = 0) -> int:
     """Split K when the tile grid cannot fill the chip (x6 / h3 kernels: 2 workgroups per
     CU; slab kernel: 256 x 128 tiles, 1 per CU, split over 32-channel chunks) and K is long
@@ -272,7 +288,10 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
     a.mma, a.w_split = _gemm_mma(mma, w_split)
     a.status = status_word(x.device).data_ptr()
     M = B * To
-    sk = _split_k(M, N, k * Cin, a.mma, _slab(a.mma, T, To, Cin, k, N, M), Cin)
+    if _skinny(a.mma, T, To, Cin, k, M):
+        sk = _skinny_split(Cin)
+    else:
+        sk = _split_k(M, N, k * Cin, a.mma, _slab(a.mma, T, To, Cin, k, N, M), Cin)
     if sk > 1:
         part = torch.empty(sk * M * N, device=x.device, dtype=_f32)
         a.split_k, a.split_ws = sk, part.data_ptr()
@@ -293,11 +312,15 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
     M = B * T
     flops = 2.0 * M * Cout * Cin * K * (K + 1) / 2
     mma, wsp = _gemm_mma(mma, w_split)
-    launch('ftmi_conv_bank', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}]', flops,
+    sk, part = 0, None
+    if _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
+        sk = _skinny_split(Cin)  # weight-streaming kernel: partial sums, finished in order
+        part = torch.empty(sk * M * K * Cout, device=x.device, dtype=_f32)
+    launch('ftmi_conv_bank_split', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}]', flops,
            4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
            x.data_ptr(), xs, B, T, Cin, w.data_ptr(), wsp, K, Cout,
            scale.data_ptr(), shift.data_ptr(), y.data_ptr(), y.stride(1), mma,
-           status_word(x.device).data_ptr(), _stream())
+           status_word(x.device).data_ptr(), sk, _ptr(part), _stream())
     return y
 
 

@@ -138,6 +138,19 @@ int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32
                    const float *bn_shift, float *y, int64_t y_stride, int32_t mma,
                    uint32_t *status, ftmi_stream_t stream);
 
+/* ftmi_conv_bank with a channel split (ABI 6): when B*T <= 256 and mma == FTMI_MMA_F16X3
+ * the bank runs on the weight-streaming "skinny" kernel (B = 1 generation, BASELINE config
+ * c2), whose blocks take ceil(ceil(Cin/32) / split_k) <= 2 channel chunks each and leave
+ * raw partial sums in split_ws (split_k * B*T * K*Cout floats, caller-owned), summed in split
+ * order by a finishing launch (deterministic).  split_k <= 1 / split_ws NULL: as
+ * ftmi_conv_bank.  Other shapes ignore the split.  ftmi_conv1d takes the same kernel for
+ * B*T_out <= 256 (its split_k / split_ws as documented there). */
+int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t Cin,
+                         const float *w, const void *w_split, int32_t K, int32_t Cout,
+                         const float *bn_scale, const float *bn_shift, float *y,
+                         int64_t y_stride, int32_t mma, uint32_t *status, int32_t split_k,
+                         float *split_ws, ftmi_stream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * One highway layer (common_layers.py:22-35):
  *   g = sigmoid(x W2^T + b2);  y = g * relu(x W1^T + b1) + (1 - g) * x

@@ -49,6 +49,8 @@ def test_strerror():
     (lambda L: L.ftmi_embedding(None, 4, None, 135, 256, None, None, None), 1001),
     (lambda L: L.ftmi_conv1d(None, None), 1001),
     (lambda L: L.ftmi_conv_bank(None, 0, 1, 1, 16, None, None, 4, 8, None, None, None, 0, 1, None, None), 1001),
+    (lambda L: L.ftmi_conv_bank_split(None, 0, 1, 1, 16, None, None, 4, 8, None, None, None, 0, 1, None, 0, None, None), 1001),
+    (lambda L: L.ftmi_conv_bank_split(ctypes.c_void_p(256), 16, 1, 1, 16, ctypes.c_void_p(256), ctypes.c_void_p(256), 4, 8, ctypes.c_void_p(256), ctypes.c_void_p(256), ctypes.c_void_p(256), 32, 2, None, 4, None, None), 1001),
     (lambda L: L.ftmi_highway(None, 0, 1, 32, None, None, None, None, None, 0, 1, None, None), 1001),
     (lambda L: L.ftmi_split_weights(None, 4, 4, None, None), 1001),
     (lambda L: L.ftmi_split_weights_f16(None, 4, 4, None, None), 1001),

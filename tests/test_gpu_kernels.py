@@ -43,13 +43,19 @@ MMAS = pytest.mark.parametrize('mma,pre', [(0, False), (1, False), (1, True), (2
                                ids=['f32', 'bf16x6', 'bf16x6-presplit', 'f16x3'])
 
 
-def slab_or_skip(kernel, mma, monkeypatch):
-    """'slab': the default choice (the f16x3 slab kernel for every eligible shape);
-    'tiled': the 128 x 128 tiled kernels only (FTMI_GEMM_SLAB_MIN above any shape here)."""
-    if kernel == 'slab':
-        if mma != 2:
-            pytest.skip('the slab kernel is an f16x3 kernel')
-    else:
+def slab_or_skip(kernel, mma, monkeypatch, M=None):
+    """'skinny': the default choice (the weight-streaming skinny kernel for M <= 256 rows,
+    the slab kernel above); 'slab': the f16x3 slab kernel for every eligible shape
+    (FTMI_GEMM_SKINNY=0); 'tiled': the 128 x 128 tiled kernels only (FTMI_GEMM_SLAB_MIN
+    above any shape here, skinny off)."""
+    if kernel in ('slab', 'skinny') and mma != 2:
+        pytest.skip(f'the {kernel} kernel is an f16x3 kernel')
+    if kernel == 'skinny':
+        if M is not None and M > 256:
+            pytest.skip('the skinny kernel takes M <= 256 rows')
+        return
+    monkeypatch.setenv('FTMI_GEMM_SKINNY', '0')
+    if kernel == 'tiled':
         monkeypatch.setenv('FTMI_GEMM_SLAB_MIN', str(1 << 62))
 
 
@@ -70,9 +76,9 @@ def wsplit(w, pre, mma=1):
     (2, 9, 32, 64, 16, True, False, False),     # slab kernel: k = 16 > T, every tap masked
     (4, 70, 64, 1536, 1, False, False, True),   # slab kernel, k = 1, many column tiles
 ])
-@pytest.mark.parametrize('kernel', ['tiled', 'slab'])
+@pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
 def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre, kernel, monkeypatch):
-    slab_or_skip(kernel, mma, monkeypatch)
+    slab_or_skip(kernel, mma, monkeypatch, B * T)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
@@ -93,9 +99,9 @@ def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre, kernel, monkeypa
 
 @MMAS
 @pytest.mark.parametrize('Cin', [128, 1024])
-@pytest.mark.parametrize('kernel', ['tiled', 'slab'])
+@pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
 def test_conv1d_maxpool_residual_transposed(rng, mma, pre, Cin, kernel, monkeypatch):
-    slab_or_skip(kernel, mma, monkeypatch)
+    slab_or_skip(kernel, mma, monkeypatch, 90)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     B, T, N = 2, 45, 80
@@ -111,6 +117,26 @@ def test_conv1d_maxpool_residual_transposed(rng, mma, pre, Cin, kernel, monkeypa
     close(host(yt), ref)
 
 
+@pytest.mark.parametrize('kernel', ['slab', 'skinny'])
+def test_conv1d_c2_proj1_maxpool(rng, kernel, monkeypatch):
+    """BASELINE config c2 (B = 1, T = 120): the prenet proj1 shape (Cin = 16 x 256, k = 3,
+    maxpool fused, ReLU then BN) — 64 channel splits on the skinny kernel."""
+    slab_or_skip(kernel, 2, monkeypatch, 120)
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    B, T, Cin, N = 1, 120, 4096, 256
+    x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
+    w = rng.normal(0, 1 / np.sqrt(Cin * 3), (N, Cin, 3)).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, N).astype(np.float32)
+    sh = rng.normal(0, 0.1, N).astype(np.float32)
+    ref = np.maximum(O.conv1d(O.maxpool_k2_s1_p1(x.transpose(0, 2, 1)), w, 1), 0)
+    ref = ref * sc[None, :, None] + sh[None, :, None]
+    wp = pack_conv(torch.from_numpy(w)).cuda()
+    y, _ = ops.conv1d(dev(x), wp, 3, 1, relu=True, bn=(dev(sc), dev(sh)), maxpool=True, mma=2,
+                      w_split=wsplit(wp, True, 2))
+    close(host(y), ref.transpose(0, 2, 1))
+
+
 @MMAS
 def test_conv1d_strided_input_view(rng, mma, pre):
     from forwardtacotron_amd import ops
@@ -123,10 +149,11 @@ def test_conv1d_strided_input_view(rng, mma, pre):
 
 
 @MMAS
-@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 2, 41), (8, 80, 2, 150), (5, 48, 3, 270)])
-@pytest.mark.parametrize('kernel', ['tiled', 'slab'])
+@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 2, 41), (8, 80, 2, 150), (5, 48, 3, 270),
+                                     (16, 256, 1, 120), (3, 80, 2, 128)])
+@pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
 def test_conv_bank(K, Cin, B, T, rng, mma, pre, kernel, monkeypatch):
-    slab_or_skip(kernel, mma, monkeypatch)
+    slab_or_skip(kernel, mma, monkeypatch, B * T)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     C = 256
