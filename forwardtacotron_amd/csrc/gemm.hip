@@ -1443,7 +1443,7 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
 // in part[s][M][ldp] (output-column order) and skinny_finish_kernel adds them in split order
 // (deterministic) and applies the epilogue; with one split the wave finishes its columns.
 constexpr int SK_BM = 128;
-constexpr int SK_BN = 64;   // 4 waves x 16 columns
+constexpr int SK_BN = 64;   // 4 column sets of 16 (x 2 step halves = 8 waves)
 constexpr int SK_CPB = 2;   // 32-channel chunks per block
 constexpr int SK_SR = SK_BM + SL_MAXK - 1;
 constexpr int SK_ZROW = SK_SR;
@@ -1452,7 +1452,7 @@ constexpr int SK_MMAX = 256;
 constexpr int SK_PF = 4;    // weight-fragment prefetch depth (steps)
 
 template <bool MAXPOOL>
-__global__ __launch_bounds__(256, 2) void conv_gemm_skinny_kernel(const GemmParams p) {
+__global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmParams p) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[SK_CPB * 2 * SK_AIMG];
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const int MT = (p.M + SK_BM - 1) / SK_BM, NT = p.g[0].ntiles;
@@ -1468,21 +1468,35 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_skinny_kernel(const GemmPara
   const int nch = min(nch_all - c_begin, p.kc_per);  // >= 1 (no empty splits)
   const int SR = SK_BM + k - 1;
 
-  // ---- prologue: the slab of this block's chunks (one float4 of 4 channels per item) ----
-  float amax = 0.f;
-  for (int idx = tid; idx < nch * SR * 8; idx += 256) {
+  // ---- prologue: the slab of this block's chunks (one float4 of 4 channels per item); every
+  // load is issued before the first split / store, so their latencies overlap ----
+  constexpr int SK_ASLOTS = (SK_CPB * SK_SR * 8 + 511) / 512;
+  const int nitems = nch * SR * 8;
+  f32x4 av[SK_ASLOTS], au[MAXPOOL ? SK_ASLOTS : 1];
+#pragma unroll
+  for (int i = 0; i < SK_ASLOTS; ++i) {
+    const int idx = tid + 512 * i;
+    av[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if constexpr (MAXPOOL) au[i] = av[i];
     const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
-    int m = m0 - pad + sr;
-    m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
     const int ch = (c_begin + c) * 32 + seg * 4;
-    f32x4 x = {0.f, 0.f, 0.f, 0.f};
-    if (ch < Cin) {
+    if (idx < nitems && ch < Cin) {
+      int m = m0 - pad + sr;
+      m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
       const float *src = p.x + (int64_t)m * p.x_stride + ch;
-      x = *(const f32x4 *)src;
+      av[i] = *(const f32x4 *)src;
       // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
-      if constexpr (MAXPOOL)
-        if (m % p.T > 0) x = fmax4(x, *(const f32x4 *)(src - p.x_stride));
+      if constexpr (MAXPOOL) au[i] = *(const f32x4 *)(src - (m % p.T > 0 ? p.x_stride : 0));
     }
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < SK_ASLOTS; ++i) {
+    const int idx = tid + 512 * i;
+    if (idx >= nitems) break;
+    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
+    f32x4 x = av[i];
+    if constexpr (MAXPOOL) x = fmax4(x, au[i]);
     amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
     f16x4 h, t;
     split2h(x, h, t);
@@ -1497,8 +1511,16 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_skinny_kernel(const GemmPara
   __syncthreads();
   bool bad = !(amax <= 65504.f);
 
-  const int col0 = nt * SK_BN + wave * 16;  // this wave's 16 columns of group gi
-  if (col0 < G.N) {  // wave-uniform; nothing below synchronises
+  // 8 waves: wave w multiplies columns col0 + [0, 16) (column set w & 3) over one half of
+  // the steps (w >> 2); the two halves meet in LDS after the loop
+  const int cw = wave & 3, half = wave >> 2;
+  const int col0 = nt * SK_BN + cw * 16;  // this wave's 16 columns of group gi
+  const int nsteps = nch * k, hs = (nsteps + 1) / 2;
+  const int s_begin = half ? hs : 0, s_end = half ? nsteps : hs;
+  f32x4 acc[8];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) acc[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (col0 < G.N && s_end > s_begin) {  // wave-uniform; no barrier inside
     // per-row tap masks: bit j set iff frame t + j - pad lies inside the sequence
     unsigned vmask[8];
 #pragma unroll
@@ -1516,47 +1538,65 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_skinny_kernel(const GemmPara
     const int n = col0 + fr < G.N ? col0 + fr : G.N - 1;
     const _Float16 *w0 = (const _Float16 *)G.w3 + (int64_t)n * G.Kpad;
     const int64_t plane = (int64_t)G.N * G.Kpad;
-    const int nsteps = nch * k;
+    // step s = (tap j = s / nch, chunk c = s % nch): the chunks of one tap are adjacent
+    // 64-B pieces of a weight row, so consecutive steps read whole 128-B lines
+    // Loads are unconditional (a missing channel segment of a partial chunk reads channel 0
+    // and is zeroed at use): a select on a loaded value would force a wait at the load.
     auto loadB = [&](int s, f16x8 &b0, f16x8 &b1) {
-      const int c = s / k, j = s - c * k;
+      const int j = s / nch, c = s - j * nch;
       const int ch = (c_begin + c) * 32 + fs * 8;
-      const bool ok = ch < Cin;  // Cin % 16 == 0: a segment is wholly in or out
-      const int off = j * Cin + (ok ? ch : 0);
-      const f16x8 z = {};
-      b0 = ok ? *(const f16x8 *)(w0 + off) : z;
-      b1 = ok ? *(const f16x8 *)(w0 + plane + off) : z;
+      const int off = j * Cin + (ch < Cin ? ch : 0);  // Cin % 16 == 0: wholly in or out
+      b0 = *(const f16x8 *)(w0 + off);
+      b1 = *(const f16x8 *)(w0 + plane + off);
     };
-    f32x4 acc[8];
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) acc[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // Every step issues exactly one (clamped) weight load pair and the loop body has no
+    // branch at all, so the wait before a step's MFMAs leaves the SK_PF - 1 newer load
+    // pairs in flight; the step's 16 A fragments are read before its 24 MFMAs.
     f16x8 rb0[SK_PF], rb1[SK_PF];
 #pragma unroll
-    for (int u = 0; u < SK_PF; ++u)
-      if (u < nsteps) loadB(u, rb0[u], rb1[u]);
-    for (int s0 = 0; s0 < nsteps; s0 += SK_PF) {
+    for (int u = 0; u < SK_PF; ++u) loadB(min(s_begin + u, s_end - 1), rb0[u], rb1[u]);
+    for (int s0 = s_begin; s0 < s_end; s0 += SK_PF) {
 #pragma unroll
       for (int u = 0; u < SK_PF; ++u) {
         const int s = s0 + u;
-        if (s >= nsteps) break;
-        const f16x8 b0 = rb0[u], b1 = rb1[u];
-        if (s + SK_PF < nsteps) loadB(s + SK_PF, rb0[u], rb1[u]);
-        const int c = s / k, j = s - c * k;
-        const _Float16 *Ab = lds + c * 2 * SK_AIMG;
-        const f16x8 bh = b0 * (_Float16)(1.0f / H3_SCALE);
+        {  // steps past the end (nsteps rounded up to SK_PF) multiply zeros: no branch
+          const int sl = min(s, s_end - 1), j = sl / nch, c = sl - j * nch;
+          const _Float16 *Ab = lds + c * 2 * SK_AIMG;
+          f16x8 ah[8], at[8];
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-          const bool ok = (vmask[mi] >> j) & 1u;
-          const int o = (ok ? mi * 16 + fr + j : SK_ZROW) * SL_P + fs * 8;
-          const f16x8 ah = *(const f16x8 *)(Ab + o);
-          const f16x8 at = *(const f16x8 *)(Ab + SK_AIMG + o);
-          f32x4 cc = acc[mi];
-          cc = mma16(at, bh, cc);  // small terms first
-          cc = mma16(ah, b1, cc);
-          cc = mma16(ah, b0, cc);
-          acc[mi] = cc;
+          for (int mi = 0; mi < 8; ++mi) {
+            const bool ok = (vmask[mi] >> j) & 1u;
+            const int o = (ok ? mi * 16 + fr + j : SK_ZROW) * SL_P + fs * 8;
+            ah[mi] = *(const f16x8 *)(Ab + o);
+            at[mi] = *(const f16x8 *)(Ab + SK_AIMG + o);
+          }
+          const f16x8 z = {};
+          const bool bok = s < s_end && (c_begin + c) * 32 + fs * 8 < Cin;
+          const f16x8 b0 = bok ? rb0[u] : z, b1 = bok ? rb1[u] : z;
+          const f16x8 bh = b0 * (_Float16)(1.0f / H3_SCALE);
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi) acc[mi] = mma16(at[mi], bh, acc[mi]);  // small terms first
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi) acc[mi] = mma16(ah[mi], b1, acc[mi]);
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi) acc[mi] = mma16(ah[mi], b0, acc[mi]);
         }
+        // refill the slot in place (a copy of a pending load would wait for it)
+        loadB(min(s + SK_PF, s_end - 1), rb0[u], rb1[u]);
       }
     }
+  }
+  // the second half's sums join the first half's through LDS (the slab is dead by then)
+  __syncthreads();
+  f32x4 *red = (f32x4 *)lds;  // [column set][mi][lane]
+  if (half) {
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) red[(cw * 8 + mi) * 64 + lane] = acc[mi];
+  }
+  __syncthreads();
+  if (!half && col0 < G.N) {
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) acc[mi] += red[(cw * 8 + mi) * 64 + lane];
     // lane (fr, fs) holds rows mi*16 + 4 fs + i of column col0 + fr
     const int col = col0 + fr;
     const bool cok = col < G.N;
@@ -1599,26 +1639,35 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_skinny_kernel(const GemmPara
   if (bad && p.status) atomicOr(p.status, 1u);
 }
 
-// sum of the skinny kernel's split partials (split order) + the conv epilogue, every group
+// sum of the skinny kernel's split partials + the conv epilogue; blockIdx.y is the group
+// (uniform: its parameters stay scalar loads).  L = 4 lanes share an element when there
+// are many splits (L = 1 below 8): lane q adds splits q, q + L, ... in order and xor-
+// shuffles combine the L sums in a fixed order, so the result is deterministic and the
+// dependent load chains are L times shorter.
+template <int L>
 __global__ __launch_bounds__(256) void skinny_finish_kernel(const GemmParams p) {
-  const int64_t total = (int64_t)p.M * p.ldp;
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * 256) {
-    const int row = (int)(idx / p.ldp), pc = (int)(idx - (int64_t)row * p.ldp);
-    int gi = 0;
-    while (gi + 1 < p.ngroups && !(pc >= p.g[gi].ycol0 && pc < p.g[gi].ycol0 + p.g[gi].N)) ++gi;
-    const GemmGroup &G = p.g[gi];
-    const int col = pc - G.ycol0;
-    float v = p.part[idx];
-    for (int s = 1; s < p.split; ++s) v += p.part[(size_t)s * total + idx];
+  const GemmGroup &G = p.g[blockIdx.y];
+  const int N = G.N, q = threadIdx.x & (L - 1);
+  const int64_t total = (int64_t)p.M * p.ldp, n_el = (int64_t)p.M * N;
+  for (int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L; idx < n_el;
+       idx += (int64_t)gridDim.x * (256 / L)) {  // the L lanes of an element iterate together
+    const int row = (int)(idx / N), col = (int)(idx - (int64_t)row * N);
+    const int64_t pi = (int64_t)row * p.ldp + G.ycol0 + col;
+    float v = 0.f;
+    for (int s = q; s < p.split; s += L) v += p.part[(size_t)s * total + pi];
+    if constexpr (L == 4) {
+      v += __shfl_xor(v, 1, 4);
+      v += __shfl_xor(v, 2, 4);
+      if (q) continue;
+    }
     if (G.bias) v += G.bias[col];
     if (p.relu) v = fmaxf(v, 0.f);
     if (G.scale) v = v * G.scale[col] + G.shift[col];
     if (p.residual) v += p.residual[(int64_t)row * p.res_stride + col];
-    if (p.y) p.y[(int64_t)row * p.y_stride + pc] = v;
+    if (p.y) p.y[(int64_t)row * p.y_stride + G.ycol0 + col] = v;
     if (p.yt) {
       const int b = row / p.To, t = row - b * p.To;
-      p.yt[((int64_t)b * p.yt_channels + pc) * p.To + t] = v;
+      p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = v;
     }
   }
 }
@@ -1825,16 +1874,21 @@ static int launch_skinny(const GemmParams &p, bool maxpool, hipStream_t s) {
     q.g[i].ntiles = NT;
     q.ldp = max(q.ldp, q.g[i].ycol0 + q.g[i].N);
   }
-  dim3 grid(MT * q.ngroups * NT, q.split), block(256);
+  dim3 grid(MT * q.ngroups * NT, q.split), block(512);
   if (maxpool)
     hipLaunchKernelGGL(conv_gemm_skinny_kernel<true>, grid, block, 0, s, q);
   else
     hipLaunchKernelGGL(conv_gemm_skinny_kernel<false>, grid, block, 0, s, q);
   FTMI_CHECK_LAUNCH();
   if (q.split > 1) {
-    const int64_t total = (int64_t)q.M * q.ldp;
-    const int eb = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
-    hipLaunchKernelGGL(skinny_finish_kernel, dim3(eb), dim3(256), 0, s, q);
+    const int64_t n_el = (int64_t)q.M * q.g[0].N;
+    if (q.split >= 8) {  // 64 elements per 256-thread block
+      const int eb = (int)((n_el + 63) / 64 < 2048 ? (n_el + 63) / 64 : 2048);
+      hipLaunchKernelGGL(skinny_finish_kernel<4>, dim3(eb, q.ngroups), dim3(256), 0, s, q);
+    } else {
+      const int eb = (int)((n_el + 255) / 256 < 1024 ? (n_el + 255) / 256 : 1024);
+      hipLaunchKernelGGL(skinny_finish_kernel<1>, dim3(eb, q.ngroups), dim3(256), 0, s, q);
+    }
     FTMI_CHECK_LAUNCH();
   }
   return FTMI_OK;

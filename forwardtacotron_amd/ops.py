@@ -122,7 +122,8 @@ def _skinny(mma: int, T: int, To: int, Cin: int, k: int, M: int) -> bool:
 def _skinny_split(Cin: int) -> int:
     """Channel split of the skinny kernel: two 32-channel chunks per block."""
     nch = -(-Cin // 32)
-    return -(-nch // 2)
+    per = int(os.environ.get('FTMI_SKINNY_CPB', 2))  # chunks per block (1 or 2; A/B runs)
+    return -(-nch // per)
 
 
 def _split_k(M: int, N: int, K: int, mma: int, slab: bool = False, Cin: int = 0) -> int:
