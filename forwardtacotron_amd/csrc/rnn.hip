@@ -225,15 +225,19 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       if (!poll_ge(p.ws + WS_ARRIVE, gridDim.x)) {
         abort = 1;
         __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else if (p.ngroups % 8 == 0) {
-        const unsigned per = (unsigned)(p.ngroups / 8) * BPG;
+      } else if (p.ngroups % 8 == 0 || (int)gridDim.x == 8 * BPG) {
+        // ngroups a multiple of 8: ngroups / 8 groups per XCD.  Fewer groups (small
+        // batches): the grid is padded to one group's worth of workgroups per XCD, XCD x
+        // hosts group x and the XCDs past the last group retire their workgroups.
+        const int gpx = p.ngroups % 8 == 0 ? p.ngroups / 8 : 1;
+        const unsigned per = (unsigned)gpx * BPG;
         bool balanced = true;
         for (int i = 0; i < 8; ++i)
           balanced &= __hip_atomic_load(p.ws + WS_CENSUS + i * CNT_PAD, __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT) == per;
         if (balanced) {
           mode = 1;
-          group = (int)(x * (p.ngroups / 8) + slot / BPG);
+          group = (int)(x * gpx + slot / BPG);
           bi = (int)(slot % BPG);
         }
       }
@@ -245,6 +249,9 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   }
   __syncthreads();
   if (s_abort) return;
+  // padded grid: the surplus workgroups (census: XCDs past the last group; fallback order:
+  // bi >= BPG) leave after the census barrier
+  if (s_group >= p.ngroups || s_bi >= BPG) return;
   const int group = s_group, bi = s_bi;
   const bool xcd_mode = s_mode == 1;
   const int dir = group & 1;
@@ -790,7 +797,16 @@ int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
       hipError_t e = hipMemsetAsync(p.ws + WS_CENSUS, 0, (WS_FLAGS - WS_CENSUS) * 4, s);
       if (e != hipSuccess) return (int)e;
     }
-    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, FUSE>), dim3(p.ngroups * BPG),
+    // fewer than 8 groups (small batches): pad the grid to BPG workgroups per XCD so that
+    // each group can run inside one XCD (the census picks the layout); FTMI_RNN_PAD=0 off
+    static const int pad_env = [] {
+      const char *v = getenv("FTMI_RNN_PAD");
+      return v ? atoi(v) : 1;
+    }();
+    int nblk = p.ngroups * BPG;
+    if (BPG > 1 && pad_env && p.xcd_local && p.ngroups < 8 && 8 * BPG <= max_blocks)
+      nblk = 8 * BPG;
+    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, FUSE>), dim3(nblk),
                        dim3(BPG == 1 ? 256 : 320), 0, s, p);
     FTMI_CHECK_LAUNCH();
   }
