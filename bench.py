@@ -58,7 +58,8 @@ PEAK_X3_TFLOPS = PEAK_BF16_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 
-PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r1_pmc_traffic.json')
+PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r1_pmc_traffic.json')        # c3
+PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r1c2_pmc_traffic.json')   # c2 (--config c2)
 
 
 def rocprof_name(label: str):
@@ -70,20 +71,21 @@ def rocprof_name(label: str):
     return None
 
 
-def pmc_traffic(label: str):
-    """HBM bytes per launch of the dominant kernel from the committed PMC passes
-    (tools/profile_round.sh + tools/summarize_prof.py: FETCH_SIZE x 2 + WRITE_SIZE), or None."""
+def pmc_traffic(label: str, path: str = PMC_PROFILE):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes of the same
+    workload (tools/profile_round.sh + tools/summarize_prof.py: FETCH_SIZE x 2 + WRITE_SIZE),
+    or None."""
     pref = rocprof_name(label)
-    if pref is None or not os.path.exists(PMC_PROFILE):
+    if pref is None or not os.path.exists(path):
         return None
-    ks = json.load(open(PMC_PROFILE))['kernels']
+    ks = json.load(open(path))['kernels']
     hit = [v for k, v in ks.items() if k.startswith(pref)]
     if len(hit) != 1:
         return None
     return {'bytes_per_launch': hit[0]['hbm_bytes_per_launch'],
             'read_bytes_corrected': hit[0]['read_bytes_corrected'],
             'write_bytes': hit[0]['write_bytes'],
-            'source': os.path.relpath(PMC_PROFILE, ROOT)}
+            'source': os.path.relpath(path, ROOT)}
 
 
 def log(*a):
@@ -107,7 +109,8 @@ def main():
     args = ap.parse_args()
     if args.config == 'c2':
         args.batch, args.tmin, args.tmax = 1, 120, 120
-    c3_shape = (args.batch, args.tmin, args.tmax) == (64, 50, 200)
+    shape = (args.batch, args.tmin, args.tmax)
+    pmc_path = {(64, 50, 200): PMC_PROFILE, (1, 120, 120): PMC_PROFILE_C2}.get(shape)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -184,7 +187,8 @@ def main():
                     'algorithmic_per_launch': dom['flops'], 'avg_launch_ms': round(dom['avg_ms'], 4),
                     'launches': dom['launches'], 'share_of_device_time': round(dom['total_ms'] / total_dev_ms, 4),
                     'traffic': None}
-            tr = pmc_traffic(dom_label) if c3_shape and args.model == 'forward_tacotron' else None
+            tr = (pmc_traffic(dom_label, pmc_path)
+                  if pmc_path and args.model == 'forward_tacotron' and world == 1 else None)
             if tr is not None:
                 roof['traffic'] = tr['bytes_per_launch']
                 roof['traffic_detail'] = tr
