@@ -50,6 +50,11 @@ def status_word(device) -> torch.Tensor:
     return t
 
 
+def forced_exact() -> bool:
+    """True inside exact_paths() (the range guard's rerun): nothing captured may replay."""
+    return bool(_FORCED)
+
+
 @contextlib.contextmanager
 def exact_paths():
     """Run the enclosed calls on the range-unlimited fp32 MFMA paths (GEMMs and

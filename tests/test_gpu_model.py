@@ -130,3 +130,24 @@ def test_baseline_size_vs_torch_cpu(gpu_model, synth_sd):
         assert a.shape == b.shape
         d = np.abs(a - b)
         assert d.mean() < MEAN_TOL and d.max() < 5e-3, (k, d.mean(), d.max())
+
+
+def test_graph_phase_matches_eager(gpu_model, monkeypatch):
+    """generate() with the default callbacks replays the phoneme phase as a HIP graph:
+    results identical (bit for bit) to the eager phase, across replays with new tokens of
+    the same shape, and the returned dur / pitch / energy are not the graph's buffers."""
+    from forwardtacotron_amd import forward_tacotron as FT
+    g = load_golden('gen_b3')
+    x1 = torch.from_numpy(g['x']).cuda()
+    x2 = x1.clone()
+    x2[x2 > 0] = (x2[x2 > 0] * 7) % 133 + 1  # other phonemes, same padding
+    monkeypatch.setattr(FT, 'GRAPH', False)
+    eager = [gpu_model.generate(x) for x in (x1, x2)]
+    monkeypatch.setattr(FT, 'GRAPH', True)
+    graph = [gpu_model.generate(x) for x in (x1, x2, x1)]
+    assert graph[0]['dur'].data_ptr() != graph[2]['dur'].data_ptr()
+    for e, gr in ((eager[0], graph[0]), (eager[1], graph[1]), (eager[0], graph[2])):
+        for k in ('mel', 'mel_post', 'dur', 'pitch', 'energy'):
+            assert torch.equal(e[k], gr[k]), k
+    # the first result survived the later replays untouched
+    assert torch.equal(graph[0]['dur'], eager[0]['dur'])
