@@ -1449,6 +1449,7 @@ constexpr int SK_SR = SK_BM + SL_MAXK - 1;
 constexpr int SK_ZROW = SK_SR;
 constexpr int SK_AIMG = (SK_SR + 1) * SL_P;  // halves per (chunk, plane) slab image
 constexpr int SK_MMAX = 256;
+constexpr int SK_MMAX_NARROW = 1024;
 constexpr int SK_PF = 4;    // weight-fragment prefetch depth (steps)
 
 template <bool MAXPOOL>
@@ -1854,7 +1855,11 @@ static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s
 static bool skinny_ok(const GemmParams &p, int epi) {
   const char *e = getenv("FTMI_GEMM_SKINNY");
   if (e && atoi(e) == 0) return false;
-  if (epi != EPI_CONV || p.To != p.T || p.Cin % 16 || p.M > SK_MMAX || p.M <= 0) return false;
+  // narrow single-group linears (lin / post_proj at batch 1: N = 80) up to SK_MMAX_NARROW
+  // rows: the 128 x 128 tiles would give them a handful of workgroups
+  const bool narrow = p.ngroups == 1 && p.g[0].N <= SK_BN * 2 && p.M <= SK_MMAX_NARROW;
+  if (epi != EPI_CONV || p.To != p.T || p.Cin % 16 || p.M <= 0) return false;
+  if (p.M > SK_MMAX && !narrow) return false;
   for (int i = 0; i < p.ngroups; ++i)
     if (p.g[i].k > SL_MAXK || p.g[i].N != p.g[0].N || !p.g[i].w3 || !p.g[i].colscale) return false;
   const int nch = (p.Cin + 31) / 32, S = p.split_req > 1 ? p.split_req : 1;

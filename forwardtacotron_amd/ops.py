@@ -114,14 +114,17 @@ def _slab(mma: int, T: int, To: int, Cin: int, k: int, N: int, M: int) -> bool:
             and M * N * k * Cin >= int(os.environ.get('FTMI_GEMM_SLAB_MIN', 0)))
 
 
-SKINNY_MMAX = 256  # gemm.hip SK_MMAX
+SKINNY_MMAX = 256          # gemm.hip SK_MMAX
+SKINNY_MMAX_NARROW = 1024  # gemm.hip SK_MMAX_NARROW (single group, N <= 128)
 
 
-def _skinny(mma: int, T: int, To: int, Cin: int, k: int, M: int) -> bool:
+def _skinny(mma: int, T: int, To: int, Cin: int, k: int, M: int, N: Optional[int] = None) -> bool:
     """Whether a conv takes the weight-streaming skinny kernel (gemm.hip skinny_ok): few
-    rows (B = 1 generation), f16x3, same-length output."""
+    rows (B = 1 generation) — or a narrow single-group linear (N <= 128) with up to 1024
+    rows — f16x3, same-length output.  N = None: a multi-group call (conv bank)."""
+    rows_ok = 0 < M <= SKINNY_MMAX or (N is not None and N <= 128 and 0 < M <= SKINNY_MMAX_NARROW)
     return (os.environ.get('FTMI_GEMM_SKINNY', '1') != '0' and mma == 2 and To == T
-            and Cin % 16 == 0 and k <= 16 and 0 < M <= SKINNY_MMAX)
+            and Cin % 16 == 0 and k <= 16 and rows_ok)
 
 
 def _skinny_split(Cin: int) -> int:
@@ -294,7 +297,7 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
     a.mma, a.w_split = _gemm_mma(mma, w_split)
     a.status = status_word(x.device).data_ptr()
     M = B * To
-    if _skinny(a.mma, T, To, Cin, k, M):
+    if _skinny(a.mma, T, To, Cin, k, M, N):
         sk = _skinny_split(Cin)
     else:
         sk = _split_k(M, N, k * Cin, a.mma, _slab(a.mma, T, To, Cin, k, N, M), Cin)

@@ -43,7 +43,7 @@ MMAS = pytest.mark.parametrize('mma,pre', [(0, False), (1, False), (1, True), (2
                                ids=['f32', 'bf16x6', 'bf16x6-presplit', 'f16x3'])
 
 
-def slab_or_skip(kernel, mma, monkeypatch, M=None):
+def slab_or_skip(kernel, mma, monkeypatch, M=None, N=None):
     """'skinny': the default choice (the weight-streaming skinny kernel for M <= 256 rows,
     the slab kernel above); 'slab': the f16x3 slab kernel for every eligible shape
     (FTMI_GEMM_SKINNY=0); 'tiled': the 128 x 128 tiled kernels only (FTMI_GEMM_SLAB_MIN
@@ -51,8 +51,8 @@ def slab_or_skip(kernel, mma, monkeypatch, M=None):
     if kernel in ('slab', 'skinny') and mma != 2:
         pytest.skip(f'the {kernel} kernel is an f16x3 kernel')
     if kernel == 'skinny':
-        if M is not None and M > 256:
-            pytest.skip('the skinny kernel takes M <= 256 rows')
+        if M is not None and M > 256 and not (N is not None and N <= 128 and M <= 1024):
+            pytest.skip('the skinny kernel takes M <= 256 rows (narrow linears: M <= 1024)')
         return
     monkeypatch.setenv('FTMI_GEMM_SKINNY', '0')
     if kernel == 'tiled':
@@ -75,10 +75,11 @@ def wsplit(w, pre, mma=1):
     (3, 301, 96, 200, 7, True, True, True),     # slab kernel: ragged rows / columns, k = 7
     (2, 9, 32, 64, 16, True, False, False),     # slab kernel: k = 16 > T, every tap masked
     (4, 70, 64, 1536, 1, False, False, True),   # slab kernel, k = 1, many column tiles
+    (1, 816, 1024, 80, 1, False, False, True),  # c2 lin: narrow linear, 816 rows (skinny)
 ])
 @pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
 def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre, kernel, monkeypatch):
-    slab_or_skip(kernel, mma, monkeypatch, B * T)
+    slab_or_skip(kernel, mma, monkeypatch, B * T, N)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
