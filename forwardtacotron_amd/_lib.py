@@ -46,6 +46,8 @@ SIGNATURES = {
     'ftmi_conv_bank_split': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P,
                                      c_int64, c_int, P, c_int, P, P]),
     'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P, P]),
+    'ftmi_highway_split': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P,
+                                   c_int, P, P]),
     'ftmi_split_weights_bytes': (c_int64, [c_int64, c_int64]),
     'ftmi_split_weights': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_split_weights_f16_bytes': (c_int64, [c_int64, c_int64]),

@@ -88,6 +88,7 @@ struct GemmParams {
   int diag;       // slab kernel timing experiments (FTMI_SLAB_DIAG; results invalid when set)
   float *part;
   int ldp;  // skinny kernel: columns of a partial-sum row (all groups, output order)
+  int force_part;  // skinny kernel: partial sums even with one split (highway finish)
   unsigned *status;  // mma = 2: bit 0 set when an accumulator became non-finite
   GemmGroup g[MAX_GROUPS];
 };
@@ -1602,7 +1603,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     const int col = col0 + fr;
     const bool cok = col < G.N;
     const float cs = G.colscale[cok ? col : G.N - 1];
-    if (p.split > 1) {
+    if (p.split > 1 || p.force_part) {
       float *part = p.part + (size_t)blockIdx.y * p.M * p.ldp + G.ycol0;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
@@ -1670,6 +1671,28 @@ __global__ __launch_bounds__(256) void skinny_finish_kernel(const GemmParams p) 
       const int b = row / p.To, t = row - b * p.To;
       p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = v;
     }
+  }
+}
+
+// the skinny kernel's highway finish (common_layers.py:22-35): GEMM columns q*64 + h (W1)
+// and q*64 + 32 + h (W2) of output column o = q*32 + h, summed over the splits in order,
+// then g = sigmoid(x W2 + b2), y = g * relu(x W1 + b1) + (1 - g) * x
+__global__ __launch_bounds__(256) void skinny_highway_finish_kernel(const GemmParams p) {
+  const int C = p.g[0].N / 2;
+  const int64_t total = (int64_t)p.M * p.ldp, n_el = (int64_t)p.M * C;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < n_el;
+       idx += (int64_t)gridDim.x * 256) {
+    const int row = (int)(idx / C), o = (int)(idx - (int64_t)row * C);
+    const int c1 = (o >> 5) * 64 + (o & 31);
+    const int64_t pi = (int64_t)row * p.ldp + c1;
+    float v1 = 0.f, v2 = 0.f;
+    for (int s = 0; s < p.split; ++s) {
+      v1 += p.part[(size_t)s * total + pi];
+      v2 += p.part[(size_t)s * total + pi + 32];
+    }
+    const float g = ftmi_sigmoid(v2 + p.b2[o]);
+    const float xin = p.x[(int64_t)row * p.x_stride + o];
+    p.y[(int64_t)row * p.y_stride + o] = g * fmaxf(v1 + p.b1[o], 0.f) + (1.f - g) * xin;
   }
 }
 
@@ -1857,8 +1880,12 @@ static bool skinny_ok(const GemmParams &p, int epi) {
   if (e && atoi(e) == 0) return false;
   // narrow single-group linears (lin / post_proj at batch 1: N = 80) up to SK_MMAX_NARROW
   // rows: the 128 x 128 tiles would give them a handful of workgroups
-  const bool narrow = p.ngroups == 1 && p.g[0].N <= SK_BN * 2 && p.M <= SK_MMAX_NARROW;
-  if (epi != EPI_CONV || p.To != p.T || p.Cin % 16 || p.M <= 0) return false;
+  // highway layers up to SK_MMAX_NARROW rows too, always through partial sums (the gating
+  // pairs columns 32 apart, which the highway finish reads)
+  const bool hw = epi == EPI_HIGHWAY;
+  const bool narrow = p.ngroups == 1 && (p.g[0].N <= SK_BN * 2 || hw) && p.M <= SK_MMAX_NARROW;
+  if ((epi != EPI_CONV && !hw) || p.To != p.T || p.Cin % 16 || p.M <= 0) return false;
+  if (hw && (!p.part || p.ngroups != 1)) return false;
   if (p.M > SK_MMAX && !narrow) return false;
   for (int i = 0; i < p.ngroups; ++i)
     if (p.g[i].k > SL_MAXK || p.g[i].N != p.g[0].N || !p.g[i].w3 || !p.g[i].colscale) return false;
@@ -1868,8 +1895,9 @@ static bool skinny_ok(const GemmParams &p, int epi) {
   return (nch + kc_per - 1) / kc_per == 1 || p.part != nullptr;
 }
 
-static int launch_skinny(const GemmParams &p, bool maxpool, hipStream_t s) {
+static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t s) {
   GemmParams q = p;
+  q.force_part = epi == EPI_HIGHWAY;
   const int nch = (q.Cin + 31) / 32, S = q.split_req > 1 ? q.split_req : 1;
   q.kc_per = (nch + S - 1) / S;
   q.split = (nch + q.kc_per - 1) / q.kc_per;  // no empty splits
@@ -1885,7 +1913,12 @@ static int launch_skinny(const GemmParams &p, bool maxpool, hipStream_t s) {
   else
     hipLaunchKernelGGL(conv_gemm_skinny_kernel<false>, grid, block, 0, s, q);
   FTMI_CHECK_LAUNCH();
-  if (q.split > 1) {
+  if (q.force_part) {
+    const int64_t n_el = (int64_t)q.M * (q.g[0].N / 2);
+    const int eb = (int)((n_el + 255) / 256 < 2048 ? (n_el + 255) / 256 : 2048);
+    hipLaunchKernelGGL(skinny_highway_finish_kernel, dim3(eb), dim3(256), 0, s, q);
+    FTMI_CHECK_LAUNCH();
+  } else if (q.split > 1) {
     const int64_t n_el = (int64_t)q.M * q.g[0].N;
     if (q.split >= 8) {  // 64 elements per 256-thread block
       const int eb = (int)((n_el + 63) / 64 < 2048 ? (n_el + 63) / 64 : 2048);
@@ -1905,7 +1938,7 @@ int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hip
   bool presplit = (mma == 1 && x6_variant() != 3) || mma == 2;
   for (int i = 0; i < p.ngroups; ++i) presplit &= p.g[i].w3 != nullptr;
   if (mma == 2 && !presplit) return FTMI_E_ARG;  // the f16 path needs the split planes
-  if (mma == 2 && presplit && skinny_ok(p, epi)) return launch_skinny(p, maxpool, s);
+  if (mma == 2 && presplit && skinny_ok(p, epi)) return launch_skinny(p, epi, maxpool, s);
   if (p.ngroups > 1 && p.split_req > 1) {  // a bank split only serves the skinny kernel
     GemmParams q = p;
     q.split_req = 0;
@@ -2136,7 +2169,17 @@ extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t
                             const float *w12, const void *w12_split, const float *b1,
                             const float *b2, float *y, int64_t y_stride, int32_t mma,
                             uint32_t *status, ftmi_stream_t stream) {
+  return ftmi_highway_split(x, x_stride, M, C, w12, w12_split, b1, b2, y, y_stride, mma,
+                            status, 0, nullptr, stream);
+}
+
+extern "C" int ftmi_highway_split(const float *x, int64_t x_stride, int64_t M, int32_t C,
+                                  const float *w12, const void *w12_split, const float *b1,
+                                  const float *b2, float *y, int64_t y_stride, int32_t mma,
+                                  uint32_t *status, int32_t split_k, float *split_ws,
+                                  ftmi_stream_t stream) {
   if (!x || !w12 || !b1 || !b2 || !y) return FTMI_E_ARG;
+  if (split_k >= 1 && !split_ws) return FTMI_E_ARG;
   if (M <= 0 || C <= 0) return FTMI_E_ARG;
   if (mma < 0 || mma > 2 || (mma == 2 && !w12_split)) return FTMI_E_ARG;
   if (C % 32 != 0 || C % 16 != 0) return FTMI_E_SHAPE;
@@ -2169,6 +2212,12 @@ extern "C" int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t
   g.tile0 = 0;
   set_split(g, w12_split, mma);
   const int mtiles = (p.M + BM - 1) / BM;
+  if (split_k >= 1 && mma == 2 && w12_split) {  // skinny kernel: partial sums + highway finish
+    GemmParams q = p;
+    q.split_req = split_k;
+    q.part = split_ws;
+    if (skinny_ok(q, EPI_HIGHWAY)) return launch_skinny(q, EPI_HIGHWAY, false, ftmi_hs(stream));
+  }
   return launch(p, EPI_HIGHWAY, false, mtiles * g.ntiles, mma, ftmi_hs(stream));
 }
 

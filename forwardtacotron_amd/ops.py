@@ -341,11 +341,16 @@ def highway(x: torch.Tensor, w12: torch.Tensor, b1: torch.Tensor, b2: torch.Tens
     y = out if out is not None else torch.empty(B, T, C, device=x.device, dtype=_f32)
     M = B * T
     mma, wsp = _gemm_mma(mma, w_split)
-    launch('ftmi_highway', f'highway[M={M},C={C},mma={mma}]', 2.0 * M * 2 * C * C,
+    sk, part = 0, None
+    if (mma == 2 and wsp is not None and os.environ.get('FTMI_GEMM_SKINNY', '1') != '0'
+            and C % 16 == 0 and 0 < M <= SKINNY_MMAX_NARROW):
+        sk = _skinny_split(C)  # weight-streaming kernel: partials + the highway finish
+        part = torch.empty(sk * M * 2 * C, device=x.device, dtype=_f32)
+    launch('ftmi_highway_split', f'highway[M={M},C={C},mma={mma}]', 2.0 * M * 2 * C * C,
            4.0 * (2 * M * C + 2 * C * C),
            x.data_ptr(), xs, M, C, w12.data_ptr(), wsp, b1.data_ptr(),
            b2.data_ptr(), y.data_ptr(), y.stride(1), mma, status_word(x.device).data_ptr(),
-           _stream())
+           sk, _ptr(part), _stream())
     return y
 
 

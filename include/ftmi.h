@@ -163,6 +163,17 @@ int ftmi_highway(const float *x, int64_t x_stride, int64_t M, int32_t C, const f
                  const void *w12_split, const float *b1, const float *b2, float *y,
                  int64_t y_stride, int32_t mma, uint32_t *status, ftmi_stream_t stream);
 
+/* ftmi_highway with a channel split (ABI 6): split_k >= 1 with M <= 1024 rows and
+ * mma == FTMI_MMA_F16X3 runs the weight-streaming skinny kernel, whose blocks leave raw
+ * partial sums of x [W1|W2]^T in split_ws (split_k * M * 2C floats, caller-owned) and a
+ * finishing launch sums them in split order and applies the gating (deterministic).
+ * split_k = 0 / other shapes: as ftmi_highway. */
+int ftmi_highway_split(const float *x, int64_t x_stride, int64_t M, int32_t C,
+                       const float *w12, const void *w12_split, const float *b1,
+                       const float *b2, float *y, int64_t y_stride, int32_t mma,
+                       uint32_t *status, int32_t split_k, float *split_ws,
+                       ftmi_stream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * Bidirectional single-layer GRU / LSTM recurrence, PyTorch semantics, h0 = c0 = 0,
  * both directions over the full padded length (no packing), output [fwd | bwd].

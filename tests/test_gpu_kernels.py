@@ -171,8 +171,8 @@ def test_conv_bank(K, Cin, B, T, rng, mma, pre, kernel, monkeypatch):
 
 
 @MMAS
-@pytest.mark.parametrize('kernel', ['tiled', 'slab'])
-@pytest.mark.parametrize('C,B,T', [(256, 3, 77), (128, 2, 300)])
+@pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
+@pytest.mark.parametrize('C,B,T', [(256, 3, 77), (128, 2, 300), (256, 1, 816)])
 def test_highway(rng, mma, pre, kernel, C, B, T, monkeypatch):
     from forwardtacotron_amd.common_layers import HighwayNetwork
     slab_or_skip(kernel, mma, monkeypatch)
