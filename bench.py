@@ -46,7 +46,7 @@ from forwardtacotron_amd import forward_tacotron as ft_module  # noqa: E402
 from forwardtacotron_amd.fast_pitch import FastPitch  # noqa: E402
 from forwardtacotron_amd.forward_tacotron import ForwardTacotron  # noqa: E402
 from forwardtacotron_amd.probe import KernelProbe  # noqa: E402
-from forwardtacotron_amd.sharded import generate_sharded  # noqa: E402
+from forwardtacotron_amd.sharded import broadcast_state, generate_sharded  # noqa: E402
 from forwardtacotron_amd.synthetic import default_config, synthetic_state_dict, synthetic_tokens  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA == vector rate), MI355X_MICROARCH.md
@@ -107,6 +107,12 @@ def main():
                     help='fast_pitch = BASELINE.json configs[4] (c5)')
     ap.add_argument('--config', choices=['c2', 'c3'], default=None,
                     help='c2 = BASELINE.json configs[1] (batch 1, 120 phonemes); c3 = the default')
+    ap.add_argument('--callbacks', choices=['identity', 'gen_forward'], default='identity',
+                    help='gen_forward: pitch_function = lambda x: x * amp, energy_function = '
+                         'lambda x: x, as gen_forward.py:103-104 passes them')
+    ap.add_argument('--amp', type=float, default=1.0, help='gen_forward.py --amp')
+    ap.add_argument('--no-host-loop', action='store_true',
+                    help='skip the second (host-to-host, PCIe-inclusive) timed loop')
     args = ap.parse_args()
     if args.config == 'c2':
         args.batch, args.tmin, args.tmax = 1, 120, 120
@@ -123,18 +129,29 @@ def main():
 
     cls = FastPitch if args.model == 'fast_pitch' else ForwardTacotron
     model = cls.from_config(default_config())
-    sd = synthetic_state_dict(model, seed=0, model=args.model)
-    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    sd = None
+    if rank == 0:  # synthetic weights on rank 0; the other ranks receive them (RCCL broadcast)
+        sd = synthetic_state_dict(model, seed=0, model=args.model)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     model = model.to(dev).eval()
+    if world > 1:
+        broadcast_state(model, src=0)
     x_np = synthetic_tokens(args.batch, args.tmax, seed=rank, min_len=args.tmin)
-    x = torch.from_numpy(x_np).to(dev)
+    x_host = torch.from_numpy(x_np)
+    x = x_host.to(dev)
 
-    if world > 1:  # c4: one global batch sharded over the ranks (reference-identical result)
-        gen = lambda: generate_sharded(model, x)
+    if args.callbacks == 'gen_forward':  # gen_forward.py:103-104 (same objects every call)
+        amp = args.amp
+        cb = dict(pitch_function=lambda v: v * amp, energy_function=lambda v: v)
     else:
-        gen = lambda: model.generate(x)
+        cb = {}
+    if world > 1:  # c4: one global batch sharded over the ranks (reference-identical result),
+        # the result collected on rank 0 (SURVEY 8(e) "result collection")
+        gen = lambda xx: generate_sharded(model, xx, gather='rank0', **cb)
+    else:
+        gen = lambda xx: model.generate(xx, **cb)
     for _ in range(args.warmup):
-        gen()
+        gen(x)
     torch.cuda.synchronize()
 
     def barrier():
@@ -143,17 +160,34 @@ def main():
         torch.cuda.synchronize()
 
     frames = 0
+    out = None
     with KernelProbe() as probe:
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            out = gen()  # N > 1: mel_post is already all-gathered (global batch)
-            frames += out['mel_post'].size(0) * out['mel_post'].size(2)
+            o = gen(x)  # N > 1: rank 0 holds the global batch's result
+            if o is not None:
+                out = o
+                frames += out['mel_post'].size(0) * out['mel_post'].size(2)
         torch.cuda.synchronize()
         barrier()
         t1 = time.perf_counter()
     elapsed = t1 - t0
     kern = probe.summary()
+
+    # Second loop, PCIe-inclusive, as gen_forward.py:111-120 runs a call: token ids H2D,
+    # generate(), mel_post D2H (.cpu()).  Reported beside `value`, never as it.
+    host_elapsed = None
+    if not args.no_host_loop:
+        barrier()
+        h0 = time.perf_counter()
+        for _ in range(args.steps):
+            o = gen(x_host.to(dev))
+            if o is not None:
+                o['mel_post'].cpu()
+        torch.cuda.synchronize()
+        barrier()
+        host_elapsed = time.perf_counter() - h0
     # The timed steps replay the phoneme phase as a HIP graph (forward_tacotron.GRAPH), whose
     # kernels the per-launch probe cannot see: one more generate() with the phase eager,
     # after the timed region, gives their per-kernel times (the prenet bank, --kernels).
@@ -162,15 +196,16 @@ def main():
             and x.numel() <= ft_module.GRAPH_MAX_TOKENS):
         ft_module.GRAPH = False
         with KernelProbe() as probe_eager:
-            gen()
+            gen(x)
             torch.cuda.synchronize()
         ft_module.GRAPH = True
         kern_all = probe_eager.summary()
 
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, host_elapsed or 0.0], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = float(t[0].item())
+        host_elapsed = float(t[1].item()) if host_elapsed is not None else None
 
     if rank == 0:
         # dominant kernel = largest device time inside the timed region
@@ -232,6 +267,12 @@ def main():
                                    '(which replay the phoneme phase as a HIP graph)'
                                    if kern_all is not kern else 'HIP events, timed steps')}
         value = frames / elapsed
+        # valid frames: frames of the non-pad phonemes (the rest of B * T_mel is padding)
+        tok = (x_np != 0) if world == 1 else None
+        valid = None
+        if tok is not None:
+            cnt = ft_oracle_counts(out['dur'].float().cpu().numpy())
+            valid = int((cnt * tok).sum())
         fp = args.model == 'fast_pitch'
         line = {
             'metric': 'mel-frames/sec at batch=64 LJSpeech shapes (%s.generate, B*T_mel per s)'
@@ -252,40 +293,97 @@ def main():
                        'T_mel': int(out['mel_post'].size(2)), 'parallelism': f'dp{world}'},
             'roofline': roof,
         }
+        if valid is not None:
+            line['valid_frames_per_step'] = valid
+            line['valid_frames_per_s'] = round(valid * args.steps / elapsed, 1)
+        if host_elapsed is not None:
+            line['host_to_host'] = {
+                'value': round(frames / host_elapsed, 1), 'unit': 'mel-frames/s',
+                'ms_per_step': round(host_elapsed / args.steps * 1e3, 3),
+                'what': 'token ids H2D + generate() + mel_post D2H per step, as gen_forward.py:111-120 '
+                        '(PCIe-inclusive; `value` has the tokens resident in HBM)'}
+        if args.callbacks != 'identity':
+            line['config']['callbacks'] = (f'gen_forward.py:103-104: pitch_function = lambda x: x * {args.amp}, '
+                                           'energy_function = lambda x: x')
         if prenet is not None:
             line['prenet_bank'] = prenet
         if world == 1 and not args.no_cpu_baseline:
-            line['cpu_baseline'], line['parity'] = cpu_baseline(sd, x_np, out, args.model)
+            line['cpu_baseline'], line['parity'] = cpu_baseline(sd, x_np, out, args.model,
+                                                                cb_kind=args.callbacks, amp=args.amp)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(sd, x_np, out, kind='forward_tacotron'):
-    """Time the torch-CPU restatement of the reference on the same batch (bounded: one call)."""
+def ft_oracle_counts(dur):
+    from oracle import ft_oracle
+    return ft_oracle.duration_counts(dur)
+
+
+def _cpu_info():
+    """(CPU model, physical cores of the host) for the cpu_baseline record."""
+    model = 'unknown'
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        import psutil
+        phys = psutil.cpu_count(logical=False)
+    except Exception:  # pragma: no cover
+        phys = None
+    return model, phys
+
+
+def cpu_baseline(sd, x_np, out, kind='forward_tacotron', cb_kind='identity', amp=1.0):
+    """Time the torch-CPU restatement of the reference on the same batch (bounded: one call
+    at the process's thread count), plus a 1-thread figure on a bounded sample of it."""
     from oracle import ft_oracle
     if kind == 'fast_pitch':
         from oracle import fp_torch_cpu as ft_torch_cpu
     else:
         from oracle import ft_torch_cpu
+    cb = {}
+    if cb_kind == 'gen_forward':
+        cb = dict(pitch_function=lambda v: v * amp, energy_function=lambda v: v)
     sdt = ft_torch_cpu.to_torch(sd)
     xt = torch.from_numpy(x_np)
+    threads = torch.get_num_threads()
     ft_torch_cpu.generate(sdt, xt[:1, :20])  # warm the CPU kernels
     t0 = time.perf_counter()
-    ref = ft_torch_cpu.generate(sdt, xt)
+    ref = ft_torch_cpu.generate(sdt, xt, **cb)
     dt = time.perf_counter() - t0
     frames = ref['mel_post'].size(0) * ref['mel_post'].size(2)
+    # 1 thread, bounded: the first min(B, 8) utterances (about 5-10 s of CPU work)
+    n1 = min(x_np.shape[0], 8)
+    x1 = xt[:n1, :int((x_np[:n1] != 0).sum(1).max())]
+    torch.set_num_threads(1)
+    try:
+        t0 = time.perf_counter()
+        r1 = ft_torch_cpu.generate(sdt, x1, **cb)
+        dt1 = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(threads)
+    f1 = r1['mel_post'].size(0) * r1['mel_post'].size(2)
     got = out['mel_post'].float().cpu().numpy()
     r = ref['mel_post'].numpy()
     same_shape = got.shape == r.shape
     d = np.abs(got - r) if same_shape else None
     counts_equal = bool(np.array_equal(ft_oracle.duration_counts(out['dur'].cpu().numpy()),
                                        ft_oracle.duration_counts(ref['dur'].numpy())))
-    base = {'value': round(frames / dt, 1), 'unit': 'mel-frames/s', 'cores': torch.get_num_threads(),
+    cpu_model, phys = _cpu_info()
+    base = {'value': round(frames / dt, 1), 'unit': 'mel-frames/s', 'cores': threads,
             'kind': 'port',
+            'threads_used': threads, 'cpu_model': cpu_model, 'host_physical_cores': phys,
+            'value_1thread': round(f1 / dt1, 1),
             'sample': f'one generate() of the same batch ({x_np.shape[0]} x {x_np.shape[1]} phonemes, '
                       f'T_mel {r.shape[2]}) with oracle/{ft_torch_cpu.__name__.split(".")[-1]}.py '
-                      f'(the reference\'s ATen CPU kernels), {dt:.2f} s'}
+                      f'(the reference\'s ATen CPU kernels) at {threads} threads, {dt:.2f} s; '
+                      f'1 thread: the first {n1} utterances (T_mel {r1["mel_post"].size(2)}), {dt1:.2f} s'}
     parity = {'mel_post_mean_abs': float(d.mean()) if same_shape else None,
               'mel_post_max_abs': float(d.max()) if same_shape else None,
               'lr_counts_equal': counts_equal}

@@ -14,12 +14,14 @@ from pathlib import Path
 
 import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
+from ._srchash import source_hash
+
 _LIB_PATH = Path(os.environ.get('FTMI_LIB', Path(__file__).resolve().parent / 'libftmi.so'))
 _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 6
+ABI_VERSION = 7
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -38,6 +40,7 @@ class ConvArgs(ctypes.Structure):
 # name -> (restype, argtypes); the exact export list of include/ftmi.h
 SIGNATURES = {
     'ftmi_abi_version': (c_int, []),
+    'ftmi_build_id': (ctypes.c_char_p, []),
     'ftmi_strerror': (ctypes.c_char_p, [c_int]),
     'ftmi_embedding': (c_int, [P, c_int64, P, c_int64, c_int64, P, P, P]),
     'ftmi_conv1d': (c_int, [ctypes.POINTER(ConvArgs), P]),
@@ -54,6 +57,8 @@ SIGNATURES = {
     'ftmi_split_weights_f16': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_rnn_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
     'ftmi_rnn_error_offset': (c_int64, [c_int]),
+    'ftmi_rnn_blocks': (c_int, [c_int, c_int, c_int, c_int]),
+    'ftmi_set_rnn_spin_limit': (ctypes.c_uint32, [ctypes.c_uint32]),
     'ftmi_rnn_bidir': (c_int, [c_int, c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,
                                c_float, P, c_int64, c_int, P, P, P]),
     'ftmi_gru_bidir_fused': (c_int, [c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,
@@ -107,6 +112,10 @@ def load():
         fn.argtypes = args
     if lib.ftmi_abi_version() != ABI_VERSION:
         raise FtmiError('libftmi.so ABI version mismatch')
+    built, here = lib.ftmi_build_id().decode(), source_hash()
+    if built != here and os.environ.get('FTMI_LIB') is None:
+        raise FtmiError(f'{_LIB_PATH} was built from other sources (build id {built[:12]}, '
+                        f'sources {here[:12]}): rebuild with `python -m forwardtacotron_amd.build`')
     _lib = lib
     return lib
 

@@ -85,7 +85,12 @@ constexpr float H3_UNSCALE = 1.f / 2048.f;
 
 constexpr int NB = 16;              // sequences per group (MFMA 16x16 columns)
 constexpr int RED_STRIDE = NB + 1;  // LDS partial-sum row stride (floats)
-constexpr unsigned SPIN_LIMIT = 1u << 22;
+// Default bound of every spin (census barrier, h hand-off); ftmi_set_rnn_spin_limit changes
+// it (tests force the timeout path with a tiny limit).
+constexpr unsigned SPIN_LIMIT_DEFAULT = 1u << 22;
+unsigned g_spin_limit = SPIN_LIMIT_DEFAULT;
+// status-word bit set when a workgroup gave up waiting (include/ftmi.h FTMI_STATUS_RNN_TIMEOUT)
+constexpr unsigned STATUS_TIMEOUT = 4u;
 constexpr int CNT_PAD = 32;  // one 128-B line per counter
 // workspace word offsets (in 32-bit words) of the control block
 constexpr int WS_ERR = 0;
@@ -121,6 +126,7 @@ struct RnnParams {
   int64_t x_stride;
   const float *w_ih;
   const float *b_ih;
+  unsigned spin_limit;  // bound of every spin (g_spin_limit at launch)
   int diag;  // timing experiments only (FTMI_RNN_DIAG, results invalid when set): bit 0 =
              // input projections from one L2-hot row, bit 1 = no hand-off waits,
              // bit 2 = no drain
@@ -165,13 +171,21 @@ __device__ __forceinline__ unsigned xcc_id() {
 }
 
 // bounded relaxed poll (one lane): returns false on timeout
-__device__ __forceinline__ bool poll_ge(unsigned *w, unsigned target) {
+__device__ __forceinline__ bool poll_ge(unsigned *w, unsigned target, unsigned limit) {
   unsigned spins = 0;
   while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > SPIN_LIMIT) return false;
+    if (++spins > limit) return false;
   }
   return true;
+}
+
+// a workgroup gave up waiting: the call's output is invalid.  Recorded in the workspace
+// error word and in the caller's status word (bit 2), which the model entry points read
+// (ops.run_checked raises RnnTimeout) — never a silently wrong result.
+__device__ __forceinline__ void report_timeout(const RnnParams &p) {
+  __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (p.status) atomicOr(p.status, STATUS_TIMEOUT);
 }
 
 constexpr int FUSE_CIN = 256;  // input width of the fused-projection instances
@@ -222,9 +236,9 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       const unsigned slot = __hip_atomic_fetch_add(p.ws + WS_CENSUS + x * CNT_PAD, 1u,
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(p.ws + WS_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (!poll_ge(p.ws + WS_ARRIVE, gridDim.x)) {
+      if (!poll_ge(p.ws + WS_ARRIVE, gridDim.x, p.spin_limit)) {
         abort = 1;
-        __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        report_timeout(p);
       } else if (p.ngroups % 8 == 0 || (int)gridDim.x == 8 * BPG) {
         // ngroups a multiple of 8: ngroups / 8 groups per XCD.  Fewer groups (small
         // batches): the grid is padded to one group's worth of workgroups per XCD, XCD x
@@ -588,10 +602,10 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
           fresh &= (d.x | d.y | d.z | d.w) == 0u;
         }
         if (__all(fresh) || (p.diag & 2)) break;
-        if (spins > SPIN_LIMIT) {
+        if (spins > p.spin_limit) {
           if (lane == 0) {
             s_abort = 1;
-            __hip_atomic_store(p.ws + WS_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            report_timeout(p);
           }
           break;
         }
@@ -827,6 +841,31 @@ int device_cu_count() {
 
 }  // namespace
 
+// hidden units per workgroup of the instance ftmi_rnn_bidir dispatches (see there)
+static int rnn_units(int cell, int H, int mma) {
+  if (cell == 0 && H == 64) {
+    static const int u64 = [] {
+      const char *v = getenv("FTMI_RNN_U64");
+      return v ? atoi(v) : 32;
+    }();
+    return (mma == 2 && u64 == 32) ? 32 : 64;
+  }
+  return 16;
+}
+
+extern "C" int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t mma) {
+  if (B <= 0 || H <= 0 || H % 16 != 0) return 0;
+  const int bpg = H / rnn_units(cell, H, mma);
+  const int maxb = device_cu_count();
+  const int max_groups = (maxb / bpg) & ~1;
+  if (max_groups < 2) return 0;
+  const int nchunks = (B + NB - 1) / NB;
+  const int ngroups = 2 * (nchunks < max_groups / 2 ? nchunks : max_groups / 2);
+  int nblk = ngroups * bpg;
+  if (bpg > 1 && ngroups < 8 && 8 * bpg <= maxb) nblk = 8 * bpg;  // launch_rnn's padding
+  return nblk;
+}
+
 // workspace: [control: err, census, flags, counters][hx: 2 * 2*nchunks * 16*H floats]
 static int64_t ctl_bytes(int64_t nchunks) {
   return (WS_GROUPS_OF((int)(2 * nchunks)) + 2 * nchunks * CNT_PAD) * (int64_t)sizeof(unsigned);
@@ -837,6 +876,12 @@ extern "C" int64_t ftmi_rnn_workspace_bytes(int32_t B, int32_t H, int32_t cell) 
   if (B <= 0 || H <= 0) return 0;
   const int64_t nchunks = (B + NB - 1) / NB;
   return ctl_bytes(nchunks) + 2 * (2 * nchunks) * NB * (int64_t)H * (int64_t)sizeof(float);
+}
+
+extern "C" uint32_t ftmi_set_rnn_spin_limit(uint32_t limit) {
+  const unsigned prev = g_spin_limit;
+  g_spin_limit = limit ? limit : SPIN_LIMIT_DEFAULT;
+  return prev;
 }
 
 extern "C" int64_t ftmi_rnn_error_offset(int32_t B) {
@@ -872,6 +917,7 @@ static int rnn_setup(RnnParams &p, int B, int T, int H, int cell, const float *w
   p.ws = (unsigned *)sync;
   p.hx = (float *)((char *)sync + ctl);
   p.status = status;
+  p.spin_limit = g_spin_limit;
   static const int diag_env = [] {
     const char *v = getenv("FTMI_RNN_DIAG");
     return v ? atoi(v) : 0;
@@ -916,11 +962,7 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   // 1.19 us/step against 1.45 for one workgroup per group (h in LDS) at B = 64;
   // FTMI_RNN_U64=64 selects the single-workgroup form
   if (cell == 0 && H == 64) {
-    static const int u64 = [] {
-      const char *v = getenv("FTMI_RNN_U64");
-      return v ? atoi(v) : 32;
-    }();
-    if (mma == 2 && u64 == 32) return launch_rnn<0, 64, 32, 2, 2>(p, nchunks, maxb, s);
+    if (rnn_units(cell, H, mma) == 32) return launch_rnn<0, 64, 32, 2, 2>(p, nchunks, maxb, s);
     FTMI_RNN_MODES(0, 64, 64, 2, 4)
   }
   // H = 128: 16 units per workgroup (8 workgroups per group): 1.04 us/step against 2.33 with

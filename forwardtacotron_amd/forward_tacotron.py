@@ -38,8 +38,8 @@ def _identity(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
-# generate() with the default callbacks replays the phoneme phase as a HIP graph (captured
-# once per (device, x shape, alpha)) when the phase is launch-bound: B*T <= GRAPH_MAX_TOKENS.
+# generate() replays the phoneme phase as a HIP graph (captured per (device, x shape, alpha,
+# callbacks), see _phoneme_graph) when the phase is launch-bound: B*T <= GRAPH_MAX_TOKENS.
 # Measured: c2 (B = 1, T = 120) 4.18 -> 3.57 ms/step; c3 (B = 64, T = 200) 9.20 -> 9.58, the
 # replay loses the prenet stream's priority and the kernels are long enough to hide the host
 # issue anyway.  FTMI_GRAPH=0, or GRAPH = False, keeps it eager.
@@ -234,52 +234,114 @@ class ForwardTacotron(nn.Module):
         return {'mel': x_mel, 'mel_post': x_post,
                 'dur': dur_hat, 'pitch': pitch_hat, 'energy': energy_hat}
 
-    def _side_streams(self, device):
+    def _side_streams(self, device, B: int):
         """(pitch, energy, prenet) streams.  The prenet CBHG -> LSTM input projection is the
         phoneme phase's critical chain: its stream gets the higher priority
         (FTMI_PRENET_PRIORITY, default -1 = high; 0 = same as the others), so the
-        predictors fill the CUs it leaves idle instead of delaying it."""
+        predictors fill the CUs it leaves idle instead of delaying it.
+        The four recurrences of the phase (three predictor GRUs, the prenet GRU) are
+        persistent kernels whose workgroups wait on each other: run concurrently they must
+        fit the CUs together.  When they do not (large batches), every stream is the
+        caller's (the phase runs serialised) — never a co-residency timeout."""
         cache = self.__dict__.setdefault('_ftmi_streams', {})
         if device not in cache:
             prio = int(os.environ.get('FTMI_PRENET_PRIORITY', '-1'))
             cache[device] = [torch.cuda.Stream(device=device), torch.cuda.Stream(device=device),
                              torch.cuda.Stream(device=device, priority=prio)]
+        fits = self.__dict__.setdefault('_ftmi_concurrent', {})
+        key = (device, B, ops.RNN_MMA, bool(ops._FORCED))
+        if key not in fits:
+            rnns = (self.dur_pred.rnn, self.pitch_pred.rnn, self.energy_pred.rnn, self.prenet.rnn)
+            need = sum(ops.rnn_blocks(r.cell, B, r.hidden) for r in rnns)
+            fits[key] = 0 < need <= ops._num_cus()
+        if not fits[key]:
+            main = torch.cuda.current_stream(device)
+            return [main, main, main]
         return cache[device]
 
-    def _phoneme_graph(self, x, alpha):
-        """The phoneme phase (default callbacks, unsharded) as a HIP graph: ~40 launches
-        from Python over four streams become one replay, which matters where the kernels
-        are short (batch 1: the host issue rate, not the device, set the phase's length).
+    def _weights_key(self):
+        """(data_ptr, _version) of every parameter and buffer: changes on load_state_dict,
+        .to(), in-place updates and replaced tensors (the list of tensors is cached and
+        rebuilt when an owner no longer holds the same object, like Packed._pack_key)."""
+        refs = self.__dict__.get('_ftmi_wrefs')
+        if refs is None or any(d.get(n) is not t for d, n, t in refs):
+            refs = [(d, n, t) for m in self.modules() for d in (m._parameters, m._buffers)
+                    for n, t in d.items() if t is not None]
+            self.__dict__['_ftmi_wrefs'] = refs
+        return tuple((t.data_ptr(), t._version) for _, _, t in refs)
+
+    def _phoneme_graph(self, x, alpha, pitch_fn, energy_fn):
+        """The phoneme phase (unsharded) as a HIP graph: ~40 launches from Python over four
+        streams become one replay, which matters where the kernels are short (batch 1: the
+        host issue rate, not the device, set the phase's length).
+        Keyed on (device, x shape, alpha, the callbacks' identity, matrix paths); a key is
+        captured the SECOND time it is seen (a one-off shape — gen_forward.py's sentences
+        of different lengths — stays eager: capture costs ~3 eager phases).  The callbacks
+        are captured with the phase, so they must be device-side torch ops whose effect
+        does not change between calls (gen_forward.py's `lambda x: x * amp` is); set
+        FTMI_GRAPH=0 (or forward_tacotron.GRAPH = False) for callbacks with host-side
+        effects.  A capture that fails (a callback that syncs or leaves the device) marks
+        the key eager for good.
         Static buffers: x is copied in, dur / pitch / energy are cloned out (they go back to
         the caller); enc, the offsets and the LSTM input projection are consumed by this
-        call's decoder, queued on the same stream before the next replay.  T_mel leaves
-        through the one pinned-scalar host sync, as on the eager path."""
+        call's decoder — the next replay waits for the decoder's completion event
+        (generate() records it), so calls on different streams never overwrite buffers a
+        decoder still reads.  The entry keeps every module's weight pack alive and the
+        model-wide weights key of its capture: after each replay (while it runs) the key is
+        compared with the model's, and on a change (load_state_dict, .to(), in-place
+        updates) every captured phase is dropped and the call falls back to the eager phase
+        (the stale replay read the old, still-allocated packs; its outputs are discarded).
+        Returns (phase outputs, entry) or None (run the eager phase)."""
         cache = self.__dict__.setdefault('_ftmi_graphs', {})
-        key = (x.device, tuple(x.shape), float(alpha), ops.MMA, ops.RNN_MMA)
+        seen = self.__dict__.setdefault('_ftmi_graph_seen', {})
+        key = (x.device, tuple(x.shape), float(alpha), pitch_fn, energy_fn, ops.MMA, ops.RNN_MMA)
         ent = cache.pop(key, None)
+        fresh = False
         if ent is None:
+            n = seen.get(key, 0)
+            if n < 0:
+                return None  # capture failed before: eager for good
+            if len(seen) >= 64 * GRAPH_CACHE:  # e.g. a new lambda per call: forget sightings
+                seen.clear()
+            seen[key] = n + 1
+            if n == 0:
+                return None  # first sighting: eager
+            wkey = self._weights_key()
             sx = x.clone()
-            self._phoneme_phase(sx, alpha, _identity, _identity, capture=True)  # warm-up
-            torch.cuda.synchronize(x.device)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                outs = self._phoneme_phase(sx, alpha, _identity, _identity, capture=True)
-            ent = (g, sx, outs)
+            try:
+                self._phoneme_phase(sx, alpha, pitch_fn, energy_fn, capture=True)  # warm-up
+                torch.cuda.synchronize(x.device)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    outs = self._phoneme_phase(sx, alpha, pitch_fn, energy_fn, capture=True)
+            except Exception:  # pylint: disable=broad-except
+                torch.cuda.synchronize(x.device)
+                seen[key] = -1
+                return None
+            packs = [m.__dict__.get('_ftmi_pack') for m in self.modules()]
+            ent = {'g': g, 'sx': sx, 'outs': outs, 'wkey': wkey, 'packs': packs,
+                   'done': torch.cuda.Event()}
+            ent['done'].record(torch.cuda.current_stream(x.device))
+            fresh = True
             while len(cache) >= GRAPH_CACHE:
                 cache.pop(next(iter(cache)))
         cache[key] = ent  # most recently used last
-        g, sx, outs = ent
         main = torch.cuda.current_stream(x.device)
-        sx.copy_(x)
-        g.replay()
-        dur_hat, pitch_hat, energy_hat, enc, offsets, tmax, xp = outs
+        main.wait_event(ent['done'])  # the previous decoder is done with the static buffers
+        ent['sx'].copy_(x)
+        ent['g'].replay()
+        if not fresh and self._weights_key() != ent['wkey']:
+            main.synchronize()  # the stale replay must finish before its graph is freed
+            cache.clear()
+            return None
+        dur_hat, pitch_hat, energy_hat, enc, offsets, tmax, xp = ent['outs']
         t_host = torch.empty((), dtype=tmax.dtype, pin_memory=True)
         t_host.copy_(tmax, non_blocking=True)
         t_ready = torch.cuda.Event()
         t_ready.record(main)
         dur_hat, pitch_hat, energy_hat = dur_hat.clone(), pitch_hat.clone(), energy_hat.clone()
         t_ready.synchronize()
-        return dur_hat, pitch_hat, energy_hat, enc, offsets, int(t_host), xp
+        return (dur_hat, pitch_hat, energy_hat, enc, offsets, int(t_host), xp), ent
 
     def _phoneme_phase(self, x, alpha, pitch_fn, energy_fn, batch=None, capture=False):
         """Duration / pitch / energy predictors and the prenet CBHG are independent: pitch,
@@ -295,7 +357,7 @@ class ForwardTacotron(nn.Module):
         capture=True (graph capture, see _phoneme_graph): no host sync, the T_mel slot holds
         max(totals) on the device."""
         main = torch.cuda.current_stream(x.device)
-        s_pitch, s_energy, s_prenet = self._side_streams(x.device)
+        s_pitch, s_energy, s_prenet = self._side_streams(x.device, x.size(0))
         for s in (s_pitch, s_energy, s_prenet):
             s.wait_stream(main)
         with torch.cuda.stream(s_prenet):
@@ -357,18 +419,23 @@ class ForwardTacotron(nn.Module):
             self.eval()
         self._check_device(x)
 
-        graph = (GRAPH and batch is None and pitch_function is _identity
-                 and energy_function is _identity and x.numel() <= GRAPH_MAX_TOKENS)
+        graph = GRAPH and batch is None and x.numel() <= GRAPH_MAX_TOKENS
 
         def run():
             with torch.no_grad():
+                phase = ent = None
                 if graph and not ops.forced_exact():
-                    phase = self._phoneme_graph(x, alpha)
-                else:
+                    r = self._phoneme_graph(x, alpha, pitch_function, energy_function)
+                    if r is not None:
+                        phase, ent = r
+                if phase is None:
                     phase = self._phoneme_phase(x, alpha, pitch_function, energy_function, batch)
                 dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel, xp = phase
-                return self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
-                                          lr=(offsets, T_mel), xp=xp)
+                out = self._generate_mel(x, dur_hat, pitch_hat, energy_hat, enc=enc,
+                                         lr=(offsets, T_mel), xp=xp)
+                if ent is not None:  # the decoder has consumed the graph's static buffers
+                    ent['done'].record(torch.cuda.current_stream(x.device))
+                return out
         return ops.run_checked(run, x.device, reduce=None if batch is None else batch.status)
 
     def generate_jit(self, x: torch.Tensor, alpha: float = 1.0, beta: float = 1.0) -> Dict[str, torch.Tensor]:

@@ -28,11 +28,13 @@ MMA = int(os.environ.get('FTMI_MMA', '2'))
 # the recurrences' W_hh h path (same codes; FTMI_RNN_MMA overrides)
 RNN_MMA = int(os.environ.get('FTMI_RNN_MMA', '2'))
 
-# f16x3 range guard.  Every GEMM / recurrence launch ORs into a per-device status word:
-# bit 0 = an f16x3 accumulator became non-finite (an activation beyond the f16 range),
-# bit 1 = a W_hh entry beyond the f16 range.  The model entry points zero it, run, read it
-# once at the end, and on a non-zero word run the call again under `exact_paths()` (fp32
-# MFMA everywhere), which has no range limit.
+# Status word (include/ftmi.h FTMI_STATUS_*).  Every GEMM / recurrence launch ORs into a
+# per-device word: bit 0 = an f16x3 accumulator became non-finite (an activation beyond the
+# f16 range), bit 1 = a W_hh entry beyond the f16 range, bit 2 = a recurrence workgroup
+# timed out waiting for its group (its output is invalid).  The model entry points zero it,
+# run, read it once at the end: bit 2 raises RnnTimeout; bits 0-1 run the call again under
+# `exact_paths()` (fp32 MFMA everywhere), which has no range limit.
+STATUS_F16_RANGE, STATUS_WHH_RANGE, STATUS_RNN_TIMEOUT = 1, 2, 4
 _STATUS = {}
 _FORCED = []  # stack of (gemm mma, rnn mma) overrides
 
@@ -83,18 +85,29 @@ def _rnn_mma() -> int:
     return _FORCED[-1][1] if _FORCED else RNN_MMA
 
 
+class RnnTimeout(RuntimeError):
+    """A persistent recurrence could not run all its workgroups at once (another stream's
+    persistent kernels held CUs): its output is invalid, so the call fails."""
+
+
 def run_checked(fn, device, reduce=None):
-    """fn() with the f16x3 range guard: zero the status word, run, read it (one host sync)
-    and, if any bit is set, run fn() again under exact_paths().  reduce(word) -> word
-    combines the status over ranks (sharded generation) before the decision."""
+    """fn() with the status-word checks: zero the word, run, read it (one host sync).
+    A recurrence timeout raises RnnTimeout.  A range bit (f16x3 overflow) runs fn() again
+    under exact_paths() — which calls the model's pitch / energy callbacks a second time
+    (the first pass's callback outputs derive from the out-of-range predictions and are not
+    reused).  reduce(word) -> word combines the status over ranks (sharded generation)
+    before the decision."""
     st = status_word(device)
     st.zero_()
     out = fn()
-    if not _FORCED:
-        s = st if reduce is None else reduce(st)
-        if int(s.item()) != 0:
-            with exact_paths():
-                out = fn()
+    s = st if reduce is None else reduce(st)
+    w = int(s.item())
+    if w & STATUS_RNN_TIMEOUT:
+        raise RnnTimeout('a recurrence workgroup timed out waiting for its group (not all '
+                         'workgroups co-resident): the result is invalid')
+    if w and not _FORCED:
+        with exact_paths():
+            out = fn()
     return out
 
 
@@ -354,8 +367,10 @@ def highway(x: torch.Tensor, w12: torch.Tensor, b1: torch.Tensor, b2: torch.Tens
     return y
 
 
-class RnnTimeout(RuntimeError):
-    pass
+def rnn_blocks(cell: int, B: int, H: int, mma: Optional[int] = None) -> int:
+    """Persistent workgroups one ftmi_rnn_bidir launch occupies (ftmi_rnn_blocks)."""
+    m = _rnn_mma() if mma is None else mma
+    return int(_lib.load().ftmi_rnn_blocks(cell, B, H, m))
 
 
 def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Optional[torch.Tensor],

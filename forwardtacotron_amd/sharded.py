@@ -59,21 +59,50 @@ def pad_tokens(x: torch.Tensor, T: int) -> torch.Tensor:
     return out
 
 
-def gather_rows(t: torch.Tensor, group=None) -> torch.Tensor:
-    """All-gather along dim 0 with per-rank row counts that may differ."""
+def shard_sizes(n_local: int, t_local: int, group=None,
+                device: torch.device = torch.device('cpu')):
+    """ONE all-gather of (rows, phoneme length) per rank -> (rows of every rank, global T)."""
     world = dist.get_world_size(group)
-    dev = _coll_device(group, t.device)
-    n = torch.tensor([t.size(0)], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
-    nmax = max(sizes)
+    dev = _coll_device(group, device)
+    mine = torch.tensor([int(n_local), int(t_local)], dtype=torch.int64, device=dev)
+    allv = torch.empty(world * 2, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allv, mine, group=group)
+    v = allv.view(world, 2).tolist()
+    return [r[0] for r in v], max(r[1] for r in v)
+
+
+def _padded(t: torch.Tensor, nmax: int, dev) -> torch.Tensor:
     src = t.to(dev).contiguous()
     if src.size(0) < nmax:
         pad = torch.zeros((nmax - src.size(0),) + tuple(src.shape[1:]), dtype=src.dtype, device=dev)
         src = torch.cat([src, pad], 0)
+    return src
+
+
+def gather_rows(t: torch.Tensor, group=None, sizes: Optional[List[int]] = None) -> torch.Tensor:
+    """All-gather along dim 0 with per-rank row counts that may differ (`sizes`: known
+    counts, e.g. from shard_sizes; otherwise one extra all-gather finds them)."""
+    world = dist.get_world_size(group)
+    dev = _coll_device(group, t.device)
+    if sizes is None:
+        sizes, _ = shard_sizes(t.size(0), 0, group, t.device)
+    src = _padded(t, max(sizes), dev)
     bufs = [torch.empty_like(src) for _ in range(world)]
     dist.all_gather(bufs, src, group=group)
+    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0).to(t.device)
+
+
+def gather_rows_to(t: torch.Tensor, sizes: List[int], dst: int = 0, group=None) -> Optional[torch.Tensor]:
+    """Gather along dim 0 to rank `dst` only (result collection: one copy of the output,
+    not one per rank); returns the concatenation on `dst`, None elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = _coll_device(group, t.device)
+    src = _padded(t, max(sizes), dev)
+    bufs = [torch.empty_like(src) for _ in range(world)] if rank == dst else None
+    dist.gather(src, bufs, dst=dst, group=group)
+    if rank != dst:
+        return None
     return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0).to(t.device)
 
 
@@ -95,41 +124,65 @@ class GlobalBatch:
         return global_max(local, self.group, totals.device)
 
     def status(self, word: torch.Tensor) -> torch.Tensor:
-        """The f16x3 range-guard word (ops.run_checked) combined over ranks (MAX: non-zero
-        anywhere -> non-zero everywhere), so every rank takes the same rerun decision."""
+        """The status word (ops.run_checked) OR-ed over ranks — one MAX all-reduce of its
+        bits — so every rank takes the same rerun / raise decision."""
         dev = _coll_device(self.group, word.device)
-        h = word.clone() if dev == word.device else word.to(dev)
-        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=self.group)
-        return h
+        w = word.to(dev).reshape(1)
+        bits = torch.cat([(w >> i) & 1 for i in range(3)])
+        dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=self.group)
+        return (bits << torch.arange(3, device=dev, dtype=bits.dtype)).sum().reshape(1).to(word.device)
 
 
 def broadcast_state(model: torch.nn.Module, src: int = 0, group=None) -> None:
-    """Copy rank `src`'s parameters and buffers to every rank (one broadcast per tensor)."""
-    for t in list(model.parameters()) + list(model.buffers()):
-        dev = _coll_device(group, t.device)
-        h = t.data if t.device == dev else t.data.to(dev)
-        dist.broadcast(h, src=src, group=group)
-        if h is not t.data:
-            t.data.copy_(h)
+    """Copy rank `src`'s parameters and buffers to every rank: the tensors are packed into
+    ONE flat buffer per dtype (98 MB fp32 for ForwardTacotron) and broadcast in one
+    collective each (RCCL over xGMI with the nccl backend: one large transfer instead of
+    ~330 small ones), then unpacked in place (so the packed-weight caches see new
+    versions and re-pack)."""
+    tensors = list(model.parameters()) + list(model.buffers())
+    by_dtype = {}
+    for t in tensors:
+        by_dtype.setdefault(t.dtype, []).append(t)
+    for dt, ts in by_dtype.items():
+        dev = _coll_device(group, ts[0].device)
+        flat = torch.cat([t.detach().reshape(-1).to(dev) for t in ts])
+        dist.broadcast(flat, src=src, group=group)
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n
 
 
 def generate_sharded(model, x: torch.Tensor, alpha: float = 1.0,
                      pitch_function: Callable = lambda p: p,
                      energy_function: Callable = lambda e: e,
-                     group=None, gather: bool = True) -> Dict[str, torch.Tensor]:
+                     group=None, gather='all') -> Optional[Dict[str, torch.Tensor]]:
     """This rank's shard x (B_local, t) of one global batch -> the reference's output for the
-    whole batch (gather=True: every rank holds all rows, in rank order) or this rank's rows
-    of it (gather=False).  ForwardTacotron and FastPitch."""
-    T = global_max(x.size(1), group, x.device)
+    whole batch.  gather: 'all' (or True) = every rank holds all rows, in rank order;
+    'rank0' = result collection on rank 0 only (other ranks return None); 'none' (or False)
+    = this rank's rows of it.  Shard sizes and the global phoneme length come from one
+    all-gather at the start.  ForwardTacotron and FastPitch."""
+    if gather is True:
+        gather = 'all'
+    elif gather is False:
+        gather = 'none'
+    sizes, T = shard_sizes(x.size(0), x.size(1), group, x.device)
     x = pad_tokens(x, T)
     out = model.generate(x, alpha, pitch_function, energy_function, batch=GlobalBatch(group))
-    if not gather:
+    if gather == 'none':
         return out
     res = {}
     for k, v in out.items():
         if k == 'mel_post' and out['mel_post'] is out['mel']:
             continue
-        res[k] = gather_rows(v, group)
+        if gather == 'rank0':
+            res[k] = gather_rows_to(v, sizes, 0, group)
+        else:
+            res[k] = gather_rows(v, group, sizes)
+    if gather == 'rank0' and dist.get_rank(group) != 0:
+        return None
     if 'mel_post' not in res:
         res['mel_post'] = res['mel']
     return res

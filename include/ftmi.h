@@ -49,8 +49,22 @@ enum {
  *                    bit 0 of *status (optional) is set — recompute on FTMI_MMA_F32. */
 enum { FTMI_MMA_F32 = 0, FTMI_MMA_BF16X6 = 1, FTMI_MMA_F16X3 = 2 };
 
+/* Bits of the optional device status word (uint32_t *status) the kernels OR into; the
+ * caller zeroes it, runs, and reads it once after the stream completed:
+ *   FTMI_STATUS_F16_RANGE    an f16x3 GEMM saw an activation beyond the f16 range (its
+ *                            output is invalid: recompute on FTMI_MMA_F32)
+ *   FTMI_STATUS_WHH_RANGE    a recurrence's W_hh entry is beyond the f16 range (idem)
+ *   FTMI_STATUS_RNN_TIMEOUT  a recurrence workgroup gave up waiting for its group (not all
+ *                            workgroups co-resident): the output is invalid — an error,
+ *                            not a precision event */
+enum { FTMI_STATUS_F16_RANGE = 1, FTMI_STATUS_WHH_RANGE = 2, FTMI_STATUS_RNN_TIMEOUT = 4 };
+
 /* ABI version; bumped on any signature change. */
 int ftmi_abi_version(void);
+/* sha256 (hex) of the sources this library was built from (csrc/*.hip, csrc/*.h,
+ * include/ftmi.h): the Python binding refuses a library whose id differs from the
+ * sources next to it (a stale prebuilt binary). */
+const char *ftmi_build_id(void);
 /* Static string for an error code (FTMI_E_* or hipError_t). */
 const char *ftmi_strerror(int code);
 
@@ -196,11 +210,20 @@ int ftmi_highway_split(const float *x, int64_t x_stride, int64_t M, int32_t C,
  * sync: 16-byte aligned device workspace of ftmi_rnn_workspace_bytes() bytes (zeroed by
  *     the call; holds the arrival counters and the h exchange buffer).  After the stream
  *     has completed, the 32-bit word at byte offset ftmi_rnn_error_offset() is non-zero if
- *     a workgroup timed out waiting for its group (not all workgroups resident).
+ *     a workgroup timed out waiting for its group (not all workgroups resident); the same
+ *     event sets FTMI_STATUS_RNN_TIMEOUT in *status.
  * Supported H: GRU 64, 128, 256; LSTM 512 (the ForwardTacotron config).
  * ---------------------------------------------------------------------------------- */
 int64_t ftmi_rnn_workspace_bytes(int32_t B, int32_t H, int32_t cell);
 int64_t ftmi_rnn_error_offset(int32_t B);
+/* Workgroups the (first) launch of ftmi_rnn_bidir(cell, B, H, mma) occupies: each is
+ * persistent (one per CU) and waits on the others, so recurrences issued concurrently on
+ * several streams must not exceed the CU count together (the host serialises them
+ * otherwise).  0 for an unsupported shape. */
+int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t mma);
+/* Test / diagnostic hook: bound of every recurrence spin (polls per wait) for launches
+ * issued after the call; 0 restores the default (2^22).  Returns the previous bound. */
+uint32_t ftmi_set_rnn_spin_limit(uint32_t limit);
 int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, const float *xp,
                    int64_t xp_stride, int32_t T_src, const int32_t *index,
                    const float *xp_zero, const float *w_hh, const float *b_hh,

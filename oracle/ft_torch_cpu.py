@@ -24,8 +24,13 @@ def _t(sd, k):
     return v if isinstance(v, torch.Tensor) else torch.from_numpy(v)
 
 
-def to_torch(sd) -> Dict[str, torch.Tensor]:
-    return {k: _t(sd, k).cpu() for k in sd}
+def to_torch(sd, dtype=None) -> Dict[str, torch.Tensor]:
+    """{key: CPU tensor}; dtype (e.g. torch.float64: the higher-precision truth of the
+    accuracy tests) converts the floating-point entries."""
+    out = {k: _t(sd, k).cpu() for k in sd}
+    if dtype is not None:
+        out = {k: v.to(dtype) if v.is_floating_point() else v for k, v in out.items()}
+    return out
 
 
 def batch_norm_conv(sd, pre, x, relu):
@@ -46,14 +51,14 @@ def _rnn_params(sd, pre):
 def gru(sd, pre, x):
     """nn.GRU(batch_first, bidirectional) forward == torch.gru (common_layers.py:84)."""
     H = sd[pre + '.weight_hh_l0'].shape[1]
-    h0 = torch.zeros(2, x.shape[0], H)
+    h0 = torch.zeros(2, x.shape[0], H, dtype=x.dtype)
     return torch.gru(x, h0, _rnn_params(sd, pre), True, 1, 0.0, False, True, True)[0]
 
 
 def lstm(sd, pre, x):
     """nn.LSTM(batch_first, bidirectional) forward == torch.lstm (forward_tacotron.py:165)."""
     H = sd[pre + '.weight_hh_l0'].shape[1]
-    z = torch.zeros(2, x.shape[0], H)
+    z = torch.zeros(2, x.shape[0], H, dtype=x.dtype)
     return torch.lstm(x, (z, z), _rnn_params(sd, pre), True, 1, 0.0, False, True, True)[0]
 
 
@@ -100,8 +105,10 @@ def _k(sd, pre):
 
 def generate(sd, ids: torch.Tensor, alpha: float = 1.0,
              pitch_function: Callable = lambda x: x, energy_function: Callable = lambda x: x,
-             pitch_strength: float = 1.0, energy_strength: float = 1.0):
-    """ForwardTacotron.generate (forward_tacotron.py:244-330)."""
+             pitch_strength: float = 1.0, energy_strength: float = 1.0, lr_dur=None):
+    """ForwardTacotron.generate (forward_tacotron.py:244-330).  lr_dur (accuracy tests
+    only): durations for the LengthRegulator in place of the computed ones, so a float64
+    run follows the fp32 reference's frame counts."""
     with torch.no_grad():
         dur = series_predictor(sd, 'dur_pred', ids, alpha).squeeze(2)
         if torch.sum(dur.long()) <= 0:
@@ -112,7 +119,7 @@ def generate(sd, ids: torch.Tensor, alpha: float = 1.0,
         x = cbhg(sd, 'prenet', x, _k(sd, 'prenet'))
         x = x + F.conv1d(pitch, sd['pitch_proj.weight'], sd['pitch_proj.bias'], padding=1).transpose(1, 2) * pitch_strength
         x = x + F.conv1d(energy, sd['energy_proj.weight'], sd['energy_proj.bias'], padding=1).transpose(1, 2) * energy_strength
-        x = length_regulator(x, dur)
+        x = length_regulator(x, dur if lr_dur is None else lr_dur.clone().to(dur.dtype))
         x = lstm(sd, 'lstm', x)
         x = F.linear(x, sd['lin.weight'], sd['lin.bias']).transpose(1, 2)
         x_post = cbhg(sd, 'postnet', x, _k(sd, 'postnet'))

@@ -41,12 +41,17 @@ def golden_meta():
     return json.loads((GOLDEN / 'goldens.json').read_text())
 
 
+def synth_sd_dict(seed: int = 0):
+    """Synthetic weights as {reference key: np.ndarray}, from the key fixture."""
+    from forwardtacotron_amd.synthetic import synthetic_array
+    keys = json.loads((GOLDEN / 'state_dict_keys.json').read_text())
+    return {k: synthetic_array(k, shape, dt, seed) for k, shape, dt in keys}
+
+
 @pytest.fixture(scope='session')
 def synth_sd():
     """Synthetic weights (seed 0) as {reference key: np.ndarray}, from the key fixture."""
-    from forwardtacotron_amd.synthetic import synthetic_array
-    keys = json.loads((GOLDEN / 'state_dict_keys.json').read_text())
-    return {k: synthetic_array(k, shape, dt, 0) for k, shape, dt in keys}
+    return synth_sd_dict(0)
 
 
 @pytest.fixture(scope='session')

@@ -15,7 +15,7 @@ from oracle import ft_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-MEAN_TOL, MAX_TOL = 1e-4, 2e-3
+MEAN_TOL, MAX_TOL = 1e-4, 2e-3  # tightened below where tests/test_gpu_accuracy.py allows
 
 
 def check(out, g, mean_tol=MEAN_TOL, max_tol=MAX_TOL):
@@ -71,12 +71,32 @@ def test_forward_teacher_forced(gpu_model):
     for k in ('dur', 'pitch', 'energy'):
         np.testing.assert_allclose(out[k].squeeze().cpu().numpy(), g[k].squeeze(), atol=1e-5)
     mel = out['mel'].cpu().numpy()
-    assert np.abs(mel - g['mel']).max() / np.abs(g['mel']).max() < 2e-6
-    # ill-conditioned padded frames, see tests/test_oracle.py::test_numpy_oracle_forward
-    d = np.abs(out['mel_post'].cpu().numpy() - g['mel_post'])
-    assert d.max() < 0.1 and d.mean() < 2e-3
-    T_pack = int(g['mel_len'].max())
+    post = out['mel_post'].cpu().numpy()
+    lens = g['mel_len']
+    T_pack = int(lens.max())
     assert np.all(mel[:, :, T_pack:] == np.float32(-11.5129))
+    # VALID frames of mel (before the postnet): the north-star bar, against the reference
+    for b, L in enumerate(lens):
+        d = np.abs(mel[b, :, :L] - g['mel'][b, :, :L])
+        assert d.max() < 1e-4, (b, d.max())
+    # mel_post mixes every frame of an item through the postnet's conv bank and its reverse
+    # GRU: the padded frames (lin(-11.5129) ~ O(850) under random weights, an ill-
+    # conditioned input) reach the valid ones.  The bar there is the fp32 reference's own
+    # distance to the float64 truth (tests/test_oracle.py::test_forward_fp64_conditioning:
+    # up to 0.013 on valid frames of a padded item): the HIP path must be no further from
+    # the fp64 oracle than 4x that (+1e-4); the unpadded item is held to 1e-4.
+    from conftest import synth_sd_dict
+    truth = O.forward(synth_sd_dict(), {'x': g['x'], 'mel': g['mel_in'], 'mel_len': g['mel_len'],
+                                        'dur': g['dur_in'], 'pitch': g['pitch_in'],
+                                        'energy': g['energy_in']}, np.float64)['mel_post']
+    for b, L in enumerate(lens):
+        e_ref = np.abs(g['mel_post'][b, :, :L] - truth[b, :, :L]).max()
+        e_gpu = np.abs(post[b, :, :L] - truth[b, :, :L]).max()
+        assert e_gpu <= 4 * e_ref + 1e-4, (b, e_gpu, e_ref)
+        if L == lens.max():  # the longest item: one padded frame (collate_tts pads +1)
+            assert np.abs(post[b] - g['mel_post'][b]).max() < 1e-4
+    e_ref = np.abs(g['mel_post'] - truth).max()
+    assert np.abs(post - truth).max() <= 4 * e_ref + 1e-4
 
 
 def test_length_regulator_layer_api(gpu_model):
@@ -132,10 +152,16 @@ def test_baseline_size_vs_torch_cpu(gpu_model, synth_sd):
         assert d.mean() < MEAN_TOL and d.max() < 5e-3, (k, d.mean(), d.max())
 
 
+def _fresh_graphs(model):
+    for k in ('_ftmi_graphs', '_ftmi_graph_seen'):
+        model.__dict__.pop(k, None)
+
+
 def test_graph_phase_matches_eager(gpu_model, monkeypatch):
-    """generate() with the default callbacks replays the phoneme phase as a HIP graph:
-    results identical (bit for bit) to the eager phase, across replays with new tokens of
-    the same shape, and the returned dur / pitch / energy are not the graph's buffers."""
+    """generate() replays the phoneme phase as a HIP graph (captured on the second call of a
+    shape): results identical (bit for bit) to the eager phase, across replays with new
+    tokens of the same shape, and the returned dur / pitch / energy are not the graph's
+    buffers."""
     from forwardtacotron_amd import forward_tacotron as FT
     g = load_golden('gen_b3')
     x1 = torch.from_numpy(g['x']).cuda()
@@ -144,10 +170,89 @@ def test_graph_phase_matches_eager(gpu_model, monkeypatch):
     monkeypatch.setattr(FT, 'GRAPH', False)
     eager = [gpu_model.generate(x) for x in (x1, x2)]
     monkeypatch.setattr(FT, 'GRAPH', True)
-    graph = [gpu_model.generate(x) for x in (x1, x2, x1)]
-    assert graph[0]['dur'].data_ptr() != graph[2]['dur'].data_ptr()
-    for e, gr in ((eager[0], graph[0]), (eager[1], graph[1]), (eager[0], graph[2])):
+    _fresh_graphs(gpu_model)
+    graph = [gpu_model.generate(x) for x in (x1, x2, x1, x2)]  # eager, capture, replay x2
+    assert len(gpu_model.__dict__['_ftmi_graphs']) == 1
+    assert graph[1]['dur'].data_ptr() != graph[3]['dur'].data_ptr()
+    for e, gr in ((eager[0], graph[0]), (eager[1], graph[1]), (eager[0], graph[2]),
+                  (eager[1], graph[3])):
         for k in ('mel', 'mel_post', 'dur', 'pitch', 'energy'):
             assert torch.equal(e[k], gr[k]), k
-    # the first result survived the later replays untouched
-    assert torch.equal(graph[0]['dur'], eager[0]['dur'])
+    # the earlier results survived the later replays untouched
+    assert torch.equal(graph[1]['dur'], eager[1]['dur'])
+    assert torch.equal(graph[2]['mel_post'], eager[0]['mel_post'])
+
+
+def test_graph_with_user_callbacks(gpu_model, monkeypatch):
+    """gen_forward.py-style callbacks (the same lambda objects on every call) are captured
+    with the phase and replay bit-identically to the eager phase."""
+    from forwardtacotron_amd import forward_tacotron as FT
+    g = load_golden('gen_callbacks')
+    x = torch.from_numpy(g['x']).cuda()
+    kw = dict(alpha=1.2, pitch_function=lambda p: p * 2.0 + 0.1, energy_function=lambda e: e - 0.05)
+    monkeypatch.setattr(FT, 'GRAPH', False)
+    eager = gpu_model.generate(x, **kw)
+    monkeypatch.setattr(FT, 'GRAPH', True)
+    _fresh_graphs(gpu_model)
+    outs = [gpu_model.generate(x, **kw) for _ in range(3)]
+    assert len(gpu_model.__dict__['_ftmi_graphs']) == 1
+    for o in outs:
+        for k in ('mel', 'mel_post', 'dur', 'pitch', 'energy'):
+            assert torch.equal(o[k], eager[k]), k
+    check(outs[-1], g)
+
+
+def test_graph_sees_new_weights(gpu_model, synth_sd, monkeypatch):
+    """a captured phase must not replay stale weights.  Capture, load a
+    different state_dict, generate again: the result equals the eager path with the new
+    weights (the stale replay is detected and discarded); restoring the old weights gives
+    the old result again."""
+    from forwardtacotron_amd import forward_tacotron as FT
+    from forwardtacotron_amd.synthetic import synthetic_array
+    g = load_golden('gen_b3')
+    x = torch.from_numpy(g['x']).cuda()
+    monkeypatch.setattr(FT, 'GRAPH', True)
+    _fresh_graphs(gpu_model)
+    a = [gpu_model.generate(x) for _ in range(3)]  # eager, capture, replay
+    other = {k: torch.from_numpy(np.asarray(synthetic_array(k, v.shape, str(v.dtype), 1)))
+             for k, v in synth_sd.items()}
+    try:
+        gpu_model.load_state_dict(other)
+        b = gpu_model.generate(x)
+        monkeypatch.setattr(FT, 'GRAPH', False)
+        b_eager = gpu_model.generate(x)
+        monkeypatch.setattr(FT, 'GRAPH', True)
+        for k in ('mel_post', 'dur', 'pitch'):
+            assert torch.equal(b[k], b_eager[k]), k
+        assert not torch.equal(b['dur'], a[0]['dur'])
+        # in-place update of one predictor weight (no load_state_dict): also seen
+        c0 = gpu_model.generate(x)
+        with torch.no_grad():
+            gpu_model.pitch_pred.lin.weight.mul_(0.5)
+        c1 = gpu_model.generate(x)
+        assert not torch.equal(c0['pitch'], c1['pitch'])
+    finally:
+        gpu_model.load_state_dict({k: torch.from_numpy(v) for k, v in synth_sd.items()})
+    d = gpu_model.generate(x)
+    assert torch.equal(d['mel_post'], a[0]['mel_post'])
+
+
+def test_recurrence_timeout_raises(gpu_model, monkeypatch):
+    """a recurrence workgroup that gives up waiting must fail the call
+    (ops.RnnTimeout), not return garbage with status 0.  A spin bound of 1 poll forces
+    the timeout path; every workgroup still leaves (bounded spins), and the next call with
+    the default bound is correct again."""
+    from forwardtacotron_amd import _lib, ops
+    from forwardtacotron_amd import forward_tacotron as FT
+    g = load_golden('gen_b3')
+    x = torch.from_numpy(g['x']).cuda()
+    monkeypatch.setattr(FT, 'GRAPH', False)
+    lib = _lib.load()
+    lib.ftmi_set_rnn_spin_limit(1)
+    try:
+        with pytest.raises(ops.RnnTimeout):
+            gpu_model.generate(x)
+    finally:
+        lib.ftmi_set_rnn_spin_limit(0)
+    torch.cuda.synchronize()
+    check(gpu_model.generate(x), g)

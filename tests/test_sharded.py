@@ -58,6 +58,61 @@ def test_collective_helpers_gloo():
     mp.spawn(_collectives, args=(2, _port()), nprocs=2, join=True)
 
 
+def _result_collection(rank, world, port):
+    from forwardtacotron_amd import sharded as S
+    _init(rank, world, port)
+    try:
+        # one all-gather gives every rank's rows and the global phoneme length
+        sizes, T = S.shard_sizes(3 - rank, 7 + 5 * rank)
+        assert sizes == [3, 2] and T == 12
+        rows = torch.arange((3 - rank) * 4, dtype=torch.float32).reshape(3 - rank, 4) + 100 * rank
+        ref = torch.cat([torch.arange(12.).reshape(3, 4), torch.arange(8.).reshape(2, 4) + 100])
+        assert torch.equal(S.gather_rows(rows, sizes=sizes), ref)
+        g = S.gather_rows_to(rows, sizes, dst=0)  # result collection on rank 0 only
+        if rank == 0:
+            assert torch.equal(g, ref)
+        else:
+            assert g is None
+        # the status word is OR-ed over ranks bit by bit (a timeout on one rank and a range
+        # event on the other -> both bits everywhere)
+        w = torch.tensor([4 if rank == 0 else 1], dtype=torch.int32)
+        assert int(S.GlobalBatch().status(w)) == 5
+    finally:
+        dist.destroy_process_group()
+
+
+def test_result_collection_gloo():
+    mp.spawn(_result_collection, args=(2, _port()), nprocs=2, join=True)
+
+
+def _broadcast(rank, world, port):
+    """broadcast_state: rank 1's model (different init) ends up identical to rank 0's,
+    every parameter and buffer, and its packed-weight caches see the new values."""
+    from forwardtacotron_amd import sharded as S
+    from forwardtacotron_amd.forward_tacotron import ForwardTacotron
+    from forwardtacotron_amd.synthetic import default_config, load_synthetic
+    _init(rank, world, port)
+    try:
+        m = ForwardTacotron.from_config(default_config())
+        if rank == 0:
+            load_synthetic(m, 0)
+        versions = [t._version for t in m.parameters()]
+        S.broadcast_state(m)
+        sd = {k: v.clone() for k, v in m.state_dict().items()}
+        if rank == 1:
+            assert all(t._version > v for t, v in zip(m.parameters(), versions))
+        ref = ForwardTacotron.from_config(default_config())
+        load_synthetic(ref, 0)
+        for k, v in ref.state_dict().items():
+            assert torch.equal(sd[k], v), k
+    finally:
+        dist.destroy_process_group()
+
+
+def test_broadcast_state_gloo():
+    mp.spawn(_broadcast, args=(2, _port()), nprocs=2, join=True)
+
+
 def _oracle_protocol(rank, world, port, alpha, out_path):
     """Each rank runs the numpy oracle on its shard with the globally decided quantities."""
     import json
