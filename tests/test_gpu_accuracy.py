@@ -24,8 +24,11 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # |path - fp64| <= FACTOR * |fp32 reference - fp64| (+ FLOOR, an absolute allowance of a
-# few fp32 ulps of |mel| ~ 5 for where the fp32 reference happens to be exact)
-MEAN_FACTOR, MAX_FACTOR = 2.0, 4.0
+# few fp32 ulps of |mel| ~ 5 for where the fp32 reference happens to be exact).
+# Measured (round 2, mel_post, c3): fp32 reference mean 1.05e-5 / max 1.23e-4; default
+# f16x3 path 1.03e-5 / 9.4e-5 (no worse than fp32); exact fp32-MFMA path 1.84e-5 / 1.80e-4
+# (c2: 1.53e-5 / 1.02e-4 against 7.1e-6 / 4.9e-5) — a different summation order.
+FACTORS = {'default': (1.5, 2.0), 'exact_fp32_mfma': (3.0, 3.0)}  # (mean, max)
 FLOOR = 2e-6
 
 
@@ -80,8 +83,9 @@ def test_accuracy_vs_fp64(cfg, gpu_model, synth_sd):
         e_ref = stats[k]['fp32_reference']
         for name in outs:
             e = stats[k][name]
-            assert e['mean'] <= MEAN_FACTOR * e_ref['mean'] + FLOOR, (k, name, e, e_ref)
-            assert e['max'] <= MAX_FACTOR * e_ref['max'] + FLOOR, (k, name, e, e_ref)
+            f_mean, f_max = FACTORS[name]
+            assert e['mean'] <= f_mean * e_ref['mean'] + FLOOR, (k, name, e, e_ref)
+            assert e['max'] <= f_max * e_ref['max'] + FLOOR, (k, name, e, e_ref)
 
 
 def test_c2_as_gen_forward_calls_it(gpu_model, synth_sd):
@@ -106,7 +110,7 @@ def test_c2_as_gen_forward_calls_it(gpu_model, synth_sd):
         assert m.shape == ref['mel_post'].shape
         d = np.abs(m.numpy() - ref['mel_post'].numpy())
         stats.append({'mean': float(d.mean()), 'max': float(d.max())})
-        assert d.mean() < 1e-4 and d.max() < 2e-3, stats[-1]
+        assert d.mean() < 1e-4 and d.max() < 5e-4, stats[-1]
         assert np.array_equal(O.duration_counts(out['dur'].cpu().numpy()),
                               O.duration_counts(ref['dur'].numpy()))
         np.testing.assert_allclose(out['pitch'].cpu().numpy(), ref['pitch'].numpy(), atol=1e-5)
@@ -134,4 +138,4 @@ def test_c5_fastpitch_full_size():
     assert got.shape == r.shape
     d = np.abs(got - r)
     _record('c5', {'T_mel': int(r.shape[2]), 'mel_mean': float(d.mean()), 'mel_max': float(d.max())})
-    assert d.mean() < 1e-4 and d.max() < 2e-3
+    assert d.mean() < 1e-4 and d.max() < 5e-4

@@ -15,7 +15,9 @@ from oracle import ft_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-MEAN_TOL, MAX_TOL = 1e-4, 2e-3  # tightened below where tests/test_gpu_accuracy.py allows
+# max: the GPU path and the fp32 reference are each ~1e-4 from the float64 truth at c3
+# (tests/test_gpu_accuracy.py), so they can differ by ~2e-4; 5e-4 leaves 2.5x margin.
+MEAN_TOL, MAX_TOL = 1e-4, 5e-4
 
 
 def check(out, g, mean_tol=MEAN_TOL, max_tol=MAX_TOL):
@@ -149,7 +151,7 @@ def test_baseline_size_vs_torch_cpu(gpu_model, synth_sd):
         a, b = out[k].cpu().numpy(), ref[k].numpy()
         assert a.shape == b.shape
         d = np.abs(a - b)
-        assert d.mean() < MEAN_TOL and d.max() < 5e-3, (k, d.mean(), d.max())
+        assert d.mean() < MEAN_TOL and d.max() < MAX_TOL, (k, d.mean(), d.max())
 
 
 def _fresh_graphs(model):
