@@ -61,9 +61,9 @@ enum { FTMI_STATUS_F16_RANGE = 1, FTMI_STATUS_WHH_RANGE = 2, FTMI_STATUS_RNN_TIM
 
 /* ABI version; bumped on any signature change. */
 int ftmi_abi_version(void);
-/* sha256 (hex) of the sources this library was built from (csrc/*.hip, csrc/*.h,
- * include/ftmi.h): the Python binding refuses a library whose id differs from the
- * sources next to it (a stale prebuilt binary). */
+/* sha256 (hex) of the sources this library was built from (the .hip and .h files of
+ * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
+ * id differs from the sources next to it (a stale prebuilt binary). */
 const char *ftmi_build_id(void);
 /* Static string for an error code (FTMI_E_* or hipError_t). */
 const char *ftmi_strerror(int code);
