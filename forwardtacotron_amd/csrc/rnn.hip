@@ -592,14 +592,24 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       const int soff = ((t - 1) & 1) * hx_par;
       // fp32 words carry the tag in bit 0; f16 pairs in bits 0 and 16 (both halves)
       const unsigned tmask = HSPLIT ? 0x00010001u : 1u;
-      const unsigned want = h_tag(t - 1) * tmask;
+      const bool want1 = h_tag(t - 1) != 0u;  // uniform
       for (unsigned spins = 0;; ++spins) {
-        bool fresh = true;
 #pragma unroll
-        for (int i = 0; i < NL; ++i) {
+        for (int i = 0; i < NL; ++i)
           hr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + i * 1024, soff, 16);
-          const u32x4 d = (hr[i] & tmask) ^ want;
-          fresh &= (d.x | d.y | d.z | d.w) == 0u;
+        // every tag equals want iff (want 1) the AND of all words has the tag bits set,
+        // (want 0) their OR has none: a 3-input reduction instead of a test per word
+        bool fresh;
+        if (want1) {
+          u32x4 a = hr[0];
+#pragma unroll
+          for (int i = 1; i < NL; ++i) a &= hr[i];
+          fresh = ((a.x & a.y & a.z & a.w) & tmask) == tmask;
+        } else {
+          u32x4 o = hr[0];
+#pragma unroll
+          for (int i = 1; i < NL; ++i) o |= hr[i];
+          fresh = ((o.x | o.y | o.z | o.w) & tmask) == 0u;
         }
         if (__all(fresh) || (p.diag & 2)) break;
         if (spins > p.spin_limit) {
@@ -798,304 +808,6 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 #endif
 }
 
-// ---- row-owning f16x3 recurrence (default for FTMI_MMA_F16X3) --------------------------
-// A 16-row block of W_hh = 4 hidden units x 4 gate slots (LSTM i, f, g, o; GRU r, z, n and
-// a zero slot), rows ordered unit-major, so the 16x16 MFMA output fragment of lane l holds
-// all gates of ONE cell (unit l / 16 of the block, sequence l % 16): the cell update runs
-// on the accumulator registers.  A workgroup = 4 waves = 4 row blocks = 16 units
-// (BPG = H / 16 workgroups per group).  Wave w = (pair w / 2, K half w % 2) multiplies the
-// pair's two row blocks by its half of h (f16x3: H / 64 k-steps x 2 blocks x 3 MFMAs, the
-// W_hh head / scaled-tail fragments in VGPRs for the whole sequence).  Its B operands are
-// the h_{t-1} fragments it polls itself — sc1 loads of its K half of the group's pre-split
-// exchange buffer (B-fragment order), re-issued until every half carries the tag of step
-// t - 1 — so no LDS sits between the hand-off and the MFMAs.  The two K halves meet
-// through LDS (one 16-B write and read per lane, one workgroup barrier: each wave
-// finishes one row block, low half + high half in that order on both sides); the wave
-// then applies the cell update and publishes its 4 units x 16 sequences of h_t (f16 head
-// / scaled tail, step-tagged, 8-B stores after an in-wave LDS transpose) and y_t.
-template <int CELL, int H>
-__global__ __launch_bounds__(256, 1) void rnn_rows_kernel(const RnnParams p) {
-  constexpr int G = CELL ? 4 : 3;
-  constexpr int KS = H / 32;   // k-steps of W_hh h
-  constexpr int KSH = KS / 2;  // k-steps per K half
-  constexpr int UW = 4;        // units per row block
-  constexpr int U = 4 * UW;    // units per workgroup
-  constexpr int BPG = H / U;   // workgroups per group
-  constexpr int CHW = 2 * KSH; // 1-KB chunks a wave polls (its k-steps x {head, tail})
-  static_assert(H % 64 == 0 && KSH >= 1, "shape");
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-
-  __shared__ __attribute__((aligned(16))) f32x4 red[2][4][64];               // parity, wave, lane
-  __shared__ __attribute__((aligned(16))) unsigned short hst[4][2][16][UW];  // wave, plane, seq, unit
-  __shared__ __attribute__((aligned(16))) float yst[4][16][UW];             // wave, seq, unit
-  __shared__ int s_abort, s_group, s_bi, s_mode;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ls = lane >> 4, lc = lane & 15;
-  const int pr = wave >> 1, kh = wave & 1;
-
-  // ---- group assignment: the census of rnn_bidir_kernel ------------------------------
-  if (tid == 0) {
-    int mode = 0, group = blockIdx.x % p.ngroups, bi = blockIdx.x / p.ngroups, abort = 0;
-    if (p.xcd_local) {
-      const unsigned x = xcc_id();
-      const unsigned slot = __hip_atomic_fetch_add(p.ws + WS_CENSUS + x * CNT_PAD, 1u,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(p.ws + WS_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (!poll_ge(p.ws + WS_ARRIVE, gridDim.x, p.spin_limit)) {
-        abort = 1;
-        report_timeout(p);
-      } else if (p.ngroups % 8 == 0 || (int)gridDim.x == 8 * BPG) {
-        const int gpx = p.ngroups % 8 == 0 ? p.ngroups / 8 : 1;
-        const unsigned per = (unsigned)gpx * BPG;
-        bool balanced = true;
-        for (int i = 0; i < 8; ++i)
-          balanced &= __hip_atomic_load(p.ws + WS_CENSUS + i * CNT_PAD, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT) == per;
-        if (balanced) {
-          mode = 1;
-          group = (int)(x * gpx + slot / BPG);
-          bi = (int)(slot % BPG);
-        }
-      }
-    }
-    s_mode = mode;
-    s_group = group;
-    s_bi = bi;
-    s_abort = abort;
-  }
-  __syncthreads();
-  if (s_abort) return;
-  if (s_group >= p.ngroups || s_bi >= BPG) return;  // padded grid: surplus workgroups
-  const int group = s_group, bi = s_bi;
-  const bool xcd_mode = s_mode == 1;
-  const int dir = group & 1;
-  const int chunk = p.chunk0 + (group >> 1);
-  const int gglob = p.chunk0 * 2 + group;
-  const int u0w = bi * U + (2 * pr + kh) * UW;  // first unit of the row block this wave finishes
-
-  // ---- W_hh: the pair's two row blocks over this wave's K half -> A fragments ---------
-  // row m = lc of block r -> unit bi*U + (2 pr + r)*4 + m / 4, gate slot m % 4
-  const float *wdir = p.w_hh + (size_t)dir * (G * H) * H;
-  f16x8 wh[2][KSH][2];  // [block][k-step][head, scaled tail]
-  bool wbad = false;
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int gate = lc & 3, unit = bi * U + (2 * pr + r) * UW + (lc >> 2);
-    const bool live = gate < G;
-    const float *src = wdir + (size_t)(gate * H + unit) * H + kh * (H / 2) + 8 * ls;
-#pragma unroll
-    for (int j = 0; j < KSH; ++j) {
-      float v[8];
-      f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
-      if (live) {
-        a = *(const f32x4 *)(src + j * 32);
-        b = *(const f32x4 *)(src + j * 32 + 4);
-      }
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-      split2h8(v, wh[r][j][0], wh[r][j][1]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) wbad |= !(__builtin_fabsf(v[e]) <= 65504.f);
-    }
-  }
-  if (wbad && p.status) atomicOr(p.status, 2u);
-
-  // ---- this lane's cell: unit uc, sequence s ---------------------------------------
-  const int uc = u0w + ls, s = lc;
-  const int b = chunk * NB + s;
-  const bool bvalid = b < p.B;
-  const int bc = bvalid ? b : 0;
-  const int len = (p.lengths && bvalid) ? p.lengths[b] : p.T;
-  float bhh[3] = {0.f, 0.f, 0.f};
-  if (CELL == 0) {
-#pragma unroll
-    for (int g = 0; g < 3; ++g) bhh[g] = p.b_hh[dir * G * H + g * H + uc];
-  }
-  float hstate = 0.f, cstate = 0.f;
-
-  // ---- h exchange addressing ---------------------------------------------------------
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.hx, (short)0, 0x7FFFFFF0, 0x00020000);
-  const unsigned gbase = (unsigned)(gglob * 16 * H * 4);  // bytes: the group's 16 x H pairs
-  const int hx_par = p.ngroups_total * 16 * H * 4;        // bytes between the parity halves
-  const unsigned cbase = gbase + (unsigned)((kh * CHW * 64 + lane) * 16);  // this wave's chunks
-  // producer: lanes 0..31 store 8 B = 4 units (plane lane / 16, sequence lane % 16)
-  unsigned pofs;
-  {
-    const int pl = (lane >> 4) & 1, ps = lane & 15;
-    const int K = u0w / 32, q = u0w % 32;
-    const int L = (q >> 3) * 16 + ps;
-    pofs = gbase + (unsigned)((((K * 2 + pl) * 64 + L) * 16) + (q & 7) * 2);
-  }
-
-  // ---- input projections: 2 steps ahead through 3 register sets (as rnn_bidir_kernel) --
-  const int32_t *iptr = p.index ? p.index + (size_t)bc * p.T : (const int32_t *)p.ws;
-  const size_t brow = (size_t)bc * p.T_src;
-  const float *xcol = p.xp + dir * G * H + uc;
-  const float *zcol = (p.index ? p.xp_zero : p.xp) + dir * G * H + uc;
-  auto frame = [&](int t) { return dir ? (p.T - 1 - t) : t; };
-  auto load_idx = [&](int t) -> int {
-    const int tt = frame(t < p.T ? t : p.T - 1);
-    return iptr[p.index ? tt : 0];
-  };
-  auto load_gx = [&](int t, int ir, float (&g)[G]) {
-    const int tt = frame(t < p.T ? t : p.T - 1);
-    const int src = p.index ? ir : tt;
-    const float *row = src >= 0 ? xcol + (brow + src) * p.xp_stride : zcol;
-#pragma unroll
-    for (int gi = 0; gi < G; ++gi) g[gi] = row[gi * H];
-  };
-  float g0[G], g1[G], g2[G];
-  int i0 = load_idx(0), i1 = load_idx(1);
-  load_gx(0, i0, g0);
-  load_gx(1, i1, g1);
-  int i2 = load_idx(2);
-
-  auto step = [&](int t, const float (&gx)[G], float (&gnext)[G], int inext, int &iload) -> bool {
-    const int tt = frame(t);
-    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    if (t > 0) {
-      // ---- acquire h_{t-1}: this wave's K half, re-loaded until every half carries the
-      // tag of step t - 1; the loaded fragments ARE the MFMA B operands
-      const int soff = ((t - 1) & 1) * hx_par;
-      const unsigned want = h_tag(t - 1) * 0x00010001u;
-      u32x4 hr[CHW];
-      for (unsigned spins = 0;; ++spins) {
-        // a compiler memory barrier: the buffer loads below must be re-issued on every
-        // poll (nothing else in the loop writes memory, so they would be hoisted)
-        __asm__ volatile("" ::: "memory");
-        bool fresh = true;
-#pragma unroll
-        for (int i = 0; i < CHW; ++i) {
-          hr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, cbase + (unsigned)(i * 1024), soff, 16);
-          const u32x4 d = (hr[i] & 0x00010001u) ^ want;
-          fresh &= (d.x | d.y | d.z | d.w) == 0u;
-        }
-        if (__all(fresh) || (p.diag & 2)) break;
-        if (spins > p.spin_limit) {
-          if (lane == 0) {
-            s_abort = 1;
-            report_timeout(p);
-          }
-          break;
-        }
-      }
-      // ---- W_hh h_{t-1} over this K half for both blocks (f16x3) --------------------
-#pragma unroll
-      for (int j = 0; j < KSH; ++j) {
-        const f16x8 hh = __builtin_bit_cast(f16x8, hr[2 * j]);
-        const f16x8 ht = __builtin_bit_cast(f16x8, hr[2 * j + 1]);
-        const f16x8 hs = hh * (_Float16)H3_SCALE;  // 2^11 h_h: exact, |h| < 1
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[r][j][1], hh, acc[r], 0, 0, 0);
-          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[r][j][0], ht, acc[r], 0, 0, 0);
-          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[r][j][0], hs, acc[r], 0, 0, 0);
-        }
-      }
-    }
-    load_gx(t + 2, inext, gnext);
-    iload = load_idx(t + 3);
-    // ---- the K halves meet: hand the partner its block's partial, take ours -----------
-    red[t & 1][wave][lane] = kh ? acc[0] : acc[1];
-    __syncthreads();
-    const f32x4 other = red[t & 1][wave ^ 1][lane];
-    const int abort_now = s_abort;  // acted on after the cell: the call fails on the status bit
-    const f32x4 gsum = (kh ? other + acc[1] : acc[0] + other) * H3_UNSCALE;
-
-    // ---- cell update in registers (gsum[g] = gate g of unit uc, sequence s) -----------
-    float hn;
-    if (CELL == 0) {
-      // ATen GRU cell: r, z, n ; h' = n + z * (h - n)
-      const float r = fast_sigmoid(gx[0] + (gsum[0] + bhh[0]));
-      const float z = fast_sigmoid(gx[1] + (gsum[1] + bhh[1]));
-      const float n = fast_tanh(gx[2] + r * (gsum[2] + bhh[2]));
-      hn = n + z * (hstate - n);
-    } else {
-      const float ig = fast_sigmoid(gx[0] + gsum[0]);
-      const float fg = fast_sigmoid(gx[1] + gsum[1]);
-      const float gg = fast_tanh(gx[2] + gsum[2]);
-      const float og = fast_sigmoid(gx[3] + gsum[3]);
-      cstate = fg * cstate + ig * gg;
-      hn = og * fast_tanh(cstate);
-    }
-    if (tt >= len) {  // packed-sequence padding: the reverse direction restarts from zero
-      hn = 0.f;
-      cstate = 0.f;
-    }
-    hstate = hn;
-    const float yout = tt >= len ? p.pad_value : hn;
-    if (abort_now) return false;
-
-    // ---- publish: pre-split tagged h_t (f16 head, scaled tail; the tail taken after the
-    // head's tag bit is set) and y_t, transposed through this wave's LDS stage
-    const unsigned short tg = (unsigned short)h_tag(t);
-    const _Float16 h16 = __builtin_bit_cast(
-        _Float16, (unsigned short)((__builtin_bit_cast(unsigned short, (_Float16)hn) & 0xFFFEu) | tg));
-    const _Float16 t16 = __builtin_bit_cast(
-        _Float16, (unsigned short)((__builtin_bit_cast(unsigned short,
-                                                       (_Float16)((hn - (float)h16) * H3_SCALE)) &
-                                    0xFFFEu) | tg));
-    hst[wave][0][s][ls] = __builtin_bit_cast(unsigned short, h16);
-    hst[wave][1][s][ls] = __builtin_bit_cast(unsigned short, t16);
-    yst[wave][s][ls] = yout;
-    __builtin_amdgcn_wave_barrier();
-    if (lane < 32) {
-      const u32x2 v = *(const u32x2 *)&hst[wave][lane >> 4][lane & 15][0];
-      const int soff = (t & 1) * hx_par;
-      if (xcd_mode)  // stays in this XCD's L2, read back by same-XCD sc1 loads
-        __builtin_amdgcn_raw_buffer_store_b64(v, rsrc, pofs, soff, 0);
-      else  // write-through (sc1)
-        __builtin_amdgcn_raw_buffer_store_b64(v, rsrc, pofs, soff, 16);
-    } else if (lane < 48) {
-      const int ys = lane - 32, yb = chunk * NB + ys;
-      const f32x4 v = *(const f32x4 *)&yst[wave][ys][0];
-      if (yb < p.B) *(f32x4 *)(p.y + ((size_t)yb * p.T + tt) * p.y_stride + dir * H + u0w) = v;
-    }
-    return true;
-  };
-
-  for (int t = 0; t < p.T; t += 3) {
-    if (!step(t, g0, g2, i2, i0)) break;
-    if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1)) break;
-    if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2)) break;
-  }
-}
-
-template <int CELL, int H>
-int launch_rows(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
-  constexpr int BPG = H / 16;
-  int max_groups = (max_blocks / BPG) & ~1;
-  if (max_groups < 2) return FTMI_E_UNSUPPORTED;
-  for (int c0 = 0; c0 < nchunks; c0 += max_groups / 2) {
-    const int nc = (nchunks - c0) < max_groups / 2 ? (nchunks - c0) : max_groups / 2;
-    p.chunk0 = c0;
-    p.ngroups = 2 * nc;
-    if (c0 > 0) {
-      hipError_t e = hipMemsetAsync(p.ws + WS_CENSUS, 0, (WS_FLAGS - WS_CENSUS) * 4, s);
-      if (e != hipSuccess) return (int)e;
-    }
-    int nblk = p.ngroups * BPG;
-    if (BPG > 1 && p.xcd_local && p.ngroups < 8 && 8 * BPG <= max_blocks) nblk = 8 * BPG;
-    // one workgroup per CU: the static LDS is padded with dynamic LDS past half of the
-    // CU's 160 KB, so two of these workgroups never share a CU's matrix pipes (a doubled-up
-    // CU would set the whole group's step time)
-    static const size_t dyn = [] {
-      hipFuncAttributes a{};
-      size_t st = 0;
-      if (hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&rnn_rows_kernel<CELL, H>)) ==
-          hipSuccess)
-        st = a.sharedSizeBytes;
-      const size_t want = 81 * 1024;
-      return st < want ? want - st : (size_t)0;
-    }();
-    hipLaunchKernelGGL((rnn_rows_kernel<CELL, H>), dim3(nblk), dim3(256), dyn, s, p);
-    FTMI_CHECK_LAUNCH();
-  }
-  return FTMI_OK;
-}
-
 template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false>
 int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
   constexpr int BPG = H / U;
@@ -1139,15 +851,8 @@ int device_cu_count() {
 
 }  // namespace
 
-// FTMI_RNN_ROWS=0 selects the K-split kernel (rnn_bidir_kernel) for f16x3 as well
-static bool rows_enabled() {
-  const char *e = getenv("FTMI_RNN_ROWS");  // read per call: tests switch kernels in-process
-  return e ? atoi(e) != 0 : true;
-}
-
 // hidden units per workgroup of the instance ftmi_rnn_bidir dispatches (see there)
 static int rnn_units(int cell, int H, int mma) {
-  if (mma == 2 && rows_enabled() && (H == 64 || H == 128 || H == 256 || H == 512)) return 16;
   if (cell == 0 && H == 64) {
     static const int u64 = [] {
       const char *v = getenv("FTMI_RNN_U64");
@@ -1257,12 +962,6 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   p.index = index;
   p.xp_zero = xp_zero;
   const int maxb = device_cu_count();
-  if (mma == 2 && rows_enabled()) {  // the row-owning f16x3 kernel (default)
-    if (cell == 1 && H == 512) return launch_rows<1, 512>(p, nchunks, maxb, s);
-    if (cell == 0 && H == 256) return launch_rows<0, 256>(p, nchunks, maxb, s);
-    if (cell == 0 && H == 128) return launch_rows<0, 128>(p, nchunks, maxb, s);
-    if (cell == 0 && H == 64) return launch_rows<0, 64>(p, nchunks, maxb, s);
-  }
 #define FTMI_RNN_MODES(CELL_, H_, U_, WKX_, WKF_)                                   \
   switch (mma) {                                                                    \
     case 2: return launch_rnn<CELL_, H_, U_, WKX_, 2>(p, nchunks, maxb, s);          \

@@ -287,20 +287,17 @@ def test_lstm_bidir(rng, rnn_mma, monkeypatch):
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize('rows', ['1', '0'], ids=['rows', 'ksplit'])
 @pytest.mark.parametrize('cell,H,B,T', [('lstm', 512, 1, 23), ('lstm', 512, 17, 12),
                                         ('lstm', 512, 64, 9), ('gru', 256, 1, 31),
                                         ('gru', 256, 64, 7), ('gru', 256, 130, 5),
                                         ('gru', 128, 20, 14), ('gru', 64, 64, 11),
                                         ('gru', 64, 1, 40)])
-def test_rnn_f16x3_kernels(cell, H, B, T, rows, rng, monkeypatch):
-    """Both f16x3 recurrence kernels (FTMI_RNN_ROWS: the row-owning default, the K-split
-    form) over batch sizes that exercise one chunk (B = 1: padded grid, one group per
-    XCD), a partial chunk, whole XCDs (B = 64: 8 groups), several launches' worth of groups
-    (B = 130) — against the numpy oracle."""
+def test_rnn_f16x3_kernels(cell, H, B, T, rng, monkeypatch):
+    """The f16x3 recurrence over batch sizes that exercise one chunk (B = 1: padded grid,
+    one group per XCD), a partial chunk, whole XCDs (B = 64: 8 groups), several launches'
+    worth of groups (B = 130) — against the numpy oracle."""
     from forwardtacotron_amd import ops
     monkeypatch.setattr(ops, 'RNN_MMA', 2)
-    monkeypatch.setenv('FTMI_RNN_ROWS', rows)
     fin = 512 if cell == 'lstm' else 256
     m, sd = _rnn_module(cell, fin, H, rng)
     x = rng.normal(0, 1, (B, T, fin)).astype(np.float32)

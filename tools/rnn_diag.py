@@ -14,7 +14,8 @@ import sys, json, torch
 sys.path.insert(0, ".")
 from forwardtacotron_amd import ops
 res = {}
-for cell, H, B, T in [(1, 512, 64, 1368), (0, 256, 64, 1368), (0, 128, 64, 200), (0, 64, 64, 200)]:
+for cell, H, B, T in [(1, 512, 64, 1368), (0, 256, 64, 1368), (0, 128, 64, 200), (0, 64, 64, 200),
+                      (1, 512, 1, 816), (0, 256, 1, 816)]:
     G = 4 if cell else 3
     xp = torch.randn(B, T, 2 * G * H, device="cuda") * 0.5
     w = torch.randn(2, G * H, H, device="cuda") / H ** 0.5
@@ -28,19 +29,24 @@ for cell, H, B, T in [(1, 512, 64, 1368), (0, 256, 64, 1368), (0, 128, 64, 200),
     for _ in range(5):
         ops.rnn_bidir(cell, xp, H, w, bh if cell == 0 else None, ws=ws)
     e.record(); torch.cuda.synchronize()
-    res[f"{'lstm' if cell else 'gru'}{H}"] = s.elapsed_time(e) / 5 / T * 1e3
+    res[f"{'lstm' if cell else 'gru'}{H}b{B}"] = s.elapsed_time(e) / 5 / T * 1e3
 print(json.dumps(res))
 '''
 rows = {}
-VAR = os.environ.get('DIAG_VAR', 'FTMI_RNN_DIAG')
-VALS = os.environ.get('DIAG_VALS', '0 16 0 16').split()
-for diag in VALS:
-    env = {**os.environ, VAR: str(diag)}
+# variants: "VAR=val,VAR2=val2;..." (DIAG_ENVS) or the legacy single-variable sweep
+if os.environ.get('DIAG_ENVS'):
+    VARIANTS = [dict(kv.split('=') for kv in v.split(',') if kv) for v in os.environ['DIAG_ENVS'].split(';')]
+else:
+    VAR = os.environ.get('DIAG_VAR', 'FTMI_RNN_DIAG')
+    VARIANTS = [{VAR: v} for v in os.environ.get('DIAG_VALS', '0 16 0 16').split()]
+for var in VARIANTS:
+    diag = ','.join(f'{k}={v}' for k, v in var.items())
+    env = {**os.environ, **var}
     r = subprocess.run([sys.executable, '-c', CHILD], env=env, capture_output=True, text=True,
                        timeout=300)
     if r.returncode != 0:
         print('diag', diag, 'FAILED', r.stderr[-2000:])
         sys.exit(1)
     rows[diag] = json.loads(r.stdout.strip().splitlines()[-1])
-    print(f'{VAR}={diag}: ' + '  '.join(f'{k} {v:6.2f} us/step' for k, v in rows[diag].items()),
+    print(f'{diag}: ' + '  '.join(f'{k} {v:6.2f} us/step' for k, v in rows[diag].items()),
           flush=True)

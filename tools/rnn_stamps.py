@@ -9,7 +9,8 @@ lib = _lib.load()
 fn = lib.ftmi_debug_rnn_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
 PH = ['xp issue', 'poll wait', 'h load', 'mfma+lds', 'cell+store', 'drain+arrive']
-for cell, H, B, T in [(1, 512, 64, 1368), (0, 256, 64, 1368), (0, 128, 64, 200), (0, 64, 64, 200)]:
+for cell, H, B, T in [(1, 512, 64, 1368), (0, 256, 64, 1368), (0, 128, 64, 200), (0, 64, 64, 200),
+                      (1, 512, 1, 816)]:
     G = 4 if cell else 3
     xp = torch.randn(B, T, 2 * G * H, device='cuda') * 0.5
     w = torch.randn(2, G * H, H, device='cuda') / H ** 0.5
@@ -19,8 +20,8 @@ for cell, H, B, T in [(1, 512, 64, 1368), (0, 256, 64, 1368), (0, 128, 64, 200),
     torch.cuda.synchronize()
     t0 = time.perf_counter(); ops.rnn_bidir(cell, xp, H, w, bh if cell == 0 else None, check=True)
     dt = time.perf_counter() - t0
-    U = {512: 16, 256: 16, 128: 64, 64: 64}[H]
-    nb = 2 * ((B + 15) // 16) * (H // U)
+    U = {512: 16, 256: 16, 128: 16, 64: 32}[H]
+    nb = max(2 * ((B + 15) // 16) * (H // U), 8 * (H // U))
     buf = (ctypes.c_ulonglong * (nb * 8))()
     assert fn(buf, nb * 8) == 0
     a = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8)[:, :6].astype(np.float64)
