@@ -1443,6 +1443,9 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
 // chunks beyond the block's two go to other blocks (blockIdx.y): their raw partial sums land
 // in part[s][M][ldp] (output-column order) and skinny_finish_kernel adds them in split order
 // (deterministic) and applies the epilogue; with one split the wave finishes its columns.
+#ifndef SKINNY_PF
+#define SKINNY_PF 4
+#endif
 constexpr int SK_BM = 128;
 constexpr int SK_BN = 64;   // 4 column sets of 16 (x 2 step halves = 8 waves)
 constexpr int SK_CPB = 2;   // 32-channel chunks per block
@@ -1451,16 +1454,51 @@ constexpr int SK_ZROW = SK_SR;
 constexpr int SK_AIMG = (SK_SR + 1) * SL_P;  // halves per (chunk, plane) slab image
 constexpr int SK_MMAX = 256;
 constexpr int SK_MMAX_NARROW = 1024;
-constexpr int SK_PF = 4;    // weight-fragment prefetch depth (steps)
+constexpr int SK_PF = SKINNY_PF;  // weight-fragment prefetch depth (steps)
 
-template <bool MAXPOOL>
+// BANK = the balanced schedule of a CBHG conv bank (groups k = K .. 1 in g[0 .. K-1], equal
+// widths, K even): a block takes two 16-column sets of the group pair (k, K + 1 - k) — four
+// (group, column set) units — and the 8 waves pair them so that each SIMD runs one unit of
+// each group of the pair (waves w and w + 4 share a SIMD): every SIMD, and every block,
+// streams (K + 1) / 2 of the average weight bytes, instead of blocks of the k = K group
+// moving K times the bytes of the k = 1 group's.  The slab is the heavier group's (its halo
+// covers the lighter group's taps, read at a row offset).
+#ifdef FTMI_SKINNY_STAMPS
+// diagnostic build only: per-block s_memtime at phase boundaries (wave 0 and wave 7)
+__device__ unsigned long long ftmi_skinny_stamps[4096 * 8];
+#define SKSTAMP(i)                                                                         \
+  do {                                                                                     \
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x == 0 || threadIdx.x == 448)) {             \
+      __builtin_amdgcn_sched_barrier(0);                                                   \
+      ftmi_skinny_stamps[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (threadIdx.x ? 4 : 0) + \
+                         (i)] = __builtin_amdgcn_s_memtime();                              \
+      __builtin_amdgcn_sched_barrier(0);                                                   \
+    }                                                                                      \
+  } while (0)
+#else
+#define SKSTAMP(i) \
+  do {             \
+  } while (0)
+#endif
+
+template <bool MAXPOOL, bool BANK = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmParams p) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[SK_CPB * 2 * SK_AIMG];
+  SKSTAMP(0);
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const int MT = (p.M + SK_BM - 1) / SK_BM, NT = p.g[0].ntiles;
   // consecutive blocks: row tiles, then column blocks of the heaviest group first; a
   // compact grid, so consecutive blocks land on different XCDs
-  const int bid = blockIdx.x, mt = bid % MT, v = bid / MT, gi = v / NT, nt = v - gi * NT;
+  const int bid = blockIdx.x, mt = bid % MT, v = bid / MT;
+  int gi, nt;
+  if constexpr (BANK) {  // v = (pair, two column sets): pair-units 2v, 2v + 1
+    const int NC = p.g[0].N / 16;
+    gi = (2 * v) / NC;  // the pair's heavier group (k = K - gi)
+    nt = (2 * v) % NC;  // first of the block's two 16-column sets
+  } else {
+    gi = v / NT;
+    nt = v - gi * NT;
+  }
   const GemmGroup &G = p.g[gi];
   const int m0 = mt * SK_BM, k = G.k, pad = G.pad, Cin = p.Cin;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1511,18 +1549,33 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     *(u32x4 *)(lds + img * SK_AIMG + SK_ZROW * SL_P + part * 8) = (u32x4){0u, 0u, 0u, 0u};
   }
   __syncthreads();
+  SKSTAMP(1);
   bool bad = !(amax <= 65504.f);
 
   // 8 waves: wave w multiplies columns col0 + [0, 16) (column set w & 3) over one half of
-  // the steps (w >> 2); the two halves meet in LDS after the loop
-  const int cw = wave & 3, half = wave >> 2;
-  const int col0 = nt * SK_BN + cw * 16;  // this wave's 16 columns of group gi
-  const int nsteps = nch * k, hs = (nsteps + 1) / 2;
+  // the steps (w >> 2); the two halves meet in LDS after the loop.  BANK: unit slot cw =
+  // (group of the pair: w >> 2, column set: (w >> 1) & 1), half w & 1
+  int cw, half, gw, col0;
+  if constexpr (BANK) {
+    cw = ((wave >> 2) << 1) | ((wave >> 1) & 1);
+    half = wave & 1;
+    gw = (wave >> 2) ? p.ngroups - 1 - gi : gi;
+    col0 = (nt + ((wave >> 1) & 1)) * 16;
+  } else {
+    cw = wave & 3;
+    half = wave >> 2;
+    gw = gi;
+    col0 = nt * SK_BN + cw * 16;  // this wave's 16 columns of group gi
+  }
+  gw = __builtin_amdgcn_readfirstlane(gw);
+  const GemmGroup &GW = p.g[gw];
+  const int kw = GW.k, padw = GW.pad, dp = pad - padw;  // slab row offset of this group's taps
+  const int nsteps = nch * kw, hs = (nsteps + 1) / 2;
   const int s_begin = half ? hs : 0, s_end = half ? nsteps : hs;
   f32x4 acc[8];
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) acc[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  if (col0 < G.N && s_end > s_begin) {  // wave-uniform; no barrier inside
+  if (col0 < GW.N && s_end > s_begin) {  // wave-uniform; no barrier inside
     // per-row tap masks: bit j set iff frame t + j - pad lies inside the sequence
     unsigned vmask[8];
 #pragma unroll
@@ -1531,15 +1584,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
       unsigned msk = 0;
       if (m < p.M) {
         const int t = m % p.T;
-        const int lo = max(pad - t, 0), hi = min(p.T - 1 + pad - t, k - 1);
+        const int lo = max(padw - t, 0), hi = min(p.T - 1 + padw - t, kw - 1);
         if (lo <= hi) msk = (2u << hi) - (1u << lo);
       }
       vmask[mi] = msk;
     }
     // weight planes B0 = 2^11 w_h, B1 = w_t of column n, taps j, channels of step s
-    const int n = col0 + fr < G.N ? col0 + fr : G.N - 1;
-    const _Float16 *w0 = (const _Float16 *)G.w3 + (int64_t)n * G.Kpad;
-    const int64_t plane = (int64_t)G.N * G.Kpad;
+    const int n = col0 + fr < GW.N ? col0 + fr : GW.N - 1;
+    const _Float16 *w0 = (const _Float16 *)GW.w3 + (int64_t)n * GW.Kpad;
+    const int64_t plane = (int64_t)GW.N * GW.Kpad;
     // step s = (tap j = s / nch, chunk c = s % nch): the chunks of one tap are adjacent
     // 64-B pieces of a weight row, so consecutive steps read whole 128-B lines
     // Loads are unconditional (a missing channel segment of a partial chunk reads channel 0
@@ -1552,8 +1605,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
       b1 = *(const f16x8 *)(w0 + plane + off);
     };
     // Every step issues exactly one (clamped) weight load pair and the loop body has no
-    // branch at all, so the wait before a step's MFMAs leaves the SK_PF - 1 newer load
-    // pairs in flight; the step's 16 A fragments are read before its 24 MFMAs.
+    // branch at all; a step's 16 A fragments are read from the slab before its 24 MFMAs.
+    // (Measured alternatives, c2 prenet bank / proj1: the loop fully unrolled with exact
+    // per-step vmcnt waits 21.7 / 18.5 us, an 8-step ring 23.5 / 20.6, against 21.1 / 15.8
+    // for this form: the waves are not bound by the weight-load latency alone.)
     f16x8 rb0[SK_PF], rb1[SK_PF];
 #pragma unroll
     for (int u = 0; u < SK_PF; ++u) loadB(min(s_begin + u, s_end - 1), rb0[u], rb1[u]);
@@ -1568,7 +1623,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
 #pragma unroll
           for (int mi = 0; mi < 8; ++mi) {
             const bool ok = (vmask[mi] >> j) & 1u;
-            const int o = (ok ? mi * 16 + fr + j : SK_ZROW) * SL_P + fs * 8;
+            const int o = (ok ? mi * 16 + fr + j + dp : SK_ZROW) * SL_P + fs * 8;
             ah[mi] = *(const f16x8 *)(Ab + o);
             at[mi] = *(const f16x8 *)(Ab + SK_AIMG + o);
           }
@@ -1588,6 +1643,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
       }
     }
   }
+  SKSTAMP(2);
   // the second half's sums join the first half's through LDS (the slab is dead by then)
   __syncthreads();
   f32x4 *red = (f32x4 *)lds;  // [column set][mi][lane]
@@ -1596,15 +1652,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     for (int mi = 0; mi < 8; ++mi) red[(cw * 8 + mi) * 64 + lane] = acc[mi];
   }
   __syncthreads();
-  if (!half && col0 < G.N) {
+  if (!half && col0 < GW.N) {
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) acc[mi] += red[(cw * 8 + mi) * 64 + lane];
     // lane (fr, fs) holds rows mi*16 + 4 fs + i of column col0 + fr
     const int col = col0 + fr;
-    const bool cok = col < G.N;
-    const float cs = G.colscale[cok ? col : G.N - 1];
+    const bool cok = col < GW.N;
+    const float cs = GW.colscale[cok ? col : GW.N - 1];
     if (p.split > 1 || p.force_part) {
-      float *part = p.part + (size_t)blockIdx.y * p.M * p.ldp + G.ycol0;
+      float *part = p.part + (size_t)blockIdx.y * p.M * p.ldp + GW.ycol0;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -1616,9 +1672,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
           }
         }
     } else {
-      const float bias = G.bias && cok ? G.bias[col] : 0.f;
-      const float sc = G.scale && cok ? G.scale[col] : 1.f;
-      const float sh = G.scale && cok ? G.shift[col] : 0.f;
+      const float bias = GW.bias && cok ? GW.bias[col] : 0.f;
+      const float sc = GW.scale && cok ? GW.scale[col] : 1.f;
+      const float sh = GW.scale && cok ? GW.shift[col] : 0.f;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -1628,16 +1684,17 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
           bad |= !__builtin_isfinite(acc[mi][i]);
           float y = acc[mi][i] * cs + bias;
           if (p.relu) y = fmaxf(y, 0.f);
-          if (G.scale) y = y * sc + sh;
+          if (GW.scale) y = y * sc + sh;
           if (p.residual) y += p.residual[(int64_t)row * p.res_stride + col];
-          if (p.y) p.y[(int64_t)row * p.y_stride + G.ycol0 + col] = y;
+          if (p.y) p.y[(int64_t)row * p.y_stride + GW.ycol0 + col] = y;
           if (p.yt) {
             const int b = row / p.To, t = row - b * p.To;
-            p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = y;
+            p.yt[((int64_t)b * p.yt_channels + GW.ycol0 + col) * p.To + t] = y;
           }
         }
     }
   }
+  SKSTAMP(3);
   if (bad && p.status) atomicOr(p.status, 1u);
 }
 
@@ -1895,6 +1952,12 @@ static bool skinny_ok(const GemmParams &p, int epi) {
   return (nch + kc_per - 1) / kc_per == 1 || p.part != nullptr;
 }
 
+// FTMI_BANK_BALANCED=0 (read per call) keeps a conv bank on the one-group-per-block schedule
+static bool bank_balanced_enabled() {
+  const char *e = getenv("FTMI_BANK_BALANCED");
+  return !(e && atoi(e) == 0);
+}
+
 static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t s) {
   GemmParams q = p;
   q.force_part = epi == EPI_HIGHWAY;
@@ -1907,11 +1970,20 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
     q.g[i].ntiles = NT;
     q.ldp = max(q.ldp, q.g[i].ycol0 + q.g[i].N);
   }
-  dim3 grid(MT * q.ngroups * NT, q.split), block(512);
-  if (maxpool)
-    hipLaunchKernelGGL(conv_gemm_skinny_kernel<true>, grid, block, 0, s, q);
-  else
-    hipLaunchKernelGGL(conv_gemm_skinny_kernel<false>, grid, block, 0, s, q);
+  // a CBHG bank (groups k = K .. 1, even K, 16-column multiples): the balanced schedule
+  bool bank = q.ngroups >= 2 && q.ngroups % 2 == 0 && !maxpool && epi == EPI_CONV &&
+              q.g[0].N % 32 == 0 && bank_balanced_enabled();
+  for (int i = 0; bank && i < q.ngroups; ++i) bank = q.g[i].k == q.ngroups - i;
+  if (bank) {
+    dim3 grid(MT * (q.ngroups / 2) * (q.g[0].N / 32), q.split), block(512);
+    hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true>), grid, block, 0, s, q);
+  } else {
+    dim3 grid(MT * q.ngroups * NT, q.split), block(512);
+    if (maxpool)
+      hipLaunchKernelGGL(conv_gemm_skinny_kernel<true>, grid, block, 0, s, q);
+    else
+      hipLaunchKernelGGL(conv_gemm_skinny_kernel<false>, grid, block, 0, s, q);
+  }
   FTMI_CHECK_LAUNCH();
   if (q.force_part) {
     const int64_t n_el = (int64_t)q.M * (q.g[0].N / 2);
@@ -2101,6 +2173,13 @@ extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32
   return ftmi_conv_bank_split(x, x_stride, B, T, Cin, w, w_split, K, Cout, bn_scale, bn_shift,
                               y, y_stride, mma, status, 0, nullptr, stream);
 }
+
+#ifdef FTMI_SKINNY_STAMPS
+extern "C" int ftmi_debug_skinny_stamps(unsigned long long *host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ftmi_skinny_stamps),
+                                  sizeof(unsigned long long) * (size_t)n, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B, int32_t T,
                                     int32_t Cin, const float *w, const void *w_split, int32_t K,

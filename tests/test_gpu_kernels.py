@@ -170,6 +170,29 @@ def test_conv_bank(K, Cin, B, T, rng, mma, pre, kernel, monkeypatch):
     close(host(y), ref.transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
 
 
+@pytest.mark.parametrize('balanced', ['1', '0'])
+@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (8, 80, 1, 100), (4, 64, 2, 50),
+                                     (16, 256, 2, 100)])
+def test_conv_bank_skinny_schedules(K, Cin, B, T, balanced, rng, monkeypatch):
+    """The weight-streaming bank at batch-1 sizes on both block schedules
+    (FTMI_BANK_BALANCED: group pairs (k, K + 1 - k) per block, or one group per block),
+    f16x3, against the numpy oracle."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    monkeypatch.setenv('FTMI_BANK_BALANCED', balanced)
+    C = 256
+    x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
+    ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
+    sc = rng.uniform(0.5, 1.5, K * C).astype(np.float32)
+    sh = rng.normal(0, 0.1, K * C).astype(np.float32)
+    refs = [np.maximum(O.conv1d(x.transpose(0, 2, 1), w, w.shape[2] // 2)[:, :, :T], 0) for w in ws]
+    ref = np.concatenate(refs, 1) * sc[None, :, None] + sh[None, :, None]
+    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
+    w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
+    y = ops.conv_bank(dev(x), wp, K, C, dev(sc), dev(sh), mma=2, w_split=w3)
+    close(host(y), ref.transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
+
+
 @MMAS
 @pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
 @pytest.mark.parametrize('C,B,T', [(256, 3, 77), (128, 2, 300), (256, 1, 816)])

@@ -39,7 +39,10 @@ def main():
     w1 = pack_conv(torch.from_numpy(rng.normal(0, 0.01, (C, K * C, 3)).astype(np.float32))).cuda()
     w1s = ops.presplit_for(w1, 2)
     p1_bytes = 4.0 * (B * T * K * C + C * K * C * 3 + B * T * C)
-    for name, env in [('skinny cpb=2', {'FTMI_GEMM_SKINNY': '1', 'FTMI_SKINNY_CPB': '2'}),
+    for name, env in [('skinny cpb=2', {'FTMI_GEMM_SKINNY': '1', 'FTMI_SKINNY_CPB': '2',
+                                        'FTMI_BANK_BALANCED': '1'}),
+                      ('unbalanced cpb=2', {'FTMI_GEMM_SKINNY': '1', 'FTMI_SKINNY_CPB': '2',
+                                            'FTMI_BANK_BALANCED': '0'}),
                       ('skinny cpb=1', {'FTMI_GEMM_SKINNY': '1', 'FTMI_SKINNY_CPB': '1'}),
                       ('slab', {'FTMI_GEMM_SKINNY': '0'})]:
         if len(sys.argv) > 1 and name.replace(' ', '') not in sys.argv[1:]:
