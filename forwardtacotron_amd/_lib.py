@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 7
+ABI_VERSION = 8
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -75,7 +75,7 @@ SIGNATURES = {
     'ftmi_lr_posenc': (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, P, P, P, c_int64, P]),
     'ftmi_layernorm': (c_int, [P, c_int64, c_int64, c_int, P, P, c_float, P, c_int64, P]),
     'ftmi_attention': (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
-                               c_float, P, c_int64, P]),
+                               c_float, P, c_int64, c_int, P, P]),
     'ftmi_stft': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P, P, P]),
     'ftmi_mel_spectrogram': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P,
                                      P, P, P, c_int, c_int, P, P]),

@@ -235,6 +235,218 @@ __global__ __launch_bounds__(256) void attention_kernel(const float *__restrict_
   }
 }
 
+// ---------------------------------------------------------------- attention, f16x3
+// The same flash-style self-attention with both contractions on the f16x3 split (the GEMM
+// family's default path, gemm.hip): every operand x = x_h + 2^-11 x_t (f16 head, scaled f16
+// tail) and a product of two split operands = a_h b_h + 2^-11 (a_t b_h + a_h b_t) (dropped
+// term < 2^-22 relative) — here the big term and the two small ones go to separate
+// accumulators (no 2^11-scaled head, so any |x| < 65504 is in range), combined once.
+// v_mfma_f32_16x16x32_f16.  Workgroup = 8 waves x 16 queries; key tiles of 64: per tile and
+// wave S = (q c) K^T is 4 key blocks x HD/32 k-steps x 3 MFMAs and O += P V is 2 k-steps x
+// HD/16 column tiles x 3 MFMAs.  The softmax stays fp32 (online; exponentials on v_exp_f32,
+// |error| ~1 ulp of the argument's product with log2 e).  K is staged [key][d] and V
+// transposed [d][key] in LDS as f16 head / tail planes with row pitches that keep the
+// ds_read_b128 fragment reads conflict free.  An operand beyond the f16 range sets bit 0
+// of *status (the caller reruns on the fp32 kernel).
+constexpr int AH_W = 8;    // waves (x 16 queries) per workgroup of the f16x3 kernel
+constexpr int AH_KT = 64;  // keys per tile
+
+template <int HD>
+__global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
+    const float *__restrict__ qkv, int64_t rs, int B, int T, int H, int q_off, int k_off,
+    int v_off, const uint8_t *__restrict__ kpm, float qscale, float *__restrict__ out,
+    int64_t os, unsigned *status) {
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  constexpr int NTH = 64 * AH_W;
+  constexpr float TS = 2048.f, TU = 1.f / 2048.f;  // tail scale 2^11
+  constexpr float LOG2E = 1.4426950408889634f;
+  constexpr int KP = HD + 16;      // K row pitch (halves)
+  constexpr int VP = AH_KT + 16;   // V^T row pitch (halves)
+  constexpr int PP = AH_KT + 4;    // P row pitch (floats)
+  constexpr int NT = HD / 16;      // output column tiles
+  constexpr int KQ = HD / 32;      // k-steps of q k^T
+  constexpr int NB = AH_KT / 16;   // key blocks per tile
+  constexpr int KK = AH_KT / 32;   // k-steps of P V
+  __shared__ __attribute__((aligned(16))) _Float16 Kh[AH_KT * KP], Kt[AH_KT * KP];
+  __shared__ __attribute__((aligned(16))) _Float16 Vh[HD * VP], Vt[HD * VP];
+  __shared__ __attribute__((aligned(16))) float Ps[AH_W][16 * PP];
+
+  // XCD-aware order (1-D grid): the query tiles of one (batch, head) are consecutive blocks
+  // of ONE XCD (blocks L and L + 8 share an XCD), so its K / V rows are fetched into that
+  // XCD's L2 once and re-read from there by every query tile; with (B H) % 8 != 0 the plain
+  // order (tile fastest).
+  const int nq = (T + 16 * AH_W - 1) / (16 * AH_W), nbh = B * H;
+  int bh, qtile;
+  if (nbh % 8 == 0) {
+    const int L = blockIdx.x, q8 = L >> 3;
+    bh = (L & 7) + 8 * (q8 / nq);
+    qtile = q8 % nq;
+  } else {
+    bh = blockIdx.x / nq;
+    qtile = blockIdx.x % nq;
+  }
+  const int b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int q0 = qtile * 16 * AH_W + wave * 16;
+  const float *base = qkv + (int64_t)b * T * rs;
+  float amax = 0.f;  // range guard
+
+  auto split8 = [&](const f32x4 a, const f32x4 c, f16x8 &hd, f16x8 &tl) {
+    float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      amax = fmaxf(amax, fabsf(v[e]));
+      const _Float16 hh = (_Float16)v[e];
+      hd[e] = hh;
+      tl[e] = (_Float16)((v[e] - (float)hh) * TS);
+    }
+  };
+
+  // A fragments of this wave's 16 query rows (lane: row c16, d = 32 ks + 8 g + j), scaled by
+  // qscale in fp32 first, like the reference
+  f16x8 qh[KQ], qt[KQ];
+  {
+    const int qr = q0 + c16;
+    const float *src = base + (int64_t)(qr < T ? qr : 0) * rs + q_off + h * HD;
+#pragma unroll
+    for (int ks = 0; ks < KQ; ++ks) {
+      f32x4 a = *(const f32x4 *)(src + 32 * ks + 8 * g);
+      f32x4 c = *(const f32x4 *)(src + 32 * ks + 8 * g + 4);
+      if (qr >= T) a = c = (f32x4){0.f, 0.f, 0.f, 0.f};
+      split8(a * qscale, c * qscale, qh[ks], qt[ks]);
+    }
+  }
+  f32x4 ob[NT], osm[NT];  // P V: big term, small terms (x 2^11)
+#pragma unroll
+  for (int n = 0; n < NT; ++n) ob[n] = osm[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    m[i] = -INFINITY;
+    l[i] = 0.f;
+  }
+
+  for (int k0 = 0; k0 < T; k0 += AH_KT) {
+    __syncthreads();
+    // ---- stage K (keys x HD, [key][d]) and V^T (HD x keys, [d][key]) as f16 planes
+    for (int e = tid; e < AH_KT * HD / 4; e += NTH) {  // K: one float4 of a key row
+      const int r = e / (HD / 4), c4 = (e - r * (HD / 4)) * 4;
+      const int key = k0 + r;
+      f32x4 kv = {0.f, 0.f, 0.f, 0.f};
+      if (key < T) kv = *(const f32x4 *)(base + (int64_t)key * rs + k_off + h * HD + c4);
+      f16x4 hh, tt;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        amax = fmaxf(amax, fabsf(kv[j]));
+        hh[j] = (_Float16)kv[j];
+        tt[j] = (_Float16)((kv[j] - (float)hh[j]) * TS);
+      }
+      *(f16x4 *)&Kh[r * KP + c4] = hh;
+      *(f16x4 *)&Kt[r * KP + c4] = tt;
+    }
+    for (int e = tid; e < HD * (AH_KT / 8); e += NTH) {  // V: 8 keys of one column d
+      const int d = e % HD, kg = e / HD;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int key = k0 + kg * 8 + j;
+        v[j] = key < T ? base[(int64_t)key * rs + v_off + h * HD + d] : 0.f;
+      }
+      f16x8 hh, tt;
+      split8((f32x4){v[0], v[1], v[2], v[3]}, (f32x4){v[4], v[5], v[6], v[7]}, hh, tt);
+      *(f16x8 *)&Vh[d * VP + kg * 8] = hh;
+      *(f16x8 *)&Vt[d * VP + kg * 8] = tt;
+    }
+    __syncthreads();
+    // ---- S = (q c) K^T: 16 rows x AH_KT keys
+    f32x4 s[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      f32x4 big = {0.f, 0.f, 0.f, 0.f}, sm = {0.f, 0.f, 0.f, 0.f};
+      const int o = (n * 16 + c16) * KP + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < KQ; ++ks) {
+        const f16x8 kh = *(const f16x8 *)&Kh[o + 32 * ks];
+        const f16x8 kt = *(const f16x8 *)&Kt[o + 32 * ks];
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_f16(qt[ks], kh, sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[ks], kt, sm, 0, 0, 0);
+        big = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[ks], kh, big, 0, 0, 0);
+      }
+      s[n] = big + sm * TU;
+      // mask: keys past T or flagged in key_padding_mask -> -inf
+      const int key = k0 + n * 16 + c16;
+      const bool dead = key >= T || (kpm && kpm[(int64_t)b * T + key]);
+      if (dead)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[n][i] = -INFINITY;
+    }
+    // ---- online softmax per row (rows 4g+i; the 16 lanes of group g hold its columns)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float mx = s[0][i];
+#pragma unroll
+      for (int n = 1; n < NB; ++n) mx = fmaxf(mx, s[n][i]);
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+      const float mn = fmaxf(m[i], mx);
+      const float alpha = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f((m[i] - mn) * LOG2E);
+      float ps = 0.f;
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const float pv = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((s[n][i] - mn) * LOG2E);
+        s[n][i] = pv;
+        ps += pv;
+      }
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) ps += __shfl_xor(ps, off);
+      l[i] = l[i] * alpha + ps;
+      m[i] = mn;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        ob[n][i] *= alpha;
+        osm[n][i] *= alpha;
+      }
+    }
+    // ---- P (C layout) -> this wave's LDS rows -> A layout (row c16, keys 32 kk + 8 g ..)
+    float *P = Ps[wave];
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) P[(4 * g + i) * PP + n * 16 + c16] = s[n][i];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      f16x8 ph, pt;
+      const f32x4 a = *(const f32x4 *)&P[c16 * PP + 32 * kk + 8 * g];
+      const f32x4 c = *(const f32x4 *)&P[c16 * PP + 32 * kk + 8 * g + 4];
+      split8(a, c, ph, pt);
+      // ---- O += P V
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int o = (n * 16 + c16) * VP + 32 * kk + 8 * g;
+        const f16x8 vh = *(const f16x8 *)&Vh[o];
+        const f16x8 vt = *(const f16x8 *)&Vt[o];
+        osm[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pt, vh, osm[n], 0, 0, 0);
+        osm[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, vt, osm[n], 0, 0, 0);
+        ob[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ph, vh, ob[n], 0, 0, 0);
+      }
+    }
+  }
+  if (!(amax <= 65504.f) && status) atomicOr(status, 1u);
+  // normalise and store
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int qr = q0 + 4 * g + i;
+    if (qr >= T) continue;
+    float *dst = out + ((int64_t)b * T + qr) * os + h * HD;
+    const float inv = l[i];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) dst[n * 16 + c16] = (ob[n][i] + osm[n][i] * TU) / inv;
+  }
+}
+
 }  // namespace
 
 extern "C" int ftmi_embedding_posenc(const int64_t *ids, int32_t B, int32_t T, const float *table,
@@ -287,13 +499,27 @@ extern "C" int ftmi_layernorm(const float *x, int64_t x_stride, int64_t M, int32
 extern "C" int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, int32_t T,
                               int32_t H, int32_t head_dim, int32_t q_off, int32_t k_off,
                               int32_t v_off, const uint8_t *key_padding_mask, float qscale,
-                              float *out, int64_t out_stride, ftmi_stream_t stream) {
+                              float *out, int64_t out_stride, int32_t mma, uint32_t *status,
+                              ftmi_stream_t stream) {
   if (!qkv || !out || B <= 0 || T <= 0 || H <= 0) return FTMI_E_ARG;
   if (head_dim != 64 && head_dim != 128) return FTMI_E_UNSUPPORTED;
+  if (mma != FTMI_MMA_F32 && mma != FTMI_MMA_F16X3) return FTMI_E_UNSUPPORTED;
   if (!ftmi_aligned16(qkv) || (row_stride & 3) || (q_off & 3) || (k_off & 3) || (v_off & 3))
     return FTMI_E_ALIGN;
   const dim3 grid((unsigned)((T + 63) / 64), (unsigned)(B * H)), block(256);
   const hipStream_t s = ftmi_hs(stream);
+  if (mma == FTMI_MMA_F16X3) {
+    const int nq = (T + 16 * AH_W - 1) / (16 * AH_W);
+    const dim3 g1((unsigned)(nq * B * H)), b1(64 * AH_W);
+    if (head_dim == 64)
+      hipLaunchKernelGGL(attention_h3_kernel<64>, g1, b1, 0, s, qkv, row_stride, B, T, H,
+                         q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride, status);
+    else
+      hipLaunchKernelGGL(attention_h3_kernel<128>, g1, b1, 0, s, qkv, row_stride, B, T, H,
+                         q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride, status);
+    FTMI_CHECK_LAUNCH();
+    return FTMI_OK;
+  }
   if (head_dim == 64)
     hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, s, qkv, row_stride, B, T, H, q_off, k_off,
                        v_off, key_padding_mask, qscale, out, out_stride);

@@ -577,9 +577,13 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
     return y
 
 
-def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Self-attention core of nn.MultiheadAttention on packed in_proj rows (B, T, 3d)."""
+def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Tensor] = None,
+              mma: Optional[int] = None) -> torch.Tensor:
+    """Self-attention core of nn.MultiheadAttention on packed in_proj rows (B, T, 3d).
+    mma: 2 = f16x3 contractions (default, MMA), 0 = fp32 MFMA (exact_paths(), MMA 0/1)."""
     _dev(qkv, key_padding_mask)
+    m = _FORCED[-1][0] if _FORCED else (MMA if mma is None else mma)
+    m = 2 if m == 2 else 0
     B, T, C3, rs = _rows(qkv)
     d = C3 // 3
     hd = d // heads
@@ -588,8 +592,8 @@ def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Te
     if key_padding_mask is not None:
         kpm = key_padding_mask.to(torch.uint8).contiguous()
     qscale = float(np.float32(np.sqrt(1.0 / hd)))
-    launch('ftmi_attention', f'attention[B={B},T={T},H={heads},hd={hd}]', 4.0 * B * heads * T * T * hd,
-           4.0 * (B * T * C3 + B * T * d),
+    launch('ftmi_attention', f'attention[B={B},T={T},H={heads},hd={hd},mma={m}]',
+           4.0 * B * heads * T * T * hd, 4.0 * (B * T * C3 + B * T * d),
            qkv.data_ptr(), rs, B, T, heads, hd, 0, d, 2 * d, _ptr(kpm), qscale,
-           out.data_ptr(), out.stride(1), _stream())
+           out.data_ptr(), out.stride(1), m, status_word(qkv.device).data_ptr(), _stream())
     return out

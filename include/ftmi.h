@@ -389,11 +389,13 @@ int ftmi_layernorm(const float *x, int64_t x_stride, int64_t M, int32_t C, const
  * from the packed in_proj output rows (row stride row_stride floats; q/k/v column
  * offsets q_off/k_off/v_off).  key_padding_mask: (B, T) bytes, nonzero = padded key
  * (-inf), or NULL.  qscale = float32(sqrt(1/head_dim)).  out: (B, T, H*head_dim) rows of
- * stride out_stride.  head_dim in {64, 128}. */
+ * stride out_stride.  head_dim in {64, 128}.  mma (ABI 8): FTMI_MMA_F16X3 (default: both
+ * contractions on the f16x3 split, softmax fp32; an operand beyond the f16 range sets
+ * FTMI_STATUS_F16_RANGE in *status, optional) or FTMI_MMA_F32 (fp32 MFMA). */
 int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, int32_t T, int32_t H,
                    int32_t head_dim, int32_t q_off, int32_t k_off, int32_t v_off,
                    const uint8_t *key_padding_mask, float qscale, float *out, int64_t out_stride,
-                   ftmi_stream_t stream);
+                   int32_t mma, uint32_t *status, ftmi_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -46,9 +46,10 @@ def test_layernorm(C):
     np.testing.assert_allclose(host(ops.layernorm(dev(x), dev(g), dev(b))), ref, atol=2e-6, rtol=2e-6)
 
 
+@pytest.mark.parametrize('mma', [2, 0], ids=['f16x3', 'f32'])
 @pytest.mark.parametrize('hd,T,masked', [(64, 37, False), (128, 200, True), (128, 33, False),
-                                         (64, 129, True), (128, 1, False)])
-def test_attention(hd, T, masked):
+                                         (64, 129, True), (128, 1, False), (128, 1400, False)])
+def test_attention(hd, T, masked, mma):
     from forwardtacotron_amd import ops
     rng = np.random.RandomState(T + hd)
     B, H = 3, 2
@@ -65,8 +66,30 @@ def test_attention(hd, T, masked):
     if kpm is not None:
         s = np.where(kpm[:, None, None, :], -np.inf, s)
     ref = (FP.softmax(s) @ sp(v)).transpose(0, 2, 1, 3).reshape(B, T, d)
-    got = host(ops.attention(dev(qkv), H, dev(kpm) if kpm is not None else None))
+    st = ops.status_word('cuda')
+    st.zero_()
+    got = host(ops.attention(dev(qkv), H, dev(kpm) if kpm is not None else None, mma=mma))
     np.testing.assert_allclose(got, ref, atol=2e-5, rtol=2e-5)
+    assert int(st.item()) == 0
+
+
+def test_attention_f16_range_guard():
+    """An attention operand beyond the f16 range sets status bit 0 on the f16x3 kernel (the
+    model entry points then rerun on the fp32 kernel), and the fp32 kernel stays exact."""
+    from forwardtacotron_amd import ops
+    rng = np.random.RandomState(5)
+    B, T, H, hd = 2, 40, 2, 64
+    qkv = rng.randn(B, T, 3 * H * hd).astype(np.float32)
+    qkv[1, 7, 2 * H * hd + 3] = 1e5  # one value entry
+    st = ops.status_word('cuda')
+    st.zero_()
+    ops.attention(dev(qkv), H, mma=2)
+    torch.cuda.synchronize()
+    assert int(st.item()) & 1
+    st.zero_()
+    ops.attention(dev(qkv), H, mma=0)
+    torch.cuda.synchronize()
+    assert int(st.item()) == 0
 
 
 def test_embedding_posenc_and_lr_posenc(fp_model):
