@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 8
+ABI_VERSION = 9
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -51,10 +51,13 @@ SIGNATURES = {
     'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P, P]),
     'ftmi_highway_split': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P,
                                    c_int, P, P]),
+    'ftmi_highway_stack': (c_int, [P, c_int64, c_int64, c_int, c_int, P, c_int, P, P, P, P, P,
+                                   c_int, P, c_int64, P, c_int64, P, P]),
     'ftmi_split_weights_bytes': (c_int64, [c_int64, c_int64]),
     'ftmi_split_weights': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_split_weights_f16_bytes': (c_int64, [c_int64, c_int64]),
     'ftmi_split_weights_f16': (c_int, [P, c_int64, c_int64, P, P]),
+    'ftmi_split_weights_f16_frag': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_rnn_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
     'ftmi_rnn_error_offset': (c_int64, [c_int]),
     'ftmi_rnn_blocks': (c_int, [c_int, c_int, c_int, c_int]),

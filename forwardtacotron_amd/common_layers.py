@@ -302,12 +302,44 @@ class CBHG(Packed):
         y = self.conv_project1.forward_cl(bank, maxpool=True)
         del bank
         y = self.conv_project2.forward_cl(y, residual=x)
+        xp = self._highway_stack(y)
+        if xp is not None:
+            return self.rnn.recur(xp)
         h, _ = ops.conv1d(y, w_pre, 1, 0, w_split=pre3)
         h2 = torch.empty_like(h)
         for hw in self.highways:
             hw.forward_cl(h, out=h2)
             h, h2 = h2, h
         return self.rnn.forward_cl(h)
+
+    def _stack_pack(self):
+        """Fragment-major f16x3 blocks of pre_highway, the highways' w12 and the GRU's W_ih
+        (the operands of ops.highway_stack), cached like every pack (rebuilt with the params)."""
+        key = self._pack_key()
+        cache = self.__dict__.get('_ftmi_stack')
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                w_pre = self.packed_weights()[3]
+                hw = [m.packed_weights() for m in self.highways]
+                w_ih, b_in = self.rnn.packed_weights()[:2]
+                f16 = ops.split_weights_f16
+                cache = (key, (f16(w_pre, frag=True), [f16(p[0], frag=True) for p in hw],
+                               [p[1] for p in hw], [p[2] for p in hw], f16(w_ih, frag=True),
+                               b_in, w_ih.size(0)))
+            self.__dict__['_ftmi_stack'] = cache
+        return cache[1]
+
+    def _highway_stack(self, y: torch.Tensor) -> Optional[torch.Tensor]:
+        """pre_highway -> highways -> the GRU's input projection in one launch (the GRU input
+        rows, or None where ops.highway_stack does not apply)."""
+        M, Cp = y.size(0) * y.size(1), y.size(2)
+        n_out = 6 * self.channels
+        if not ops.highway_stack_ok(M, Cp, self.channels, len(self.highways), n_out,
+                                    (self.packed_weights()[5],)):
+            return None
+        pre_f, hw_f, b1s, b2s, ih_f, b_in, n_out = self._stack_pack()
+        xp, _ = ops.highway_stack(y, pre_f, self.channels, hw_f, b1s, b2s, ih_f, b_in, n_out)
+        return xp
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """(B, Cin, T) -> (B, T, 2*channels), like the reference."""

@@ -122,6 +122,13 @@ __device__ __forceinline__ void split2h(f32x4 v, f16x4 &h, f16x4 &t) {
   t = __builtin_convertvector((v - __builtin_convertvector(h, f32x4)) * H3_SCALE, f16x4);
 }
 
+// highway output g relu(x1) + (1 - g) x with one fixed rounding sequence in every kernel
+// (no compiler-chosen contraction: the fused stack is bit-identical to the per-layer path)
+__device__ __forceinline__ float highway_mix(float g, float x1, float x) {
+#pragma clang fp contract(off)
+  return fmaf(g, fmaxf(x1, 0.f), (1.f - g) * x);
+}
+
 constexpr int X6_BK = 32;
 constexpr int X6_STRIDE = 48;  // bf16 per staged row (32 + 16 pad): 96-B rows make the
                                // ds_read_b128 fragment reads of 16x16x32 conflict free
@@ -289,7 +296,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const GemmParams p) {
         const float x2 = acc[mi][1][r] + b2;
         const float g = ftmi_sigmoid(x2);
         const float xin = p.x[(int64_t)row * p.x_stride + col];
-        p.y[(int64_t)row * p.y_stride + col] = g * fmaxf(x1, 0.f) + (1.f - g) * xin;
+        p.y[(int64_t)row * p.y_stride + col] = highway_mix(g, x1, xin);
       }
   }
 }
@@ -513,7 +520,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6_kernel(const GemmParams p
           const float x2 = acc[mi][ni + 2][i] + b2;
           const float g = ftmi_sigmoid(x2);
           const float xin = p.x[(int64_t)row * p.x_stride + col];
-          p.y[(int64_t)row * p.y_stride + col] = g * fmaxf(x1, 0.f) + (1.f - g) * xin;
+          p.y[(int64_t)row * p.y_stride + col] = highway_mix(g, x1, xin);
         }
     }
   }
@@ -723,7 +730,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_x6p_kernel(const GemmParams 
           const float x2 = acc[mi][ni + 2][i] + b2;
           const float g = ftmi_sigmoid(x2);
           const float xin = p.x[(int64_t)row * p.x_stride + col];
-          p.y[(int64_t)row * p.y_stride + col] = g * fmaxf(x1, 0.f) + (1.f - g) * xin;
+          p.y[(int64_t)row * p.y_stride + col] = highway_mix(g, x1, xin);
         }
     }
   }
@@ -1018,7 +1025,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6b_kernel(const GemmParams 
             const float x2 = acc[mi][ni + 2][i] + b2;
             const float g = ftmi_sigmoid(x2);
             const float xin = p.x[(int64_t)row * p.x_stride + col];
-            p.y[(int64_t)row * p.y_stride + col] = g * fmaxf(x1, 0.f) + (1.f - g) * xin;
+            p.y[(int64_t)row * p.y_stride + col] = highway_mix(g, x1, xin);
           }
       }
   }
@@ -1424,7 +1431,7 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float g = ftmi_sigmoid(x2[e]);
-        out[e] = g * fmaxf(x1[e], 0.f) + (1.f - g) * xin[e];
+        out[e] = highway_mix(g, x1[e], xin[e]);
       }
       *(f32x4 *)(p.y + (int64_t)row * p.y_stride + col) = out;
     }
@@ -1749,7 +1756,7 @@ __global__ __launch_bounds__(256) void skinny_highway_finish_kernel(const GemmPa
     }
     const float g = ftmi_sigmoid(v2 + p.b2[o]);
     const float xin = p.x[(int64_t)row * p.x_stride + o];
-    p.y[(int64_t)row * p.y_stride + o] = g * fmaxf(v1 + p.b1[o], 0.f) + (1.f - g) * xin;
+    p.y[(int64_t)row * p.y_stride + o] = highway_mix(g, v1 + p.b1[o], xin);
   }
 }
 
@@ -1774,10 +1781,14 @@ __global__ void split_weights_kernel(const float *__restrict__ w, int64_t N, int
 // column-scaled row w s_n) followed by colscale[N] = 2^-11 / s_n.  One workgroup per row:
 // s_n = 2^-e with the smallest e >= 0 such that max|w[n]| s_n < 16 (so 2^11 w_h stays
 // inside the f16 range).
+// frag: planes in the fragment-major order [N/16][Kpad/32][64 lanes][8] of the
+// v_mfma_f32_16x16x32_f16 B operand (lane = n % 16 + 16 ((k / 8) % 4), element k % 8) —
+// the layout of ftmi_highway_stack; else row-major [N][Kpad].
 __global__ __launch_bounds__(256) void split_weights_f16_kernel(const float *__restrict__ w,
                                                                 int64_t N, int64_t K, int64_t Kpad,
                                                                 _Float16 *__restrict__ out,
-                                                                float *__restrict__ colscale) {
+                                                                float *__restrict__ colscale,
+                                                                int frag) {
   __shared__ float red[4];
   const int64_t n = blockIdx.x;
   const float *row = w + n * K;
@@ -1795,9 +1806,12 @@ __global__ __launch_bounds__(256) void split_weights_f16_kernel(const float *__r
     const float v = k < K ? ldexpf(row[k], -e) : 0.f;
     const _Float16 h = (_Float16)v;
     const _Float16 t = (_Float16)((v - (float)h) * H3_SCALE);
-    out[n * Kpad + k] = (_Float16)((float)h * H3_SCALE);
-    out[plane + n * Kpad + k] = t;
-    out[2 * plane + n * Kpad + k] = h;
+    const int64_t o = frag ? ((n >> 4) * (Kpad / 32) + (k >> 5)) * 512 + ((k >> 3) & 3) * 128 +
+                                 (n & 15) * 8 + (k & 7)
+                           : n * Kpad + k;
+    out[o] = (_Float16)((float)h * H3_SCALE);
+    out[plane + o] = t;
+    out[2 * plane + o] = h;
   }
   if (threadIdx.x == 0) colscale[n] = ldexpf(1.f, e - 11);
 }
@@ -1822,6 +1836,252 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const GemmParams p
       p.yt[((int64_t)b * p.yt_channels + G.ycol0 + col) * p.To + t] = v;
     }
   }
+}
+
+// ---- highway stack: pre_highway -> L highways -> GRU input projection, one launch -------
+// models/common_layers.py:110-115 (CBHG: x = pre_highway(x); for h in highways: x = h(x);
+// then the bidirectional GRU, whose input projection x W_ih^T + b_ih is the last GEMM here).
+// The unfused chain writes and re-reads the (M, 256) activations in HBM between every layer
+// and its short-K launches (K = 256: 8 k-steps per 256 x 128 tile) are prologue-bound.  Here
+// one workgroup owns 64 rows x all 256 channels for the whole chain: 8 waves, wave w owns h
+// columns [32w, 32w + 32).  Each layer's output is split (f16 head / scaled tail, as the
+// other f16x3 kernels) into one of two LDS images — the next layer's A operand — while the
+// wave keeps its own 64 x 32 block in fp32 registers: exactly the x its next gating needs,
+// since the W1 and W2 columns of one h column (packed 32-column blocks) land in the same lane.
+// B fragments (the pre-split f16 planes; every workgroup reads the same 1.4 MB, L2-resident)
+// are loaded straight into registers one k-step ahead.  Per k-step, per product, the MFMA
+// order and the epilogue arithmetic are the slab kernel's, so the result is bit-identical to
+// the unfused chain.  HBM traffic per row: Cp floats in, n_out floats out (+ C with h).
+constexpr int HS_BM = 64;
+constexpr int HS_C = 256;
+constexpr int HS_P = HS_C + 16;  // halves per LDS row: conflict-free ds_read_b128 fragments
+constexpr int HS_IMG = HS_BM * HS_P;
+constexpr int HS_MAXL = 8;
+constexpr int HS_NPASS = 512;  // output-projection columns per pass (8 waves x 64)
+
+struct HwStackParams {
+  const float *x;
+  int64_t x_stride;
+  int M, Cp, kp_pre;      // rows, input channels, K of the pre_highway planes (roundup 32)
+  const _Float16 *w_pre;  // f16 planes [3][C][kp_pre] (B0 = 2^11 w_h, B1 = w_t, B2 = w_h)
+  const float *cs_pre;    // its column scales
+  int L;
+  const _Float16 *w_hw[HS_MAXL];  // [3][2C][C], W1 | W2 packed in 32-row blocks
+  const float *cs_hw[HS_MAXL];
+  const float *b1[HS_MAXL];
+  const float *b2[HS_MAXL];
+  const _Float16 *w_out;  // [3][n_out][C] (null: no projection)
+  const float *cs_out;
+  const float *b_out;
+  int n_out;
+  float *y;
+  int64_t y_stride;
+  float *h;  // optional: the last highway's output (fp32)
+  int64_t h_stride;
+  unsigned *status;
+};
+
+// acc[mi][ni] (rows 16 mi + 4 fs + i, GEMM column of bp[ni] + fr) = A x B^T over nks k-steps
+// of 32, f16x3 (small terms first, as the slab kernel).  bp[ni]: the lane's B0 row + 8 fs.
+template <int NI>
+__device__ __forceinline__ void hs_step(f32x4 (&acc)[4][NI], const _Float16 *Ah,
+                                        const _Float16 *At, const f16x8 (&b0)[NI],
+                                        const f16x8 (&b1)[NI], int ks, int fr, int fs) {
+  f16x8 bh[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) bh[ni] = b0[ni] * (_Float16)(1.0f / H3_SCALE);
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {  // A fragments one row block at a time (register budget)
+    const int o = (16 * mi + fr) * HS_P + 32 * ks + 8 * fs;
+    const f16x8 ah = *(const f16x8 *)(Ah + o);
+    const f16x8 at = *(const f16x8 *)(At + o);
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      f32x4 c = acc[mi][ni];
+      c = mma16(at, bh[ni], c);
+      c = mma16(ah, b1[ni], c);
+      c = mma16(ah, b0[ni], c);
+      acc[mi][ni] = c;
+    }
+  }
+}
+
+// acc[mi][ni] (rows 16 mi + 4 fs + i, GEMM column of bp[ni] + fr) = A x B^T over nks k-steps
+// of 32, f16x3 (small terms first, as the slab kernel).  bp[ni]: the lane's B0 row + 8 fs.
+// B fragments ping-pong between two register sets, loaded one k-step ahead (the loop is
+// kept rolled: unrolled, the compiler hoists further loads and spills).
+template <int NI>
+__device__ __forceinline__ void hs_gemm(f32x4 (&acc)[4][NI], const _Float16 *Ah,
+                                        const _Float16 *At, const _Float16 *const (&bp)[NI],
+                                        int64_t plane, int nks, int fr, int fs) {
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f16x8 x0[NI], x1[NI], y0[NI], y1[NI];
+  auto load = [&](f16x8 (&r0)[NI], f16x8 (&r1)[NI], int ks) {
+    const int k = ks < nks ? ks : nks - 1;  // past the end: a clamped (unused) re-read
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      r0[ni] = *(const f16x8 *)(bp[ni] + 512 * k);
+      r1[ni] = *(const f16x8 *)(bp[ni] + plane + 512 * k);
+    }
+  };
+  load(x0, x1, 0);
+#pragma unroll 1
+  for (int ks = 0; ks < nks; ks += 2) {
+    load(y0, y1, ks + 1);
+    hs_step<NI>(acc, Ah, At, x0, x1, ks, fr, fs);
+    if (ks + 1 >= nks) break;
+    load(x0, x1, ks + 2);
+    hs_step<NI>(acc, Ah, At, y0, y1, ks + 1, fr, fs);
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackParams p) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 2 * HS_IMG];  // [image][head|tail]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fs = lane >> 4;
+  // column block of this wave, rotated per workgroup so that the CUs of one XCD (blocks
+  // b, b + 8, ...) stream different weight rows at any moment instead of all hitting the
+  // same L2 lines (channel hot spots); the arithmetic per column is unchanged
+  const int cb = (wave + (blockIdx.x >> 3)) & 7;
+  // the lane's B0 fragment of columns [n0, n0 + 16), k-step 0, in the fragment-major planes
+  // [N/16][Kpad/32][64 lanes][8] (ftmi_split_weights_f16_frag): every wave load is one
+  // contiguous 1-KB run (8 whole cache lines; row-major planes cost 16 half lines, measured
+  // 1.48x slower at c3: the per-CU fetch rate, not MFMA, bounds this kernel)
+  auto bptr = [&](const _Float16 *base, int n0, int Kpad) -> const _Float16 * {
+    return base + (int64_t)(n0 >> 4) * (Kpad / 32) * 512 + lane * 8;
+  };
+  const int m0 = blockIdx.x * HS_BM;
+  float amax = 0.f;  // range guard: largest |activation| fed to the f16 split
+
+  // ---- the input rows (Cp channels, zero-padded to kp_pre; rows past M zero) -> image 0
+  const int q4 = p.kp_pre / 4;
+  for (int e = tid; e < HS_BM * q4; e += 512) {
+    const int r = e / q4, c = (e - r * q4) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (m0 + r < p.M && c < p.Cp) v = *(const f32x4 *)(p.x + (int64_t)(m0 + r) * p.x_stride + c);
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    f16x4 hh, tt;
+    split2h(v, hh, tt);
+    *(f16x4 *)(lds + r * HS_P + c) = hh;
+    *(f16x4 *)(lds + HS_IMG + r * HS_P + c) = tt;
+  }
+  __syncthreads();
+
+  f32x4 xs[4][2];  // this wave's 64 x 32 block of the current activations, fp32
+  auto put = [&](int img) {  // xs -> LDS image img (split)
+    _Float16 *Hd = lds + img * 2 * HS_IMG, *Tl = Hd + HS_IMG;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = xs[mi][nj][i];
+          amax = fmaxf(amax, fabsf(v));
+          const _Float16 hh = (_Float16)v;
+          const int o = (16 * mi + 4 * fs + i) * HS_P + 32 * cb + 16 * nj + fr;
+          Hd[o] = hh;
+          Tl[o] = (_Float16)((v - (float)hh) * H3_SCALE);
+        }
+  };
+
+  // ---- pre_highway (Linear, no bias): x W_pre^T, K = kp_pre
+  {
+    f32x4 acc[4][2];
+    const _Float16 *bp[2];
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+      bp[ni] = bptr(p.w_pre, 32 * cb + 16 * ni, p.kp_pre);
+    hs_gemm<2>(acc, lds, lds + HS_IMG, bp, (int64_t)HS_C * p.kp_pre, p.kp_pre / 32, fr, fs);
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const float cs = p.cs_pre[32 * cb + 16 * ni + fr];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) xs[mi][ni] = acc[mi][ni] * cs;
+    }
+  }
+  put(1);
+  __syncthreads();
+  int cur = 1;
+
+  // ---- highways: g = sigmoid(x W2^T + b2), x <- g relu(x W1^T + b1) + (1 - g) x
+  for (int l = 0; l < p.L; ++l) {
+    f32x4 acc[4][4];
+    const _Float16 *bp[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      bp[ni] = bptr(p.w_hw[l], 64 * cb + 16 * ni, HS_C);
+    const _Float16 *A = lds + cur * 2 * HS_IMG;
+    hs_gemm<4>(acc, A, A + HS_IMG, bp, (int64_t)2 * HS_C * HS_C, HS_C / 32, fr, fs);
+#pragma unroll
+    for (int nj = 0; nj < 2; ++nj) {
+      const int col = 32 * cb + 16 * nj + fr;
+      const float c1 = p.cs_hw[l][64 * cb + 16 * nj + fr];
+      const float c2 = p.cs_hw[l][64 * cb + 32 + 16 * nj + fr];
+      const float bb1 = p.b1[l][col], bb2 = p.b2[l][col];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float x1, x2;
+          {
+#pragma clang fp contract(off)
+            // rounded like the slab kernel: the column scale, then the bias
+            x1 = acc[mi][nj][i] * c1 + bb1;
+            x2 = acc[mi][nj + 2][i] * c2 + bb2;
+          }
+          const float g = ftmi_sigmoid(x2);
+          xs[mi][nj][i] = highway_mix(g, x1, xs[mi][nj][i]);
+        }
+    }
+    cur ^= 1;
+    put(cur);  // the image read two layers ago: every wave passed the barrier since
+    __syncthreads();
+  }
+  if (p.h) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + 16 * mi + 4 * fs + i;
+        if (row >= p.M) continue;
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj)
+          p.h[(int64_t)row * p.h_stride + 32 * cb + 16 * nj + fr] = xs[mi][nj][i];
+      }
+  }
+
+  // ---- output projection (the GRU's x W_ih^T + b_ih), HS_NPASS columns per pass
+  if (p.w_out) {
+    const _Float16 *A = lds + cur * 2 * HS_IMG;
+    for (int q = 0; q < p.n_out / HS_NPASS; ++q) {
+      f32x4 acc[4][4];
+      const _Float16 *bp[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        bp[ni] = bptr(p.w_out, HS_NPASS * q + 64 * cb + 16 * ni, HS_C);
+      hs_gemm<4>(acc, A, A + HS_IMG, bp, (int64_t)p.n_out * HS_C, HS_C / 32, fr, fs);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int col = HS_NPASS * q + 64 * cb + 16 * ni + fr;
+        const float cs = p.cs_out[col], b = p.b_out ? p.b_out[col] : 0.f;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+#pragma clang fp contract(off)
+            const int row = m0 + 16 * mi + 4 * fs + i;
+            float v = acc[mi][ni][i] * cs;
+            if (p.b_out) v += b;
+            if (row < p.M) p.y[(int64_t)row * p.y_stride + col] = v;
+          }
+      }
+    }
+  }
+  if (!(amax <= 65504.f) && p.status) atomicOr(p.status, 1u);
 }
 
 static int x6_variant() {
@@ -2300,21 +2560,86 @@ extern "C" int ftmi_highway_split(const float *x, int64_t x_stride, int64_t M, i
   return launch(p, EPI_HIGHWAY, false, mtiles * g.ntiles, mma, ftmi_hs(stream));
 }
 
+// f16 planes + column scales of a split_weights_f16 block [3][N][Kpad] + colscale[N]
+static const float *f16_colscale(const void *w3, int64_t N, int64_t K) {
+  const int64_t Kpad = (K + X6_BK - 1) / X6_BK * X6_BK;
+  return (const float *)((const char *)w3 + 3 * N * Kpad * 2);
+}
+
+extern "C" int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, int32_t Cp,
+                                  int32_t C, const void *w_pre_split, int32_t L,
+                                  const void *const *w_hw_split, const float *const *b1,
+                                  const float *const *b2, const void *w_out_split,
+                                  const float *b_out, int32_t n_out, float *y, int64_t y_stride,
+                                  float *h, int64_t h_stride, uint32_t *status,
+                                  ftmi_stream_t stream) {
+  if (!x || !w_pre_split || M <= 0 || Cp <= 0 || L < 0) return FTMI_E_ARG;
+  if (L > 0 && (!w_hw_split || !b1 || !b2)) return FTMI_E_ARG;
+  if (w_out_split ? (!y || n_out <= 0) : (n_out != 0 || y != nullptr)) return FTMI_E_ARG;
+  if (!y && !h) return FTMI_E_ARG;
+  if (C != HS_C || Cp > HS_C || Cp % 4 != 0 || L > HS_MAXL) return FTMI_E_SHAPE;
+  if (n_out % HS_NPASS != 0 || M > INT32_MAX) return FTMI_E_SHAPE;
+  if (!ftmi_aligned16(x) || (x_stride & 3) || !ftmi_aligned16(w_pre_split)) return FTMI_E_ALIGN;
+  if (w_out_split && !ftmi_aligned16(w_out_split)) return FTMI_E_ALIGN;
+  if ((const float *)x == y || (const float *)x == h) return FTMI_E_ARG;
+  HwStackParams p = {};
+  p.x = x;
+  p.x_stride = x_stride;
+  p.M = (int)M;
+  p.Cp = Cp;
+  p.kp_pre = (Cp + X6_BK - 1) / X6_BK * X6_BK;
+  p.w_pre = (const _Float16 *)w_pre_split;
+  p.cs_pre = f16_colscale(w_pre_split, C, Cp);
+  p.L = L;
+  for (int l = 0; l < L; ++l) {
+    if (!w_hw_split[l] || !b1[l] || !b2[l] || !ftmi_aligned16(w_hw_split[l])) return FTMI_E_ARG;
+    p.w_hw[l] = (const _Float16 *)w_hw_split[l];
+    p.cs_hw[l] = f16_colscale(w_hw_split[l], 2 * C, C);
+    p.b1[l] = b1[l];
+    p.b2[l] = b2[l];
+  }
+  if (w_out_split) {
+    p.w_out = (const _Float16 *)w_out_split;
+    p.cs_out = f16_colscale(w_out_split, n_out, C);
+    p.b_out = b_out;
+    p.n_out = n_out;
+    p.y = y;
+    p.y_stride = y_stride;
+  }
+  p.h = h;
+  p.h_stride = h_stride;
+  p.status = status;
+  const unsigned blocks = (unsigned)((M + HS_BM - 1) / HS_BM);
+  hipLaunchKernelGGL(highway_stack_kernel, dim3(blocks), dim3(512), 0, ftmi_hs(stream), p);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
 extern "C" int64_t ftmi_split_weights_f16_bytes(int64_t N, int64_t K) {
   return split_block_bytes(N, K, 2);
 }
 
-extern "C" int ftmi_split_weights_f16(const float *w, int64_t N, int64_t K, void *out,
-                                      ftmi_stream_t stream) {
+static int split_f16(const float *w, int64_t N, int64_t K, void *out, int frag,
+                     ftmi_stream_t stream) {
   if (!w || !out || N <= 0 || K <= 0) return FTMI_E_ARG;
-  if (N > INT32_MAX) return FTMI_E_SHAPE;
+  if (N > INT32_MAX || (frag && N % 16 != 0)) return FTMI_E_SHAPE;
   if (!ftmi_aligned16(out)) return FTMI_E_ALIGN;
   const int64_t Kpad = (K + X6_BK - 1) / X6_BK * X6_BK;
   hipLaunchKernelGGL(split_weights_f16_kernel, dim3((unsigned)N), dim3(256), 0, ftmi_hs(stream), w,
                      N, K, Kpad, (_Float16 *)out,
-                     (float *)((char *)out + 3 * N * Kpad * 2));
+                     (float *)((char *)out + 3 * N * Kpad * 2), frag);
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
+}
+
+extern "C" int ftmi_split_weights_f16(const float *w, int64_t N, int64_t K, void *out,
+                                      ftmi_stream_t stream) {
+  return split_f16(w, N, K, out, 0, stream);
+}
+
+extern "C" int ftmi_split_weights_f16_frag(const float *w, int64_t N, int64_t K, void *out,
+                                           ftmi_stream_t stream) {
+  return split_f16(w, N, K, out, 1, stream);
 }
 
 extern "C" int ftmi_split_weights(const float *w, int64_t N, int64_t K, void *out,

@@ -233,18 +233,20 @@ def split_weights(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def split_weights_f16(w: torch.Tensor) -> torch.Tensor:
+def split_weights_f16(w: torch.Tensor, frag: bool = False) -> torch.Tensor:
     """fp32 [N][K] -> the f16x3 operand of `ftmi_split_weights_f16` (uint8 bytes: f16 planes
     [3][N][roundup(K, 32)] = (2^11 h, t, h) of the power-of-two column-scaled rows, then
-    float colscale[N])."""
+    float colscale[N]).  frag: the planes in the fragment-major order of
+    `ftmi_split_weights_f16_frag` (the operand of `highway_stack`)."""
     _dev(w)
     if w.dim() != 2 or w.dtype != _f32 or not w.is_contiguous():
         raise ValueError('split_weights_f16: contiguous fp32 [N][K] expected')
     N, K = w.shape
     nbytes = int(_lib.load().ftmi_split_weights_f16_bytes(N, K))
     out = torch.empty(nbytes, device=w.device, dtype=torch.uint8)
-    launch('ftmi_split_weights_f16', f'split_weights_f16[N={N},K={K}]', 0, 4.0 * N * K + nbytes,
-           w.data_ptr(), N, K, out.data_ptr(), _stream())
+    name = 'ftmi_split_weights_f16_frag' if frag else 'ftmi_split_weights_f16'
+    launch(name, f'split_weights_f16[N={N},K={K}{",frag" if frag else ""}]', 0,
+           4.0 * N * K + nbytes, w.data_ptr(), N, K, out.data_ptr(), _stream())
     return out
 
 
@@ -365,6 +367,52 @@ def highway(x: torch.Tensor, w12: torch.Tensor, b1: torch.Tensor, b2: torch.Tens
            b2.data_ptr(), y.data_ptr(), y.stride(1), mma, status_word(x.device).data_ptr(),
            sk, _ptr(part), _stream())
     return y
+
+
+HS_C, HS_NPASS, HS_MAXL = 256, 512, 8  # gemm.hip highway_stack_kernel shape limits
+# The fused stack below FTMI_HS_MIN rows falls back to the per-layer launches (the skinny
+# weight-streaming kernels win there: a handful of row tiles cannot spread the weight reads)
+HS_MIN_ROWS = int(os.environ.get('FTMI_HS_MIN', 256))
+
+
+def highway_stack_ok(M: int, Cp: int, C: int, L: int, n_out: int, splits) -> bool:
+    """Whether `highway_stack` applies: the f16x3 path is the one in force (not inside
+    exact_paths()), every weight has its f16 planes, and the shapes fit the kernel."""
+    if os.environ.get('FTMI_HS', '1') == '0' or (_FORCED and _FORCED[-1][0] != 2):
+        return False
+    if not _FORCED and MMA != 2:
+        return False
+    return (C == HS_C and 0 < Cp <= C and Cp % 4 == 0 and L <= HS_MAXL
+            and n_out % HS_NPASS == 0 and M >= max(HS_MIN_ROWS, 1)
+            and all(w is not None and w.dtype == torch.uint8 for w in splits))
+
+
+def highway_stack(x: torch.Tensor, pre_split: torch.Tensor, C: int, hw_splits, b1s, b2s,
+                  out_split: Optional[torch.Tensor], b_out: Optional[torch.Tensor], n_out: int,
+                  want_h: bool = False):
+    """CBHG pre_highway -> highways -> GRU input projection in one launch
+    (`ftmi_highway_stack`; models/common_layers.py:110-115).  x: (B, T, Cp) channels-last;
+    every weight block is `split_weights_f16(w, frag=True)`.  Returns (y (B, T, n_out) or
+    None, h (B, T, C) or None)."""
+    _dev(x, pre_split, out_split, b_out, *hw_splits, *b1s, *b2s)
+    B, T, Cp, xs = _rows(x)
+    M = B * T
+    L = len(hw_splits)
+    y = torch.empty(B, T, n_out, device=x.device, dtype=_f32) if out_split is not None else None
+    h = torch.empty(B, T, C, device=x.device, dtype=_f32) if want_h else None
+    arr = ctypes.c_void_p * max(L, 1)
+    w_arr = arr(*[w.data_ptr() for w in hw_splits])
+    b1_arr = arr(*[b.data_ptr() for b in b1s])
+    b2_arr = arr(*[b.data_ptr() for b in b2s])
+    flops = 2.0 * M * C * (Cp + L * 2 * C + n_out)
+    nbytes = 4.0 * M * (Cp + n_out + (C if want_h else 0))
+    launch('ftmi_highway_stack', f'highway_stack[M={M},Cp={Cp},L={L},N={n_out}]', flops, nbytes,
+           x.data_ptr(), xs, M, Cp, C, pre_split.data_ptr(), L, ctypes.addressof(w_arr),
+           ctypes.addressof(b1_arr), ctypes.addressof(b2_arr), _ptr(out_split), _ptr(b_out),
+           n_out if out_split is not None else 0, _ptr(y), y.stride(1) if y is not None else 0,
+           _ptr(h), h.stride(1) if h is not None else 0, status_word(x.device).data_ptr(),
+           _stream())
+    return y, h
 
 
 def rnn_blocks(cell: int, B: int, H: int, mma: Optional[int] = None) -> int:

@@ -188,6 +188,33 @@ int ftmi_highway_split(const float *x, int64_t x_stride, int64_t M, int32_t C,
                        uint32_t *status, int32_t split_k, float *split_ws,
                        ftmi_stream_t stream);
 
+/* CBHG highway stack in one launch (ABI 9; common_layers.py:110-115 + the GRU's input
+ * projection): h = x W_pre^T (pre_highway, no bias), then L highway layers as ftmi_highway,
+ * then y = h W_out^T + b_out.  Activations stay on chip between layers; the result is
+ * bit-identical to the unfused ftmi_conv1d / ftmi_highway chain on FTMI_MMA_F16X3.
+ *   x: M rows of Cp floats (Cp % 4 == 0, Cp <= C), C == 256 (the CBHG channels)
+ * Every weight operand is an ftmi_split_weights_f16_FRAG block (fragment-major planes):
+ *   w_pre_split: of W_pre [C][Cp]
+ *   w_hw_split[l], b1[l], b2[l]: host arrays of L (<= 8) device pointers — the block of
+ *     each highway's packed w12 [2C][C] and its biases
+ *   w_out_split: of W_out [n_out][C] (n_out % 512 == 0) and b_out
+ *     (nullable) -> y (M x n_out, row stride y_stride); NULL with n_out = 0, y = NULL: none
+ *   h: optional (nullable) copy of the last highway's output (M x C, row stride h_stride)
+ * status: bit 0 when an activation is beyond the f16 range (rerun on the unfused exact path).
+ * ---------------------------------------------------------------------------------- */
+/* ftmi_split_weights_f16 with the planes in the fragment-major order of the 16x16x32 f16
+ * MFMA B operand, [N/16][Kpad/32][64][8] (lane = n % 16 + 16 ((k / 8) % 4), element k % 8;
+ * ABI 9): same byte size (ftmi_split_weights_f16_bytes), N % 16 == 0. */
+int ftmi_split_weights_f16_frag(const float *w, int64_t N, int64_t K, void *out,
+                                ftmi_stream_t stream);
+
+int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, int32_t Cp, int32_t C,
+                       const void *w_pre_split, int32_t L, const void *const *w_hw_split,
+                       const float *const *b1, const float *const *b2,
+                       const void *w_out_split, const float *b_out, int32_t n_out, float *y,
+                       int64_t y_stride, float *h, int64_t h_stride, uint32_t *status,
+                       ftmi_stream_t stream);
+
 /* ------------------------------------------------------------------------------------
  * Bidirectional single-layer GRU / LSTM recurrence, PyTorch semantics, h0 = c0 = 0,
  * both directions over the full padded length (no packing), output [fwd | bwd].

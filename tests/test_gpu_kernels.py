@@ -211,6 +211,66 @@ def test_highway(rng, mma, pre, kernel, C, B, T, monkeypatch):
     close(host(ops.highway(dev(x), w12, b1, b2, mma=mma, w_split=wsplit(w12, pre, mma))), ref)
 
 
+@pytest.mark.parametrize('B,T,Cp,L', [(2, 1600, 80, 4), (3, 77, 256, 4), (1, 40, 80, 2),
+                                     (2, 300, 128, 0)])
+def test_highway_stack(B, T, Cp, L, rng, monkeypatch):
+    """pre_highway -> L highways -> GRU input projection in one launch
+    (ftmi_highway_stack) against the numpy oracle (fp32 bound) and against the unfused
+    f16x3 slab-kernel chain it replaces (conv1d, L x highway, conv1d): bit for bit where
+    those launches run unsplit, else within 1e-6."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import CBHG
+    monkeypatch.setenv('FTMI_GEMM_SKINNY', '0')  # the unfused chain on the slab kernel
+    C = 256
+    torch.manual_seed(3)
+    m = CBHG(K=2, in_channels=Cp, channels=C, proj_channels=[C, Cp], num_highways=L)
+    with torch.no_grad():
+        for hw in m.highways:
+            hw.W1.bias.normal_(0, 0.1)
+    m = m.cuda()
+    x = rng.normal(0, 1, (B, T, Cp)).astype(np.float32)
+    *_, w_pre, _, pre3 = m.packed_weights()
+    hws = [hw.packed_weights() for hw in m.highways]
+    w_ih, b_in, _, _, w3 = m.rnn.packed_weights()
+    xd = dev(x)
+    pre_f, hw_f, b1s, b2s, ih_f, _, n_out = m._stack_pack()
+    y, h = ops.highway_stack(xd, pre_f, C, hw_f, b1s, b2s, ih_f, b_in, n_out, want_h=True)
+    # numpy oracle
+    ref = x.reshape(-1, Cp).astype(np.float64) @ host(w_pre).astype(np.float64).T
+    for i, hw in enumerate(m.highways):
+        sd = {f'h.{k}': host(v) for k, v in hw.state_dict().items()}
+        ref = O.highway(sd, 'h', ref, np.float64)
+    close(host(h).reshape(-1, C), ref)
+    refp = ref @ host(w_ih).astype(np.float64).T + host(b_in)
+    close(host(y).reshape(-1, w_ih.size(0)), refp)
+    # the unfused chain
+    hu, _ = ops.conv1d(xd, w_pre, 1, 0, w_split=pre3)
+    for w12, b1, b2, s3 in hws:
+        hu = ops.highway(hu, w12, b1, b2, w_split=s3)
+    yu, _ = ops.conv1d(hu, w_ih, 1, 0, bias=b_in, w_split=w3)
+    if B * T >= 3200:  # unfused launches without a split-K (whose partial sums round apart)
+        np.testing.assert_array_equal(host(h), host(hu))
+        np.testing.assert_array_equal(host(y), host(yu))
+    else:
+        close(host(h), host(hu), rtol=1e-6, atol=1e-6)
+        close(host(y), host(yu), rtol=1e-6, atol=1e-6)
+
+
+def test_highway_stack_range_guard(rng):
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import CBHG
+    m = CBHG(K=2, in_channels=80, channels=256, proj_channels=[256, 80], num_highways=2).cuda()
+    pre_f, hw_f, b1s, b2s, *_ = m._stack_pack()
+    x = rng.normal(0, 1, (1, 100, 80)).astype(np.float32)
+    st = ops.status_word('cuda')
+    for bad in (False, True):
+        if bad:
+            x[0, 17, 5] = 7e4
+        st.zero_()
+        ops.highway_stack(dev(x), pre_f, 256, hw_f, b1s, b2s, None, None, 0, want_h=True)
+        assert bool(int(st.item()) & 1) == bad
+
+
 def test_split_weights_exact(rng):
     """The three bf16 pieces sum back to the fp32 weights exactly; K padding is zero."""
     from forwardtacotron_amd import ops
@@ -242,6 +302,20 @@ def test_split_weights_f16_layout(rng):
     ws = w.astype(np.float64)
     assert np.all(np.abs(back[:, :K] - ws) <= 2.0 ** -22 * np.abs(ws) + 1e-30)
     assert not planes[:, :, K:].any()
+
+
+def test_split_weights_f16_frag_layout(rng):
+    """The fragment-major planes hold the row-major planes' elements at
+    [n/16][k/32][n%16 + 16 (k/8 % 4)][k%8]; the column scales are the same."""
+    from forwardtacotron_amd import ops
+    N, K = 48, 80
+    w = dev(rng.normal(0, 1, (N, K)).astype(np.float32))
+    rm, fm = host(ops.split_weights_f16(w)), host(ops.split_weights_f16(w, frag=True))
+    Kp = 96
+    a = rm[:3 * N * Kp * 2].view(np.float16).reshape(3, N // 16, 16, Kp // 32, 4, 8)
+    b = fm[:3 * N * Kp * 2].view(np.float16).reshape(3, N // 16, Kp // 32, 4, 16, 8)
+    np.testing.assert_array_equal(a.transpose(0, 1, 3, 4, 2, 5), b)
+    np.testing.assert_array_equal(rm[3 * N * Kp * 2:], fm[3 * N * Kp * 2:])
 
 
 def test_f16x3_range_guard(rng):
