@@ -168,6 +168,29 @@ class ForwardTacotron(nn.Module):
                 self.energy_proj.weight.detach().reshape(-1, 3).contiguous(),
                 self.energy_proj.bias.detach().contiguous())
 
+    def _folded_series_weights(self):
+        """The pitch / energy projections carried through the LSTM's input projection:
+        W_ih (enc + ps proj_p(pitch) + es proj_e(energy)) + b
+          = (W_ih enc + b) + ps (W_ih W_p * pitch + W_ih b_p) + es (W_ih W_e * energy + W_ih b_e),
+        so the projection of enc can start as soon as the prenet ends and the predictors'
+        outputs are added to its (B, T, 4H) rows afterwards (the same series_proj_add kernel
+        with 4H-wide weights).  Made once per weights version, in float64."""
+        key = (self.lstm._pack_key(), self.pitch_proj.weight._version, self.pitch_proj.bias._version,
+               self.energy_proj.weight._version, self.energy_proj.bias._version,
+               self.pitch_proj.weight.data_ptr(), self.energy_proj.weight.data_ptr())
+        cache = self.__dict__.get('_ftmi_fold')
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                w_ih = self.lstm.packed_weights()[0].double()  # [2*4H][In], both directions
+                out = []
+                for w, b in (self.pitch_proj.weight, self.pitch_proj.bias), \
+                            (self.energy_proj.weight, self.energy_proj.bias):
+                    out.append((w_ih @ w.detach().double().reshape(-1, 3)).float().contiguous())
+                    out.append((w_ih @ b.detach().double()).float().contiguous())
+            cache = (key, tuple(out))
+            self.__dict__['_ftmi_fold'] = cache
+        return cache[1]
+
     def _encode(self, x: torch.Tensor, pitch: torch.Tensor, energy: torch.Tensor) -> torch.Tensor:
         """embedding -> prenet CBHG -> + pitch / energy projections: (B, T, 2*prenet_dims)."""
         h = ops.embedding(x, self.embedding.weight.detach())
@@ -348,12 +371,14 @@ class ForwardTacotron(nn.Module):
         energy and the prenet run on three side streams while the caller's stream runs the
         duration predictor and the LengthRegulator bookkeeping (fill-2 rule, counts, T_mel).
         The prenet stream (high priority: its chain is the phase's critical path) continues
-        with the encoder tail (pitch / energy projections, after those streams) and the
-        LSTM input projection: neither depends on T_mel, so they run while the duration path
-        finishes and the host waits for T_mel (the one host sync, a pinned copy queued right
-        after the duration kernel).  Issue order = priority order: prenet, durations, pitch,
+        with the LSTM input projection of the prenet output (independent of the predictors)
+        and then, after the pitch / energy streams, adds their projections through W_ih:
+        none of it depends on T_mel, so it runs while the duration path finishes and the
+        host waits for T_mel (the one host sync, a pinned copy queued right after the
+        duration kernel).  Issue order = priority order: prenet, durations, pitch,
         energy.  Returns (dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel, xp) with every
-        tensor ready on the caller's stream (xp: the LSTM input projection of enc).
+        tensor ready on the caller's stream (xp: the LSTM input projection of enc plus the
+        pitch / energy projections, folded through W_ih; enc itself does not carry them).
         capture=True (graph capture, see _phoneme_graph): no host sync, the T_mel slot holds
         max(totals) on the device."""
         main = torch.cuda.current_stream(x.device)
@@ -362,6 +387,9 @@ class ForwardTacotron(nn.Module):
             s.wait_stream(main)
         with torch.cuda.stream(s_prenet):
             enc = self.prenet.forward_cl(ops.embedding(x, self.embedding.weight.detach()))
+            # the LSTM input projection right after the prenet; the pitch / energy terms are
+            # added to its rows once the predictors are done (_folded_series_weights)
+            xp = self.lstm.project(enc)
         dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
         t_host = t_ready = None
         tmax = None
@@ -385,10 +413,9 @@ class ForwardTacotron(nn.Module):
                 s_prenet.wait_stream(s)
                 if not capture:
                     t.record_stream(s_prenet)
-            wp, bp, we, be = self._series_proj_weights()
-            ops.series_proj_add(enc, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we,
+            wp, bp, we, be = self._folded_series_weights()
+            ops.series_proj_add(xp, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we,
                                 be, self.energy_strength)
-            xp = self.lstm.project(enc)
         if batch is not None:  # a shard of a larger batch (sharded.GlobalBatch): batch-global
             offsets, totals = batch.duration_counts(dur_hat)  # fill rule / T_mel
             T_mel = batch.t_mel(totals)
@@ -457,7 +484,7 @@ class ForwardTacotron(nn.Module):
         """`models/forward_tacotron.py:289-330`.  enc: the prenet output if already computed;
         lr: (offsets, T_mel) if the LengthRegulator counts were already computed (then
         dur_hat has already been clipped / filled in place); xp: the LSTM input projection
-        if already queued (then enc already carries the pitch / energy projections)."""
+        with the pitch / energy terms if already queued (then enc is not read)."""
         if enc is None:
             enc = self.prenet.forward_cl(ops.embedding(x, self.embedding.weight.detach()))
         if xp is None:
