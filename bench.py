@@ -3,28 +3,40 @@
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
 
-Workload (BASELINE.json configs[2], "c3"; --model fast_pitch: configs[4], "c5"): ForwardTacotron LJSpeech config, batch = 64
-synthetic phoneme sequences per GPU (lengths U{50..200}, ids U{1..134}, pad 0; seed =
-rank), synthetic weights (forwardtacotron_amd.synthetic, no checkpoint download), fp32.
-A step is one full `generate()` call on one batch whose tokens are already resident in HBM
-(pitch / energy identity callbacks, alpha = 1).  Frames = B * T_mel of the returned
-mel_post (padded frames, as the reference returns them).
+Workload (default: BASELINE.json configs[2], "c3"): ForwardTacotron LJSpeech config, batch =
+64 synthetic phoneme sequences per GPU (lengths U{50..200}, ids U{1..134}, pad 0; seed =
+rank), synthetic weights (forwardtacotron_amd.synthetic, no checkpoint download), fp32-level
+arithmetic (f16x3 MFMA split, range-guarded).  A step is one full `generate()` call on one
+batch whose tokens are already resident in HBM (pitch / energy identity callbacks, alpha =
+1).  Frames = B * T_mel of the returned mel_post (padded frames, as the reference returns
+them); `valid_frames_per_s` counts only each utterance's own frames.
+  --config c2            configs[1]: batch 1, 120 phonemes
+  --callbacks gen_forward  the callbacks gen_forward.py:103-104 passes
+                         (pitch_function = lambda x: x * amp, energy_function = lambda x: x)
+  --model fast_pitch     configs[4], "c5": FastPitch, batch 64, lengths U{50..200}
 
-Multi-GPU (c4, BASELINE.json configs[3]): the ranks hold the shards (64 utterances each,
-seed = rank) of ONE global batch and run forwardtacotron_amd.sharded.generate_sharded:
-global phoneme padding, the batch-global fill-2 rule and T_mel by scalar RCCL all-reduces,
-the mel_post all-gathered to every rank — the reference's output for the global batch
-(weak scaling: per-GPU work fixed).  Barrier + synchronize around the K timed steps, max
-elapsed over ranks, value = frames of the global mel_post / that time.
+Multi-GPU (c4, BASELINE.json configs[3]): rank 0 makes the synthetic weights and
+broadcasts them (sharded.broadcast_state: one bucketed RCCL broadcast per dtype); the
+ranks hold the shards (64 utterances each, seed = rank) of ONE global batch and run
+forwardtacotron_amd.sharded.generate_sharded(gather='rank0'): global phoneme padding, the
+batch-global fill-2 rule and T_mel by scalar RCCL all-reduces, mel_post gathered to rank 0
+only (result collection) — the reference's output for the global batch (weak scaling:
+per-GPU work fixed).  Barrier + synchronize around the K timed steps, max elapsed over
+ranks, value = frames of the global mel_post / that time.
 
 The JSON line also carries
   roofline     the dominant kernel (largest device time inside the timed steps, measured
-               with HIP events on the launch stream): algorithmic FLOPs (or bytes) per launch
-               / its average duration, against the peak of the arithmetic that kernel
-               issues: bf16 MFMA / 6 for the fp32-accurate bf16x6 path (labels mma=1),
-               the fp32 MFMA peak otherwise, or HBM bandwidth for byte-bound kernels;
+               with HIP events on the launch stream): algorithmic FLOPs per launch / its
+               average duration, against the peak of the arithmetic that kernel issues
+               (f16x3 "mma=2": dense f16 MFMA / 3; bf16x6 "mma=1": / 6; fp32 MFMA), and
+               `traffic` = HBM bytes per launch from the committed PMC passes;
+  host_to_host the PCIe-inclusive rate: token ids H2D + generate() + mel_post D2H per step,
+               as gen_forward.py:111-120 does (a second timed loop; never `value`);
+  prenet_bank  the north-star kernel (fused Conv1d+ReLU+BN CBHG bank) against HBM and MFMA;
   cpu_baseline rank 0, N = 1: the torch-CPU restatement of the reference (oracle/
-               ft_torch_cpu.py, same ATen CPU kernels as the reference) on the same batch;
+               ft_torch_cpu.py, the reference's ATen CPU kernels) on the same batch at all
+               host threads given (CPU model, physical cores, threads used) and on 1 thread
+               for the first 8 utterances;
   parity       mean / max |mel_post GPU - CPU| on that batch, and LR counts equality.
 """
 from __future__ import annotations
