@@ -808,6 +808,265 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 #endif
 }
 
+// ---- small batches (B <= 4, e.g. batch-1 generation, config c2): exact fp32 GEMV -----
+// At B = 1 the MFMA kernel above multiplies 16-column tiles with one live column and runs
+// three f16 products per fp32 product on the per-step critical chain.  Here a group is one
+// DIRECTION (all B <= NBV sequences), spread over BPG = H / U workgroups that each own U
+// hidden units (R = G*U rows of W_hh, fp32, in VGPRs).  Thread (row pair rg, k-segment ks)
+// holds 2 rows x SEG = H / 8 weights; per step it multiplies them by its segment of h_{t-1}
+// (LDS, broadcast to the 8 row pairs of a wave), the 8 segments of a row are summed with
+// xor shuffles, and U*B threads apply the cell update to the (unit, sequence) cells they
+// own.  Exact fp32 FMAs, no split: the recurrence is fp32 like the reference's.  The h
+// hand-off is the MFMA kernel's: step-tagged values (mantissa LSB), two parity halves,
+// polled with sc1 loads, the census placing a direction's workgroups on one XCD (plain
+// stores, L2-local) with the global write-through fallback.  Layout of a group's slab in
+// the exchange buffer: [sequence][H] floats.
+constexpr int GV_KSEG = 8;  // k-segments per row (lanes summed by shuffles)
+constexpr int GV_RPT = 2;   // rows per thread
+
+template <int CELL, int H, int U, int NBV>
+__global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * GV_KSEG) void rnn_gemv_kernel(
+    const RnnParams p) {
+  constexpr int G = CELL ? 4 : 3;
+  constexpr int R = G * U;
+  constexpr int NT = R / GV_RPT * GV_KSEG;  // threads
+  constexpr int SEG = H / GV_KSEG;
+  constexpr int SEGP = SEG + 4;             // LDS pitch of a segment: conflict-free b128 reads
+  constexpr int BPG = H / U;
+  constexpr int HF4 = H / 4;                // float4 of one sequence's h
+  static_assert(R % GV_RPT == 0 && SEG % 4 == 0 && U * NBV <= NT && NT % 64 == 0, "shape");
+  static_assert(BPG <= FLAGS_PER_GROUP, "group size");
+  __shared__ __attribute__((aligned(16))) float hl[2][NBV * GV_KSEG * SEGP];
+  __shared__ float red[R][NBV];
+  __shared__ int s_abort, s_group, s_bi, s_mode;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int ks = tid % GV_KSEG, rg = tid / GV_KSEG;
+
+  // ---- group (= direction) assignment: the census of the MFMA kernel ----------------
+  if (tid == 0) {
+    int mode = 0, group = blockIdx.x % p.ngroups, bi = blockIdx.x / p.ngroups, abort = 0;
+    if (p.xcd_local) {
+      const unsigned x = xcc_id();
+      const unsigned slot = __hip_atomic_fetch_add(p.ws + WS_CENSUS + x * CNT_PAD, 1u,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(p.ws + WS_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!poll_ge(p.ws + WS_ARRIVE, gridDim.x, p.spin_limit)) {
+        abort = 1;
+        report_timeout(p);
+      } else if ((int)gridDim.x == 8 * BPG) {  // XCD x hosts group x (x < 2)
+        bool balanced = true;
+        for (int i = 0; i < 8; ++i)
+          balanced &= __hip_atomic_load(p.ws + WS_CENSUS + i * CNT_PAD, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT) == (unsigned)BPG;
+        if (balanced) {
+          mode = 1;
+          group = (int)x;
+          bi = (int)slot;
+        }
+      }
+    }
+    s_mode = mode;
+    s_group = group;
+    s_bi = bi;
+    s_abort = abort;
+  }
+  __syncthreads();
+  if (s_abort) return;
+  if (s_group >= p.ngroups || s_bi >= BPG) return;  // surplus workgroups of the padded grid
+  const int dir = s_group, u0 = s_bi * U;
+  const bool xcd_mode = s_mode == 1;
+
+  // ---- W_hh rows (gate g, unit u0 + u) of this thread's pair, its k-segment, fp32 ------
+  const float *wdir = p.w_hh + (size_t)dir * (G * H) * H;
+  float w[GV_RPT][SEG];
+#pragma unroll
+  for (int i = 0; i < GV_RPT; ++i) {
+    const int r = rg * GV_RPT + i;
+    const float *src = wdir + (size_t)((r / U) * H + u0 + r % U) * H + ks * SEG;
+#pragma unroll
+    for (int j = 0; j < SEG; j += 4) {
+      const f32x4 v = *(const f32x4 *)(src + j);
+      w[i][j] = v.x;
+      w[i][j + 1] = v.y;
+      w[i][j + 2] = v.z;
+      w[i][j + 3] = v.w;
+    }
+  }
+
+  // ---- the cell of this thread (threads < U * B): unit cu, sequence cb -----------------
+  const bool is_cell = tid < U * p.B;
+  const int cu = tid % U, cb = is_cell ? tid / U : 0;
+  float hstate = 0.f, cstate = 0.f, bhh[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) bhh[g] = (CELL == 0) ? p.b_hh[dir * G * H + g * H + u0 + cu] : 0.f;
+  const int len = (p.lengths && is_cell) ? p.lengths[cb] : p.T;
+  const int32_t *iptr = p.index ? p.index + (size_t)cb * p.T : (const int32_t *)p.ws;
+  const float *xcol = p.xp + dir * G * H + u0 + cu;
+  const float *zcol = (p.index ? p.xp_zero : p.xp) + dir * G * H + u0 + cu;
+  auto frame = [&](int t) { return dir ? (p.T - 1 - t) : t; };
+  auto load_idx = [&](int t) -> int { return iptr[p.index ? frame(t < p.T ? t : p.T - 1) : 0]; };
+  auto load_gx = [&](int t, int ir, float (&g)[G]) {
+    const int tt = frame(t < p.T ? t : p.T - 1);
+    const int src = p.index ? ir : tt;
+    const float *row = src >= 0 ? xcol + ((size_t)cb * p.T_src + src) * p.xp_stride : zcol;
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) g[gi] = row[gi * H];
+  };
+  float g0[G], g1[G], g2[G];
+  int i0 = load_idx(0), i1 = load_idx(1);
+  load_gx(0, i0, g0);
+  load_gx(1, i1, g1);
+  int i2 = load_idx(2);
+
+  // ---- exchange: parity halves [2][2 dirs][NBV][H] --------------------------------------
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.hx, (short)0, 0x7FFFFFF0, 0x00020000);
+  const int par_bytes = 2 * NBV * H * 4;
+  const int nf4 = p.B * HF4;  // float4 of h a workgroup acquires per step
+  const unsigned hx_off = (unsigned)(((dir * NBV + cb) * H + u0 + cu) * 4);  // this cell's h
+
+  auto step = [&](int t, const float (&gx)[G], float (&gnext)[G], int inext, int &iload) -> bool {
+    const int tt = frame(t);
+    float *hb = hl[t & 1];
+    // ---- acquire h_{t-1} (zero at t = 0) into LDS, segment-padded ------------------------
+    const unsigned want = h_tag(t - 1);
+    for (int f = tid; f < nf4; f += NT) {
+      const int b = f / HF4, k = (f - b * HF4) * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (t > 0) {
+        const unsigned off = (unsigned)(((dir * NBV + b) * H + k) * 4);
+        const int soff = ((t - 1) & 1) * par_bytes;
+        for (unsigned spins = 0;; ++spins) {
+          typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, soff, 16);
+          const bool fresh = want ? ((r.x & r.y & r.z & r.w) & 1u) != 0u
+                                  : ((r.x | r.y | r.z | r.w) & 1u) == 0u;
+          if (fresh || (p.diag & 2)) {
+            v = __builtin_bit_cast(f32x4, r);
+            break;
+          }
+          if (spins > p.spin_limit) {
+            s_abort = 1;
+            report_timeout(p);
+            break;
+          }
+        }
+      }
+      *(f32x4 *)&hb[b * GV_KSEG * SEGP + (k / SEG) * SEGP + k % SEG] = v;
+    }
+    // sequences past B (NBV > B): zero segments
+    for (int f = nf4 + tid; f < NBV * HF4; f += NT) {
+      const int b = f / HF4, k = (f - b * HF4) * 4;
+      *(f32x4 *)&hb[b * GV_KSEG * SEGP + (k / SEG) * SEGP + k % SEG] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();
+    if (s_abort) return false;
+    if (is_cell) {  // the projections two steps ahead (independent of h)
+      load_gx(t + 2, inext, gnext);
+      iload = load_idx(t + 3);
+    }
+    // ---- partial gate sums over this thread's segment, then over the 8 segments ---------
+    float acc[GV_RPT][NBV];
+#pragma unroll
+    for (int i = 0; i < GV_RPT; ++i)
+#pragma unroll
+      for (int b = 0; b < NBV; ++b) acc[i][b] = 0.f;
+#pragma unroll
+    for (int b = 0; b < NBV; ++b) {
+      const float *hs = hb + b * GV_KSEG * SEGP + ks * SEGP;
+#pragma unroll
+      for (int j = 0; j < SEG; j += 4) {
+        const f32x4 hv = *(const f32x4 *)(hs + j);
+#pragma unroll
+        for (int i = 0; i < GV_RPT; ++i) {
+          acc[i][b] = fmaf(w[i][j], hv.x, acc[i][b]);
+          acc[i][b] = fmaf(w[i][j + 1], hv.y, acc[i][b]);
+          acc[i][b] = fmaf(w[i][j + 2], hv.z, acc[i][b]);
+          acc[i][b] = fmaf(w[i][j + 3], hv.w, acc[i][b]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GV_RPT; ++i)
+#pragma unroll
+      for (int b = 0; b < NBV; ++b) {
+        float v = acc[i][b];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        acc[i][b] = v;
+      }
+    if (ks < GV_RPT)
+#pragma unroll
+      for (int b = 0; b < NBV; ++b)
+        red[rg * GV_RPT + ks][b] = ks == 0 ? acc[0][b] : acc[GV_RPT - 1][b];
+    __syncthreads();
+    // ---- cell update (the MFMA kernel's formulas) -----------------------------------------
+    if (is_cell) {
+      float gs[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) gs[g] = red[g * U + cu][cb];
+      float hn;
+      if (CELL == 0) {
+        const float r = fast_sigmoid(gx[0] + (gs[0] + bhh[0]));
+        const float z = fast_sigmoid(gx[1] + (gs[1] + bhh[1]));
+        const float n = fast_tanh(gx[2] + r * (gs[2] + bhh[2]));
+        hn = n + z * (hstate - n);
+      } else {
+        const float ig = fast_sigmoid(gx[0] + gs[0]);
+        const float fg = fast_sigmoid(gx[1] + gs[1]);
+        const float gg = fast_tanh(gx[2] + gs[2]);
+        const float og = fast_sigmoid(gx[3] + gs[3]);
+        cstate = fg * cstate + ig * gg;
+        hn = og * fast_tanh(cstate);
+      }
+      if (tt >= len) {
+        hn = 0.f;
+        cstate = 0.f;
+      }
+      hn = __uint_as_float((__float_as_uint(hn) & ~1u) | h_tag(t));
+      hstate = hn;
+      const float yout = tt >= len ? p.pad_value : hn;
+      const int soff = (t & 1) * par_bytes;
+      if (xcd_mode)  // stays in this XCD's L2, read back by same-XCD sc1 loads
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hn), rsrc, hx_off, soff, 0);
+      else  // write-through (sc1)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hn), rsrc, hx_off, soff, 16);
+      p.y[((size_t)cb * p.T + tt) * p.y_stride + dir * H + u0 + cu] = yout;
+    }
+    return true;
+  };
+
+  for (int t = 0; t < p.T; t += 3) {
+    if (!step(t, g0, g2, i2, i0)) break;
+    if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1)) break;
+    if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2)) break;
+  }
+}
+
+template <int CELL, int H, int U>
+int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
+  constexpr int BPG = H / U;
+  constexpr int NT = (CELL ? 4 : 3) * U / GV_RPT * GV_KSEG;
+  if (8 * BPG > max_blocks) return FTMI_E_UNSUPPORTED;
+  p.chunk0 = 0;
+  p.ngroups = 2;
+  // one direction's BPG workgroups per XCD (the census seats direction x on XCD x; the
+  // other XCDs' workgroups retire after the census barrier)
+  const int nblk = p.xcd_local ? 8 * BPG : 2 * BPG;
+#define FTMI_GEMV_LAUNCH(NBV_)                                                           \
+  hipLaunchKernelGGL((rnn_gemv_kernel<CELL, H, U, NBV_>), dim3(nblk), dim3(NT), 0, s, p); \
+  break;
+  switch (p.B) {
+    case 1: FTMI_GEMV_LAUNCH(1)
+    case 2: FTMI_GEMV_LAUNCH(2)
+    default: FTMI_GEMV_LAUNCH(4)
+  }
+#undef FTMI_GEMV_LAUNCH
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
 template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false>
 int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
   constexpr int BPG = H / U;
@@ -851,6 +1110,22 @@ int device_cu_count() {
 
 }  // namespace
 
+// B <= GV_MAXB: the exact-fp32 GEMV recurrence (rnn_gemv_kernel), 16 units per workgroup;
+// FTMI_RNN_GEMV=0 keeps the MFMA kernel
+constexpr int GV_MAXB = 4;
+static bool gemv_path(int cell, int B, int H) {
+  const char *v = getenv("FTMI_RNN_GEMV");  // read per call: tests switch it
+  const int env = v ? atoi(v) : 1;
+  return env && B <= GV_MAXB && ((cell == 1 && H == 512) || (cell == 0 && (H == 64 || H == 128 || H == 256)));
+}
+static int xcd_local_env() {
+  static const int v = [] {
+    const char *e = getenv("FTMI_RNN_XCD_LOCAL");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 // hidden units per workgroup of the instance ftmi_rnn_bidir dispatches (see there)
 static int rnn_units(int cell, int H, int mma) {
   if (cell == 0 && H == 64) {
@@ -865,6 +1140,7 @@ static int rnn_units(int cell, int H, int mma) {
 
 extern "C" int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t mma) {
   if (B <= 0 || H <= 0 || H % 16 != 0) return 0;
+  if (gemv_path(cell, B, H)) return (xcd_local_env() ? 8 : 2) * (H / 16);  // launch_gemv
   const int bpg = H / rnn_units(cell, H, mma);
   const int maxb = device_cu_count();
   const int max_groups = (maxb / bpg) & ~1;
@@ -910,10 +1186,6 @@ static int rnn_setup(RnnParams &p, int B, int T, int H, int cell, const float *w
   const int64_t wsb = ftmi_rnn_workspace_bytes(B, H, cell);
   hipError_t e = hipMemsetAsync(sync, 0, (size_t)wsb, s);
   if (e != hipSuccess) return (int)e;
-  static const int xcd_env = [] {
-    const char *v = getenv("FTMI_RNN_XCD_LOCAL");
-    return v ? atoi(v) : 1;
-  }();
   p.w_hh = w_hh;
   p.b_hh = b_hh;
   p.y = y;
@@ -923,7 +1195,7 @@ static int rnn_setup(RnnParams &p, int B, int T, int H, int cell, const float *w
   p.B = B;
   p.T = T;
   p.ngroups_total = 2 * nchunks;
-  p.xcd_local = xcd_env;
+  p.xcd_local = xcd_local_env();
   p.ws = (unsigned *)sync;
   p.hx = (float *)((char *)sync + ctl);
   p.status = status;
@@ -962,6 +1234,13 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   p.index = index;
   p.xp_zero = xp_zero;
   const int maxb = device_cu_count();
+  // small batches: exact fp32 GEMV recurrence (any mma: it is exact)
+  if (gemv_path(cell, B, H)) {
+    if (cell == 1) return launch_gemv<1, 512, 16>(p, maxb, s);
+    if (H == 256) return launch_gemv<0, 256, 16>(p, maxb, s);
+    if (H == 128) return launch_gemv<0, 128, 16>(p, maxb, s);
+    return launch_gemv<0, 64, 16>(p, maxb, s);
+  }
 #define FTMI_RNN_MODES(CELL_, H_, U_, WKX_, WKF_)                                   \
   switch (mma) {                                                                    \
     case 2: return launch_rnn<CELL_, H_, U_, WKX_, 2>(p, nchunks, maxb, s);          \

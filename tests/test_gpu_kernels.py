@@ -392,9 +392,11 @@ def test_lstm_bidir(rng, rnn_mma, monkeypatch):
 def test_rnn_f16x3_kernels(cell, H, B, T, rng, monkeypatch):
     """The f16x3 recurrence over batch sizes that exercise one chunk (B = 1: padded grid,
     one group per XCD), a partial chunk, whole XCDs (B = 64: 8 groups), several launches'
-    worth of groups (B = 130) — against the numpy oracle."""
+    worth of groups (B = 130) — against the numpy oracle.  (B <= 4 normally takes the GEMV
+    kernel: switched off here.)"""
     from forwardtacotron_amd import ops
     monkeypatch.setattr(ops, 'RNN_MMA', 2)
+    monkeypatch.setenv('FTMI_RNN_GEMV', '0')
     fin = 512 if cell == 'lstm' else 256
     m, sd = _rnn_module(cell, fin, H, rng)
     x = rng.normal(0, 1, (B, T, fin)).astype(np.float32)
@@ -402,9 +404,29 @@ def test_rnn_f16x3_kernels(cell, H, B, T, rng, monkeypatch):
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
 
 
-def test_rnn_f16_weight_range_guard(rng):
+@pytest.mark.parametrize('cell,H,B,T', [('lstm', 512, 1, 37), ('lstm', 512, 2, 20),
+                                        ('lstm', 512, 4, 15), ('gru', 256, 1, 50),
+                                        ('gru', 256, 3, 21), ('gru', 128, 1, 33),
+                                        ('gru', 128, 4, 17), ('gru', 64, 1, 40),
+                                        ('gru', 64, 2, 25)])
+def test_rnn_gemv(cell, H, B, T, rng, monkeypatch):
+    """B <= 4: the exact-fp32 GEMV recurrence against the numpy oracle in fp64 (a tighter
+    bound than the f16x3 kernels') and against the MFMA kernel."""
+    fin = 512 if cell == 'lstm' else 256
+    m, sd = _rnn_module(cell, fin, H, rng)
+    x = rng.normal(0, 1, (B, T, fin)).astype(np.float32)
+    f = O.lstm_bidir if cell == 'lstm' else O.gru_bidir
+    ref = f({k: v.astype(np.float64) for k, v in sd.items()}, 'r', x.astype(np.float64), np.float64)
+    got = host(m.forward_cl(dev(x)))
+    close(got, ref, rtol=2e-5, atol=2e-6)
+    monkeypatch.setenv('FTMI_RNN_GEMV', '0')
+    close(got, host(m.forward_cl(dev(x))), rtol=1e-4, atol=1e-5)
+
+
+def test_rnn_f16_weight_range_guard(rng, monkeypatch):
     """A W_hh entry beyond the f16 range sets status bit 1 on the f16x3 recurrence."""
     from forwardtacotron_amd import ops
+    monkeypatch.setenv('FTMI_RNN_GEMV', '0')  # B = 2 would take the (exact) GEMV kernel
     m, sd = _rnn_module('gru', 256, 64, rng)
     with torch.no_grad():
         m.weight_hh_l0[5, 7] = 1e6
