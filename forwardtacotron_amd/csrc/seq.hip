@@ -135,6 +135,49 @@ __global__ void length_regulate_kernel(const float *__restrict__ x, int64_t x_st
   }
 }
 
+// the same on 4 channels per thread (C % 4 == 0, 16-B aligned rows) for a chunk of SP_ROWS
+// rows: the 4 channels' weights (3 taps x 2 series + 2 biases) are loaded once into
+// registers and reused for every row of the chunk (re-reading them per row moved 8x the x
+// bytes through L2 in the folded form, where x is the (B, T, 4H) LSTM input projection)
+constexpr int SP_ROWS = 32;
+__global__ __launch_bounds__(256) void series_proj_add4_kernel(
+    float *x, int64_t x_stride, int B, int T, int C, const float *__restrict__ pitch,
+    const float *__restrict__ wp, const float *__restrict__ bp, float ps,
+    const float *__restrict__ energy, const float *__restrict__ we,
+    const float *__restrict__ be, float es) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= C) return;
+  float wpa[12], wea[12];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const f32x4 a = *(const f32x4 *)(wp + 3 * c + 4 * q), d = *(const f32x4 *)(we + 3 * c + 4 * q);
+    wpa[4 * q] = a.x; wpa[4 * q + 1] = a.y; wpa[4 * q + 2] = a.z; wpa[4 * q + 3] = a.w;
+    wea[4 * q] = d.x; wea[4 * q + 1] = d.y; wea[4 * q + 2] = d.z; wea[4 * q + 3] = d.w;
+  }
+  const f32x4 bpv = *(const f32x4 *)(bp + c), bev = *(const f32x4 *)(be + c);
+  const int64_t rows = (int64_t)B * T;
+  const int64_t r0 = (int64_t)blockIdx.y * SP_ROWS;
+  for (int64_t r = r0; r < r0 + SP_ROWS && r < rows; ++r) {
+    const int b = (int)(r / T), t = (int)(r - (int64_t)b * T);
+    const float *pr = pitch + (int64_t)b * T;
+    const float *er = energy + (int64_t)b * T;
+    const float p0 = t > 0 ? pr[t - 1] : 0.f, p1 = pr[t], p2 = t + 1 < T ? pr[t + 1] : 0.f;
+    const float e0 = t > 0 ? er[t - 1] : 0.f, e1 = er[t], e2 = t + 1 < T ? er[t + 1] : 0.f;
+    float *xr = x + r * x_stride + c;
+    f32x4 v = *(f32x4 *)xr;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float P = bpv[e] + wpa[3 * e] * p0 + wpa[3 * e + 1] * p1 + wpa[3 * e + 2] * p2;
+      const float E = bev[e] + wea[3 * e] * e0 + wea[3 * e + 1] * e1 + wea[3 * e + 2] * e2;
+      float u = v[e];
+      u = u + P * ps;
+      u = u + E * es;
+      v[e] = u;
+    }
+    *(f32x4 *)xr = v;
+  }
+}
+
 // x += proj(pitch)*ps ; x += proj(energy)*es   (forward_tacotron.py:308-314)
 __global__ void series_proj_add_kernel(float *x, int64_t x_stride, int B, int T, int C,
                                        const float *__restrict__ pitch,
@@ -266,6 +309,17 @@ extern "C" int ftmi_series_proj_add(float *x, int64_t x_stride, int32_t B, int32
                                     ftmi_stream_t stream) {
   if (!x || !pitch || !wp || !bp || !energy || !we || !be) return FTMI_E_ARG;
   if (B <= 0 || T <= 0 || C <= 0) return FTMI_E_ARG;
+  const bool vec = C % 4 == 0 && !(x_stride & 3) && ftmi_aligned16(x) && ftmi_aligned16(wp) &&
+                   ftmi_aligned16(we) && ftmi_aligned16(bp) && ftmi_aligned16(be);
+  if (vec) {
+    const int64_t rows = (int64_t)B * T;
+    hipLaunchKernelGGL(series_proj_add4_kernel,
+                       dim3((unsigned)((C / 4 + 255) / 256), (unsigned)((rows + SP_ROWS - 1) / SP_ROWS)),
+                       dim3(256), 0, ftmi_hs(stream), x, x_stride, B, T, C, pitch, wp, bp,
+                       pitch_strength, energy, we, be, energy_strength);
+    FTMI_CHECK_LAUNCH();
+    return FTMI_OK;
+  }
   hipLaunchKernelGGL(series_proj_add_kernel, dim3((unsigned)((int64_t)B * T)), dim3(256), 0,
                      ftmi_hs(stream), x, x_stride, B, T, C, pitch, wp, bp, pitch_strength,
                      energy, we, be, energy_strength);
