@@ -78,7 +78,8 @@ SIGNATURES = {
     'ftmi_lr_posenc': (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, P, P, P, c_int64, P]),
     'ftmi_layernorm': (c_int, [P, c_int64, c_int64, c_int, P, P, c_float, P, c_int64, P]),
     'ftmi_attention': (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
-                               c_float, P, c_int64, c_int, P, P]),
+                               c_float, P, c_int64, c_int, P, P, c_int64, P]),
+    'ftmi_attention_workspace_bytes': (c_int64, [c_int, c_int, c_int, c_int]),
     'ftmi_stft': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P, P, P]),
     'ftmi_mel_spectrogram': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P,
                                      P, P, P, c_int, c_int, P, P]),

@@ -251,11 +251,14 @@ __global__ __launch_bounds__(256) void attention_kernel(const float *__restrict_
 constexpr int AH_W = 8;    // waves (x 16 queries) per workgroup of the f16x3 kernel
 constexpr int AH_KT = 64;  // keys per tile
 
-template <int HD>
+// PRE: K and V come pre-split from attn_split_kv_kernel (kv: f16 planes K head, K tail
+// [B*H][Tp][HD] and V head, V tail transposed [B*H][HD][Tp]): the tile staging is a copy, the
+// split VALU (which every query tile of a head repeated) is gone.
+template <int HD, bool PRE>
 __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
     const float *__restrict__ qkv, int64_t rs, int B, int T, int H, int q_off, int k_off,
     int v_off, const uint8_t *__restrict__ kpm, float qscale, float *__restrict__ out,
-    int64_t os, unsigned *status) {
+    int64_t os, unsigned *status, const _Float16 *__restrict__ kv, int Tp) {
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   constexpr int NTH = 64 * AH_W;
@@ -328,38 +331,104 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
     l[i] = 0.f;
   }
 
+  // ---- K / V tile staging, software-pipelined: the global loads of tile k0 + AH_KT are in
+  // flight (registers) while tile k0 is multiplied; after the next barrier they are split
+  // (or, PRE, copied) into the LDS planes.  Without it every tile waited the full memory
+  // latency (PMC: 53 % of wave cycles in waits, MFMA 17 % busy).
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int NKC = PRE ? 2 * AH_KT * HD / 8 / NTH : AH_KT * HD / 4 / NTH;  // K slots
+  constexpr int NVC = PRE ? 2 * HD * AH_KT / 8 / NTH : HD * (AH_KT / 8) / NTH;  // V slots
+  static_assert(NKC * NTH == (PRE ? 2 * AH_KT * HD / 8 : AH_KT * HD / 4) &&
+                NVC * NTH == (PRE ? 2 * HD * AH_KT / 8 : HD * (AH_KT / 8)), "staging slots");
+  u32x4 kr[NKC], vr[PRE ? NVC : 1];
+  float vs[PRE ? 1 : NVC][8];
+  const size_t plane = PRE ? (size_t)B * H * Tp * HD : 0;
+  const int last0 = (T - 1) / AH_KT * AH_KT;  // start of the last tile
+  auto load_tile = [&](int k0) {
+    k0 = k0 < last0 ? k0 : last0;  // past the end: a clamped (unused) reload
+    if constexpr (PRE) {
+      const _Float16 *kb = kv + ((size_t)bh * Tp + k0) * HD;
+      const _Float16 *vb = kv + 2 * plane + (size_t)bh * HD * Tp + k0;
+#pragma unroll
+      for (int i = 0; i < NKC; ++i) {
+        const int e = tid + NTH * i, pl = e / (AH_KT * HD / 8), q = e - pl * (AH_KT * HD / 8);
+        const int r = q / (HD / 8), c8 = (q - r * (HD / 8)) * 8;
+        kr[i] = *(const u32x4 *)(kb + pl * plane + (size_t)r * HD + c8);
+      }
+#pragma unroll
+      for (int i = 0; i < NVC; ++i) {
+        const int e = tid + NTH * i, pl = e / (HD * AH_KT / 8), q = e - pl * (HD * AH_KT / 8);
+        const int d = q / (AH_KT / 8), c8 = (q - d * (AH_KT / 8)) * 8;
+        vr[i] = *(const u32x4 *)(vb + pl * plane + (size_t)d * Tp + c8);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NKC; ++i) {  // K: one float4 of a key row (row clamped to T - 1)
+        const int e = tid + NTH * i, r = e / (HD / 4), c4 = (e - r * (HD / 4)) * 4;
+        const int key = min(k0 + r, T - 1);
+        kr[i] = *(const u32x4 *)(base + (int64_t)key * rs + k_off + h * HD + c4);
+      }
+#pragma unroll
+      for (int i = 0; i < NVC; ++i) {  // V: 8 keys of one column d
+        const int e = tid + NTH * i, d = e % HD, kg = e / HD;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int key = min(k0 + kg * 8 + j, T - 1);
+          vs[i][j] = base[(int64_t)key * rs + v_off + h * HD + d];
+        }
+      }
+    }
+  };
+  auto store_tile = [&](int k0) {
+    if constexpr (PRE) {
+#pragma unroll
+      for (int i = 0; i < NKC; ++i) {
+        const int e = tid + NTH * i, pl = e / (AH_KT * HD / 8), q = e - pl * (AH_KT * HD / 8);
+        const int r = q / (HD / 8), c8 = (q - r * (HD / 8)) * 8;
+        *(u32x4 *)&(pl ? Kt : Kh)[r * KP + c8] = kr[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NVC; ++i) {
+        const int e = tid + NTH * i, pl = e / (HD * AH_KT / 8), q = e - pl * (HD * AH_KT / 8);
+        const int d = q / (AH_KT / 8), c8 = (q - d * (AH_KT / 8)) * 8;
+        *(u32x4 *)&(pl ? Vt : Vh)[d * VP + c8] = vr[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NKC; ++i) {
+        const int e = tid + NTH * i, r = e / (HD / 4), c4 = (e - r * (HD / 4)) * 4;
+        f32x4 kvv = __builtin_bit_cast(f32x4, kr[i]);
+        if (k0 + r >= T) kvv = (f32x4){0.f, 0.f, 0.f, 0.f};
+        f16x4 hh, tt;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          amax = fmaxf(amax, fabsf(kvv[j]));
+          hh[j] = (_Float16)kvv[j];
+          tt[j] = (_Float16)((kvv[j] - (float)hh[j]) * TS);
+        }
+        *(f16x4 *)&Kh[r * KP + c4] = hh;
+        *(f16x4 *)&Kt[r * KP + c4] = tt;
+      }
+#pragma unroll
+      for (int i = 0; i < NVC; ++i) {
+        const int e = tid + NTH * i, d = e % HD, kg = e / HD;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = k0 + kg * 8 + j < T ? vs[i][j] : 0.f;
+        f16x8 hh, tt;
+        split8((f32x4){v[0], v[1], v[2], v[3]}, (f32x4){v[4], v[5], v[6], v[7]}, hh, tt);
+        *(f16x8 *)&Vh[d * VP + kg * 8] = hh;
+        *(f16x8 *)&Vt[d * VP + kg * 8] = tt;
+      }
+    }
+  };
+  load_tile(0);
+
   for (int k0 = 0; k0 < T; k0 += AH_KT) {
+    __syncthreads();  // every wave is done with the previous tile's LDS planes
+    store_tile(k0);
     __syncthreads();
-    // ---- stage K (keys x HD, [key][d]) and V^T (HD x keys, [d][key]) as f16 planes
-    for (int e = tid; e < AH_KT * HD / 4; e += NTH) {  // K: one float4 of a key row
-      const int r = e / (HD / 4), c4 = (e - r * (HD / 4)) * 4;
-      const int key = k0 + r;
-      f32x4 kv = {0.f, 0.f, 0.f, 0.f};
-      if (key < T) kv = *(const f32x4 *)(base + (int64_t)key * rs + k_off + h * HD + c4);
-      f16x4 hh, tt;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        amax = fmaxf(amax, fabsf(kv[j]));
-        hh[j] = (_Float16)kv[j];
-        tt[j] = (_Float16)((kv[j] - (float)hh[j]) * TS);
-      }
-      *(f16x4 *)&Kh[r * KP + c4] = hh;
-      *(f16x4 *)&Kt[r * KP + c4] = tt;
-    }
-    for (int e = tid; e < HD * (AH_KT / 8); e += NTH) {  // V: 8 keys of one column d
-      const int d = e % HD, kg = e / HD;
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int key = k0 + kg * 8 + j;
-        v[j] = key < T ? base[(int64_t)key * rs + v_off + h * HD + d] : 0.f;
-      }
-      f16x8 hh, tt;
-      split8((f32x4){v[0], v[1], v[2], v[3]}, (f32x4){v[4], v[5], v[6], v[7]}, hh, tt);
-      *(f16x8 *)&Vh[d * VP + kg * 8] = hh;
-      *(f16x8 *)&Vt[d * VP + kg * 8] = tt;
-    }
-    __syncthreads();
+    load_tile(k0 + AH_KT);
     // ---- S = (q c) K^T: 16 rows x AH_KT keys
     f32x4 s[NB];
 #pragma unroll
@@ -447,6 +516,59 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
   }
 }
 
+// K and V of every (batch, head) split once into f16 head / scaled tail planes for the
+// PRE attention kernel: K [B*H][Tp][HD], V transposed [B*H][HD][Tp] (keys >= T zero).  One
+// workgroup per (64 keys, b*h): K rows straight through, V through an LDS tile.  A value
+// beyond the f16 range sets bit 0 of *status.
+template <int HD>
+__global__ __launch_bounds__(256) void attn_split_kv_kernel(const float *__restrict__ qkv,
+                                                            int64_t rs, int B, int T, int H,
+                                                            int k_off, int v_off, int Tp,
+                                                            _Float16 *__restrict__ kv,
+                                                            unsigned *status) {
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  constexpr float TS = 2048.f;
+  __shared__ float vt[64][HD + 1];
+  const int k0 = blockIdx.x * 64, bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const size_t plane = (size_t)B * H * Tp * HD;
+  const float *base = qkv + (size_t)b * T * rs;
+  float amax = 0.f;
+  for (int e = threadIdx.x; e < 64 * HD / 4; e += 256) {
+    const int r = e / (HD / 4), c4 = (e - r * (HD / 4)) * 4, key = k0 + r;
+    f32x4 kvv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+    if (key < T) {
+      kvv = *(const f32x4 *)(base + (size_t)key * rs + k_off + h * HD + c4);
+      vv = *(const f32x4 *)(base + (size_t)key * rs + v_off + h * HD + c4);
+    }
+    f16x4 hh, tt;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      amax = fmaxf(amax, fmaxf(fabsf(kvv[j]), fabsf(vv[j])));
+      hh[j] = (_Float16)kvv[j];
+      tt[j] = (_Float16)((kvv[j] - (float)hh[j]) * TS);
+      vt[r][c4 + j] = vv[j];
+    }
+    const size_t o = ((size_t)bh * Tp + key) * HD + c4;
+    *(f16x4 *)(kv + o) = hh;
+    *(f16x4 *)(kv + plane + o) = tt;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < HD * 16; e += 256) {  // V^T: row d, 4 keys per thread
+    const int d = e / 16, kq = (e - d * 16) * 4;
+    f16x4 hh, tt;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float v = vt[kq + j][d];
+      hh[j] = (_Float16)v;
+      tt[j] = (_Float16)((v - (float)hh[j]) * TS);
+    }
+    const size_t o = ((size_t)bh * HD + d) * Tp + k0 + kq;
+    *(f16x4 *)(kv + 2 * plane + o) = hh;
+    *(f16x4 *)(kv + 3 * plane + o) = tt;
+  }
+  if (!(amax <= 65504.f) && status) atomicOr(status, 1u);
+}
+
 }  // namespace
 
 extern "C" int ftmi_embedding_posenc(const int64_t *ids, int32_t B, int32_t T, const float *table,
@@ -496,27 +618,50 @@ extern "C" int ftmi_layernorm(const float *x, int64_t x_stride, int64_t M, int32
   return FTMI_OK;
 }
 
+extern "C" int64_t ftmi_attention_workspace_bytes(int32_t B, int32_t T, int32_t H,
+                                                  int32_t head_dim) {
+  if (B <= 0 || T <= 0 || H <= 0 || head_dim <= 0) return 0;
+  const int64_t Tp = (T + 63) / 64 * 64;
+  return 4 * (int64_t)B * H * Tp * head_dim * 2;
+}
+
 extern "C" int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, int32_t T,
                               int32_t H, int32_t head_dim, int32_t q_off, int32_t k_off,
                               int32_t v_off, const uint8_t *key_padding_mask, float qscale,
                               float *out, int64_t out_stride, int32_t mma, uint32_t *status,
-                              ftmi_stream_t stream) {
+                              void *workspace, int64_t workspace_bytes, ftmi_stream_t stream) {
   if (!qkv || !out || B <= 0 || T <= 0 || H <= 0) return FTMI_E_ARG;
   if (head_dim != 64 && head_dim != 128) return FTMI_E_UNSUPPORTED;
   if (mma != FTMI_MMA_F32 && mma != FTMI_MMA_F16X3) return FTMI_E_UNSUPPORTED;
   if (!ftmi_aligned16(qkv) || (row_stride & 3) || (q_off & 3) || (k_off & 3) || (v_off & 3))
     return FTMI_E_ALIGN;
+  if (workspace && !ftmi_aligned16(workspace)) return FTMI_E_ALIGN;
   const dim3 grid((unsigned)((T + 63) / 64), (unsigned)(B * H)), block(256);
   const hipStream_t s = ftmi_hs(stream);
   if (mma == FTMI_MMA_F16X3) {
     const int nq = (T + 16 * AH_W - 1) / (16 * AH_W);
     const dim3 g1((unsigned)(nq * B * H)), b1(64 * AH_W);
-    if (head_dim == 64)
-      hipLaunchKernelGGL(attention_h3_kernel<64>, g1, b1, 0, s, qkv, row_stride, B, T, H,
-                         q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride, status);
-    else
-      hipLaunchKernelGGL(attention_h3_kernel<128>, g1, b1, 0, s, qkv, row_stride, B, T, H,
-                         q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride, status);
+    const int Tp = (T + 63) / 64 * 64;
+    const bool pre = workspace && workspace_bytes >= ftmi_attention_workspace_bytes(B, T, H, head_dim);
+    _Float16 *kv = (_Float16 *)workspace;
+#define FTMI_ATTN_H3(HD_)                                                                       \
+  if (pre) {                                                                                     \
+    hipLaunchKernelGGL(attn_split_kv_kernel<HD_>, dim3((unsigned)(Tp / 64), (unsigned)(B * H)),  \
+                       dim3(256), 0, s, qkv, row_stride, B, T, H, k_off, v_off, Tp, kv, status); \
+    hipLaunchKernelGGL((attention_h3_kernel<HD_, true>), g1, b1, 0, s, qkv, row_stride, B, T, H, \
+                       q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride, status,  \
+                       (const _Float16 *)kv, Tp);                                               \
+  } else {                                                                                       \
+    hipLaunchKernelGGL((attention_h3_kernel<HD_, false>), g1, b1, 0, s, qkv, row_stride, B, T,  \
+                       H, q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride,       \
+                       status, (const _Float16 *)nullptr, 0);                                   \
+  }
+    if (head_dim == 64) {
+      FTMI_ATTN_H3(64)
+    } else {
+      FTMI_ATTN_H3(128)
+    }
+#undef FTMI_ATTN_H3
     FTMI_CHECK_LAUNCH();
     return FTMI_OK;
   }

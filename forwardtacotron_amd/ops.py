@@ -625,10 +625,16 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
     return y
 
 
+ATTN_PRESPLIT = os.environ.get('FTMI_ATTN_PRESPLIT', '1') != '0'
+
+
 def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Tensor] = None,
-              mma: Optional[int] = None) -> torch.Tensor:
+              mma: Optional[int] = None, presplit: Optional[bool] = None) -> torch.Tensor:
     """Self-attention core of nn.MultiheadAttention on packed in_proj rows (B, T, 3d).
-    mma: 2 = f16x3 contractions (default, MMA), 0 = fp32 MFMA (exact_paths(), MMA 0/1)."""
+    mma: 2 = f16x3 contractions (default, MMA), 0 = fp32 MFMA (exact_paths(), MMA 0/1).
+    presplit (f16x3; default: ATTN_PRESPLIT and T > 384): K and V split once into f16
+    planes in a workspace instead of per query tile (identical results; measured at c5's
+    postnet T = 1400: 825 -> 618 us incl. the split pass, slower at T = 200)."""
     _dev(qkv, key_padding_mask)
     m = _FORCED[-1][0] if _FORCED else (MMA if mma is None else mma)
     m = 2 if m == 2 else 0
@@ -640,8 +646,15 @@ def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Te
     if key_padding_mask is not None:
         kpm = key_padding_mask.to(torch.uint8).contiguous()
     qscale = float(np.float32(np.sqrt(1.0 / hd)))
+    ws, nws = None, 0
+    if presplit is None:  # pays off once K / V are re-read by >= 4 query tiles (T > 384)
+        presplit = ATTN_PRESPLIT and T > 384
+    if m == 2 and presplit:
+        nws = int(_lib.load().ftmi_attention_workspace_bytes(B, T, heads, hd))
+        ws = torch.empty(nws, device=qkv.device, dtype=torch.uint8)
     launch('ftmi_attention', f'attention[B={B},T={T},H={heads},hd={hd},mma={m}]',
            4.0 * B * heads * T * T * hd, 4.0 * (B * T * C3 + B * T * d),
            qkv.data_ptr(), rs, B, T, heads, hd, 0, d, 2 * d, _ptr(kpm), qscale,
-           out.data_ptr(), out.stride(1), m, status_word(qkv.device).data_ptr(), _stream())
+           out.data_ptr(), out.stride(1), m, status_word(qkv.device).data_ptr(), _ptr(ws), nws,
+           _stream())
     return out

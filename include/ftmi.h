@@ -418,11 +418,16 @@ int ftmi_layernorm(const float *x, int64_t x_stride, int64_t M, int32_t C, const
  * (-inf), or NULL.  qscale = float32(sqrt(1/head_dim)).  out: (B, T, H*head_dim) rows of
  * stride out_stride.  head_dim in {64, 128}.  mma (ABI 8): FTMI_MMA_F16X3 (default: both
  * contractions on the f16x3 split, softmax fp32; an operand beyond the f16 range sets
- * FTMI_STATUS_F16_RANGE in *status, optional) or FTMI_MMA_F32 (fp32 MFMA). */
+ * FTMI_STATUS_F16_RANGE in *status, optional) or FTMI_MMA_F32 (fp32 MFMA).  workspace
+ * (ABI 9, nullable): with >= ftmi_attention_workspace_bytes caller-owned bytes the f16x3
+ * path splits K and V once per call into f16 planes there (instead of once per query tile
+ * inside the attention kernel); results are identical. */
+int64_t ftmi_attention_workspace_bytes(int32_t B, int32_t T, int32_t H, int32_t head_dim);
 int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, int32_t T, int32_t H,
                    int32_t head_dim, int32_t q_off, int32_t k_off, int32_t v_off,
-                   const uint8_t *key_padding_mask, float qscale, float *out, int64_t out_stride,
-                   int32_t mma, uint32_t *status, ftmi_stream_t stream);
+                   const uint8_t *key_padding_mask, float qscale, float *out,
+                   int64_t out_stride, int32_t mma, uint32_t *status, void *workspace,
+                   int64_t workspace_bytes, ftmi_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -46,10 +46,11 @@ def test_layernorm(C):
     np.testing.assert_allclose(host(ops.layernorm(dev(x), dev(g), dev(b))), ref, atol=2e-6, rtol=2e-6)
 
 
-@pytest.mark.parametrize('mma', [2, 0], ids=['f16x3', 'f32'])
+@pytest.mark.parametrize('mma,presplit', [(2, True), (2, False), (0, False)],
+                         ids=['f16x3-presplit', 'f16x3', 'f32'])
 @pytest.mark.parametrize('hd,T,masked', [(64, 37, False), (128, 200, True), (128, 33, False),
                                          (64, 129, True), (128, 1, False), (128, 1400, False)])
-def test_attention(hd, T, masked, mma):
+def test_attention(hd, T, masked, mma, presplit):
     from forwardtacotron_amd import ops
     rng = np.random.RandomState(T + hd)
     B, H = 3, 2
@@ -68,9 +69,14 @@ def test_attention(hd, T, masked, mma):
     ref = (FP.softmax(s) @ sp(v)).transpose(0, 2, 1, 3).reshape(B, T, d)
     st = ops.status_word('cuda')
     st.zero_()
-    got = host(ops.attention(dev(qkv), H, dev(kpm) if kpm is not None else None, mma=mma))
+    got = host(ops.attention(dev(qkv), H, dev(kpm) if kpm is not None else None, mma=mma,
+                             presplit=presplit))
     np.testing.assert_allclose(got, ref, atol=2e-5, rtol=2e-5)
     assert int(st.item()) == 0
+    if presplit:  # the same arithmetic as the in-kernel split: identical results
+        other = host(ops.attention(dev(qkv), H, dev(kpm) if kpm is not None else None, mma=mma,
+                                   presplit=False))
+        np.testing.assert_array_equal(got, other)
 
 
 def test_attention_f16_range_guard():
@@ -82,10 +88,11 @@ def test_attention_f16_range_guard():
     qkv = rng.randn(B, T, 3 * H * hd).astype(np.float32)
     qkv[1, 7, 2 * H * hd + 3] = 1e5  # one value entry
     st = ops.status_word('cuda')
-    st.zero_()
-    ops.attention(dev(qkv), H, mma=2)
-    torch.cuda.synchronize()
-    assert int(st.item()) & 1
+    for presplit in (True, False):
+        st.zero_()
+        ops.attention(dev(qkv), H, mma=2, presplit=presplit)
+        torch.cuda.synchronize()
+        assert int(st.item()) & 1
     st.zero_()
     ops.attention(dev(qkv), H, mma=0)
     torch.cuda.synchronize()

@@ -26,9 +26,9 @@ for B, T, H, hd in [(64, 1400, 2, 128), (64, 200, 2, 128), (64, 200, 2, 64)]:
     flops = 4.0 * B * H * T * T * hd
     line = f'B={B} T={T} H={H} hd={hd}:'
     outs = {}
-    for m in (0, 2):
-        ms = timed(lambda: ops.attention(qkv, H, mma=m))
-        outs[m] = ops.attention(qkv, H, mma=m)
-        line += f'  mma={m} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TF/s'
-    line += f'  max|f16x3 - f32| {float((outs[0] - outs[2]).abs().max()):.2e}'
+    for m, pre in ((0, False), (2, False), (2, True)):
+        ms = timed(lambda: ops.attention(qkv, H, mma=m, presplit=pre))
+        outs[(m, pre)] = ops.attention(qkv, H, mma=m, presplit=pre)
+        line += f'  mma={m}{"p" if pre else ""} {ms * 1e3:8.1f} us {flops / ms / 1e9:7.1f} TF/s'
+    line += f'  max|f16x3 - f32| {float((outs[(0, False)] - outs[(2, True)]).abs().max()):.2e}'
     print(line, flush=True)
