@@ -106,6 +106,24 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict_
 // online softmax in registers (MFMA C layout: lane holds rows 4(lane>>4)+i, col lane&15).
 constexpr int AT_KT = 32;
 
+// max / sum over the 16 lanes of a DPP row (the 16 columns of an MFMA row group):
+// rotations by 8, 4, 2, 1 within the row (row_ror), VALU only — the ds_bpermute of
+// __shfl_xor is an LDS-pipe op with ~100 cycles of latency per step of the chain
+template <int CTRL>
+__device__ __forceinline__ float dpp_ror(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v),
+                                                               __builtin_bit_cast(int, v),
+                                                               CTRL, 0xF, 0xF, false));
+}
+#define FTMI_ROW16(OP, v)             \
+  do {                                \
+    v = OP(v, dpp_ror<0x128>(v));     \
+    v = OP(v, dpp_ror<0x124>(v));     \
+    v = OP(v, dpp_ror<0x122>(v));     \
+    v = OP(v, dpp_ror<0x121>(v));     \
+  } while (0)
+__device__ __forceinline__ float add2(float a, float b) { return a + b; }
+
 template <int HD>
 __global__ __launch_bounds__(256) void attention_kernel(const float *__restrict__ qkv, int64_t rs,
                                                         int B, int T, int H, int q_off, int k_off,
@@ -189,7 +207,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const float *__restrict_
     for (int i = 0; i < 4; ++i) {
       float mx = fmaxf(s[0][i], s[1][i]);
 #pragma unroll
-      for (int off = 8; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+      FTMI_ROW16(fmaxf, mx);
       const float mn = fmaxf(m[i], mx);
       const float alpha = mn == -INFINITY ? 1.f : expf(m[i] - mn);
       float ps = 0.f;
@@ -200,7 +218,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const float *__restrict_
         ps += pv;
       }
 #pragma unroll
-      for (int off = 8; off > 0; off >>= 1) ps += __shfl_xor(ps, off);
+      FTMI_ROW16(add2, ps);
       l[i] = l[i] * alpha + ps;
       m[i] = mn;
 #pragma unroll
@@ -458,7 +476,7 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
 #pragma unroll
       for (int n = 1; n < NB; ++n) mx = fmaxf(mx, s[n][i]);
 #pragma unroll
-      for (int off = 8; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+      FTMI_ROW16(fmaxf, mx);
       const float mn = fmaxf(m[i], mx);
       const float alpha = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f((m[i] - mn) * LOG2E);
       float ps = 0.f;
@@ -469,7 +487,7 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
         ps += pv;
       }
 #pragma unroll
-      for (int off = 8; off > 0; off >>= 1) ps += __shfl_xor(ps, off);
+      FTMI_ROW16(add2, ps);
       l[i] = l[i] * alpha + ps;
       m[i] = mn;
 #pragma unroll
