@@ -47,7 +47,7 @@ SIGNATURES = {
     'ftmi_conv_bank': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P, c_int64,
                                c_int, P, P]),
     'ftmi_conv_bank_split': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P,
-                                     c_int64, c_int, P, c_int, P, P]),
+                                     c_int64, c_int, P, c_int, P, c_int, P]),
     'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P, P]),
     'ftmi_highway_split': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P,
                                    c_int, P, P]),

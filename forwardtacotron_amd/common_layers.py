@@ -298,8 +298,10 @@ class CBHG(Packed):
     def forward_cl(self, x: torch.Tensor) -> torch.Tensor:
         """(B, T, Cin) channels-last -> (B, T, 2*channels)."""
         bank_w, scale, shift, w_pre, bank3, pre3 = self.packed_weights()
-        bank = ops.conv_bank(x, bank_w, self.K, self.channels, scale, shift, w_split=bank3)
-        y = self.conv_project1.forward_cl(bank, maxpool=True)
+        pooled = ops.bank_pools(x, self.K, self.channels, w_split=bank3)
+        bank = ops.conv_bank(x, bank_w, self.K, self.channels, scale, shift, w_split=bank3,
+                             pool=pooled)  # pooled: the bank kernel applied the maxpool
+        y = self.conv_project1.forward_cl(bank, maxpool=not pooled)
         del bank
         y = self.conv_project2.forward_cl(y, residual=x)
         xp = self._highway_stack(y)

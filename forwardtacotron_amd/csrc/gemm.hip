@@ -90,6 +90,10 @@ struct GemmParams {
   int ldp;  // skinny kernel: columns of a partial-sum row (all groups, output order)
   int force_part;  // skinny kernel: partial sums even with one split (highway finish)
   unsigned *status;  // mma = 2: bit 0 set when an accumulator became non-finite
+  // slab kernel, EPI_CONV: store maxpool(2, 1) of the finished rows (CBHG bank -> its pooled
+  // input of proj1, common_layers.py:100): y[t] = max(v[t - 1], v[t]), y[0] = v[0] per
+  // sequence.  Tiles then step by SL_BM - 1 rows and carry one halo row.
+  int pool_out;
   GemmGroup g[MAX_GROUPS];
 };
 
@@ -954,7 +958,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_x6b_kernel(const GemmParams 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = m0 + wave * 32 + mi * 16 + 4 * fs + i;
-          bad |= col < G.N && row < p.M && !__builtin_isfinite(acc[mi][ni][i]);
+          bad |= col < G.N && row >= 0 && row < p.M && !__builtin_isfinite(acc[mi][ni][i]);
           acc[mi][ni][i] *= cs;
         }
     }
@@ -1073,7 +1077,8 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
   // (every column tile of every group: a conv bank's groups all read the same input rows)
   // are consecutive in that XCD's order, so its slab rows are shared through L2.  Groups
   // (conv bank: one per kernel size, heaviest first) all have NT column tiles.
-  const int MT = (p.M + SL_BM - 1) / SL_BM, NT = p.g[0].ntiles, VT = p.ngroups * NT;
+  const int TS = p.pool_out ? SL_BM - 1 : SL_BM;  // rows a tile produces
+  const int MT = (p.M + TS - 1) / TS, NT = p.g[0].ntiles, VT = p.ngroups * NT;
   // With fewer than 8 row tiles (small batches) that order would put every working block on
   // one XCD: the grid is then compact, row tile fastest, and consecutive blocks spread.
   const int bid = blockIdx.x, s8 = bid >> 3, q8 = s8 / VT;
@@ -1085,7 +1090,8 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
   const int gi = v8 / NT, nt = v8 - gi * NT;
   if (mt >= MT) return;  // the grid is padded to whole XCD rounds
   const GemmGroup &G = p.g[gi];
-  const int m0 = mt * SL_BM, n0 = nt * SL_BN;
+  // pool_out: the tile's row 0 is the halo row m0 = mt * TS - 1 (only feeds the pooling)
+  const int m0 = p.pool_out ? mt * TS - 1 : mt * SL_BM, n0 = nt * SL_BN;
   const int k = G.k, pad = G.pad, Cin = p.Cin;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1207,7 +1213,7 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
   for (int mi = 0; mi < 4; ++mi) {
     const int m = m0 + wm * 64 + mi * 16 + fr;
     unsigned msk = 0;
-    if (m < p.M) {
+    if (m >= 0 && m < p.M) {
       const int t = m % p.T;
       const int lo = max(pad - t, 0), hi = min(p.T - 1 + pad - t, k - 1);
       if (lo <= hi) msk = (2u << hi) - (1u << lo);
@@ -1396,6 +1402,28 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
     return;
   }
   if constexpr (EPI == EPI_CONV) {
+    if (p.pool_out) {  // finish every row in the tile, then store max(row - 1, row)
+      for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
+        const int r = idx >> 5, c = (idx & 31) * 4;
+        if (r >= rows || c >= ncols) continue;
+        const int col = n0 + c;
+        f32x4 v = *(const f32x4 *)(tile + r * SL_TP + c);
+        if (G.bias) v += *(const f32x4 *)(G.bias + col);
+        if (p.relu) v = fmax4(v, (f32x4){0.f, 0.f, 0.f, 0.f});
+        if (G.scale) v = v * *(const f32x4 *)(G.scale + col) + *(const f32x4 *)(G.shift + col);
+        *(f32x4 *)(tile + r * SL_TP + c) = v;
+      }
+      __syncthreads();
+      for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
+        const int r = idx >> 5, c = (idx & 31) * 4;
+        if (r == 0 || r >= rows || c >= ncols) continue;
+        const int row = m0 + r, col = n0 + c;
+        f32x4 v = *(const f32x4 *)(tile + r * SL_TP + c);
+        if (row % p.T > 0) v = fmax4(v, *(const f32x4 *)(tile + (r - 1) * SL_TP + c));
+        *(f32x4 *)(p.y + (int64_t)row * p.y_stride + G.ycol0 + col) = v;
+      }
+      return;
+    }
     for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
       const int r = idx >> 5, c = (idx & 31) * 4;
       if (r >= rows || c >= ncols) continue;
@@ -2160,7 +2188,8 @@ static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s
     q.kc_per = (nch + p.split_req - 1) / p.split_req;
     q.split = (nch + q.kc_per - 1) / q.kc_per;
   }
-  const int MT = (q.M + SL_BM - 1) / SL_BM;
+  const int TS = q.pool_out ? SL_BM - 1 : SL_BM;
+  const int MT = (q.M + TS - 1) / TS;
   const int nblk = (MT < 8 ? MT : (MT + 7) / 8 * 8) * q.ngroups * q.g[0].ntiles;  // whole XCD rounds
   dim3 grid(nblk, q.split), block(512);
   if (slab_ws(q)) {
@@ -2270,6 +2299,15 @@ int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hip
   bool presplit = (mma == 1 && x6_variant() != 3) || mma == 2;
   for (int i = 0; i < p.ngroups; ++i) presplit &= p.g[i].w3 != nullptr;
   if (mma == 2 && !presplit) return FTMI_E_ARG;  // the f16 path needs the split planes
+  if (p.pool_out) {  // only the slab kernel pools its output
+    GemmParams q = p;
+    q.split_req = 0;
+    q.part = nullptr;
+    if (!(mma == 2 && presplit && epi == EPI_CONV && !maxpool && !p.residual && !p.yt &&
+          p.y && slab_ok(q, epi)))
+      return FTMI_E_UNSUPPORTED;
+    return launch_slab(q, epi, false, s);
+  }
   if (mma == 2 && presplit && skinny_ok(p, epi)) return launch_skinny(p, epi, maxpool, s);
   if (p.ngroups > 1 && p.split_req > 1) {  // a bank split only serves the skinny kernel
     GemmParams q = p;
@@ -2431,7 +2469,7 @@ extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32
                               float *y, int64_t y_stride, int32_t mma, uint32_t *status,
                               ftmi_stream_t stream) {
   return ftmi_conv_bank_split(x, x_stride, B, T, Cin, w, w_split, K, Cout, bn_scale, bn_shift,
-                              y, y_stride, mma, status, 0, nullptr, stream);
+                              y, y_stride, mma, status, 0, nullptr, 0, stream);
 }
 
 #ifdef FTMI_SKINNY_STAMPS
@@ -2445,8 +2483,9 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
                                     int32_t Cin, const float *w, const void *w_split, int32_t K,
                                     int32_t Cout, const float *bn_scale, const float *bn_shift,
                                     float *y, int64_t y_stride, int32_t mma, uint32_t *status,
-                                    int32_t split_k, float *split_ws, ftmi_stream_t stream) {
-  if (split_k > 1 && !split_ws) return FTMI_E_ARG;
+                                    int32_t split_k, float *split_ws, int32_t pool_out,
+                                    ftmi_stream_t stream) {
+  if (split_k > 1 && !split_ws && !pool_out) return FTMI_E_ARG;
   if (!x || !w || !bn_scale || !bn_shift || !y) return FTMI_E_ARG;
   if (B <= 0 || T <= 0 || Cin <= 0 || Cout <= 0 || K <= 0) return FTMI_E_ARG;
   if (mma < 0 || mma > 2 || (mma == 2 && !w_split)) return FTMI_E_ARG;
@@ -2468,6 +2507,7 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
   p.y = y;
   p.y_stride = y_stride;
   p.status = status;
+  p.pool_out = pool_out ? 1 : 0;
   const int mtiles = (p.M + BM - 1) / BM;
   const int ntiles = (Cout + BN - 1) / BN;
   int tile0 = 0;

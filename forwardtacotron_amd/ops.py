@@ -326,10 +326,23 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
     return y, out_t
 
 
+POOL_BANK = os.environ.get('FTMI_POOL_BANK', '1') != '0'
+
+
+def bank_pools(x: torch.Tensor, K: int, Cout: int, mma: Optional[int] = None, w_split=None) -> bool:
+    """Whether conv_bank(pool=True) applies (gemm.hip launch: the f16x3 slab kernel, not the
+    few-row skinny kernel): then the bank stores the CBHG maxpool of its output itself."""
+    m, wsp = _gemm_mma(mma, w_split)
+    B, T, Cin = x.size(0), x.size(1), x.size(2)
+    return (POOL_BANK and m == 2 and wsp is not None and not _skinny(m, T, T, Cin, K, B * T)
+            and _slab(m, T, T, Cin, K, Cout, B * T))
+
+
 def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.Tensor,
               shift: torch.Tensor, mma: Optional[int] = None,
-              w_split: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """CBHG conv bank, (B, T, Cin) -> (B, T, K*Cout)."""
+              w_split: Optional[torch.Tensor] = None, pool: bool = False) -> torch.Tensor:
+    """CBHG conv bank, (B, T, Cin) -> (B, T, K*Cout); pool: the maxpool(2, 1) of it
+    (common_layers.py:73,100), stored by the bank kernel (see bank_pools)."""
     _dev(x, w, scale, shift, w_split)
     B, T, Cin, xs = _rows(x)
     y = torch.empty(B, T, K * Cout, device=x.device, dtype=_f32)
@@ -337,14 +350,14 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
     flops = 2.0 * M * Cout * Cin * K * (K + 1) / 2
     mma, wsp = _gemm_mma(mma, w_split)
     sk, part = 0, None
-    if _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
+    if not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
         sk = _skinny_split(Cin)  # weight-streaming kernel: partial sums, finished in order
         part = torch.empty(sk * M * K * Cout, device=x.device, dtype=_f32)
-    launch('ftmi_conv_bank_split', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}]', flops,
-           4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
+    launch('ftmi_conv_bank_split', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}{",pool" if pool else ""}]',
+           flops, 4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
            x.data_ptr(), xs, B, T, Cin, w.data_ptr(), wsp, K, Cout,
            scale.data_ptr(), shift.data_ptr(), y.data_ptr(), y.stride(1), mma,
-           status_word(x.device).data_ptr(), sk, _ptr(part), _stream())
+           status_word(x.device).data_ptr(), sk, _ptr(part), int(pool), _stream())
     return y
 
 

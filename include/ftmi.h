@@ -158,12 +158,16 @@ int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32
  * raw partial sums in split_ws (split_k * B*T * K*Cout floats, caller-owned), summed in split
  * order by a finishing launch (deterministic).  split_k <= 1 / split_ws NULL: as
  * ftmi_conv_bank.  Other shapes ignore the split.  ftmi_conv1d takes the same kernel for
- * B*T_out <= 256 (its split_k / split_ws as documented there). */
+ * B*T_out <= 256 (its split_k / split_ws as documented there).
+ * pool_out (ABI 9): y receives the CBHG maxpool(2, 1) of the bank output (common_layers.py
+ * :73,100: y[t] = max(bank[t - 1], bank[t]) within each sequence, y[0] = bank[0]) — the input
+ * proj1 then reads with ftmi_conv_args.maxpool = 0.  Only on the f16x3 slab kernel
+ * (mma = FTMI_MMA_F16X3, B*T > 256 rows, no split); elsewhere FTMI_E_UNSUPPORTED. */
 int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t Cin,
                          const float *w, const void *w_split, int32_t K, int32_t Cout,
                          const float *bn_scale, const float *bn_shift, float *y,
                          int64_t y_stride, int32_t mma, uint32_t *status, int32_t split_k,
-                         float *split_ws, ftmi_stream_t stream);
+                         float *split_ws, int32_t pool_out, ftmi_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * One highway layer (common_layers.py:22-35):

@@ -170,6 +170,32 @@ def test_conv_bank(K, Cin, B, T, rng, mma, pre, kernel, monkeypatch):
     close(host(y), ref.transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
 
 
+@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 2, 300), (8, 80, 3, 200), (8, 80, 1, 700),
+                                     (3, 64, 5, 61)])
+def test_conv_bank_pooled(K, Cin, B, T, rng, monkeypatch):
+    """pool=True: the slab bank kernel stores the CBHG maxpool(2, 1) of its output (tiles of
+    255 rows + a halo row; sequences starting inside a tile) — bit-identical to the maxpool
+    of the unpooled bank, and within the fp32 bound of the oracle."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    C = 256
+    x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
+    ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
+    sc = rng.uniform(0.5, 1.5, K * C).astype(np.float32)
+    sh = rng.normal(0, 0.1, K * C).astype(np.float32)
+    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
+    w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
+    xd = dev(x)
+    assert ops.bank_pools(xd, K, C, w_split=w3)
+    y = host(ops.conv_bank(xd, wp, K, C, dev(sc), dev(sh), mma=2, w_split=w3))
+    yp = host(ops.conv_bank(xd, wp, K, C, dev(sc), dev(sh), mma=2, w_split=w3, pool=True))
+    ref_pool = O.maxpool_k2_s1_p1(y.transpose(0, 2, 1)).transpose(0, 2, 1)
+    np.testing.assert_array_equal(yp, ref_pool)
+    refs = [np.maximum(O.conv1d(x.transpose(0, 2, 1), w, w.shape[2] // 2)[:, :, :T], 0) for w in ws]
+    ref = np.concatenate(refs, 1) * sc[None, :, None] + sh[None, :, None]
+    close(yp, O.maxpool_k2_s1_p1(ref).transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
+
+
 @pytest.mark.parametrize('balanced', ['1', '0'])
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (8, 80, 1, 100), (4, 64, 2, 50),
                                      (16, 256, 2, 100)])
