@@ -49,8 +49,8 @@ def test_strerror():
     (lambda L: L.ftmi_embedding(None, 4, None, 135, 256, None, None, None), 1001),
     (lambda L: L.ftmi_conv1d(None, None), 1001),
     (lambda L: L.ftmi_conv_bank(None, 0, 1, 1, 16, None, None, 4, 8, None, None, None, 0, 1, None, None), 1001),
-    (lambda L: L.ftmi_conv_bank_split(None, 0, 1, 1, 16, None, None, 4, 8, None, None, None, 0, 1, None, 0, None, None), 1001),
-    (lambda L: L.ftmi_conv_bank_split(ctypes.c_void_p(256), 16, 1, 1, 16, ctypes.c_void_p(256), ctypes.c_void_p(256), 4, 8, ctypes.c_void_p(256), ctypes.c_void_p(256), ctypes.c_void_p(256), 32, 2, None, 4, None, None), 1001),
+    (lambda L: L.ftmi_conv_bank_split(None, 0, 1, 1, 16, None, None, 4, 8, None, None, None, 0, 1, None, 0, None, 0, None), 1001),
+    (lambda L: L.ftmi_conv_bank_split(ctypes.c_void_p(256), 16, 1, 1, 16, ctypes.c_void_p(256), ctypes.c_void_p(256), 4, 8, ctypes.c_void_p(256), ctypes.c_void_p(256), ctypes.c_void_p(256), 32, 2, None, 4, None, 0, None), 1001),
     (lambda L: L.ftmi_highway(None, 0, 1, 32, None, None, None, None, None, 0, 1, None, None), 1001),
     (lambda L: L.ftmi_split_weights(None, 4, 4, None, None), 1001),
     (lambda L: L.ftmi_split_weights_f16(None, 4, 4, None, None), 1001),
@@ -61,6 +61,17 @@ def test_strerror():
     (lambda L: L.ftmi_lr_index(None, 1, 1, 1, None, None), 1001),
     (lambda L: L.ftmi_length_regulate(None, 0, 1, 1, 4, None, 1, None, 0, None), 1001),
     (lambda L: L.ftmi_rowdot(None, 0, 1, 4, None, None, 1.0, None, None), 1001),
+    # ftmi_highway_stack: null input, C != 256, Cp % 4, n_out % 512, misaligned x
+    (lambda L: L.ftmi_highway_stack(None, 80, 10, 80, 256, ctypes.c_void_p(256), 0, None, None, None, None, None, 0, None, 0, ctypes.c_void_p(256), 256, None, None), 1001),
+    (lambda L: L.ftmi_highway_stack(ctypes.c_void_p(256), 80, 10, 80, 128, ctypes.c_void_p(256), 0, None, None, None, None, None, 0, None, 0, ctypes.c_void_p(512), 256, None, None), 1002),
+    (lambda L: L.ftmi_highway_stack(ctypes.c_void_p(256), 80, 10, 78, 256, ctypes.c_void_p(256), 0, None, None, None, None, None, 0, None, 0, ctypes.c_void_p(512), 256, None, None), 1002),
+    (lambda L: L.ftmi_highway_stack(ctypes.c_void_p(256), 80, 10, 80, 256, ctypes.c_void_p(256), 0, None, None, None, ctypes.c_void_p(256), None, 500, ctypes.c_void_p(1024), 500, None, 0, None, None), 1002),
+    (lambda L: L.ftmi_highway_stack(ctypes.c_void_p(260), 80, 10, 80, 256, ctypes.c_void_p(256), 0, None, None, None, None, None, 0, None, 0, ctypes.c_void_p(512), 256, None, None), 1004),
+    (lambda L: L.ftmi_split_weights_f16_frag(None, 16, 4, None, None), 1001),
+    (lambda L: L.ftmi_split_weights_f16_frag(ctypes.c_void_p(256), 20, 4, ctypes.c_void_p(256), None), 1002),
+    (lambda L: L.ftmi_attention(None, 0, 1, 1, 1, 64, 0, 64, 128, None, 1.0, None, 0, 2, None, None, 0, None), 1001),
+    (lambda L: L.ftmi_attention(ctypes.c_void_p(256), 192, 1, 1, 1, 96, 0, 96, 192, None, 1.0, ctypes.c_void_p(256), 96, 2, None, None, 0, None), 1003),
+    (lambda L: L.ftmi_attention(ctypes.c_void_p(256), 384, 1, 4, 2, 64, 0, 128, 256, None, 1.0, ctypes.c_void_p(256), 128, 2, None, ctypes.c_void_p(260), 1 << 20, None), 1004),
 ])
 def test_argument_errors(call, code):
     assert call(_lib.load()) == code
