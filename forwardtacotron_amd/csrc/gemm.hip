@@ -1877,7 +1877,10 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const GemmParams p
 // wave keeps its own 64 x 32 block in fp32 registers: exactly the x its next gating needs,
 // since the W1 and W2 columns of one h column (packed 32-column blocks) land in the same lane.
 // B fragments (the pre-split f16 planes; every workgroup reads the same 1.4 MB, L2-resident)
-// are loaded straight into registers one k-step ahead.  Per k-step, per product, the MFMA
+// are loaded straight into registers three k-steps ahead; each GEMM runs in 16-column
+// halves (a highway's W1 tile with its W2 tile) to keep that ring in the register budget.
+// (A 128-row variant with 8 waves x 128 x 32 measured 671 vs 694 us at the c3 postnet and
+// 209 vs 121 us at the prenet, where 100 tiles leave CUs idle: dropped.)  Per k-step, per product, the MFMA
 // order and the epilogue arithmetic are the slab kernel's, so the result is bit-identical to
 // the unfused chain.  HBM traffic per row: Cp floats in, n_out floats out (+ C with h).
 constexpr int HS_BM = 64;
@@ -1936,8 +1939,9 @@ __device__ __forceinline__ void hs_step(f32x4 (&acc)[4][NI], const _Float16 *Ah,
 
 // acc[mi][ni] (rows 16 mi + 4 fs + i, GEMM column of bp[ni] + fr) = A x B^T over nks k-steps
 // of 32, f16x3 (small terms first, as the slab kernel).  bp[ni]: the lane's B0 row + 8 fs.
-// B fragments ping-pong between two register sets, loaded one k-step ahead (the loop is
-// kept rolled: unrolled, the compiler hoists further loads and spills).
+// B fragments rotate through three register sets, loaded three k-steps ahead (the loop is
+// kept rolled and the steps fenced by sched barriers: otherwise the compiler hoists further
+// loads and LDS reads across steps and spills).
 template <int NI>
 __device__ __forceinline__ void hs_gemm(f32x4 (&acc)[4][NI], const _Float16 *Ah,
                                         const _Float16 *At, const _Float16 *const (&bp)[NI],
@@ -1946,7 +1950,10 @@ __device__ __forceinline__ void hs_gemm(f32x4 (&acc)[4][NI], const _Float16 *Ah,
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f16x8 x0[NI], x1[NI], y0[NI], y1[NI];
+  // three register sets in a ring: the loads of k-step ks + 3 are issued right after step
+  // ks consumed its set (one step of look-ahead left the L2 latency exposed: the MFMAs of a
+  // step are ~800 cycles per wave, a loaded L2 round trip is more)
+  f16x8 x0[NI], x1[NI], y0[NI], y1[NI], z0[NI], z1[NI];
   auto load = [&](f16x8 (&r0)[NI], f16x8 (&r1)[NI], int ks) {
     const int k = ks < nks ? ks : nks - 1;  // past the end: a clamped (unused) re-read
 #pragma unroll
@@ -1956,13 +1963,21 @@ __device__ __forceinline__ void hs_gemm(f32x4 (&acc)[4][NI], const _Float16 *Ah,
     }
   };
   load(x0, x1, 0);
+  load(y0, y1, 1);
+  load(z0, z1, 2);
 #pragma unroll 1
-  for (int ks = 0; ks < nks; ks += 2) {
-    load(y0, y1, ks + 1);
+  for (int ks = 0; ks < nks; ks += 3) {
     hs_step<NI>(acc, Ah, At, x0, x1, ks, fr, fs);
+    load(x0, x1, ks + 3);
+    __builtin_amdgcn_sched_barrier(0);  // no hoisting across steps (register budget)
     if (ks + 1 >= nks) break;
-    load(x0, x1, ks + 2);
     hs_step<NI>(acc, Ah, At, y0, y1, ks + 1, fr, fs);
+    load(y0, y1, ks + 4);
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + 2 >= nks) break;
+    hs_step<NI>(acc, Ah, At, z0, z1, ks + 2, fr, fs);
+    load(z0, z1, ks + 5);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -2037,15 +2052,15 @@ __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackPara
 
   // ---- highways: g = sigmoid(x W2^T + b2), x <- g relu(x W1^T + b1) + (1 - g) x
   for (int l = 0; l < p.L; ++l) {
-    f32x4 acc[4][4];
-    const _Float16 *bp[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-      bp[ni] = bptr(p.w_hw[l], 64 * cb + 16 * ni, HS_C);
     const _Float16 *A = lds + cur * 2 * HS_IMG;
-    hs_gemm<4>(acc, A, A + HS_IMG, bp, (int64_t)2 * HS_C * HS_C, HS_C / 32, fr, fs);
+    // two halves: W1 tile nj with its W2 tile (GEMM columns 64 cb + 16 nj, + 32), so one
+    // half's accumulators and B ring stay small
 #pragma unroll
     for (int nj = 0; nj < 2; ++nj) {
+      f32x4 acc[4][2];
+      const _Float16 *bp[2] = {bptr(p.w_hw[l], 64 * cb + 16 * nj, HS_C),
+                               bptr(p.w_hw[l], 64 * cb + 32 + 16 * nj, HS_C)};
+      hs_gemm<2>(acc, A, A + HS_IMG, bp, (int64_t)2 * HS_C * HS_C, HS_C / 32, fr, fs);
       const int col = 32 * cb + 16 * nj + fr;
       const float c1 = p.cs_hw[l][64 * cb + 16 * nj + fr];
       const float c2 = p.cs_hw[l][64 * cb + 32 + 16 * nj + fr];
@@ -2058,8 +2073,8 @@ __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackPara
           {
 #pragma clang fp contract(off)
             // rounded like the slab kernel: the column scale, then the bias
-            x1 = acc[mi][nj][i] * c1 + bb1;
-            x2 = acc[mi][nj + 2][i] * c2 + bb2;
+            x1 = acc[mi][0][i] * c1 + bb1;
+            x2 = acc[mi][1][i] * c2 + bb2;
           }
           const float g = ftmi_sigmoid(x2);
           xs[mi][nj][i] = highway_mix(g, x1, xs[mi][nj][i]);
@@ -2085,16 +2100,14 @@ __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackPara
   // ---- output projection (the GRU's x W_ih^T + b_ih), HS_NPASS columns per pass
   if (p.w_out) {
     const _Float16 *A = lds + cur * 2 * HS_IMG;
-    for (int q = 0; q < p.n_out / HS_NPASS; ++q) {
-      f32x4 acc[4][4];
-      const _Float16 *bp[4];
+    for (int q = 0; q < 2 * p.n_out / HS_NPASS; ++q) {  // 256 columns (32 per wave) a pass
+      f32x4 acc[4][2];
+      const int n0 = (HS_NPASS / 2) * q + 32 * cb;
+      const _Float16 *bp[2] = {bptr(p.w_out, n0, HS_C), bptr(p.w_out, n0 + 16, HS_C)};
+      hs_gemm<2>(acc, A, A + HS_IMG, bp, (int64_t)p.n_out * HS_C, HS_C / 32, fr, fs);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        bp[ni] = bptr(p.w_out, HS_NPASS * q + 64 * cb + 16 * ni, HS_C);
-      hs_gemm<4>(acc, A, A + HS_IMG, bp, (int64_t)p.n_out * HS_C, HS_C / 32, fr, fs);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const int col = HS_NPASS * q + 64 * cb + 16 * ni + fr;
+      for (int ni = 0; ni < 2; ++ni) {
+        const int col = n0 + 16 * ni + fr;
         const float cs = p.cs_out[col], b = p.b_out ? p.b_out[col] : 0.f;
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
