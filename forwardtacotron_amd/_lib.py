@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 9
+ABI_VERSION = 10
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -33,7 +33,7 @@ class ConvArgs(ctypes.Structure):
         ('bias', P), ('relu', c_int), ('bn_scale', P), ('bn_shift', P), ('maxpool', c_int),
         ('residual', P), ('res_stride', c_int64),
         ('y', P), ('y_stride', c_int64), ('yt', P), ('T_out', c_int), ('mma', c_int),
-        ('split_k', c_int), ('split_ws', P), ('w_split', P), ('status', P),
+        ('split_k', c_int), ('split_ws', P), ('w_split', P), ('status', P), ('x_split', c_int),
     ]
 
 
@@ -56,6 +56,7 @@ SIGNATURES = {
     'ftmi_split_weights_bytes': (c_int64, [c_int64, c_int64]),
     'ftmi_split_weights': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_split_weights_f16_bytes': (c_int64, [c_int64, c_int64]),
+    'ftmi_split_rows': (c_int, [P, c_int64, c_int64, c_int, P, c_int64, P, P]),
     'ftmi_split_weights_f16': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_split_weights_f16_frag': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_rnn_workspace_bytes': (c_int64, [c_int, c_int, c_int]),

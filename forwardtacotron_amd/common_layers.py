@@ -164,12 +164,13 @@ class BatchNormConv(Packed):
         w = pack_conv(self.conv.weight)
         return w, self.bnorm.folded(), presplit(w)
 
-    def forward_cl(self, x: torch.Tensor, T_out: int = 0, residual=None, maxpool=False) -> torch.Tensor:
+    def forward_cl(self, x: torch.Tensor, T_out: int = 0, residual=None, maxpool=False,
+                   x_split=False) -> torch.Tensor:
         w, bn, w3 = self.packed_weights()
         # bf16x6: the pre-split kernel measured slower on the maxpool (CBHG proj1) shapes
         y, _ = ops.conv1d(x, w, self.kernel, self.kernel // 2, relu=self.relu, bn=bn,
                           residual=residual, maxpool=maxpool, T_out=T_out,
-                          w_split=None if (maxpool and ops.MMA == 1) else w3)
+                          w_split=None if (maxpool and ops.MMA == 1) else w3, x_split=x_split)
         return y
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -299,9 +300,14 @@ class CBHG(Packed):
         """(B, T, Cin) channels-last -> (B, T, 2*channels)."""
         bank_w, scale, shift, w_pre, bank3, pre3 = self.packed_weights()
         pooled = ops.bank_pools(x, self.K, self.channels, w_split=bank3)
-        bank = ops.conv_bank(x, bank_w, self.K, self.channels, scale, shift, w_split=bank3,
-                             pool=pooled)  # pooled: the bank kernel applied the maxpool
-        y = self.conv_project1.forward_cl(bank, maxpool=not pooled)
+        # pooled: the bank kernel applied the maxpool, and (split) stored its output as the
+        # f16x3 split rows proj1 multiplies
+        split = pooled and ops.SPLIT_ROWS
+        xin = pooled and ops.SPLIT_BANK_IN  # x stays fp32 too: it is the proj2 residual
+        bank = ops.conv_bank(ops.split_rows(x) if xin else x, bank_w, self.K, self.channels,
+                             scale, shift, w_split=bank3, pool=pooled, split_out=split,
+                             x_split=xin)
+        y = self.conv_project1.forward_cl(bank, maxpool=not pooled, x_split=split)
         del bank
         y = self.conv_project2.forward_cl(y, residual=x)
         xp = self._highway_stack(y)

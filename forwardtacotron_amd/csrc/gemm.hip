@@ -94,6 +94,12 @@ struct GemmParams {
   // input of proj1, common_layers.py:100): y[t] = max(v[t - 1], v[t]), y[0] = v[0] per
   // sequence.  Tiles then step by SL_BM - 1 rows and carry one halo row.
   int pool_out;
+  // slab kernel, f16x3 activation rows ("split rows": per row C f16 heads, then C f16
+  // tails, x_stride / y_stride still counted in floats): x_split = the operand x is given
+  // split (staged as is, no split while staging; its producer checked the f16 range);
+  // y_split_c > 0 = the pool_out epilogue writes y as split rows of y_split_c channels
+  int x_split;
+  int y_split_c;
   GemmGroup g[MAX_GROUPS];
 };
 
@@ -1073,6 +1079,7 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
   _Float16 *const lds_a = lds;
   _Float16 *const lds_b = lds + 2 * 2 * SL_AIMG;
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   // XCD-aware order: blocks b and b + 8 run on the same XCD, and the tiles of one row tile
   // (every column tile of every group: a conv bank's groups all read the same input rows)
   // are consecutive in that XCD's order, so its slab rows are shared through L2.  Groups
@@ -1139,6 +1146,16 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
     const unsigned ch = cbase + (ach < a_last ? ach : a_last) + aseg;
     r.ok = ch < (unsigned)Cin;
     const unsigned o = r.ok ? ch : 0u;
+    if (!MAXPOOL && p.x_split) {  // split rows: 4 heads + the same 4 tails in one register
+#pragma unroll
+      for (int i = 0; i < SL_ASLOTS; ++i) {
+        const _Float16 *xr = (const _Float16 *)(p.x + aoff[i]) + o;
+        const u32x2 h = *(const u32x2 *)xr, t = *(const u32x2 *)(xr + Cin);
+        r.v[i] = __builtin_bit_cast(f32x4, ((u32x4){h.x, h.y, t.x, t.y}));
+      }
+      ach += 32;
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < SL_ASLOTS; ++i) {
       r.v[i] = *(const f32x4 *)(p.x + aoff[i] + o);
@@ -1156,6 +1173,13 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
       if (sr0 + (NSTG / 8) * i >= SR) continue;
       const int adst = adst0 + (NSTG / 8) * i * SL_P;
       f32x4 v = r.v[i];
+      if (!MAXPOOL && p.x_split) {  // already split (and range-checked by the producer)
+        u32x4 b = __builtin_bit_cast(u32x4, v);
+        if (!r.ok) b = (u32x4){0u, 0u, 0u, 0u};
+        *(u32x2 *)(dst + adst) = (u32x2){b.x, b.y};
+        *(u32x2 *)(dst + SL_AIMG + adst) = (u32x2){b.z, b.w};
+        continue;
+      }
       if constexpr (MAXPOOL) v = fmax4(v, r.u[i]);
       v = sel4(r.ok, v);
       amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
@@ -1414,14 +1438,25 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
         *(f32x4 *)(tile + r * SL_TP + c) = v;
       }
       __syncthreads();
+      float ymax = 0.f;
       for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
         const int r = idx >> 5, c = (idx & 31) * 4;
         if (r == 0 || r >= rows || c >= ncols) continue;
         const int row = m0 + r, col = n0 + c;
         f32x4 v = *(const f32x4 *)(tile + r * SL_TP + c);
         if (row % p.T > 0) v = fmax4(v, *(const f32x4 *)(tile + (r - 1) * SL_TP + c));
-        *(f32x4 *)(p.y + (int64_t)row * p.y_stride + G.ycol0 + col) = v;
+        if (p.y_split_c) {  // split rows for the next f16x3 GEMM (proj1), range-checked here
+          ymax = fmaxf(ymax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          f16x4 h, t;
+          split2h(v, h, t);
+          _Float16 *yr = (_Float16 *)(p.y + (int64_t)row * p.y_stride) + G.ycol0 + col;
+          *(f16x4 *)yr = h;
+          *(f16x4 *)(yr + p.y_split_c) = t;
+        } else {
+          *(f32x4 *)(p.y + (int64_t)row * p.y_stride + G.ycol0 + col) = v;
+        }
       }
+      if (!(ymax <= 65504.f) && p.status) atomicOr(p.status, 1u);
       return;
     }
     for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
@@ -1846,6 +1881,26 @@ __global__ __launch_bounds__(256) void split_weights_f16_kernel(const float *__r
 
 // Split-K finish: v = sum_s part[s][m][n] (fixed order: deterministic), then the
 // EPI_CONV epilogue (bias, ReLU, BN, residual, plain and transposed stores).
+// fp32 rows -> f16x3 split rows (include/ftmi.h): 4 channels per thread, range-checked
+__global__ __launch_bounds__(256) void split_rows_kernel(const float *__restrict__ x,
+                                                         int64_t x_stride, int64_t rows, int C,
+                                                         float *__restrict__ y, int64_t y_stride,
+                                                         unsigned *status) {
+  const int C4 = C >> 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * C4) return;
+  const int64_t r = i / C4;
+  const int c = (int)(i - r * C4) * 4;
+  const f32x4 v = *(const f32x4 *)(x + r * x_stride + c);
+  f16x4 h, t;
+  split2h(v, h, t);
+  _Float16 *yr = (_Float16 *)(y + r * y_stride) + c;
+  *(f16x4 *)yr = h;
+  *(f16x4 *)(yr + C) = t;
+  const float m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+  if (!(m <= 65504.f) && status) atomicOr(status, 1u);
+}
+
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const GemmParams p) {
   const GemmGroup &G = p.g[0];
   const int64_t total = (int64_t)p.M * G.N;
@@ -2321,6 +2376,11 @@ int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hip
       return FTMI_E_UNSUPPORTED;
     return launch_slab(q, epi, false, s);
   }
+  if (p.y_split_c) return FTMI_E_UNSUPPORTED;  // split output rows: pool_out only
+  if (p.x_split) {  // split operand rows: only the slab kernel stages them
+    if (!(mma == 2 && presplit && !maxpool && slab_ok(p, epi))) return FTMI_E_UNSUPPORTED;
+    return launch_slab(p, epi, false, s);
+  }
   if (mma == 2 && presplit && skinny_ok(p, epi)) return launch_skinny(p, epi, maxpool, s);
   if (p.ngroups > 1 && p.split_req > 1) {  // a bank split only serves the skinny kernel
     GemmParams q = p;
@@ -2448,6 +2508,9 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   p.yt = a->yt;
   p.yt_channels = a->N;
   p.status = a->status;
+  p.x_split = a->x_split != 0;
+  if (p.x_split && (a->mma != 2 || a->maxpool || a->x_stride < a->Cin))
+    return FTMI_E_UNSUPPORTED;
   GemmGroup &g = p.g[0];
   g.w = a->w;
   g.Kpad = (a->k * a->Cin + X6_BK - 1) / X6_BK * X6_BK;
@@ -2498,7 +2561,7 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
                                     float *y, int64_t y_stride, int32_t mma, uint32_t *status,
                                     int32_t split_k, float *split_ws, int32_t pool_out,
                                     ftmi_stream_t stream) {
-  if (split_k > 1 && !split_ws && !pool_out) return FTMI_E_ARG;
+  if (split_k > 1 && !split_ws && !(pool_out & FTMI_BANK_POOL)) return FTMI_E_ARG;
   if (!x || !w || !bn_scale || !bn_shift || !y) return FTMI_E_ARG;
   if (B <= 0 || T <= 0 || Cin <= 0 || Cout <= 0 || K <= 0) return FTMI_E_ARG;
   if (mma < 0 || mma > 2 || (mma == 2 && !w_split)) return FTMI_E_ARG;
@@ -2520,7 +2583,15 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
   p.y = y;
   p.y_stride = y_stride;
   p.status = status;
-  p.pool_out = pool_out ? 1 : 0;
+  if (pool_out & ~(FTMI_BANK_POOL | FTMI_BANK_Y_SPLIT | FTMI_BANK_X_SPLIT)) return FTMI_E_ARG;
+  p.pool_out = pool_out & FTMI_BANK_POOL;
+  if (pool_out & FTMI_BANK_Y_SPLIT) {  // split output rows need the pooled epilogue
+    if (!p.pool_out) return FTMI_E_UNSUPPORTED;
+    p.y_split_c = K * Cout;
+    if (y_stride < (int64_t)K * Cout) return FTMI_E_SHAPE;
+  }
+  p.x_split = (pool_out & FTMI_BANK_X_SPLIT) != 0;
+  if (p.x_split && mma != 2) return FTMI_E_UNSUPPORTED;
   const int mtiles = (p.M + BM - 1) / BM;
   const int ntiles = (Cout + BN - 1) / BN;
   int tile0 = 0;
@@ -2693,6 +2764,22 @@ extern "C" int ftmi_split_weights_f16(const float *w, int64_t N, int64_t K, void
 extern "C" int ftmi_split_weights_f16_frag(const float *w, int64_t N, int64_t K, void *out,
                                            ftmi_stream_t stream) {
   return split_f16(w, N, K, out, 1, stream);
+}
+
+extern "C" int ftmi_split_rows(const float *x, int64_t x_stride, int64_t rows, int32_t C,
+                               float *y, int64_t y_stride, uint32_t *status,
+                               ftmi_stream_t stream) {
+  if (!x || !y || rows < 0 || C <= 0) return FTMI_E_ARG;
+  if (C % 4 || x_stride < C || y_stride < C) return FTMI_E_SHAPE;
+  if (!ftmi_aligned16(x) || (x_stride & 3) || !ftmi_aligned16(y) || (y_stride & 3))
+    return FTMI_E_ALIGN;
+  if ((void *)x == (void *)y) return FTMI_E_ARG;  // rows are rewritten in another layout
+  const int64_t n = rows * (C / 4);
+  if (n == 0) return FTMI_OK;
+  hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     ftmi_hs(stream), x, x_stride, rows, C, y, y_stride, status);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
 }
 
 extern "C" int ftmi_split_weights(const float *w, int64_t N, int64_t K, void *out,

@@ -276,12 +276,15 @@ def split_bank_weights(w: torch.Tensor, K: int, Cin: int, Cout: int,
 
 def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, relu=False,
            bn=None, maxpool=False, residual=None, out=None, out_t=None, want_y=True,
-           T_out: int = 0, mma: Optional[int] = None, w_split: Optional[torch.Tensor] = None):
+           T_out: int = 0, mma: Optional[int] = None, w_split: Optional[torch.Tensor] = None,
+           x_split: bool = False):
     """Fused Conv1d (+bias, ReLU, BN, residual) on a channels-last (B, T, Cin) view.
 
     w: packed [N][k*Cin].  Returns (y, yt) where y is (B, T_out, N) (or `out`) and yt is
     the optional (B, N, T_out) transposed copy (`out_t`).  w_split: optional
-    `split_weights(w)` (bf16x6 path without the per-call weight split).
+    `split_weights(w)` (bf16x6 path without the per-call weight split).  x_split: x holds
+    f16x3 split rows (include/ftmi.h, e.g. conv_bank(split_out=True)); f16x3 slab kernel
+    only (the C side refuses other shapes with FTMI_E_UNSUPPORTED).
     """
     _dev(x, w, bias, residual, out, out_t, w_split)
     B, T, Cin, xs = _rows(x)
@@ -311,6 +314,7 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
     a.T_out = To
     a.mma, a.w_split = _gemm_mma(mma, w_split)
     a.status = status_word(x.device).data_ptr()
+    a.x_split = int(x_split)
     M = B * To
     if _skinny(a.mma, T, To, Cin, k, M, N):
         sk = _skinny_split(Cin)
@@ -319,7 +323,8 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
     if sk > 1:
         part = torch.empty(sk * M * N, device=x.device, dtype=_f32)
         a.split_k, a.split_ws = sk, part.data_ptr()
-    label = f'conv1d[M={M},N={N},K={k * Cin}{",maxpool" if maxpool else ""},mma={a.mma}]'
+    label = (f'conv1d[M={M},N={N},K={k * Cin}{",maxpool" if maxpool else ""}'
+             f'{",xsplit" if x_split else ""},mma={a.mma}]')
     launch('ftmi_conv1d', label, 2.0 * M * N * k * Cin,
            4.0 * (B * T * Cin + N * k * Cin + M * N * (1 + (residual is not None))),
            ctypes.byref(a), _stream())
@@ -327,6 +332,13 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
 
 
 POOL_BANK = os.environ.get('FTMI_POOL_BANK', '1') != '0'
+# the pooled bank hands proj1 its operand as f16x3 split rows (split once, not per column
+# tile of proj1: c3 proj1 -2..3 %, tools/ab_split.sh); FTMI_SPLIT_ROWS=0: fp32 rows
+SPLIT_ROWS = os.environ.get('FTMI_SPLIT_ROWS', '1') != '0'
+# FTMI_SPLIT_BANK_IN=1: the bank also takes its own input split once (split_rows) instead of
+# per group / column tile — measured neutral at c3 (the bank kernel saved what the extra
+# split launch cost: tools/ab_split.sh), so off by default
+SPLIT_BANK_IN = os.environ.get('FTMI_SPLIT_BANK_IN', '0') == '1'
 
 
 def bank_pools(x: torch.Tensor, K: int, Cout: int, mma: Optional[int] = None, w_split=None) -> bool:
@@ -340,9 +352,14 @@ def bank_pools(x: torch.Tensor, K: int, Cout: int, mma: Optional[int] = None, w_
 
 def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.Tensor,
               shift: torch.Tensor, mma: Optional[int] = None,
-              w_split: Optional[torch.Tensor] = None, pool: bool = False) -> torch.Tensor:
+              w_split: Optional[torch.Tensor] = None, pool: bool = False,
+              split_out: bool = False, x_split: bool = False) -> torch.Tensor:
     """CBHG conv bank, (B, T, Cin) -> (B, T, K*Cout); pool: the maxpool(2, 1) of it
-    (common_layers.py:73,100), stored by the bank kernel (see bank_pools)."""
+    (common_layers.py:73,100), stored by the bank kernel (see bank_pools); split_out (with
+    pool): stored as f16x3 split rows for proj1 (conv1d(x_split=True)); x_split: x holds
+    split rows (split_rows)."""
+    if split_out and not pool:
+        raise ValueError('split_out needs pool')
     _dev(x, w, scale, shift, w_split)
     B, T, Cin, xs = _rows(x)
     y = torch.empty(B, T, K * Cout, device=x.device, dtype=_f32)
@@ -353,11 +370,25 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
     if not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
         sk = _skinny_split(Cin)  # weight-streaming kernel: partial sums, finished in order
         part = torch.empty(sk * M * K * Cout, device=x.device, dtype=_f32)
-    launch('ftmi_conv_bank_split', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}{",pool" if pool else ""}]',
+    launch('ftmi_conv_bank_split', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}'
+           f'{",pool" if pool else ""}{",split" if split_out else ""}{",xsplit" if x_split else ""}]',
            flops, 4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
            x.data_ptr(), xs, B, T, Cin, w.data_ptr(), wsp, K, Cout,
            scale.data_ptr(), shift.data_ptr(), y.data_ptr(), y.stride(1), mma,
-           status_word(x.device).data_ptr(), sk, _ptr(part), int(pool), _stream())
+           status_word(x.device).data_ptr(), sk, _ptr(part),
+           int(pool) | (2 * int(split_out)) | (4 * int(x_split)), _stream())
+    return y
+
+
+def split_rows(x: torch.Tensor) -> torch.Tensor:
+    """(B, T, C) fp32 rows -> the same-size buffer holding them as f16x3 split rows (per row C
+    f16 heads then C scaled tails, include/ftmi.h), range-checked into the status word."""
+    _dev(x)
+    B, T, C, xs = _rows(x)
+    y = torch.empty(B, T, C, device=x.device, dtype=_f32)
+    launch('ftmi_split_rows', f'split_rows[M={B * T},C={C}]', 0.0, 8.0 * B * T * C,
+           x.data_ptr(), xs, B * T, C, y.data_ptr(), y.stride(1),
+           status_word(x.device).data_ptr(), _stream())
     return y
 
 

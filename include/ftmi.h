@@ -59,6 +59,11 @@ enum { FTMI_MMA_F32 = 0, FTMI_MMA_BF16X6 = 1, FTMI_MMA_F16X3 = 2 };
  *                            not a precision event */
 enum { FTMI_STATUS_F16_RANGE = 1, FTMI_STATUS_WHH_RANGE = 2, FTMI_STATUS_RNN_TIMEOUT = 4 };
 
+/* ftmi_conv_bank_split pool_out flags (ABI 10; 0 / 1 keep their ABI 9 meaning) */
+enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
+       FTMI_BANK_Y_SPLIT = 2, /* with FTMI_BANK_POOL: y as f16x3 split rows of K*Cout */
+       FTMI_BANK_X_SPLIT = 4  /* x given as f16x3 split rows of Cin (FTMI_MMA_F16X3) */ };
+
 /* ABI version; bumped on any signature change. */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
@@ -117,7 +122,16 @@ typedef struct ftmi_conv_args {
                           per-call weight split); FTMI_MMA_F16X3: REQUIRED
                           ftmi_split_weights_f16 planes */
   uint32_t *status;    /* optional device word: bit 0 set on f16 range overflow (F16X3) */
+  int32_t x_split;     /* ABI 10: x holds f16x3 SPLIT ROWS (below) instead of floats; only
+                          FTMI_MMA_F16X3 without maxpool on the slab kernel (B*T_out > 256
+                          rows), else FTMI_E_UNSUPPORTED.  x_stride (floats) >= Cin. */
 } ftmi_conv_args;
+
+/* f16x3 split rows (ABI 10): the activation layout one f16x3 GEMM hands the next.  Row r
+ * of a (rows, C) operand with row stride S floats holds, as halves, C heads h = f16(v) then
+ * C scaled tails t = f16((v - h) * 2^11) (v = h + 2^-11 t to ~2^-22 relative): the same 4
+ * bytes per element as fp32, the split done once by the producer instead of by every
+ * column tile of every consumer, which also checks the f16 range (status bit 0). */
 
 /* Split fp32 weights [N][K] once into three bf16 pieces (w = p0 + p1 + p2 exactly), laid
  * out [3][N][Kpad], Kpad = roundup(K, 32), zero padded; out must hold
@@ -159,10 +173,12 @@ int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32
  * order by a finishing launch (deterministic).  split_k <= 1 / split_ws NULL: as
  * ftmi_conv_bank.  Other shapes ignore the split.  ftmi_conv1d takes the same kernel for
  * B*T_out <= 256 (its split_k / split_ws as documented there).
- * pool_out (ABI 9): y receives the CBHG maxpool(2, 1) of the bank output (common_layers.py
- * :73,100: y[t] = max(bank[t - 1], bank[t]) within each sequence, y[0] = bank[0]) — the input
- * proj1 then reads with ftmi_conv_args.maxpool = 0.  Only on the f16x3 slab kernel
- * (mma = FTMI_MMA_F16X3, B*T > 256 rows, no split); elsewhere FTMI_E_UNSUPPORTED. */
+ * pool_out (ABI 9, flags since ABI 10): FTMI_BANK_POOL — y receives the CBHG maxpool(2, 1)
+ * of the bank output (common_layers.py:73,100: y[t] = max(bank[t - 1], bank[t]) within each
+ * sequence, y[0] = bank[0]) — the input proj1 then reads with ftmi_conv_args.maxpool = 0;
+ * only on the f16x3 slab kernel (mma = FTMI_MMA_F16X3, B*T > 256 rows, no split), elsewhere
+ * FTMI_E_UNSUPPORTED.  | FTMI_BANK_Y_SPLIT: y as split rows (proj1 then reads them with
+ * ftmi_conv_args.x_split = 1).  FTMI_BANK_X_SPLIT: x is given as split rows. */
 int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t Cin,
                          const float *w, const void *w_split, int32_t K, int32_t Cout,
                          const float *bn_scale, const float *bn_shift, float *y,
@@ -211,6 +227,13 @@ int ftmi_highway_split(const float *x, int64_t x_stride, int64_t M, int32_t C,
  * ABI 9): same byte size (ftmi_split_weights_f16_bytes), N % 16 == 0. */
 int ftmi_split_weights_f16_frag(const float *w, int64_t N, int64_t K, void *out,
                                 ftmi_stream_t stream);
+
+/* fp32 rows (rows, C) -> f16x3 split rows (ABI 10; the operand of ftmi_conv_args.x_split /
+ * FTMI_BANK_X_SPLIT) for an activation that is also needed in fp32 (a CBHG input is its
+ * residual too).  Sets status bit 0 (optional word) if |x| > 65504.  C % 4 == 0, strides in
+ * floats >= C, 16-B aligned, y must not alias x. */
+int ftmi_split_rows(const float *x, int64_t x_stride, int64_t rows, int32_t C, float *y,
+                    int64_t y_stride, uint32_t *status, ftmi_stream_t stream);
 
 int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, int32_t Cp, int32_t C,
                        const void *w_pre_split, int32_t L, const void *const *w_hw_split,

@@ -49,6 +49,13 @@ int main() {
                               nullptr), FTMI_E_UNSUPPORTED);
   EXPECT(ftmi_conv_bank_split(mis, 16, 1, 1, 16, a, a, 4, 8, a, a, a, 32, 2, nullptr, 0, nullptr, 0,
                               nullptr), FTMI_E_ALIGN);
+  EXPECT(ftmi_conv_bank_split(a, 16, 1, 1, 16, a, a, 4, 8, a, a, a, 32, 2, nullptr, 0, nullptr, 8,
+                              nullptr), FTMI_E_ARG);  // unknown pool_out flag
+  EXPECT(ftmi_conv_bank_split(a, 16, 1, 1, 16, a, a, 4, 8, a, a, a, 32, 2, nullptr, 0, nullptr,
+                              FTMI_BANK_Y_SPLIT, nullptr), FTMI_E_UNSUPPORTED);
+  ca.x_split = 1; ca.mma = FTMI_MMA_F32;
+  EXPECT(ftmi_conv1d(&ca, nullptr), FTMI_E_UNSUPPORTED);  // split rows off the f16x3 path
+  ca.x_split = 0; ca.mma = FTMI_MMA_F16X3;
   EXPECT(ftmi_highway(nullptr, 0, 1, 32, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 1, nullptr,
                       nullptr), FTMI_E_ARG);
   EXPECT(ftmi_highway(a, 32, 1, 40, a, a, a, a, buf + 1024, 40, 0, nullptr, nullptr), FTMI_E_SHAPE);

@@ -51,6 +51,9 @@ def test_strerror():
     (lambda L: L.ftmi_conv_bank(None, 0, 1, 1, 16, None, None, 4, 8, None, None, None, 0, 1, None, None), 1001),
     (lambda L: L.ftmi_conv_bank_split(None, 0, 1, 1, 16, None, None, 4, 8, None, None, None, 0, 1, None, 0, None, 0, None), 1001),
     (lambda L: L.ftmi_conv_bank_split(ctypes.c_void_p(256), 16, 1, 1, 16, ctypes.c_void_p(256), ctypes.c_void_p(256), 4, 8, ctypes.c_void_p(256), ctypes.c_void_p(256), ctypes.c_void_p(256), 32, 2, None, 4, None, 0, None), 1001),
+    # pool_out flags: unknown bit / split output rows without the pooled epilogue
+    (lambda L: L.ftmi_conv_bank_split(ctypes.c_void_p(256), 16, 1, 1, 16, ctypes.c_void_p(256), ctypes.c_void_p(256), 4, 8, ctypes.c_void_p(256), ctypes.c_void_p(256), ctypes.c_void_p(256), 32, 2, None, 0, None, 8, None), 1001),
+    (lambda L: L.ftmi_conv_bank_split(ctypes.c_void_p(256), 16, 1, 1, 16, ctypes.c_void_p(256), ctypes.c_void_p(256), 4, 8, ctypes.c_void_p(256), ctypes.c_void_p(256), ctypes.c_void_p(256), 32, 2, None, 0, None, 2, None), 1003),
     (lambda L: L.ftmi_highway(None, 0, 1, 32, None, None, None, None, None, 0, 1, None, None), 1001),
     (lambda L: L.ftmi_split_weights(None, 4, 4, None, None), 1001),
     (lambda L: L.ftmi_split_weights_f16(None, 4, 4, None, None), 1001),
@@ -91,6 +94,10 @@ def test_conv_shape_errors():
     assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1001
     a.mma = 2  # the f16x3 path needs the pre-split planes
     assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1001
+    a.mma, a.x_split = 0, 1  # split rows only on the f16x3 path
+    assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1003
+    a.mma, a.w_split, a.maxpool = 2, fake, 1  # ... and never under the maxpool operand
+    assert lib.ftmi_conv1d(ctypes.byref(a), None) == 1003
 
 
 def test_rnn_unsupported_hidden():

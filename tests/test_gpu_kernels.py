@@ -196,6 +196,59 @@ def test_conv_bank_pooled(K, Cin, B, T, rng, monkeypatch):
     close(yp, O.maxpool_k2_s1_p1(ref).transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
 
 
+def split_rows_host(v):
+    """The f16x3 split rows of include/ftmi.h (per row C heads, then C scaled tails)."""
+    h = v.astype(np.float16)
+    t = ((v - h.astype(np.float32)) * np.float32(2048)).astype(np.float16)
+    return np.concatenate([h, t], -1)
+
+
+@pytest.mark.parametrize('K,Cin,B,T,split_k', [(16, 256, 2, 300, 0), (8, 80, 3, 200, 0),
+                                               (8, 80, 1, 700, 3), (3, 64, 5, 61, 0)])
+def test_split_rows_bank_to_proj1(K, Cin, B, T, split_k, rng, monkeypatch):
+    """conv_bank(pool, split_out) stores the pooled bank as f16x3 split rows (bit-equal to
+    splitting the fp32 pooled output on the host) and proj1 with x_split=True gives exactly
+    the output of proj1 on the fp32 rows (the same head / tail feed the MFMAs), with and
+    without a channel split; the C side refuses x_split where the slab kernel does not run."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd._lib import FtmiError
+    from forwardtacotron_amd.common_layers import pack_conv
+    C = 256
+    x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
+    ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
+    sc = dev(rng.uniform(0.5, 1.5, K * C).astype(np.float32))
+    sh = dev(rng.normal(0, 0.1, K * C).astype(np.float32))
+    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
+    w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
+    xd = dev(x)
+    yp = ops.conv_bank(xd, wp, K, C, sc, sh, mma=2, w_split=w3, pool=True)
+    ys = ops.conv_bank(xd, wp, K, C, sc, sh, mma=2, w_split=w3, pool=True, split_out=True)
+    got = host(ys).view(np.float16)  # (B, T, 2*K*C) halves
+    np.testing.assert_array_equal(got, split_rows_host(host(yp)))
+    # the bank's own input as split rows (split_rows): the same bank output, bit for bit
+    xs = ops.split_rows(xd)
+    np.testing.assert_array_equal(host(xs).view(np.float16), split_rows_host(x))
+    yx = ops.conv_bank(xs, wp, K, C, sc, sh, mma=2, w_split=w3, pool=True, x_split=True)
+    np.testing.assert_array_equal(host(yx), host(yp))
+    st = ops.status_word(xd.device)
+    assert int(st.item()) == 0
+    ops.split_rows(xd * 1e5)  # beyond the f16 range: the producer flags it
+    assert int(st.item()) & 1
+    st.zero_()
+    w1 = dev(rng.normal(0, 1 / np.sqrt(3 * K * C), (256, 3 * K * C)).astype(np.float32))
+    w13 = ops.split_weights_f16(w1)
+    bn = (dev(rng.uniform(0.5, 1.5, 256).astype(np.float32)), dev(rng.normal(0, .1, 256).astype(np.float32)))
+    if split_k:
+        monkeypatch.setattr(ops, '_split_k', lambda *a: split_k)
+    ref, _ = ops.conv1d(yp, w1, 3, 1, relu=True, bn=bn, mma=2, w_split=w13)
+    out, _ = ops.conv1d(ys, w1, 3, 1, relu=True, bn=bn, mma=2, w_split=w13, x_split=True)
+    np.testing.assert_array_equal(host(out), host(ref))
+    with pytest.raises(FtmiError):  # maxpool on split rows: refused, not misread
+        ops.conv1d(ys, w1, 3, 1, maxpool=True, mma=2, w_split=w13, x_split=True)
+    with pytest.raises(FtmiError):  # x_split off the f16x3 path
+        ops.conv1d(ys, w1, 3, 1, mma=0, x_split=True)
+
+
 @pytest.mark.parametrize('balanced', ['1', '0'])
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (8, 80, 1, 100), (4, 64, 2, 50),
                                      (16, 256, 2, 100)])
