@@ -376,11 +376,12 @@ class ForwardTacotron(nn.Module):
         none of it depends on T_mel, so it runs while the duration path finishes and the
         host waits for T_mel (the one host sync, a pinned copy queued right after the
         duration kernel).  Issue order = priority order: prenet, durations, pitch,
-        energy.  Returns (dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel, xp) with every
-        tensor ready on the caller's stream (xp: the LSTM input projection of enc plus the
-        pitch / energy projections, folded through W_ih; enc itself does not carry them).
-        capture=True (graph capture, see _phoneme_graph): no host sync, the T_mel slot holds
-        max(totals) on the device."""
+        energy.  Returns (dur_hat, pitch_hat, energy_hat, enc, (offsets, index), T_mel, xp)
+        with every tensor ready on the caller's stream (xp: the LSTM input projection of enc
+        plus the pitch / energy projections, folded through W_ih; enc itself does not carry
+        them; index: the LR index map, queued on the caller's stream before it joins the side
+        streams).  capture=True (graph capture, see _phoneme_graph): no host sync, the T_mel
+        slot holds max(totals) on the device and the offsets slot plain offsets."""
         main = torch.cuda.current_stream(x.device)
         s_pitch, s_energy, s_prenet = self._side_streams(x.device, x.size(0))
         for s in (s_pitch, s_energy, s_prenet):
@@ -419,6 +420,14 @@ class ForwardTacotron(nn.Module):
         if batch is not None:  # a shard of a larger batch (sharded.GlobalBatch): batch-global
             offsets, totals = batch.duration_counts(dur_hat)  # fill rule / T_mel
             T_mel = batch.t_mel(totals)
+        index = None
+        if not capture:
+            if t_ready is not None:
+                t_ready.synchronize()
+                T_mel = int(t_host)
+            # the LR index map only needs the durations: queued before the caller's stream
+            # joins the side streams, so it is not held behind the prenet chain's tail
+            index = ops.lr_index(offsets, T_mel)
         for s, ts in ((s_pitch, (pitch_hat,)), (s_energy, (energy_hat,)),
                       (s_prenet, (enc, xp))):
             main.wait_stream(s)
@@ -427,10 +436,7 @@ class ForwardTacotron(nn.Module):
                     t.record_stream(main)
         if capture:
             return dur_hat, pitch_hat, energy_hat, enc, offsets, tmax, xp
-        if t_ready is not None:
-            t_ready.synchronize()
-            T_mel = int(t_host)
-        return dur_hat, pitch_hat, energy_hat, enc, offsets, T_mel, xp
+        return dur_hat, pitch_hat, energy_hat, enc, (offsets, index), T_mel, xp
 
     def generate(self,
                  x: torch.Tensor,
@@ -491,12 +497,16 @@ class ForwardTacotron(nn.Module):
             wp, bp, we, be = self._series_proj_weights()
             ops.series_proj_add(enc, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
                                 self.energy_strength)
+        index = None
         if lr is None:
             offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=False)
             T_mel = int(totals.max().item())  # the one host sync: output size is data dependent
         else:
             offsets, T_mel = lr
-        index = ops.lr_index(offsets, T_mel)
+            if isinstance(offsets, tuple):  # (offsets, index map already queued)
+                offsets, index = offsets
+        if index is None:
+            index = ops.lr_index(offsets, T_mel)
         mel, mel_post = self._decode(enc, index, xp=xp)
         return {'mel': mel, 'mel_post': mel_post, 'dur': dur_hat,
                 'pitch': pitch_hat, 'energy': energy_hat}
