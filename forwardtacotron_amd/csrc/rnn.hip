@@ -215,6 +215,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   constexpr int KWI = FUSE ? FUSE_CIN / WK : 32;  // input channels per wave
   constexpr int KSI = KWI / 32;                   // their 32-deep k-steps
   constexpr int RR = FUSE ? 2 * R : R;            // reduction rows: W_hh h [+ W_ih x]
+  constexpr float GSC = H3 ? H3_UNSCALE : 1.f;     // scale of the reduced W_hh h sums
 
   __shared__ __attribute__((aligned(16))) float red[WK * RR * RED_STRIDE];
   __shared__ __attribute__((aligned(16))) float hloc[LOCAL ? 2 * 16 * H : 4];
@@ -668,8 +669,8 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
           acc[i] = c;
         }
       }
-#pragma unroll
-      for (int i = 0; i < RBW; ++i) acc[i] *= H3_UNSCALE;
+      // the 2^11 scale of the products stays in the partial sums: the cell applies 2^-11
+      // in its first FMA (exact: a power of two), off the MFMA -> LDS critical path
     } else if constexpr (X6) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -725,7 +726,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         float sum = red[row * RED_STRIDE + bl];
 #pragma unroll
         for (int w = 1; w < WK; ++w) sum += red[(w * RR + row) * RED_STRIDE + bl];
-        gs[g] = sum;
+        gs[g] = sum;  // H3: 2^11 (W_hh h)
         if constexpr (FUSE) {  // x_t W_ih^T + b_ih (the unfused path adds b_ih in its GEMM)
           float sx = red[(R + row) * RED_STRIDE + bl];
 #pragma unroll
@@ -738,16 +739,16 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       float hn;
       if (CELL == 0) {
         // ATen GRU cell: r, z, n ; h' = n + z * (h - n)
-        const float r = fast_sigmoid(gi[0] + (gs[0] + bhh[j][0]));
-        const float z = fast_sigmoid(gi[1] + (gs[1] + bhh[j][1]));
-        const float n = fast_tanh(gi[2] + r * (gs[2] + bhh[j][2]));
+        const float r = fast_sigmoid(gi[0] + fmaf(gs[0], GSC, bhh[j][0]));
+        const float z = fast_sigmoid(gi[1] + fmaf(gs[1], GSC, bhh[j][1]));
+        const float n = fast_tanh(gi[2] + r * fmaf(gs[2], GSC, bhh[j][2]));
         hn = n + z * (hstate[j] - n);
       } else {
         // LSTM cell: i, f, g, o
-        const float ig = fast_sigmoid(gi[0] + gs[0]);
-        const float fg = fast_sigmoid(gi[1] + gs[1]);
-        const float gg = fast_tanh(gi[2] + gs[2]);
-        const float og = fast_sigmoid(gi[3] + gs[3]);
+        const float ig = fast_sigmoid(fmaf(gs[0], GSC, gi[0]));
+        const float fg = fast_sigmoid(fmaf(gs[1], GSC, gi[1]));
+        const float gg = fast_tanh(fmaf(gs[2], GSC, gi[2]));
+        const float og = fast_sigmoid(fmaf(gs[3], GSC, gi[3]));
         cstate[j] = fg * cstate[j] + ig * gg;
         hn = og * fast_tanh(cstate[j]);
       }
