@@ -18,6 +18,11 @@ FastPitch (model='fast_pitch'): LayerNorm gamma ~ U(0.75, 1.25), beta ~ N(0, 0.1
 pos_encoder.scale ~ U(0.9, 1.1); pos_encoder.pe is the model's own sinusoid buffer (not
 drawn); dur_pred.lin weight x FP_DUR_GAIN, bias = FP_DUR_BIAS (~6.5 frames / phoneme);
 lin.weight x FP_MEL_GAIN (the transformer output is LayerNorm-ed, O(1) per channel).
+
+WaveRNN vocoder (model='wavernn', models/fatchord_version.py): BatchNorm as above; the
+upsampling smoothers `upsample.up_layers.{1,3,5}.weight` keep the reference's own init
+(fill 1/k, :78-79); fc3.weight x WR_FC3_GAIN (peaked class posteriors, so the sampled
+sequence depends on the logits and not only on the noise).
 """
 from __future__ import annotations
 
@@ -34,6 +39,7 @@ POST_GAIN = 6.0
 FP_DUR_BIAS = 6.0
 FP_DUR_GAIN = 1.5
 FP_MEL_GAIN = 4.0
+WR_FC3_GAIN = 0.25
 
 # forward_tacotron.model and dsp sections of the reference config.yaml (:9-34, :76-106)
 DEFAULT_CONFIG = {
@@ -73,6 +79,14 @@ DEFAULT_CONFIG['fast_pitch'] = {'model': {
 }}
 
 
+# vocoder.model section of the reference config.yaml (:187-198), and its generation
+# defaults (:213-215, gen_forward.py:55-56)
+DEFAULT_CONFIG['vocoder'] = {'model': {
+    'mode': 'RAW', 'upsample_factors': [4, 8, 8], 'rnn_dims': 512, 'fc_dims': 512,
+    'compute_dims': 128, 'res_out_dims': 128, 'res_blocks': 10, 'pad': 2,
+}, 'generate': {'gen_batched': True, 'target': 11000, 'overlap': 550}}
+
+
 def default_config() -> dict:
     return copy.deepcopy(DEFAULT_CONFIG)
 
@@ -89,6 +103,16 @@ def synthetic_array(key: str, shape, dtype: str, seed: int = 0,
     shape = tuple(shape)
     if dtype.startswith('int'):
         return np.zeros(shape, dtype=np.int64)
+    if model == 'wavernn':
+        if '.up_layers.' in key:
+            return np.full(shape, 1.0 / shape[-1], dtype=np.float32)
+        if '.batch_norm' in key:
+            a = rng.uniform(0.75, 1.25, shape) if leaf in ('weight', 'running_var') else rng.normal(0.0, 0.1, shape)
+            return a.astype(np.float32)
+        a = _generic(rng, key, leaf, shape)
+        if key == 'fc3.weight':
+            a = a * WR_FC3_GAIN
+        return a.astype(np.float32)
     if model == 'fast_pitch':
         parent = key.rsplit('.', 2)[-2] if key.count('.') >= 1 else ''
         if parent.startswith('norm'):
