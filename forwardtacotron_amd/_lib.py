@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 10
+ABI_VERSION = 11
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -35,6 +35,16 @@ class ConvArgs(ctypes.Structure):
         ('y', P), ('y_stride', c_int64), ('yt', P), ('T_out', c_int), ('mma', c_int),
         ('split_k', c_int), ('split_ws', P), ('w_split', P), ('status', P), ('x_split', c_int),
     ]
+
+
+class WaveRNNArgs(ctypes.Structure):
+    """Mirror of ftmi_wavernn_args (include/ftmi.h)."""
+    _fields_ = [(n, P) for n in ('w_hh1', 'w_hh2', 'w_ih2a', 'w_fc1a', 'w_fc2a', 'w_fc3', 'b_fc3',
+                                 'b_hh1', 'b_hh2', 'u1', 'u2', 'v1', 'wm', 'cond', 'mel', 'xin',
+                                 'samples', 'logits', 'workspace', 'status')] + [
+        ('seed', ctypes.c_uint64)] + [(n, c_int) for n in (
+            'bias_row', 'item_rows', 'frames_per_item', 'hop', 'fold_stride', 'batched', 'B', 'L',
+            'n_classes', 'mol', 'rnn_dims', 'fc_dims', 'feat_dims', 'aux_dims')]
 
 
 # name -> (restype, argtypes); the exact export list of include/ftmi.h
@@ -89,6 +99,12 @@ SIGNATURES = {
     'ftmi_spec_mul': (c_int, [P, P, c_int64, P, P]),
     'ftmi_istft_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
     'ftmi_istft': (c_int, [P, c_int, c_int, P, c_int, c_int, P, P, P, P, P, c_int64, c_int64, P]),
+    'ftmi_wr_stretch_conv': (c_int, [P, c_int64, c_int, c_int, c_int, c_int, P, P, c_int64, c_int,
+                                     c_int, P]),
+    'ftmi_wavernn_workspace_bytes': (c_int64, []),
+    'ftmi_wavernn': (c_int, [ctypes.POINTER(WaveRNNArgs), P]),
+    'ftmi_set_wavernn_spin_limit': (ctypes.c_uint32, [ctypes.c_uint32]),
+    'ftmi_wr_unfold': (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     'ftmi_mel_nnls': (c_int, [P, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P,
                               c_float, c_int, P, P]),
 }

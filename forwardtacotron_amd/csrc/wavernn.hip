@@ -1,0 +1,806 @@
+// WaveRNN vocoder (reference: models/fatchord_version.py, the `gen_forward.py wavernn`
+// option) on gfx950.
+//
+//   wr_stretch_conv_kernel   Stretch2d(s, 1) + Conv2d(1, 1, (1, 2s+1), pad (0, s)), one
+//                            UpsampleNetwork.up_layers pair (:74-81, :88), on time-major rows
+//   wavernn_kernel           the sample loop of WaveRNN.generate (:203-241) — or, teacher-
+//                            forced, WaveRNN.forward (:145-169) — as ONE persistent launch
+//   wr_unfold_kernel         generate's tail (:246-261): mu-law decode, xfade_and_unfold
+//                            (:343-406), crop, 20-hop fade-out; float64 like the reference
+//
+// The sample loop.  Per step t and fold b the reference computes
+//   x = I([s_{t-1}, m_t, a1_t]);  h1 = GRU1(x, h1);  x += h1;  h2 = GRU2([x, a2_t], h2);
+//   x += h2;  y1 = relu(fc1([x, a3_t]));  y2 = relu(fc2([y1, a4_t]));  l = fc3(y2);
+//   s_t ~ Categorical(softmax(l))  (RAW)  |  discretized mix-of-logistics draw (MOL)
+// Everything that does not depend on the sample chain is moved off it (host packing,
+// float64, once per weights version):
+//   W_ih1 x + b_ih1  = G1(m_t, a1_t) + u1 s_{t-1},  u1 = W_ih1 w0  (w0 = I.weight[:, 0])
+//   W_ih2 [x, a2] + b = Q(m_t, a1_t, a2_t) + u2 s_{t-1} + W_ih2a h1
+//   fc1([x, a3])     = R(m_t, a1_t, a3_t) + v1 s_{t-1} + W_fc1a (h1 + h2)
+//   fc2([y1, a4])    = S(a4_t) + W_fc2a y1
+// G1, Q, R, S split into a per-FRAME part (the aux features are constant over a hop: one
+// small GEMM on the caller side, `cond` rows) and a per-SAMPLE part from the 80 upsampled
+// mel features (`wm`, computed here in the idle phase of each step).  What stays on the
+// chain per step: W_hh1 h1 / W_hh2 h2 (both from the previous step: off the chain too),
+// W_ih2a h1_t, W_fc1a (h1 + h2), W_fc2a y1, W_fc3 y2 and the draw — five all-to-all edges.
+//
+// Decomposition: 256 workgroups (one per CU, co-residency checked by an arrival barrier
+// with a bounded spin), two roles:
+//   GRU workgroups g < 128: units 4g..4g+3 of both GRUs (12 gate rows of W_hh1, W_hh2,
+//     W_ih2a in VGPRs), the cell updates, h1 / h2 publication.
+//   FC workgroups f = 128..255: rows 4f..4f+3 of fc1 and fc2, NCR rows of fc3, the Gumbel
+//     draw of those rows, publication of y1, y2 and the rows' best (value, index).
+// Matrix-vector products are exact fp32 FMAs on the VALU: a 16-wide MFMA tile would carry
+// B <= 32 live columns at most and the chain is bound by the hand-offs, not the flops.
+// Thread layout of a product: slot s = tid / 8 owns (row, k-part), its 8 lanes hold
+// interleaved 4-float chunks of that row's k-part (a wave-wide LDS read of the vector is
+// 8 consecutive 128-B runs: broadcast across slots, conflict-free within one); the 8
+// lanes meet by xor shuffles, the k-parts in a fixed order through LDS.
+//
+// Hand-off: the data is the flag (rnn.hip): every exchanged value carries the step tag in
+// its mantissa LSB (the tagged value is the one used everywhere), two parity halves,
+// write-through (`sc1`) 4-byte stores, `sc1` 16-byte polls until every word carries the tag
+// (MI355X_MICROARCH.md, data-tagged granules).  The draw's partials are 8-byte {value,
+// index|tag} granules written by one store.  Parity double buffering is race-free: a
+// producer of step t has acquired s_{t-1}, which every workgroup published only after
+// consuming step t-2's data.  Every spin is bounded: a timeout sets the error word and
+// FTMI_STATUS_RNN_TIMEOUT in *status, never a silent result.
+//
+// Randomness: Philox4x32-10 (Salmon et al., Random123), key = seed, counter (t, b, k/4, 0)
+// for class k of RAW (the Gumbel form argmax_k l_k - log(-log u_k) of torch.multinomial's
+// single draw argmax p_k / E_k, E_k ~ Exp(1)); MOL: counters (t, b, k/4, 1) for the
+// mixture choice and (t, b, 0, 2) for the logistic draw, mapped to uniform_(1e-5, 1-1e-5)
+// like utils/distribution.py:113,122.  oracle/wr_torch_cpu.py restates the same stream.
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int WR_R = 512;    // rnn_dims
+constexpr int WR_F = 512;    // fc_dims
+constexpr int WR_NM = 80;    // mel features (feat_dims)
+constexpr int WR_NA = 32;    // aux_dims = res_out_dims / 4
+constexpr int WR_NT = 256;   // threads per workgroup
+constexpr int WR_NG = 128;   // GRU workgroups
+constexpr int WR_NF = 128;   // FC workgroups
+constexpr int WR_UG = WR_R / WR_NG;  // 4 units per GRU workgroup
+constexpr int WR_FR = WR_F / WR_NF;  // 4 fc1 / fc2 rows per FC workgroup
+constexpr int WR_GRID = WR_NG + WR_NF;
+constexpr int WR_NBMAX = 32;         // folds per launch
+constexpr int WR_COND = 6 * WR_R + 2 * WR_F;  // cond row: [G1 3R | Q 3R | R F | S F]
+// exchange slots: h1, h2, y1, y2 ([2][NBV][512] floats each), then the draw partials
+// ([2][NBV][128] 8-byte granules)
+constexpr int XS_VEC = 2 * WR_NBMAX * 512;   // floats per vector slot
+constexpr int XS_Z = 2 * WR_NBMAX * WR_NF * 2;  // words of the draw slot
+constexpr int WS_CTRL = 64;                  // control words (error, arrival)
+constexpr unsigned SPIN_DEFAULT = 1u << 22;
+constexpr unsigned STATUS_TIMEOUT = 4u;
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned step_tag(int t) { return (((unsigned)t >> 1) & 1u) ^ 1u; }
+__device__ __forceinline__ float tagged(float v, int t) {
+  return __uint_as_float((__float_as_uint(v) & ~1u) | step_tag(t));
+}
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// Philox4x32-10 (Random123): 10 rounds of two 32x32->64 multiplies
+__device__ __forceinline__ u32x4 philox(u32x4 c, unsigned k0, unsigned k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c.x;
+    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c.z;
+    const unsigned hi0 = (unsigned)(p0 >> 32), lo0 = (unsigned)p0;
+    const unsigned hi1 = (unsigned)(p1 >> 32), lo1 = (unsigned)p1;
+    c = (u32x4){hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+__device__ __forceinline__ float u01(unsigned x) {  // (0, 1), exact in fp32
+  return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-08f;
+}
+__device__ __forceinline__ unsigned pword(const u32x4 &v, int i) {
+  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+
+struct WrParams {
+  const float *w_hh1, *w_hh2, *w_ih2a;  // [3R][R]
+  const float *w_fc1a, *w_fc2a;         // [F][R], [F][F]
+  const float *w_fc3, *b_fc3;           // [NC][F], [NC]
+  const float *b_hh1, *b_hh2;           // [3R]
+  const float *u1, *u2, *v1;            // [3R], [3R], [F]
+  const float *wm;                      // [6R + F][80]: mel columns of G1 | Q | R
+  const float *cond;                    // (n_frames + 1) rows of WR_COND floats
+  const float *mel;                     // (items * item_rows) rows of 80 floats
+  int bias_row;                         // cond row of a padded position (biases only)
+  int item_rows, frames_per_item, hop, fold_stride, batched;
+  int fold0;                            // first fold of this launch (batched: its offset)
+  const float *xin;                     // teacher-forced input samples (B_total, L) or NULL
+  float *samples;                       // generate: (B_total, L) output samples
+  float *logits;                        // teacher-forced: (B_total, L, NC) or NULL
+  float *xch;                           // exchange slots
+  unsigned *ws;                         // control words
+  unsigned *status;
+  int B, L, NC, mol;
+  unsigned k0, k1;                      // Philox key
+  unsigned spin_limit;
+};
+
+__device__ __forceinline__ void report_timeout(const WrParams &p) {
+  __hip_atomic_store(p.ws, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (p.status) atomicOr(p.status, STATUS_TIMEOUT);
+}
+
+// position of fold b (launch-local), step t in the conditioning rows
+struct Pos {
+  int mel_row;    // -1: padded (zero) position
+  int cond_row;
+};
+__device__ __forceinline__ Pos position(const WrParams &p, int b, int t) {
+  const int fb = p.fold0 + b;
+  const int g = p.batched ? fb * p.fold_stride + t : t;
+  const int item = p.batched ? 0 : fb;
+  Pos r;
+  if (t < p.L && g < p.item_rows) {
+    r.mel_row = item * p.item_rows + g;
+    r.cond_row = item * p.frames_per_item + g / p.hop;
+  } else {
+    r.mel_row = -1;
+    r.cond_row = p.bias_row;
+  }
+  return r;
+}
+
+template <int NBV>
+struct WrShared {
+  float vec[NBV * 512];          // the acquired vector (h1 / h2 / h1+h2 / y1 / y2)
+  float part[3][32][NBV];        // per-slot partial sums of the products
+  float partm[32][NBV];          // per-slot partial sums of the mel conditioning
+  float melv[NBV * WR_NM];       // this step's mel rows
+  float sval[NBV];               // s_{t-1}
+  int abort_flag;
+};
+
+// acquire the tagged vector of exchange slot `slot`, step t, into LDS (add: accumulate).
+// Every chunk of the thread is requested at once, then only the stale ones are polled
+// again (a serial poll per chunk would pay the hand-off latency once per chunk).  On a
+// timeout the workgroup's abort flag is set; the caller barriers and checks it.
+template <int NBV>
+__device__ __forceinline__ void acquire_vec(const WrParams &p, WrShared<NBV> &sh, int slot, int t,
+                                            bool add) {
+  constexpr int PER = NBV * 128 / WR_NT;  // 16-B chunks per thread
+  const int tid = threadIdx.x;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.xch, (short)0, 0x7FFFFFF0, 0x00020000);
+  const unsigned want = step_tag(t);
+  const int soff = (slot * XS_VEC + (t & 1) * WR_NBMAX * 512) * 4;
+  u32x4 r[PER];
+  unsigned stale = 0;  // bit i: chunk i still to be (re)loaded
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    r[i] = (u32x4){0u, 0u, 0u, 0u};
+    if (((tid + i * WR_NT) >> 7) < p.B) stale |= 1u << i;
+  }
+  for (unsigned spins = 0; stale; ++spins) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (stale & (1u << i))
+        r[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (unsigned)((tid + i * WR_NT) * 16), soff, 16);
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (stale & (1u << i)) {
+        const u32x4 v = r[i];
+        const bool fresh = want ? ((v.x & v.y & v.z & v.w) & 1u) != 0u
+                                : ((v.x | v.y | v.z | v.w) & 1u) == 0u;
+        if (fresh) stale &= ~(1u << i);
+      }
+    if (stale && spins > p.spin_limit) {
+      sh.abort_flag = 1;
+      report_timeout(p);
+      break;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const f32x4 v = __builtin_bit_cast(f32x4, r[i]);
+    f32x4 *dst = (f32x4 *)&sh.vec[(tid + i * WR_NT) * 4];
+    if (add) *dst = *dst + v;
+    else *dst = v;
+  }
+}
+
+__device__ __forceinline__ void publish(const WrParams &p, int slot, int t, int b, int col, float v) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.xch, (short)0, 0x7FFFFFF0, 0x00020000);
+  const int soff = (slot * XS_VEC + (t & 1) * WR_NBMAX * 512) * 4;
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (unsigned)((b * 512 + col) * 4),
+                                        soff, 16);
+}
+
+// draw slot granule (t, b, producer f): {value (tagged LSB), index | tag << 16}
+__device__ __forceinline__ void publish_z(const WrParams &p, int t, int b, int f, float v, int idx) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.xch, (short)0, 0x7FFFFFF0, 0x00020000);
+  const int soff = (4 * XS_VEC + (t & 1) * WR_NBMAX * WR_NF * 2) * 4;
+  const u32x2 g = {__float_as_uint(tagged(v, t)), (unsigned)idx | (step_tag(t) << 16)};
+  __builtin_amdgcn_raw_buffer_store_b64(g, rsrc, (unsigned)(((b * WR_NF) + f) * 8), soff, 16);
+}
+
+// s_t (the sample drawn from step t's logits) of every fold into sh.sval; with `store`
+// also to p.samples.  Producers of the draw slot: RAW the 128 FC workgroups (their rows'
+// best Gumbel score and its class), MOL the NC logits.  8 threads per fold, each with its
+// (up to 8) 16-byte granule pairs requested at once.  On a timeout the abort flag is set
+// (visible after the internal barrier).
+template <int NBV>
+__device__ void acquire_sample(const WrParams &p, WrShared<NBV> &sh, int t, bool store) {
+  const int tid = threadIdx.x;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.xch, (short)0, 0x7FFFFFF0, 0x00020000);
+  const unsigned want = step_tag(t);
+  const int soff = (4 * XS_VEC + (t & 1) * WR_NBMAX * WR_NF * 2) * 4;
+  const int np = p.mol ? p.NC : WR_NF;
+  const int b = tid >> 3, part = tid & 7;
+  constexpr int PER = WR_NF / 16;
+  u32x4 r[PER];
+  unsigned stale = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    r[i] = (u32x4){0u, 0u, 0u, 0u};
+    if (b < p.B && part * 2 + 16 * i < np) stale |= 1u << i;
+  }
+  for (unsigned spins = 0; stale; ++spins) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (stale & (1u << i))
+        r[i] = __builtin_amdgcn_raw_buffer_load_b128(
+            rsrc, (unsigned)((b * WR_NF + part * 2 + 16 * i) * 8), soff, 16);
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (stale & (1u << i)) {
+        const u32x4 v = r[i];
+        const bool two = part * 2 + 16 * i + 1 < np;
+        const bool f0 = (v.x & 1u) == want && ((v.y >> 16) & 1u) == want;
+        const bool f1 = !two || ((v.z & 1u) == want && ((v.w >> 16) & 1u) == want);
+        if (f0 && f1) stale &= ~(1u << i);
+      }
+    if (stale && spins > p.spin_limit) {
+      sh.abort_flag = 1;
+      report_timeout(p);
+      break;
+    }
+  }
+  float best = -INFINITY;
+  int bidx = 0x7fffffff;
+  if (b < p.B) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = part * 2 + 16 * i;
+      if (q >= np) continue;
+      const u32x4 v = r[i];
+      const float v0 = __uint_as_float(v.x), v1 = __uint_as_float(v.z);
+      const int i0 = (int)(v.y & 0xFFFFu), i1 = (int)(v.w & 0xFFFFu);
+      if (p.mol) {
+        sh.vec[b * 512 + q] = v0;
+        if (q + 1 < np) sh.vec[b * 512 + q + 1] = v1;
+      } else {
+        if (v0 > best || (v0 == best && i0 < bidx)) best = v0, bidx = i0;
+        if (q + 1 < np && (v1 > best || (v1 == best && i1 < bidx))) best = v1, bidx = i1;
+      }
+    }
+  }
+  if (!p.mol) {
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      const float ob = __shfl_xor(best, m);
+      const int oi = __shfl_xor(bidx, m);
+      if (ob > best || (ob == best && oi < bidx)) best = ob, bidx = oi;
+    }
+    if (part == 0 && b < NBV) {
+      // reference :237: 2 * idx.float() / (n_classes - 1.) - 1. in fp32
+      const float v = (2.0f * (float)bidx) / (float)(p.NC - 1) - 1.0f;
+      sh.sval[b] = b < p.B ? v : 0.f;
+    }
+  }
+  __syncthreads();
+  if (p.mol) {
+    if (tid < p.B) {
+      // utils/distribution.py:105-127 for one step, fp32, each op rounded like torch's
+      const int nr = p.NC / 3;
+      const float *l = &sh.vec[tid * 512];
+      int am = 0;
+      float bt = -INFINITY;
+      for (int k = 0; k < nr; ++k) {
+        const u32x4 w = philox((u32x4){(unsigned)t, (unsigned)(p.fold0 + tid), (unsigned)(k >> 2), 1u},
+                               p.k0, p.k1);
+        const float u = 1e-5f + u01(pword(w, k & 3)) * (1.0f - 2e-5f);
+        const float tv = l[k] - logf(-logf(u));
+        if (tv > bt) bt = tv, am = k;
+      }
+      const u32x4 w2 = philox((u32x4){(unsigned)t, (unsigned)(p.fold0 + tid), 0u, 2u}, p.k0, p.k1);
+      const float u = 1e-5f + u01(w2.x) * (1.0f - 2e-5f);
+      const float mean = l[nr + am];
+      const float ls = fmaxf(l[2 * nr + am], -32.23619130191664f);  // log(1e-14), fp32
+      const float d = logf(u) - logf(1.0f - u);
+      float x = mean + expf(ls) * d;
+      x = fminf(fmaxf(x, -1.0f), 1.0f);
+      sh.sval[tid] = x;
+    }
+    __syncthreads();
+  }
+  if (store && tid < p.B && p.samples) p.samples[(size_t)(p.fold0 + tid) * p.L + t] = sh.sval[tid];
+}
+
+template <int NBV>
+__device__ __forceinline__ void load_mel(const WrParams &p, WrShared<NBV> &sh, int t) {
+  for (int f = threadIdx.x; f < NBV * (WR_NM / 4); f += WR_NT) {
+    const int b = f / (WR_NM / 4), c = (f % (WR_NM / 4)) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (b < p.B) {
+      const Pos ps = position(p, b, t);
+      if (ps.mel_row >= 0) v = *(const f32x4 *)&p.mel[(size_t)ps.mel_row * WR_NM + c];
+    }
+    *(f32x4 *)&sh.melv[b * WR_NM + c] = v;
+  }
+}
+
+// the slot's product over its k-part: 8 lanes x NJ float4 chunks, interleaved; one fold
+// at a time (a rolled loop over the B live folds keeps the register footprint at the
+// weights plus one chunk set)
+template <int NJ>
+__device__ __forceinline__ void matvec(const float (&w)[NJ * 4], const float *vec, int kbase,
+                                       int kl, float *out, bool active, int B) {
+#pragma unroll 2
+  for (int b = 0; b < B; ++b) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const f32x4 h = *(const f32x4 *)&vec[b * 512 + kbase + j * 32 + kl * 4];
+      acc = fmaf(w[4 * j], h.x, acc);
+      acc = fmaf(w[4 * j + 1], h.y, acc);
+      acc = fmaf(w[4 * j + 2], h.z, acc);
+      acc = fmaf(w[4 * j + 3], h.w, acc);
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    if (active && kl == 0) out[b] = acc;
+  }
+}
+
+// mel conditioning: 80 = 8 lanes x 10, lane kl takes k = kl + 8 j
+__device__ __forceinline__ void matvec_mel(const float (&w)[10], const float *melv, int kl, float *out,
+                                           bool active, int B) {
+#pragma unroll 2
+  for (int b = 0; b < B; ++b) {
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) a = fmaf(w[j], melv[b * WR_NM + kl + 8 * j], a);
+    a += __shfl_xor(a, 1);
+    a += __shfl_xor(a, 2);
+    a += __shfl_xor(a, 4);
+    if (active && kl == 0) out[b] = a;
+  }
+}
+
+template <int NBV, int NCR>
+__global__ __launch_bounds__(WR_NT, 1) void wavernn_kernel(const WrParams p) {
+  __shared__ WrShared<NBV> sh;
+  const int tid = threadIdx.x;
+  const int s = tid >> 3, kl = tid & 7;
+
+  // ---- arrival barrier: all WR_GRID workgroups must be resident (bounded) -----------
+  if (tid == 0) {
+    sh.abort_flag = 0;
+    __hip_atomic_fetch_add(p.ws + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(p.ws + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)WR_GRID) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > p.spin_limit) {
+        sh.abort_flag = 1;
+        report_timeout(p);
+        break;
+      }
+    }
+  }
+  for (int i = tid; i < NBV * 512; i += WR_NT) sh.vec[i] = 0.f;
+  for (int i = tid; i < NBV; i += WR_NT) sh.sval[i] = 0.f;
+  __syncthreads();
+  if (sh.abort_flag) return;
+
+  const bool gru = blockIdx.x < WR_NG;
+  if (gru) {
+    // ================================ GRU workgroup =====================================
+    const int u0 = blockIdx.x * WR_UG;
+    const bool act = s < 24;  // 12 rows x 2 k-parts
+    const int r = s >> 1, kp = s & 1;
+    const int mrow = (r >> 2) * WR_R + u0 + (r & 3);
+    float w1[32], w2[32], w3[32], wmr[10];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = kp * 256 + j * 32 + kl * 4 + e;
+        w1[4 * j + e] = act ? p.w_hh1[(size_t)mrow * WR_R + k] : 0.f;
+        w2[4 * j + e] = act ? p.w_hh2[(size_t)mrow * WR_R + k] : 0.f;
+        w3[4 * j + e] = act ? p.w_ih2a[(size_t)mrow * WR_R + k] : 0.f;
+      }
+    {  // mel rows: slot s < 24 = (block s / 12: G1 | Q, gate row s % 12)
+      const int rr = s % 12;
+      const int row = (s / 12) * 3 * WR_R + (rr >> 2) * WR_R + u0 + (rr & 3);
+#pragma unroll
+      for (int j = 0; j < 10; ++j) wmr[j] = act ? p.wm[(size_t)row * WR_NM + kl + 8 * j] : 0.f;
+    }
+    // cell thread (unit cu, fold cb)
+    const bool cell = tid < WR_UG * p.B;
+    const int cu = tid & 3, cb = tid >> 2;
+    const int unit = u0 + cu;
+    float bh1[3], bh2[3], uu1[3], uu2[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      bh1[q] = p.b_hh1[q * WR_R + unit];
+      bh2[q] = p.b_hh2[q * WR_R + unit];
+      uu1[q] = p.u1[q * WR_R + unit];
+      uu2[q] = p.u2[q * WR_R + unit];
+    }
+    float h1 = 0.f, h2 = 0.f;
+
+    for (int t = 0; t < p.L; ++t) {
+      // ---- idle phase: everything not on the sample chain --------------------------
+      float gc[3] = {0.f, 0.f, 0.f}, qc[3] = {0.f, 0.f, 0.f};
+      if (cell) {
+        const Pos ps = position(p, cb, t);
+        const float *crow = p.cond + (size_t)ps.cond_row * WR_COND;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          gc[q] = crow[q * WR_R + unit];
+          qc[q] = crow[3 * WR_R + q * WR_R + unit];
+        }
+      }
+      load_mel(p, sh, t);
+      matvec<8>(w1, sh.vec, kp * 256, kl, sh.part[0][s], act, p.B);  // W_hh1 h1_{t-1}
+      __syncthreads();
+      if (t > 0) acquire_vec(p, sh, 1, t - 1, false);  // h2_{t-1}
+      __syncthreads();
+      if (sh.abort_flag) return;
+      matvec<8>(w2, sh.vec, kp * 256, kl, sh.part[1][s], act, p.B);  // W_hh2 h2_{t-1}
+      matvec_mel(wmr, sh.melv, kl, sh.partm[s], act, p.B);
+      // ---- the chain: s_{t-1} -------------------------------------------------------
+      __syncthreads();
+      if (t > 0) acquire_sample(p, sh, t - 1, !p.xin && blockIdx.x == 0);  // teacher-forced: pace only
+      if (p.xin && tid < p.B) sh.sval[tid] = p.xin[(size_t)(p.fold0 + tid) * p.L + t];
+      __syncthreads();
+      if (sh.abort_flag) return;
+      float sv = 0.f;
+      if (cell) {
+        sv = sh.sval[cb];
+        float gi[3], gh[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int rw = q * 4 + cu;
+          gh[q] = sh.part[0][2 * rw][cb] + sh.part[0][2 * rw + 1][cb];
+          gi[q] = (gc[q] + sh.partm[rw][cb]) + uu1[q] * sv;
+        }
+        const float rg = sigm(gi[0] + (gh[0] + bh1[0]));
+        const float zg = sigm(gi[1] + (gh[1] + bh1[1]));
+        const float ng = tanhf(gi[2] + rg * (gh[2] + bh1[2]));
+        h1 = tagged(ng + zg * (h1 - ng), t);
+        publish(p, 0, t, cb, unit, h1);
+      }
+      acquire_vec(p, sh, 0, t, false);  // h1_t
+      __syncthreads();
+      if (sh.abort_flag) return;
+      matvec<8>(w3, sh.vec, kp * 256, kl, sh.part[2][s], act, p.B);  // W_ih2a h1_t
+      __syncthreads();
+      if (cell) {
+        float gi[3], gh[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int rw = q * 4 + cu;
+          gh[q] = sh.part[1][2 * rw][cb] + sh.part[1][2 * rw + 1][cb];
+          const float gx = sh.part[2][2 * rw][cb] + sh.part[2][2 * rw + 1][cb];
+          gi[q] = ((qc[q] + sh.partm[12 + rw][cb]) + uu2[q] * sv) + gx;
+        }
+        const float rg = sigm(gi[0] + (gh[0] + bh2[0]));
+        const float zg = sigm(gi[1] + (gh[1] + bh2[1]));
+        const float ng = tanhf(gi[2] + rg * (gh[2] + bh2[2]));
+        h2 = tagged(ng + zg * (h2 - ng), t);
+        publish(p, 1, t, cb, unit, h2);
+      }
+      // sh.vec keeps h1_t: the next step's W_hh1 product reads it
+    }
+    if (!p.xin && blockIdx.x == 0) {  // the last sample
+      __syncthreads();
+      acquire_sample(p, sh, p.L - 1, true);
+    }
+  } else {
+    // ================================= FC workgroup =====================================
+    const int f = blockIdx.x - WR_NG;
+    const int r0 = f * WR_FR;
+    const int r = s >> 3, kp = s & 7;  // 4 rows x 8 k-parts
+    float wf1[8], wf2[8], wf3[8], wmr[10];
+    const int k3 = f * NCR + r;  // fc3 row of this slot
+    const bool act3 = r < NCR && k3 < p.NC;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = kp * 64 + j * 32 + kl * 4 + e;
+        wf1[4 * j + e] = p.w_fc1a[(size_t)(r0 + r) * WR_R + k];
+        wf2[4 * j + e] = p.w_fc2a[(size_t)(r0 + r) * WR_F + k];
+        wf3[4 * j + e] = act3 ? p.w_fc3[(size_t)k3 * WR_F + k] : 0.f;
+      }
+    const bool actm = s < WR_FR;
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      wmr[j] = actm ? p.wm[(size_t)(6 * WR_R + r0 + s) * WR_NM + kl + 8 * j] : 0.f;
+    // cell thread (row cr, fold cb)
+    const bool cell = tid < WR_FR * p.B;
+    const int cr = tid & 3, cb = tid >> 2;
+    const float vv1 = p.v1[r0 + cr];
+
+    for (int t = 0; t < p.L; ++t) {
+      float rc = 0.f, sc = 0.f;
+      if (cell) {
+        const Pos ps = position(p, cb, t);
+        const float *crow = p.cond + (size_t)ps.cond_row * WR_COND;
+        rc = crow[6 * WR_R + r0 + cr];
+        sc = crow[6 * WR_R + WR_F + r0 + cr];
+      }
+      load_mel(p, sh, t);
+      __syncthreads();
+      matvec_mel(wmr, sh.melv, kl, sh.partm[s], actm, p.B);
+      // ---- s_{t-1} -------------------------------------------------------------------
+      if (t > 0) acquire_sample(p, sh, t - 1, false);
+      if (p.xin && tid < p.B) sh.sval[tid] = p.xin[(size_t)(p.fold0 + tid) * p.L + t];
+      // ---- h1_t + h2_t ----------------------------------------------------------------
+      acquire_vec(p, sh, 0, t, false);
+      __syncthreads();
+      if (sh.abort_flag) return;
+      acquire_vec(p, sh, 1, t, true);
+      __syncthreads();
+      if (sh.abort_flag) return;
+      matvec<2>(wf1, sh.vec, kp * 64, kl, sh.part[0][s], true, p.B);
+      __syncthreads();
+      if (cell) {
+        float acc = sh.part[0][cr * 8][cb];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) acc += sh.part[0][cr * 8 + i][cb];
+        const float pre = ((rc + sh.partm[cr][cb]) + vv1 * sh.sval[cb]) + acc;
+        publish(p, 2, t, cb, r0 + cr, tagged(fmaxf(pre, 0.f), t));
+      }
+      acquire_vec(p, sh, 2, t, false);  // y1
+      __syncthreads();
+      if (sh.abort_flag) return;
+      matvec<2>(wf2, sh.vec, kp * 64, kl, sh.part[1][s], true, p.B);
+      __syncthreads();
+      if (cell) {
+        float acc = sh.part[1][cr * 8][cb];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) acc += sh.part[1][cr * 8 + i][cb];
+        publish(p, 3, t, cb, r0 + cr, tagged(fmaxf(sc + acc, 0.f), t));
+      }
+      acquire_vec(p, sh, 3, t, false);  // y2
+      __syncthreads();
+      if (sh.abort_flag) return;
+      matvec<2>(wf3, sh.vec, kp * 64, kl, sh.part[2][s], act3, p.B);
+      __syncthreads();
+      // ---- fc3 rows of this workgroup: logits, then the draw's partial ------------------
+      if (tid < p.B && f * NCR < p.NC) {
+        const int b = tid;
+        float best = -INFINITY;
+        int bidx = 0;
+        for (int rr = 0; rr < NCR; ++rr) {
+          const int k = f * NCR + rr;
+          if (k >= p.NC) break;
+          float l = sh.part[2][rr * 8][b];
+#pragma unroll
+          for (int i = 1; i < 8; ++i) l += sh.part[2][rr * 8 + i][b];
+          l = l + p.b_fc3[k];
+          if (p.logits) p.logits[((size_t)(p.fold0 + b) * p.L + t) * p.NC + k] = l;
+          if (p.mol) {
+            best = l;
+            bidx = k;
+          } else {
+            const u32x4 w = philox((u32x4){(unsigned)t, (unsigned)(p.fold0 + b), (unsigned)(k >> 2), 0u},
+                                   p.k0, p.k1);
+            const float u = u01(pword(w, k & 3));
+            const float z = l - logf(-logf(u));
+            if (z > best) best = z, bidx = k;
+          }
+        }
+        publish_z(p, t, b, f, best, bidx);
+      }
+    }
+  }
+}
+
+__global__ void wr_stretch_conv_kernel(const float *x, int64_t xs_b, int W, int C, int s,
+                                       const float *w, float *y, int64_t ys_b, int Wout, int crop0,
+                                       int B) {
+  const int64_t n = (int64_t)B * Wout * C;
+  const int taps = 2 * s + 1;
+  const int64_t Ws = (int64_t)W * s;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const int64_t jb = i / C;
+    const int j = (int)(jb % Wout), b = (int)(jb / Wout);
+    const float *xb = x + b * xs_b;
+    float acc = 0.f;
+    for (int k = 0; k < taps; ++k) {
+      const int64_t q = (int64_t)j + crop0 + k - s;
+      const float v = (q >= 0 && q < Ws) ? xb[(q / s) * C + c] : 0.f;
+      acc = fmaf(w[k], v, acc);
+    }
+    y[b * ys_b + (int64_t)j * C + c] = acc;
+  }
+}
+
+// numpy.linspace(start, stop, num)[i] (float64: i * step + start, last = stop)
+__device__ __forceinline__ double np_linspace(double start, double stop, int num, int i) {
+  if (num > 1 && i == num - 1) return stop;
+  if (num <= 1) return start;
+  const double step = (stop - start) / (double)(num - 1);
+  return (double)i * step + start;
+}
+
+__device__ __forceinline__ double mu_decode(double y, int mu_law, int n_classes) {
+  if (!mu_law) return y;
+  // DSP.decode_mu_law(y, n_classes, from_labels=False): sign(y)/mu * ((1+mu)^|y| - 1),
+  // mu = n_classes - 1; (1+mu) = 2^bits: (1+mu)^|y| = 2^(bits |y|), bits |y| exact
+  const double mu = (double)(n_classes - 1);
+  const double sg = y > 0.0 ? 1.0 : (y < 0.0 ? -1.0 : 0.0);
+  const double bits = log2((double)n_classes);
+  return sg / mu * (exp2(bits * fabs(y)) - 1.0);
+}
+
+__global__ void wr_unfold_kernel(const float *smp, int B, int L, int target, int overlap,
+                                 int batched, int mu_law, int n_classes, int wave_len, int nf,
+                                 double *out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= wave_len) return;
+  double v;
+  if (batched) {
+    const int stride = target + overlap;
+    const int silence = overlap / 2, fade_len = overlap - silence;
+    auto term = [&](int i) -> double {
+      const int pos = j - i * stride;
+      double y = mu_decode((double)smp[(size_t)i * L + pos], mu_law, n_classes);
+      if (pos < overlap) {  // fade_in = [zeros(silence), sqrt(0.5 (1 + t))]
+        const double g = pos < silence ? 0.0
+                                       : sqrt(0.5 * (1.0 + np_linspace(-1.0, 1.0, fade_len, pos - silence)));
+        y = y * g;
+      }
+      if (pos >= L - overlap) {  // fade_out = [ones(silence), sqrt(0.5 (1 - t))]
+        const int q = pos - (L - overlap);
+        const double g = q < silence ? 1.0 : sqrt(0.5 * (1.0 - np_linspace(-1.0, 1.0, fade_len, q - silence)));
+        y = y * g;
+      }
+      return y;
+    };
+    const int ihi = j / stride;
+    v = 0.0;
+    if (ihi >= 1 && ihi - 1 < B && j - (ihi - 1) * stride < L) v = v + term(ihi - 1);
+    if (ihi < B) v = v + term(ihi);
+  } else {
+    v = mu_decode((double)smp[j], mu_law, n_classes);
+  }
+  if (nf > 0 && j >= wave_len - nf) v = v * np_linspace(1.0, 0.0, nf, j - (wave_len - nf));
+  out[j] = v;
+}
+
+unsigned g_wr_spin = SPIN_DEFAULT;
+
+int cu_count() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return cus;
+}
+
+}  // namespace
+
+extern "C" int64_t ftmi_wavernn_workspace_bytes(void) {
+  return (int64_t)(WS_CTRL + 4 * XS_VEC + XS_Z) * 4;
+}
+
+extern "C" uint32_t ftmi_set_wavernn_spin_limit(uint32_t limit) {
+  const uint32_t old = g_wr_spin;
+  g_wr_spin = limit ? limit : SPIN_DEFAULT;
+  return old;
+}
+
+extern "C" int ftmi_wavernn(const ftmi_wavernn_args *a, ftmi_stream_t stream) {
+  if (!a) return FTMI_E_ARG;
+  if (!a->w_hh1 || !a->w_hh2 || !a->w_ih2a || !a->w_fc1a || !a->w_fc2a || !a->w_fc3 ||
+      !a->b_fc3 || !a->b_hh1 || !a->b_hh2 || !a->u1 || !a->u2 || !a->v1 || !a->wm || !a->cond ||
+      !a->mel || !a->workspace)
+    return FTMI_E_ARG;
+  if (a->B <= 0 || a->L <= 0 || a->hop <= 0 || a->item_rows <= 0 || a->frames_per_item <= 0)
+    return FTMI_E_ARG;
+  if (a->rnn_dims != WR_R || a->fc_dims != WR_F || a->feat_dims != WR_NM || a->aux_dims != WR_NA)
+    return FTMI_E_UNSUPPORTED;
+  // RAW: 2^bits classes spread over all 128 FC workgroups (1..4 rows each): bits 7..9
+  if (a->mol ? a->n_classes != 30
+             : (a->n_classes < WR_NF || a->n_classes > 4 * WR_NF || (a->n_classes & (a->n_classes - 1)) != 0))
+    return FTMI_E_UNSUPPORTED;
+  if (a->xin ? !a->logits : !a->samples) return FTMI_E_ARG;
+  if (a->batched && a->fold_stride <= 0) return FTMI_E_ARG;
+  if (!ftmi_aligned16(a->mel) || !ftmi_aligned16(a->workspace)) return FTMI_E_ALIGN;
+  if (cu_count() < WR_GRID) return FTMI_E_UNSUPPORTED;
+  hipStream_t s = ftmi_hs(stream);
+  WrParams p{};
+  p.w_hh1 = a->w_hh1, p.w_hh2 = a->w_hh2, p.w_ih2a = a->w_ih2a;
+  p.w_fc1a = a->w_fc1a, p.w_fc2a = a->w_fc2a, p.w_fc3 = a->w_fc3, p.b_fc3 = a->b_fc3;
+  p.b_hh1 = a->b_hh1, p.b_hh2 = a->b_hh2, p.u1 = a->u1, p.u2 = a->u2, p.v1 = a->v1;
+  p.wm = a->wm, p.cond = a->cond, p.mel = a->mel;
+  p.bias_row = a->bias_row, p.item_rows = a->item_rows, p.frames_per_item = a->frames_per_item;
+  p.hop = a->hop, p.fold_stride = a->fold_stride, p.batched = a->batched;
+  p.xin = a->xin, p.samples = a->samples, p.logits = a->logits;
+  unsigned *ws = (unsigned *)a->workspace;
+  p.ws = ws;
+  p.xch = (float *)(ws + WS_CTRL);
+  p.status = a->status;
+  p.L = a->L, p.NC = a->n_classes, p.mol = a->mol;
+  p.k0 = (unsigned)(a->seed & 0xFFFFFFFFull), p.k1 = (unsigned)(a->seed >> 32);
+  p.spin_limit = g_wr_spin;
+  const int ncr = a->mol ? 1 : (a->n_classes + WR_NF - 1) / WR_NF;
+  for (int f0 = 0; f0 < a->B; f0 += WR_NBMAX) {
+    p.fold0 = f0;
+    p.B = a->B - f0 < WR_NBMAX ? a->B - f0 : WR_NBMAX;
+    hipError_t e = hipMemsetAsync(a->workspace, 0, (size_t)ftmi_wavernn_workspace_bytes(), s);
+    if (e != hipSuccess) return (int)e;
+#define FTMI_WR_LAUNCH(NBV_, NCR_) \
+  hipLaunchKernelGGL((wavernn_kernel<NBV_, NCR_>), dim3(WR_GRID), dim3(WR_NT), 0, s, p)
+#define FTMI_WR_NCR(NBV_)                          \
+  switch (ncr) {                                   \
+    case 1: FTMI_WR_LAUNCH(NBV_, 1); break;        \
+    case 2: FTMI_WR_LAUNCH(NBV_, 2); break;        \
+    default: FTMI_WR_LAUNCH(NBV_, 4); break;       \
+  }
+    if (p.B <= 8) {
+      FTMI_WR_NCR(8)
+    } else if (p.B <= 16) {
+      FTMI_WR_NCR(16)
+    } else {
+      FTMI_WR_NCR(32)
+    }
+#undef FTMI_WR_NCR
+#undef FTMI_WR_LAUNCH
+    FTMI_CHECK_LAUNCH();
+  }
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_wr_stretch_conv(const float *x, int64_t x_batch_stride, int32_t B, int32_t W,
+                                    int32_t C, int32_t scale, const float *w, float *y,
+                                    int64_t y_batch_stride, int32_t W_out, int32_t crop0,
+                                    ftmi_stream_t stream) {
+  if (!x || !w || !y) return FTMI_E_ARG;
+  if (B <= 0 || W <= 0 || C <= 0 || scale <= 0 || W_out <= 0 || crop0 < 0) return FTMI_E_ARG;
+  if ((int64_t)crop0 + W_out > (int64_t)W * scale) return FTMI_E_SHAPE;
+  const int64_t n = (int64_t)B * W_out * C;
+  const int blocks = (int)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536);
+  hipLaunchKernelGGL(wr_stretch_conv_kernel, dim3(blocks), dim3(256), 0, ftmi_hs(stream), x,
+                     x_batch_stride, W, C, scale, w, y, y_batch_stride, W_out, crop0, B);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_wr_unfold(const float *samples, int32_t B, int32_t L, int32_t target,
+                              int32_t overlap, int32_t batched, int32_t mu_law, int32_t n_classes,
+                              int32_t wave_len, int32_t fade_len, double *out,
+                              ftmi_stream_t stream) {
+  if (!samples || !out) return FTMI_E_ARG;
+  if (B <= 0 || L <= 0 || wave_len <= 0 || fade_len < 0 || n_classes < 2) return FTMI_E_ARG;
+  if (mu_law && (n_classes & (n_classes - 1)) != 0) return FTMI_E_UNSUPPORTED;
+  if (batched && (target < 0 || overlap < 0 || L != target + 2 * overlap)) return FTMI_E_SHAPE;
+  if (wave_len < fade_len) return FTMI_E_SHAPE;  // the reference's fade-out needs 20 hops
+  if (batched ? (int64_t)wave_len > (int64_t)B * (target + overlap) + overlap : wave_len > L)
+    return FTMI_E_SHAPE;
+  hipLaunchKernelGGL(wr_unfold_kernel, dim3((wave_len + 255) / 256), dim3(256), 0, ftmi_hs(stream),
+                     samples, B, L, target, overlap, batched, mu_law, n_classes, wave_len, fade_len, out);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}

@@ -702,3 +702,52 @@ def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Te
            out.data_ptr(), out.stride(1), m, status_word(qkv.device).data_ptr(), _ptr(ws), nws,
            _stream())
     return out
+
+
+# ---- WaveRNN vocoder (csrc/wavernn.hip) --------------------------------------------------
+
+def wr_stretch_conv(x: torch.Tensor, scale: int, w: torch.Tensor, W_out: Optional[int] = None,
+                    crop0: int = 0) -> torch.Tensor:
+    """Stretch2d(scale, 1) + Conv2d(1, 1, (1, 2 scale + 1), pad (0, scale)) along time on
+    (B, W, C) rows -> (B, W_out, C) (default W * scale; crop0 = first output sample)."""
+    _dev(x, w)
+    x = x.contiguous()
+    w = w.reshape(-1).float().contiguous()
+    B, W, C = x.shape
+    if w.numel() != 2 * scale + 1:
+        raise ValueError(f'smoothing kernel of {w.numel()} taps for scale {scale}')
+    W_out = W * scale if W_out is None else W_out
+    y = torch.empty(B, W_out, C, device=x.device, dtype=_f32)
+    launch('ftmi_wr_stretch_conv', f'wr_stretch_conv[B={B},W={W},C={C},s={scale}]',
+           2.0 * B * W_out * C * (2 * scale + 1), 4.0 * (B * W * C + B * W_out * C),
+           x.data_ptr(), W * C, B, W, C, scale, w.data_ptr(), y.data_ptr(), W_out * C, W_out, crop0,
+           _stream())
+    return y
+
+
+def wavernn(args, B: int, L: int, flops: float, device) -> None:
+    """Enqueue ftmi_wavernn (args: a filled _lib.WaveRNNArgs; the caller keeps every buffer
+    alive).  The status word pointer is set here."""
+    args.status = status_word(device).data_ptr()
+    mode = 'forward' if args.xin else 'generate'
+    launch('ftmi_wavernn', f'wavernn[{mode},B={B},L={L},NC={args.n_classes}]', flops,
+           4.0 * B * L * (1 + (args.n_classes if args.logits else 0)), ctypes.byref(args), _stream())
+
+
+def wavernn_workspace(device) -> torch.Tensor:
+    n = int(_lib.load().ftmi_wavernn_workspace_bytes())
+    return torch.empty(n // 4, device=device, dtype=torch.int32)
+
+
+def wr_unfold(samples: torch.Tensor, target: int, overlap: int, batched: bool, mu_law: bool,
+              n_classes: int, wave_len: int, fade_len: int) -> torch.Tensor:
+    """generate's tail in float64 on the device: (B, L) samples -> (wave_len,) wave
+    (fade_len: the final linear fade-out, 20 hop in generate, 0 for none)."""
+    _dev(samples)
+    samples = samples.contiguous()
+    B, L = samples.shape
+    out = torch.empty(wave_len, device=samples.device, dtype=torch.float64)
+    launch('ftmi_wr_unfold', f'wr_unfold[B={B},L={L}]', 0, 4.0 * B * L + 8.0 * wave_len,
+           samples.data_ptr(), B, L, target, overlap, int(batched), int(mu_law), n_classes,
+           wave_len, fade_len, out.data_ptr(), _stream())
+    return out

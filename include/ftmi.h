@@ -64,7 +64,7 @@ enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
        FTMI_BANK_Y_SPLIT = 2, /* with FTMI_BANK_POOL: y as f16x3 split rows of K*Cout */
        FTMI_BANK_X_SPLIT = 4  /* x given as f16x3 split rows of Cin (FTMI_MMA_F16X3) */ };
 
-/* ABI version; bumped on any signature change. */
+/* ABI version; bumped on any signature change (11: the WaveRNN vocoder entry points). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
@@ -455,6 +455,72 @@ int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, int32_t T, i
                    const uint8_t *key_padding_mask, float qscale, float *out,
                    int64_t out_stride, int32_t mma, uint32_t *status, void *workspace,
                    int64_t workspace_bytes, ftmi_stream_t stream);
+
+
+/* ---- WaveRNN vocoder (models/fatchord_version.py; gen_forward.py `wavernn`) -------------
+ * Fixed architecture of the reference config (config.yaml:189-198): rnn_dims = fc_dims = 512,
+ * feat_dims = 80, aux_dims = res_out_dims / 4 = 32; RAW with n_classes = 2^bits <= 512, or
+ * MOL (n_classes = 30).  Anything else returns FTMI_E_UNSUPPORTED. */
+
+/* One UpsampleNetwork.up_layers pair (:74-81, :88): Stretch2d(scale, 1) then
+ * Conv2d(1, 1, (1, 2 scale + 1), padding (0, scale), no bias) along time, on time-major rows:
+ *   y[b, j, c] = sum_i w[i] xs[j + crop0 + i - scale, c],  xs[q] = x[b, q / scale, c]
+ * (zero outside [0, W scale)).  x (B, W, C) rows, y (B, W_out, C); crop0 + W_out <= W scale
+ * (the final layer writes only the [indent, -indent) crop of :89). */
+int ftmi_wr_stretch_conv(const float *x, int64_t x_batch_stride, int32_t B, int32_t W, int32_t C,
+                         int32_t scale, const float *w, float *y, int64_t y_batch_stride,
+                         int32_t W_out, int32_t crop0, ftmi_stream_t stream);
+
+/* Arguments of ftmi_wavernn.  Weights are fp32, packed once per weights version (float64
+ * products, forwardtacotron_amd/wavernn.py `_pack`):
+ *   w_hh1, w_hh2 [3R][R]          rnn1/rnn2.weight_hh_l0 (gate rows r, z, n)
+ *   w_ih2a [3R][R]                rnn2.weight_ih_l0[:, :R] (the x + h1 part)
+ *   w_fc1a [F][R], w_fc2a [F][F]  fc1.weight[:, :R], fc2.weight[:, :F]
+ *   w_fc3 [NC][F], b_fc3 [NC]     fc3
+ *   b_hh1, b_hh2 [3R]             rnn1/rnn2.bias_hh_l0
+ *   u1 = W_ih1 w0, u2 = W_ih2a w0 [3R], v1 = W_fc1a w0 [F]   (w0 = I.weight[:, 0]: the
+ *                                 sample's column, carried through the linear layers)
+ *   wm [3R + 3R + F][80]          mel columns of G1 = W_ih1 I, Q = W_ih2a I, R = W_fc1a I
+ *   cond (bias_row + 1) rows of [3R | 3R | F | F] floats: per mel FRAME the aux terms of
+ *                                 G1, Q (+ W_ih2b a2), R (+ W_fc1b a3), S = W_fc2b a4, with
+ *                                 every bias folded in; row bias_row = biases only (padding)
+ *   mel (items * item_rows, 80)   upsampled mel rows (UpsampleNetwork output)
+ * Position of fold b, step t: batched: sample g = b fold_stride + t of item 0 (fold_stride
+ * = target + overlap, fold_with_overlap :294-341); else g = t of item b.  g >= item_rows
+ * is the fold padding (zero conditioning).  cond row = item frames_per_item + g / hop.
+ * Mode: xin == NULL: generate — samples (B, L) receives each fold's drawn samples (:237 /
+ * distribution.py:127 values); xin (B, L): teacher-forced forward — logits (B, L, NC).
+ * seed: Philox4x32-10 key of the draws (oracle/wr_torch_cpu.py PhiloxSampler).
+ * workspace: >= ftmi_wavernn_workspace_bytes() bytes, 16-B aligned (zeroed by the call). */
+typedef struct {
+  const float *w_hh1, *w_hh2, *w_ih2a, *w_fc1a, *w_fc2a, *w_fc3, *b_fc3, *b_hh1, *b_hh2;
+  const float *u1, *u2, *v1, *wm, *cond, *mel;
+  const float *xin;
+  float *samples, *logits;
+  void *workspace;
+  uint32_t *status;
+  uint64_t seed;
+  int32_t bias_row, item_rows, frames_per_item, hop, fold_stride, batched;
+  int32_t B, L, n_classes, mol;
+  int32_t rnn_dims, fc_dims, feat_dims, aux_dims;
+} ftmi_wavernn_args;
+
+/* The sample loop of WaveRNN.generate (:203-241) — teacher-forced: WaveRNN.forward
+ * (:145-169) — for B folds as persistent launches of 256 workgroups (one per CU; fewer CUs:
+ * FTMI_E_UNSUPPORTED), <= 32 folds per launch.  A workgroup that cannot meet the others
+ * (not co-resident) sets FTMI_STATUS_RNN_TIMEOUT in *status: the output is then invalid. */
+int64_t ftmi_wavernn_workspace_bytes(void);
+int ftmi_wavernn(const ftmi_wavernn_args *args, ftmi_stream_t stream);
+uint32_t ftmi_set_wavernn_spin_limit(uint32_t limit);
+
+/* generate's tail (:246-261) in float64: samples (B, L) -> mu-law decode
+ * (DSP.decode_mu_law(y, n_classes, False), utils/dsp.py:156-161; n_classes a power of two)
+ * -> batched: xfade_and_unfold (:343-406), else fold 0 -> [:wave_len] -> the last fade_len
+ * samples times linspace(1, 0, fade_len) (generate: fade_len = 20 hop; 0: none).
+ * wave_len >= fade_len (the reference raises otherwise). */
+int ftmi_wr_unfold(const float *samples, int32_t B, int32_t L, int32_t target, int32_t overlap,
+                   int32_t batched, int32_t mu_law, int32_t n_classes, int32_t wave_len,
+                   int32_t fade_len, double *out, ftmi_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,36 @@
+"""Time the WaveRNN sample loop on the GPU (gen_forward.py's batched defaults: target 11000,
+overlap 550) for a mel of T frames; prints ms per call, us per step and samples/s."""
+import argparse
+import time
+
+import numpy as np
+import torch
+
+from forwardtacotron_amd.synthetic import default_config, load_synthetic
+from forwardtacotron_amd.wavernn import WaveRNN
+
+ap = argparse.ArgumentParser()
+ap.add_argument('--frames', type=int, default=821)
+ap.add_argument('--reps', type=int, default=3)
+ap.add_argument('--mode', default='RAW')
+a = ap.parse_args()
+cfg = default_config()
+cfg['vocoder']['model']['mode'] = a.mode
+m = load_synthetic(WaveRNN.from_config(cfg), kind='wavernn').cuda().eval()
+rng = np.random.Generator(np.random.PCG64(0))
+mels = torch.from_numpy((rng.normal(0, 1, (1, 80, a.frames)) - 4).astype(np.float32)).cuda()
+smp = m.generate_samples(mels, True, 11000, 550, seed=1)
+torch.cuda.synchronize()
+B, L = smp.shape
+ts = []
+for r in range(a.reps):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m.generate_samples(mels, True, 11000, 550, seed=r)
+    torch.cuda.synchronize()
+    ts.append(time.perf_counter() - t0)
+t = min(ts)
+wav = m.generate(mels, True, 11000, 550, True, seed=3)
+print(f'folds {B} steps {L}: {t * 1e3:.1f} ms/call, {t / L * 1e6:.2f} us/step, '
+      f'{(a.frames - 1) * 256 / t / 1e6:.2f} M samples/s (wave {wav.shape[0]} samples, '
+      f'mean |x| {np.abs(wav).mean():.4f})', flush=True)
