@@ -25,17 +25,22 @@
 // W_ih2a h1_t, W_fc1a (h1 + h2), W_fc2a y1, W_fc3 y2 and the draw — five all-to-all edges.
 //
 // Decomposition: 256 workgroups (one per CU, co-residency checked by an arrival barrier
-// with a bounded spin), two roles:
-//   GRU workgroups g < 128: units 4g..4g+3 of both GRUs (12 gate rows of W_hh1, W_hh2,
-//     W_ih2a in VGPRs), the cell updates, h1 / h2 publication.
-//   FC workgroups f = 128..255: rows 4f..4f+3 of fc1 and fc2, NCR rows of fc3, the Gumbel
-//     draw of those rows, publication of y1, y2 and the rows' best (value, index).
+// with a bounded spin).  With two or more folds they form TWO INSTANCES of 128 workgroups,
+// each the whole pipeline for half of the folds: the per-step cost is the hand-off latency
+// of the five edges, which does not shrink with fewer folds, so two half-size pipelines
+// side by side run twice the folds per unit of time.  Per instance (NI instances,
+// 512 threads per workgroup at NI = 2), two roles:
+//   GRU workgroups: UG = 4 NI units of both GRUs (3 UG gate rows of W_hh1, W_hh2, W_ih2a
+//     in VGPRs), the cell updates, h1 / h2 publication.
+//   FC workgroups: FR = 4 NI rows of fc1 and fc2, NCR rows of fc3, the Gumbel draw of
+//     those rows, publication of y1, y2 and the rows' best (value, index).
 // Matrix-vector products are exact fp32 FMAs on the VALU: a 16-wide MFMA tile would carry
 // B <= 32 live columns at most and the chain is bound by the hand-offs, not the flops.
 // Thread layout of a product: slot s = tid / 8 owns (row, k-part), its 8 lanes hold
-// interleaved 4-float chunks of that row's k-part (a wave-wide LDS read of the vector is
-// 8 consecutive 128-B runs: broadcast across slots, conflict-free within one); the 8
-// lanes meet by xor shuffles, the k-parts in a fixed order through LDS.
+// interleaved 4-float chunks of that row's k-part, placed so that the slots of one wave
+// read one contiguous run of the vector per instruction (conflict-free; slots of other
+// rows read the same addresses: broadcast); the 8 lanes meet by DPP adds, the k-parts in
+// a fixed order through LDS.
 //
 // Hand-off: the data is the flag (rnn.hip): every exchanged value carries the step tag in
 // its mantissa LSB (the tagged value is the one used everywhere), two parity halves,
@@ -61,19 +66,17 @@ constexpr int WR_R = 512;    // rnn_dims
 constexpr int WR_F = 512;    // fc_dims
 constexpr int WR_NM = 80;    // mel features (feat_dims)
 constexpr int WR_NA = 32;    // aux_dims = res_out_dims / 4
-constexpr int WR_NT = 256;   // threads per workgroup
-constexpr int WR_NG = 128;   // GRU workgroups
-constexpr int WR_NF = 128;   // FC workgroups
-constexpr int WR_UG = WR_R / WR_NG;  // 4 units per GRU workgroup
-constexpr int WR_FR = WR_F / WR_NF;  // 4 fc1 / fc2 rows per FC workgroup
-constexpr int WR_GRID = WR_NG + WR_NF;
+constexpr int WR_NT = 256;   // threads per workgroup of a single-instance launch
+constexpr int WR_NF = 128;   // FC workgroups of a single-instance launch (draw-slot stride)
+constexpr int WR_GRID = 256; // workgroups per launch
 constexpr int WR_NBMAX = 32;         // folds per launch
 constexpr int WR_COND = 6 * WR_R + 2 * WR_F;  // cond row: [G1 3R | Q 3R | R F | S F]
 // exchange slots: h1, h2, y1, y2 ([2][NBV][512] floats each), then the draw partials
 // ([2][NBV][128] 8-byte granules)
 constexpr int XS_VEC = 2 * WR_NBMAX * 512;   // floats per vector slot
 constexpr int XS_Z = 2 * WR_NBMAX * WR_NF * 2;  // words of the draw slot
-constexpr int WS_CTRL = 64;                  // control words (error, arrival)
+constexpr int WS_CTRL = 128;                 // control words (error, arrival, diag stamps)
+constexpr int WS_STAMPS = 64;                // 2 x 16 u64 phase sums (FTMI_WR_STAMPS=1)
 constexpr unsigned SPIN_DEFAULT = 1u << 22;
 constexpr unsigned STATUS_TIMEOUT = 4u;
 
@@ -107,6 +110,24 @@ __device__ __forceinline__ unsigned pword(const u32x4 &v, int i) {
   return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
 }
 
+// lane exchanges inside groups of 8 lanes by DPP (no LDS round trip like ds_bpermute):
+// quad_perm [1,0,3,2] (xor 1), quad_perm [2,3,0,1] (xor 2), row_half_mirror (i <-> 7 - i)
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+// sum over the 8 lanes of a group (every lane gets it)
+__device__ __forceinline__ float sum8(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  return v;
+}
+
 struct WrParams {
   const float *w_hh1, *w_hh2, *w_ih2a;  // [3R][R]
   const float *w_fc1a, *w_fc2a;         // [F][R], [F][F]
@@ -126,6 +147,7 @@ struct WrParams {
   unsigned *ws;                         // control words
   unsigned *status;
   int B, L, NC, mol;
+  int stamps;                           // diag: per-phase s_memtime sums of WG 0 / WG 128
   unsigned k0, k1;                      // Philox key
   unsigned spin_limit;
 };
@@ -155,13 +177,26 @@ __device__ __forceinline__ Pos position(const WrParams &p, int b, int t) {
   return r;
 }
 
-template <int NBV>
+// Geometry of one instance (a replica of the weight-distributed pipeline over its own
+// share of the folds): NI instances x (NG GRU + NF FC workgroups) = 256 workgroups of
+// NT = 256 NI threads; a GRU workgroup owns UG = 4 NI units, an FC workgroup FR = 4 NI rows.
+template <int NI>
+struct Geo {
+  static constexpr int NT = WR_NT * NI;
+  static constexpr int W = WR_GRID / NI;  // workgroups per instance
+  static constexpr int NG = W / 2, NF = W / 2;
+  static constexpr int UG = WR_R / NG, FR = WR_F / NF;
+  static constexpr int SLOTS = NT / 8;
+};
+
+template <int NBV, int NI>
 struct WrShared {
   float vec[NBV * 512];          // the acquired vector (h1 / h2 / h1+h2 / y1 / y2)
-  float part[3][32][NBV];        // per-slot partial sums of the products
-  float partm[32][NBV];          // per-slot partial sums of the mel conditioning
+  float part[3][Geo<NI>::SLOTS][NBV];  // per-slot partial sums of the products
+  float partm[Geo<NI>::SLOTS][NBV];    // per-slot partial sums of the mel conditioning
   float melv[NBV * WR_NM];       // this step's mel rows
   float sval[NBV];               // s_{t-1}
+  unsigned long long stamp[12];  // diag phase sums (thread 0)
   int abort_flag;
 };
 
@@ -169,10 +204,11 @@ struct WrShared {
 // Every chunk of the thread is requested at once, then only the stale ones are polled
 // again (a serial poll per chunk would pay the hand-off latency once per chunk).  On a
 // timeout the workgroup's abort flag is set; the caller barriers and checks it.
-template <int NBV>
-__device__ __forceinline__ void acquire_vec(const WrParams &p, WrShared<NBV> &sh, int slot, int t,
+template <int NBV, int NI>
+__device__ __forceinline__ void acquire_vec(const WrParams &p, WrShared<NBV, NI> &sh, int slot, int t,
                                             bool add) {
-  constexpr int PER = NBV * 128 / WR_NT;  // 16-B chunks per thread
+  constexpr int NT = Geo<NI>::NT;
+  constexpr int PER = NBV * 128 / NT;  // 16-B chunks per thread
   const int tid = threadIdx.x;
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.xch, (short)0, 0x7FFFFFF0, 0x00020000);
   const unsigned want = step_tag(t);
@@ -182,13 +218,13 @@ __device__ __forceinline__ void acquire_vec(const WrParams &p, WrShared<NBV> &sh
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     r[i] = (u32x4){0u, 0u, 0u, 0u};
-    if (((tid + i * WR_NT) >> 7) < p.B) stale |= 1u << i;
+    if (((tid + i * NT) >> 7) < p.B) stale |= 1u << i;
   }
   for (unsigned spins = 0; stale; ++spins) {
 #pragma unroll
     for (int i = 0; i < PER; ++i)
       if (stale & (1u << i))
-        r[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (unsigned)((tid + i * WR_NT) * 16), soff, 16);
+        r[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (unsigned)((tid + i * NT) * 16), soff, 16);
 #pragma unroll
     for (int i = 0; i < PER; ++i)
       if (stale & (1u << i)) {
@@ -206,7 +242,7 @@ __device__ __forceinline__ void acquire_vec(const WrParams &p, WrShared<NBV> &sh
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const f32x4 v = __builtin_bit_cast(f32x4, r[i]);
-    f32x4 *dst = (f32x4 *)&sh.vec[(tid + i * WR_NT) * 4];
+    f32x4 *dst = (f32x4 *)&sh.vec[(tid + i * NT) * 4];
     if (add) *dst = *dst + v;
     else *dst = v;
   }
@@ -232,15 +268,15 @@ __device__ __forceinline__ void publish_z(const WrParams &p, int t, int b, int f
 // best Gumbel score and its class), MOL the NC logits.  8 threads per fold, each with its
 // (up to 8) 16-byte granule pairs requested at once.  On a timeout the abort flag is set
 // (visible after the internal barrier).
-template <int NBV>
-__device__ void acquire_sample(const WrParams &p, WrShared<NBV> &sh, int t, bool store) {
+template <int NBV, int NI>
+__device__ __forceinline__ void acquire_sample(const WrParams &p, WrShared<NBV, NI> &sh, int t, bool store) {
   const int tid = threadIdx.x;
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.xch, (short)0, 0x7FFFFFF0, 0x00020000);
   const unsigned want = step_tag(t);
   const int soff = (4 * XS_VEC + (t & 1) * WR_NBMAX * WR_NF * 2) * 4;
-  const int np = p.mol ? p.NC : WR_NF;
+  const int np = p.mol ? p.NC : Geo<NI>::NF;
   const int b = tid >> 3, part = tid & 7;
-  constexpr int PER = WR_NF / 16;
+  constexpr int PER = Geo<NI>::NF / 16;
   u32x4 r[PER];
   unsigned stale = 0;
 #pragma unroll
@@ -289,10 +325,15 @@ __device__ void acquire_sample(const WrParams &p, WrShared<NBV> &sh, int t, bool
     }
   }
   if (!p.mol) {
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) {
-      const float ob = __shfl_xor(best, m);
-      const int oi = __shfl_xor(bidx, m);
+    {  // (max, first index) over the fold's 8 lanes
+      float ob = dppf<0xB1>(best);
+      int oi = dppi<0xB1>(bidx);
+      if (ob > best || (ob == best && oi < bidx)) best = ob, bidx = oi;
+      ob = dppf<0x4E>(best);
+      oi = dppi<0x4E>(bidx);
+      if (ob > best || (ob == best && oi < bidx)) best = ob, bidx = oi;
+      ob = dppf<0x141>(best);
+      oi = dppi<0x141>(bidx);
       if (ob > best || (ob == best && oi < bidx)) best = ob, bidx = oi;
     }
     if (part == 0 && b < NBV) {
@@ -330,63 +371,121 @@ __device__ void acquire_sample(const WrParams &p, WrShared<NBV> &sh, int t, bool
   if (store && tid < p.B && p.samples) p.samples[(size_t)(p.fold0 + tid) * p.L + t] = sh.sval[tid];
 }
 
-template <int NBV>
-__device__ __forceinline__ void load_mel(const WrParams &p, WrShared<NBV> &sh, int t) {
-  for (int f = threadIdx.x; f < NBV * (WR_NM / 4); f += WR_NT) {
-    const int b = f / (WR_NM / 4), c = (f % (WR_NM / 4)) * 4;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (b < p.B) {
-      const Pos ps = position(p, b, t);
-      if (ps.mel_row >= 0) v = *(const f32x4 *)&p.mel[(size_t)ps.mel_row * WR_NM + c];
+// this step's mel rows, fetched one step ahead into registers (the global-load latency
+// hides behind a whole step) and stored to LDS at the top of the step
+template <int NBV, int NI>
+struct MelPrefetch {
+  static constexpr int NT = Geo<NI>::NT;
+  static constexpr int N = (NBV * (WR_NM / 4) + NT - 1) / NT;
+  f32x4 r[N];
+  __device__ __forceinline__ void fetch(const WrParams &p, int t) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int f = threadIdx.x + i * NT;
+      const int b = f / (WR_NM / 4), c = (f % (WR_NM / 4)) * 4;
+      r[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (f < NBV * (WR_NM / 4) && b < p.B) {
+        const Pos ps = position(p, b, t);
+        if (ps.mel_row >= 0) r[i] = *(const f32x4 *)&p.mel[(size_t)ps.mel_row * WR_NM + c];
+      }
     }
-    *(f32x4 *)&sh.melv[b * WR_NM + c] = v;
   }
-}
+  __device__ __forceinline__ void store(WrShared<NBV, NI> &sh) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int f = threadIdx.x + i * NT;
+      if (f < NBV * (WR_NM / 4)) *(f32x4 *)&sh.melv[f * 4] = r[i];
+    }
+  }
+};
 
-// the slot's product over its k-part: 8 lanes x NJ float4 chunks, interleaved; one fold
-// at a time (a rolled loop over the B live folds keeps the register footprint at the
-// weights plus one chunk set)
-template <int NJ>
+// (k = kbase + j JS + 4 kl + e: the lanes of a wave read contiguous runs, conflict-free).
+// Four folds per pass with independent accumulators: one wave per SIMD cannot hide the
+// LDS and FMA latencies of a single fold's chain.  Folds past B read the zeroed rows of
+// the vector (B is rounded up to 4 <= NBV); their partials are never read.
+template <int NJ, int JS>
 __device__ __forceinline__ void matvec(const float (&w)[NJ * 4], const float *vec, int kbase,
                                        int kl, float *out, bool active, int B) {
-#pragma unroll 2
-  for (int b = 0; b < B; ++b) {
-    float acc = 0.f;
+  for (int b = 0; b < B; b += 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const f32x4 h = *(const f32x4 *)&vec[b * 512 + kbase + j * 32 + kl * 4];
-      acc = fmaf(w[4 * j], h.x, acc);
-      acc = fmaf(w[4 * j + 1], h.y, acc);
-      acc = fmaf(w[4 * j + 2], h.z, acc);
-      acc = fmaf(w[4 * j + 3], h.w, acc);
+    for (int j = 0; j < NJ; j += 2) {
+      // two k-chunks of four folds in flight (8 loads); the barrier keeps the compiler from
+      // hoisting every chunk's loads (a register per loaded float) while letting the
+      // arithmetic of this pair sink below the next pair's loads
+      f32x4 h[2][4];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          h[jj][q] = *(const f32x4 *)&vec[(b + q) * 512 + kbase + (j + jj) * JS + kl * 4];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[q] = fmaf(w[4 * (j + jj)], h[jj][q].x, acc[q]);
+          acc[q] = fmaf(w[4 * (j + jj) + 1], h[jj][q].y, acc[q]);
+          acc[q] = fmaf(w[4 * (j + jj) + 2], h[jj][q].z, acc[q]);
+          acc[q] = fmaf(w[4 * (j + jj) + 3], h[jj][q].w, acc[q]);
+        }
+      __builtin_amdgcn_sched_barrier(0x0006);  // only VALU / SALU may cross
     }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    acc += __shfl_xor(acc, 4);
-    if (active && kl == 0) out[b] = acc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = sum8(acc[q]);
+    if (active && kl == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) out[b + q] = acc[q];
+    }
   }
 }
 
-// mel conditioning: 80 = 8 lanes x 10, lane kl takes k = kl + 8 j
+// mel conditioning: 80 = 8 lanes x 10, lane kl takes k = kl + 8 j; four folds per pass
 __device__ __forceinline__ void matvec_mel(const float (&w)[10], const float *melv, int kl, float *out,
                                            bool active, int B) {
-#pragma unroll 2
-  for (int b = 0; b < B; ++b) {
-    float a = 0.f;
+  for (int b = 0; b < B; b += 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 10; ++j) a = fmaf(w[j], melv[b * WR_NM + kl + 8 * j], a);
-    a += __shfl_xor(a, 1);
-    a += __shfl_xor(a, 2);
-    a += __shfl_xor(a, 4);
-    if (active && kl == 0) out[b] = a;
+    for (int j = 0; j < 10; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = fmaf(w[j], melv[(b + q) * WR_NM + kl + 8 * j], acc[q]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = sum8(acc[q]);
+    if (active && kl == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) out[b + q] = acc[q];
+    }
   }
 }
 
-template <int NBV, int NCR>
-__global__ __launch_bounds__(WR_NT, 1) void wavernn_kernel(const WrParams p) {
-  __shared__ WrShared<NBV> sh;
+template <int NBV, int NCR, int NI>
+__global__ __launch_bounds__(Geo<NI>::NT, 1) void wavernn_kernel(const WrParams p0) {
+  using G = Geo<NI>;
+  constexpr int NT = G::NT, UG = G::UG, FR = G::FR, NG = G::NG;
+  __shared__ WrShared<NBV, NI> sh;
   const int tid = threadIdx.x;
   const int s = tid >> 3, kl = tid & 7;
+  // this workgroup's instance: its folds and exchange buffers
+  const int inst = blockIdx.x / G::W, local = blockIdx.x % G::W;
+  WrParams p = p0;
+  {
+    const int bi = (p0.B + NI - 1) / NI;
+    p.fold0 = p0.fold0 + inst * bi;
+    p.B = p0.B - inst * bi < bi ? p0.B - inst * bi : bi;
+    p.xch = p0.xch + (size_t)inst * (4 * XS_VEC + XS_Z);
+  }
+  // diag (FTMI_WR_STAMPS=1): thread 0 of instance 0's first GRU and first FC workgroup sum
+  // s_memtime deltas per phase into the workspace (timing only; outputs unchanged)
+  const bool stamping = p.stamps && tid == 0 && (blockIdx.x == 0 || blockIdx.x == NG);
+  if (tid < 12) sh.stamp[tid] = 0;
+  if (tid == 0) sh.stamp[11] = __builtin_amdgcn_s_memtime();  // slot 11: last stamp
+#define WR_STAMP(i)                                              \
+  do {                                                           \
+    if (stamping) {                                              \
+      const unsigned long long now__ = __builtin_amdgcn_s_memtime(); \
+      sh.stamp[i] += now__ - sh.stamp[11];                       \
+      sh.stamp[11] = now__;                                      \
+    }                                                            \
+  } while (0)
 
   // ---- arrival barrier: all WR_GRID workgroups must be resident (bounded) -----------
   if (tid == 0) {
@@ -402,37 +501,44 @@ __global__ __launch_bounds__(WR_NT, 1) void wavernn_kernel(const WrParams p) {
       }
     }
   }
-  for (int i = tid; i < NBV * 512; i += WR_NT) sh.vec[i] = 0.f;
-  for (int i = tid; i < NBV; i += WR_NT) sh.sval[i] = 0.f;
+  for (int i = tid; i < NBV * 512; i += NT) sh.vec[i] = 0.f;
+  for (int i = tid; i < NBV; i += NT) sh.sval[i] = 0.f;
   __syncthreads();
-  if (sh.abort_flag) return;
+  if (sh.abort_flag || p.B <= 0) return;
 
-  const bool gru = blockIdx.x < WR_NG;
+  const bool gru = local < NG;
   if (gru) {
     // ================================ GRU workgroup =====================================
-    const int u0 = blockIdx.x * WR_UG;
-    const bool act = s < 24;  // 12 rows x 2 k-parts
+    const int u0 = local * UG;
+    const bool act = s < 6 * UG;  // 3 UG gate rows x 2 k-parts
     const int r = s >> 1, kp = s & 1;
-    const int mrow = (r >> 2) * WR_R + u0 + (r & 3);
+    // inactive slots (s >= 6 UG) hold a valid row's weights: their sums are never stored
+    const int rc = act ? r : 0;
+    const int mrow = (rc / UG) * WR_R + u0 + rc % UG;
     float w1[32], w2[32], w3[32], wmr[10];
+    {
+      // one base address per matrix, 16-B loads at immediate offsets (k = 64 j + 32 kp + 4 kl + e)
+      const size_t off = (size_t)mrow * WR_R + kp * 32 + kl * 4;
+      const float *a1 = p.w_hh1 + off, *a2 = p.w_hh2 + off, *a3 = p.w_ih2a + off;
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < 8; ++j) {
+        const f32x4 x1 = *(const f32x4 *)(a1 + j * 64), x2 = *(const f32x4 *)(a2 + j * 64),
+                    x3 = *(const f32x4 *)(a3 + j * 64);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = kp * 256 + j * 32 + kl * 4 + e;
-        w1[4 * j + e] = act ? p.w_hh1[(size_t)mrow * WR_R + k] : 0.f;
-        w2[4 * j + e] = act ? p.w_hh2[(size_t)mrow * WR_R + k] : 0.f;
-        w3[4 * j + e] = act ? p.w_ih2a[(size_t)mrow * WR_R + k] : 0.f;
+        for (int e = 0; e < 4; ++e) w1[4 * j + e] = x1[e], w2[4 * j + e] = x2[e], w3[4 * j + e] = x3[e];
       }
-    {  // mel rows: slot s < 24 = (block s / 12: G1 | Q, gate row s % 12)
-      const int rr = s % 12;
-      const int row = (s / 12) * 3 * WR_R + (rr >> 2) * WR_R + u0 + (rr & 3);
+    }
+    {  // mel rows: slot s < 6 UG = (block s / 3 UG: G1 | Q, gate row s % 3 UG)
+      const int sc = act ? s : 0;
+      const int rr = sc % (3 * UG);
+      const int row = (sc / (3 * UG)) * 3 * WR_R + (rr / UG) * WR_R + u0 + rr % UG;
+      const float *am = p.wm + (size_t)row * WR_NM + kl;
 #pragma unroll
-      for (int j = 0; j < 10; ++j) wmr[j] = act ? p.wm[(size_t)row * WR_NM + kl + 8 * j] : 0.f;
+      for (int j = 0; j < 10; ++j) wmr[j] = am[8 * j];
     }
     // cell thread (unit cu, fold cb)
-    const bool cell = tid < WR_UG * p.B;
-    const int cu = tid & 3, cb = tid >> 2;
+    const bool cell = tid < UG * p.B;
+    const int cu = tid % UG, cb = tid / UG;
     const int unit = u0 + cu;
     float bh1[3], bh2[3], uu1[3], uu2[3];
 #pragma unroll
@@ -443,32 +549,49 @@ __global__ __launch_bounds__(WR_NT, 1) void wavernn_kernel(const WrParams p) {
       uu2[q] = p.u2[q * WR_R + unit];
     }
     float h1 = 0.f, h2 = 0.f;
-
-    for (int t = 0; t < p.L; ++t) {
-      // ---- idle phase: everything not on the sample chain --------------------------
-      float gc[3] = {0.f, 0.f, 0.f}, qc[3] = {0.f, 0.f, 0.f};
+    // conditioning of the cell's unit (frame terms) and the mel rows, one step ahead
+    float gn[3] = {0.f, 0.f, 0.f}, qn[3] = {0.f, 0.f, 0.f};
+    auto fetch_cond = [&](int t) {
       if (cell) {
         const Pos ps = position(p, cb, t);
         const float *crow = p.cond + (size_t)ps.cond_row * WR_COND;
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          gc[q] = crow[q * WR_R + unit];
-          qc[q] = crow[3 * WR_R + q * WR_R + unit];
+          gn[q] = crow[q * WR_R + unit];
+          qn[q] = crow[3 * WR_R + q * WR_R + unit];
         }
       }
-      load_mel(p, sh, t);
-      matvec<8>(w1, sh.vec, kp * 256, kl, sh.part[0][s], act, p.B);  // W_hh1 h1_{t-1}
+    };
+    MelPrefetch<NBV, NI> mp;
+    mp.fetch(p, 0);
+    fetch_cond(0);
+
+    for (int t = 0; t < p.L; ++t) {
+      // ---- idle phase: everything not on the sample chain --------------------------
+      float gc[3], qc[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) gc[q] = gn[q], qc[q] = qn[q];
+      mp.store(sh);
+      if (t + 1 < p.L) {
+        mp.fetch(p, t + 1);
+        fetch_cond(t + 1);
+      }
+      matvec<8, 64>(w1, sh.vec, kp * 32, kl, sh.part[0][s], act, p.B);  // W_hh1 h1_{t-1}
       __syncthreads();
+      WR_STAMP(0);
       if (t > 0) acquire_vec(p, sh, 1, t - 1, false);  // h2_{t-1}
       __syncthreads();
+      WR_STAMP(1);
       if (sh.abort_flag) return;
-      matvec<8>(w2, sh.vec, kp * 256, kl, sh.part[1][s], act, p.B);  // W_hh2 h2_{t-1}
+      matvec<8, 64>(w2, sh.vec, kp * 32, kl, sh.part[1][s], act, p.B);  // W_hh2 h2_{t-1}
       matvec_mel(wmr, sh.melv, kl, sh.partm[s], act, p.B);
       // ---- the chain: s_{t-1} -------------------------------------------------------
       __syncthreads();
-      if (t > 0) acquire_sample(p, sh, t - 1, !p.xin && blockIdx.x == 0);  // teacher-forced: pace only
+      WR_STAMP(2);
+      if (t > 0) acquire_sample(p, sh, t - 1, !p.xin && local == 0);  // teacher-forced: pace only
       if (p.xin && tid < p.B) sh.sval[tid] = p.xin[(size_t)(p.fold0 + tid) * p.L + t];
       __syncthreads();
+      WR_STAMP(3);
       if (sh.abort_flag) return;
       float sv = 0.f;
       if (cell) {
@@ -476,7 +599,7 @@ __global__ __launch_bounds__(WR_NT, 1) void wavernn_kernel(const WrParams p) {
         float gi[3], gh[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          const int rw = q * 4 + cu;
+          const int rw = q * UG + cu;
           gh[q] = sh.part[0][2 * rw][cb] + sh.part[0][2 * rw + 1][cb];
           gi[q] = (gc[q] + sh.partm[rw][cb]) + uu1[q] * sv;
         }
@@ -488,17 +611,19 @@ __global__ __launch_bounds__(WR_NT, 1) void wavernn_kernel(const WrParams p) {
       }
       acquire_vec(p, sh, 0, t, false);  // h1_t
       __syncthreads();
+      WR_STAMP(4);
       if (sh.abort_flag) return;
-      matvec<8>(w3, sh.vec, kp * 256, kl, sh.part[2][s], act, p.B);  // W_ih2a h1_t
+      matvec<8, 64>(w3, sh.vec, kp * 32, kl, sh.part[2][s], act, p.B);  // W_ih2a h1_t
       __syncthreads();
+      WR_STAMP(5);
       if (cell) {
         float gi[3], gh[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          const int rw = q * 4 + cu;
+          const int rw = q * UG + cu;
           gh[q] = sh.part[1][2 * rw][cb] + sh.part[1][2 * rw + 1][cb];
           const float gx = sh.part[2][2 * rw][cb] + sh.part[2][2 * rw + 1][cb];
-          gi[q] = ((qc[q] + sh.partm[12 + rw][cb]) + uu2[q] * sv) + gx;
+          gi[q] = ((qc[q] + sh.partm[3 * UG + rw][cb]) + uu2[q] * sv) + gx;
         }
         const float rg = sigm(gi[0] + (gh[0] + bh2[0]));
         const float zg = sigm(gi[1] + (gh[1] + bh2[1]));
@@ -506,61 +631,83 @@ __global__ __launch_bounds__(WR_NT, 1) void wavernn_kernel(const WrParams p) {
         h2 = tagged(ng + zg * (h2 - ng), t);
         publish(p, 1, t, cb, unit, h2);
       }
+      WR_STAMP(6);
       // sh.vec keeps h1_t: the next step's W_hh1 product reads it
     }
-    if (!p.xin && blockIdx.x == 0) {  // the last sample
+    if (!p.xin && local == 0) {  // the last sample
       __syncthreads();
       acquire_sample(p, sh, p.L - 1, true);
     }
   } else {
     // ================================= FC workgroup =====================================
-    const int f = blockIdx.x - WR_NG;
-    const int r0 = f * WR_FR;
-    const int r = s >> 3, kp = s & 7;  // 4 rows x 8 k-parts
+    const int f = local - NG;
+    const int r0 = f * FR;
+    const int r = s >> 3, kp = s & 7;  // FR rows x 8 k-parts
     float wf1[8], wf2[8], wf3[8], wmr[10];
     const int k3 = f * NCR + r;  // fc3 row of this slot
     const bool act3 = r < NCR && k3 < p.NC;
+    {
+      const int koff = kp * 32 + kl * 4;  // k = 256 j + 32 kp + 4 kl + e
+      const float *a1 = p.w_fc1a + (size_t)(r0 + r) * WR_R + koff;
+      const float *a2 = p.w_fc2a + (size_t)(r0 + r) * WR_F + koff;
+      const float *a3 = p.w_fc3 + (size_t)(act3 ? k3 : 0) * WR_F + koff;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 x1 = *(const f32x4 *)(a1 + j * 256), x2 = *(const f32x4 *)(a2 + j * 256),
+                    x3 = *(const f32x4 *)(a3 + j * 256);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = kp * 64 + j * 32 + kl * 4 + e;
-        wf1[4 * j + e] = p.w_fc1a[(size_t)(r0 + r) * WR_R + k];
-        wf2[4 * j + e] = p.w_fc2a[(size_t)(r0 + r) * WR_F + k];
-        wf3[4 * j + e] = act3 ? p.w_fc3[(size_t)k3 * WR_F + k] : 0.f;
+        for (int e = 0; e < 4; ++e) wf1[4 * j + e] = x1[e], wf2[4 * j + e] = x2[e], wf3[4 * j + e] = x3[e];
       }
-    const bool actm = s < WR_FR;
+    }
+    const bool actm = s < FR;
+    {
+      const float *am = p.wm + (size_t)(6 * WR_R + r0 + (actm ? s : 0)) * WR_NM + kl;
 #pragma unroll
-    for (int j = 0; j < 10; ++j)
-      wmr[j] = actm ? p.wm[(size_t)(6 * WR_R + r0 + s) * WR_NM + kl + 8 * j] : 0.f;
+      for (int j = 0; j < 10; ++j) wmr[j] = am[8 * j];
+    }
     // cell thread (row cr, fold cb)
-    const bool cell = tid < WR_FR * p.B;
-    const int cr = tid & 3, cb = tid >> 2;
+    const bool cell = tid < FR * p.B;
+    const int cr = tid % FR, cb = tid / FR;
     const float vv1 = p.v1[r0 + cr];
-
-    for (int t = 0; t < p.L; ++t) {
-      float rc = 0.f, sc = 0.f;
+    float rn = 0.f, sn = 0.f;
+    auto fetch_cond = [&](int t) {
       if (cell) {
         const Pos ps = position(p, cb, t);
         const float *crow = p.cond + (size_t)ps.cond_row * WR_COND;
-        rc = crow[6 * WR_R + r0 + cr];
-        sc = crow[6 * WR_R + WR_F + r0 + cr];
+        rn = crow[6 * WR_R + r0 + cr];
+        sn = crow[6 * WR_R + WR_F + r0 + cr];
       }
-      load_mel(p, sh, t);
+    };
+    MelPrefetch<NBV, NI> mp;
+    mp.fetch(p, 0);
+    fetch_cond(0);
+
+    for (int t = 0; t < p.L; ++t) {
+      const float rc = rn, sc = sn;
+      mp.store(sh);
+      if (t + 1 < p.L) {
+        mp.fetch(p, t + 1);
+        fetch_cond(t + 1);
+      }
       __syncthreads();
       matvec_mel(wmr, sh.melv, kl, sh.partm[s], actm, p.B);
+      WR_STAMP(0);
       // ---- s_{t-1} -------------------------------------------------------------------
       if (t > 0) acquire_sample(p, sh, t - 1, false);
+      WR_STAMP(1);
       if (p.xin && tid < p.B) sh.sval[tid] = p.xin[(size_t)(p.fold0 + tid) * p.L + t];
       // ---- h1_t + h2_t ----------------------------------------------------------------
       acquire_vec(p, sh, 0, t, false);
       __syncthreads();
       if (sh.abort_flag) return;
+      WR_STAMP(2);
       acquire_vec(p, sh, 1, t, true);
       __syncthreads();
       if (sh.abort_flag) return;
-      matvec<2>(wf1, sh.vec, kp * 64, kl, sh.part[0][s], true, p.B);
+      WR_STAMP(3);
+      matvec<2, 256>(wf1, sh.vec, kp * 32, kl, sh.part[0][s], true, p.B);
       __syncthreads();
+      WR_STAMP(4);
       if (cell) {
         float acc = sh.part[0][cr * 8][cb];
 #pragma unroll
@@ -571,8 +718,10 @@ __global__ __launch_bounds__(WR_NT, 1) void wavernn_kernel(const WrParams p) {
       acquire_vec(p, sh, 2, t, false);  // y1
       __syncthreads();
       if (sh.abort_flag) return;
-      matvec<2>(wf2, sh.vec, kp * 64, kl, sh.part[1][s], true, p.B);
+      WR_STAMP(5);
+      matvec<2, 256>(wf2, sh.vec, kp * 32, kl, sh.part[1][s], true, p.B);
       __syncthreads();
+      WR_STAMP(6);
       if (cell) {
         float acc = sh.part[1][cr * 8][cb];
 #pragma unroll
@@ -582,36 +731,48 @@ __global__ __launch_bounds__(WR_NT, 1) void wavernn_kernel(const WrParams p) {
       acquire_vec(p, sh, 3, t, false);  // y2
       __syncthreads();
       if (sh.abort_flag) return;
-      matvec<2>(wf3, sh.vec, kp * 64, kl, sh.part[2][s], act3, p.B);
+      WR_STAMP(7);
+      matvec<2, 256>(wf3, sh.vec, kp * 32, kl, sh.part[2][s], act3, p.B);
       __syncthreads();
-      // ---- fc3 rows of this workgroup: logits, then the draw's partial ------------------
-      if (tid < p.B && f * NCR < p.NC) {
-        const int b = tid;
-        float best = -INFINITY;
-        int bidx = 0;
-        for (int rr = 0; rr < NCR; ++rr) {
-          const int k = f * NCR + rr;
-          if (k >= p.NC) break;
+      WR_STAMP(8);
+      // ---- fc3 rows of this workgroup: logits and Gumbel scores (one thread per (row,
+      // fold): the Philox rounds and logs in parallel), then the draw's partial ----------
+      if (tid < NCR * p.B) {
+        const int rr = tid % NCR, b = tid / NCR, k = f * NCR + rr;
+        float z = -INFINITY;
+        if (k < p.NC) {
           float l = sh.part[2][rr * 8][b];
 #pragma unroll
           for (int i = 1; i < 8; ++i) l += sh.part[2][rr * 8 + i][b];
           l = l + p.b_fc3[k];
           if (p.logits) p.logits[((size_t)(p.fold0 + b) * p.L + t) * p.NC + k] = l;
           if (p.mol) {
-            best = l;
-            bidx = k;
+            z = l;
           } else {
             const u32x4 w = philox((u32x4){(unsigned)t, (unsigned)(p.fold0 + b), (unsigned)(k >> 2), 0u},
                                    p.k0, p.k1);
-            const float u = u01(pword(w, k & 3));
-            const float z = l - logf(-logf(u));
-            if (z > best) best = z, bidx = k;
+            z = l - logf(-logf(u01(pword(w, k & 3))));
           }
         }
-        publish_z(p, t, b, f, best, bidx);
+        sh.partm[rr][b] = z;  // the mel partials of this step are consumed
       }
+      __syncthreads();
+      if (tid < p.B && f * NCR < p.NC) {
+        float best = sh.partm[0][tid];
+        int bidx = f * NCR;
+#pragma unroll
+        for (int rr = 1; rr < NCR; ++rr)
+          if (sh.partm[rr][tid] > best) best = sh.partm[rr][tid], bidx = f * NCR + rr;
+        publish_z(p, t, tid, f, best, bidx);
+      }
+      WR_STAMP(9);
     }
   }
+  if (stamping) {
+    unsigned long long *dst = (unsigned long long *)(p.ws + WS_STAMPS) + (blockIdx.x == 0 ? 0 : 16);
+    for (int i = 0; i < 11; ++i) dst[i] = sh.stamp[i];
+  }
+#undef WR_STAMP
 }
 
 __global__ void wr_stretch_conv_kernel(const float *x, int64_t xs_b, int W, int C, int s,
@@ -701,8 +862,10 @@ int cu_count() {
 
 }  // namespace
 
+constexpr int WR_NI_MAX = 2;  // instances per launch
+
 extern "C" int64_t ftmi_wavernn_workspace_bytes(void) {
-  return (int64_t)(WS_CTRL + 4 * XS_VEC + XS_Z) * 4;
+  return (int64_t)(WS_CTRL + WR_NI_MAX * (4 * XS_VEC + XS_Z)) * 4;
 }
 
 extern "C" uint32_t ftmi_set_wavernn_spin_limit(uint32_t limit) {
@@ -745,28 +908,63 @@ extern "C" int ftmi_wavernn(const ftmi_wavernn_args *a, ftmi_stream_t stream) {
   p.L = a->L, p.NC = a->n_classes, p.mol = a->mol;
   p.k0 = (unsigned)(a->seed & 0xFFFFFFFFull), p.k1 = (unsigned)(a->seed >> 32);
   p.spin_limit = g_wr_spin;
-  const int ncr = a->mol ? 1 : (a->n_classes + WR_NF - 1) / WR_NF;
-  for (int f0 = 0; f0 < a->B; f0 += WR_NBMAX) {
+  static const int stamps_env = [] {
+    const char *v = getenv("FTMI_WR_STAMPS");
+    return v ? atoi(v) : 0;
+  }();
+  p.stamps = stamps_env;
+  // two instances (each the whole pipeline on 128 workgroups, half the folds) whenever
+  // there are two folds to share: the per-step hand-off latency is paid once for both
+  const int per_launch = WR_NBMAX * WR_NI_MAX;
+  for (int f0 = 0; f0 < a->B; f0 += p.B) {
     p.fold0 = f0;
-    p.B = a->B - f0 < WR_NBMAX ? a->B - f0 : WR_NBMAX;
+    p.B = a->B - f0 < per_launch ? a->B - f0 : per_launch;
+    // FTMI_WR_NI=2: two instances.  Measured slower (c2-size mel: 36.6 vs 32.9 us/step):
+    // at 512 threads a workgroup gets half the registers and the GRU weights spill
+    static const int ni_env = [] {
+      const char *v = getenv("FTMI_WR_NI");
+      return v ? atoi(v) : 1;
+    }();
+    const int ni = (p.B >= 2 && ni_env == 2) ? 2 : 1;
+    const int bi = (p.B + ni - 1) / ni;
+    const int ncr = a->mol ? 1 : a->n_classes / (WR_GRID / ni / 2);
     hipError_t e = hipMemsetAsync(a->workspace, 0, (size_t)ftmi_wavernn_workspace_bytes(), s);
     if (e != hipSuccess) return (int)e;
-#define FTMI_WR_LAUNCH(NBV_, NCR_) \
-  hipLaunchKernelGGL((wavernn_kernel<NBV_, NCR_>), dim3(WR_GRID), dim3(WR_NT), 0, s, p)
+#define FTMI_WR_LAUNCH(NBV_, NCR_, NI_)                                                  \
+  hipLaunchKernelGGL((wavernn_kernel<NBV_, NCR_, NI_>), dim3(WR_GRID), dim3(WR_NT * NI_), 0, s, p)
+    if (ni == 1) {
+      p.B = p.B < WR_NBMAX ? p.B : WR_NBMAX;  // one instance: <= 32 folds per launch
+#define FTMI_WR_NCR1(NBV_)                         \
+  switch (ncr) {                                   \
+    case 1: FTMI_WR_LAUNCH(NBV_, 1, 1); break;     \
+    case 2: FTMI_WR_LAUNCH(NBV_, 2, 1); break;     \
+    default: FTMI_WR_LAUNCH(NBV_, 4, 1); break;    \
+  }
+      if (p.B <= 8) {
+        FTMI_WR_NCR1(8)
+      } else if (p.B <= 16) {
+        FTMI_WR_NCR1(16)
+      } else {
+        FTMI_WR_NCR1(32)
+      }
+#undef FTMI_WR_NCR1
+    } else {
 #define FTMI_WR_NCR(NBV_)                          \
   switch (ncr) {                                   \
-    case 1: FTMI_WR_LAUNCH(NBV_, 1); break;        \
-    case 2: FTMI_WR_LAUNCH(NBV_, 2); break;        \
-    default: FTMI_WR_LAUNCH(NBV_, 4); break;       \
+    case 1: FTMI_WR_LAUNCH(NBV_, 1, 2); break;     \
+    case 2: FTMI_WR_LAUNCH(NBV_, 2, 2); break;     \
+    case 4: FTMI_WR_LAUNCH(NBV_, 4, 2); break;     \
+    default: FTMI_WR_LAUNCH(NBV_, 8, 2); break;    \
   }
-    if (p.B <= 8) {
-      FTMI_WR_NCR(8)
-    } else if (p.B <= 16) {
-      FTMI_WR_NCR(16)
-    } else {
-      FTMI_WR_NCR(32)
-    }
+      if (bi <= 8) {
+        FTMI_WR_NCR(8)
+      } else if (bi <= 16) {
+        FTMI_WR_NCR(16)
+      } else {
+        FTMI_WR_NCR(32)
+      }
 #undef FTMI_WR_NCR
+    }
 #undef FTMI_WR_LAUNCH
     FTMI_CHECK_LAUNCH();
   }

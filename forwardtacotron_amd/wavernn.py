@@ -240,6 +240,7 @@ class WaveRNN(Packed):
         a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         ws = ops.wavernn_workspace(dev)
         a.workspace = ws.data_ptr()
+        self.__dict__['_ftmi_last_ws'] = ws  # diag readers (tools/wr_stamps.py)
         out = None
         if xin is not None:
             xin = xin.to(device=dev, dtype=_f32).contiguous()

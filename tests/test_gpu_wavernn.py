@@ -51,8 +51,9 @@ def test_upsample_matches_reference():
     g = load_golden('wr_upsample')
     m, _ = _model()
     up, aux = m.upsample_forward(torch.from_numpy(g['mels']).to(DEV))
-    np.testing.assert_allclose(up.cpu().numpy(), g['up'], rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(aux.cpu().numpy(), g['aux'], rtol=1e-5, atol=2e-5)
+    # fp32-level: the GEMM path's summation order, scaled by each output's magnitude
+    for got, ref in ((up, g['up']), (aux, g['aux'])):
+        np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=1e-5, atol=2e-6 * np.abs(ref).max())
 
 
 def test_forward_logits_match_reference():
@@ -119,9 +120,13 @@ def test_generate_unbatched_matches_oracle():
 def test_generate_mol_matches_oracle():
     g = load_golden('wr_gen_mol')
     m, cfg = _model('MOL')
-    _check_draws(m, cfg, g['mels'], 5, 400, 40)
-    wav = m.generate(torch.from_numpy(g['mels']), True, 400, 40, True, seed=5)
-    assert wav.shape == g['wav'].shape and np.all(np.abs(wav) <= 1.0)
+    smp = _check_draws(m, cfg, g['mels'], 5, 400, 40)
+    assert np.all(np.abs(smp) <= 1.0)  # clamp(x, -1, 1) of distribution.py:125
+    wav = m.generate(torch.from_numpy(g['mels']), True, 400, 40, True, seed=5)  # mu_law ignored (MOL)
+    ref = wr.finish(smp.astype(np.float64), True, 400, 40, False, m.n_classes,
+                    (g['mels'].shape[-1] - 1) * 256, 256)
+    assert wav.shape == ref.shape == g['wav'].shape
+    np.testing.assert_allclose(wav, ref, rtol=0, atol=1e-12)
 
 
 def test_generate_many_folds_two_launches():
