@@ -14,6 +14,12 @@ them); `valid_frames_per_s` counts only each utterance's own frames.
   --callbacks gen_forward  the callbacks gen_forward.py:103-104 passes
                          (pitch_function = lambda x: x * amp, energy_function = lambda x: x)
   --model fast_pitch     configs[4], "c5": FastPitch, batch 64, lengths U{50..200}
+  --model wavernn        the `gen_forward.py wavernn` vocoder (no BASELINE
+                         number): WaveRNN.generate of one c2-length mel (821 frames, synthetic
+                         log-mel values) with gen_forward's batched defaults (target 11000,
+                         overlap 550, 19 folds), RAW 9 bits, mu-law; metric audio samples/s
+                         (wave_len per generate() call, the float64 wave on the host); N > 1:
+                         replicas only (each rank its own utterance, no collective)
 
 Multi-GPU (c4, BASELINE.json configs[3]): rank 0 makes the synthetic weights and
 broadcasts them (sharded.broadcast_state: one bucketed RCCL broadcast per dtype); the
@@ -115,8 +121,10 @@ def main():
     ap.add_argument('--tmin', type=int, default=50)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--kernels', action='store_true', help='print the per-kernel table to stderr')
-    ap.add_argument('--model', choices=['forward_tacotron', 'fast_pitch'], default='forward_tacotron',
-                    help='fast_pitch = BASELINE.json configs[4] (c5)')
+    ap.add_argument('--model', choices=['forward_tacotron', 'fast_pitch', 'wavernn'],
+                    default='forward_tacotron',
+                    help='fast_pitch = BASELINE.json configs[4] (c5); wavernn = the vocoder (8(f))')
+    ap.add_argument('--mel-frames', type=int, default=821, help='wavernn: mel length (c2: 821)')
     ap.add_argument('--config', choices=['c2', 'c3'], default=None,
                     help='c2 = BASELINE.json configs[1] (batch 1, 120 phonemes); c3 = the default')
     ap.add_argument('--callbacks', choices=['identity', 'gen_forward'], default='identity',
@@ -138,6 +146,11 @@ def main():
     dev = torch.device('cuda', local)
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
+    if args.model == 'wavernn':
+        bench_wavernn(args, world, rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     cls = FastPitch if args.model == 'fast_pitch' else ForwardTacotron
     model = cls.from_config(default_config())
@@ -325,6 +338,109 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_wavernn(args, world, rank, dev):
+    """The WaveRNN vocoder line (see the module docstring)."""
+    from forwardtacotron_amd.wavernn import WaveRNN
+    cfg = default_config()
+    model = WaveRNN.from_config(cfg)
+    sd = synthetic_state_dict(model, seed=0, model='wavernn')
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model = model.to(dev).eval()
+    gcfg = cfg['vocoder']['generate']
+    target, overlap = gcfg['target'], gcfg['overlap']
+    rng = np.random.Generator(np.random.PCG64([rank, 321]))
+    mels_np = (rng.normal(0.0, 1.0, (1, 80, args.mel_frames)) - 4.0).astype(np.float32)
+    mels = torch.from_numpy(mels_np).to(dev)
+    mu_law = cfg['dsp']['mu_law']
+    gen = lambda seed: model.generate(mels, True, target, overlap, mu_law, seed=seed)
+    for i in range(args.warmup):
+        gen(1000 + i)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    samples = 0
+    with KernelProbe() as probe:
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            wav = gen(i)
+            samples += wav.shape[0]
+        barrier()
+        elapsed = time.perf_counter() - t0
+    kern = probe.summary()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0].item())
+    if rank != 0:
+        return
+    if args.kernels:
+        for lab, v in sorted(kern.items(), key=lambda kv: -kv[1]['total_ms']):
+            log(f'{lab:60s} {v["launches"]:4d} {v["avg_ms"]:9.3f}')
+    dom_label, dom = max(kern.items(), key=lambda kv: kv[1]['total_ms'])
+    s = dom['avg_ms'] / 1e3
+    B = int(dom_label.split('B=')[1].split(',')[0])
+    L = int(dom_label.split('L=')[1].split(',')[0])
+    achieved = dom['flops'] / s / 1e12
+    roof = {'kernel': dom_label, 'bound': 'mfma', 'achieved': round(achieved, 4),
+            'peak': PEAK_FP32_TFLOPS, 'unit': 'TFLOP/s',
+            'peak_basis': 'fp32 (the loop is exact fp32 FMAs on the VALU: the fp32 MFMA and vector '
+                          'peaks are equal on gfx950); the loop is bound by its per-step all-to-all '
+                          'hand-offs, not by either roof (DESIGN.md 5b)',
+            'frac': round(achieved / PEAK_FP32_TFLOPS, 5),
+            'algorithmic_per_launch': dom['flops'], 'avg_launch_ms': round(dom['avg_ms'], 3),
+            'us_per_step': round(dom['avg_ms'] * 1e3 / L, 3), 'folds': B, 'steps_per_launch': L,
+            'launches': dom['launches'],
+            'share_of_device_time': round(dom['total_ms'] / sum(v['total_ms'] for v in kern.values()), 4),
+            'traffic': None}
+    line = {
+        'metric': 'audio samples/s of WaveRNN.generate (gen_forward.py wavernn, batched folds)',
+        'value': round(samples * world / elapsed, 1), 'unit': 'samples/s', 'n_gpus': world,
+        'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+        'data': 'synthetic (log-mel-like N(-4, 1) mels, synthetic WaveRNN weights)',
+        'config': {'workload': f'WaveRNN vocoder: generate(mels (1, 80, {args.mel_frames}), batched=True, '
+                               f'target={target}, overlap={overlap}, mu_law={mu_law}), RAW 9 bits',
+                   'folds': B, 'steps': L, 'wave_len': int(wav.shape[0]),
+                   'parallelism': f'replicas{world}' if world > 1 else 'single'},
+        'roofline': roof,
+        'realtime_factor': round(samples * world / elapsed / cfg['dsp']['sample_rate'], 2),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line['cpu_baseline'] = cpu_baseline_wavernn(sd, cfg, mels_np, target, overlap, B, L, samples,
+                                                    args.steps)
+    print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_wavernn(sd, cfg, mels_np, target, overlap, B, L, samples, steps):
+    """The torch-CPU restatement of the reference vocoder (oracle/wr_torch_cpu.py, the
+    reference's ATen kernels and its Categorical draws) on a bounded sample: the same 19
+    folds for the first 300 steps (the sample loop dominates; scaled to the whole call's
+    wave samples by steps / L)."""
+    from oracle import wr_torch_cpu as wr
+    n = min(300, L)
+    sdt = wr.to_torch(sd)
+    vcfg = dict(cfg['vocoder']['model'])
+    info = _cpu_info()
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    threads = torch.get_num_threads()
+    torch.manual_seed(0)
+    t0 = time.perf_counter()
+    wr.generate(sdt, vcfg, torch.from_numpy(mels_np), True, target, overlap, True, steps=n)
+    dt = time.perf_counter() - t0
+    per_call = dt * L / n  # the whole loop of one generate() call at that rate
+    wave = samples / steps
+    return {'value': round(wave / per_call, 1), 'unit': 'samples/s', 'cores': threads,
+            'kind': 'port', 'cpu_model': info[0], 'physical_cores': info[1],
+            'sample': f'{B} folds x first {n} of {L} steps of one generate() call '
+                      f'({dt:.2f} s), scaled by {L}/{n}'}
 
 
 def ft_oracle_counts(dur):

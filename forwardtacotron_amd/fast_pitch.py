@@ -258,6 +258,15 @@ class FastPitch(nn.Module):
             cache[device] = [torch.cuda.Stream(device=device) for _ in range(3)]
         return cache[device]
 
+
+    def __prepare_scriptable__(self):
+        """`torch.jit.script(model)` (README.md:149-161 exports the reference this way) is not
+        possible here: the compute runs in libftmi.so through ctypes, which TorchScript
+        cannot call.  Fail with the reason instead of a TorchScript frontend error; the
+        scripted entry point's behaviour is available eagerly (`generate_jit`)."""
+        raise RuntimeError(f'{type(self).__name__} runs on libftmi.so (HIP kernels called through '
+                           'ctypes) and cannot be compiled by torch.jit.script; call generate_jit / '
+                           'generate eagerly')
     def generate(self,
                  x: torch.Tensor,
                  alpha=1.0,

@@ -471,6 +471,15 @@ class ForwardTacotron(nn.Module):
                 return out
         return ops.run_checked(run, x.device, reduce=None if batch is None else batch.status)
 
+    def __prepare_scriptable__(self):
+        """`torch.jit.script(model)` (README.md:149-161 exports the reference this way) is not
+        possible here: the compute runs in libftmi.so through ctypes, which TorchScript
+        cannot call.  Fail with the reason instead of a TorchScript frontend error; the
+        scripted entry point's behaviour is available eagerly (`generate_jit`)."""
+        raise RuntimeError(f'{type(self).__name__} runs on libftmi.so (HIP kernels called through '
+                           'ctypes) and cannot be compiled by torch.jit.script; call generate_jit / '
+                           'generate eagerly')
+
     def generate_jit(self, x: torch.Tensor, alpha: float = 1.0, beta: float = 1.0) -> Dict[str, torch.Tensor]:
         """`models/forward_tacotron.py:270-284` (pitch scaled by beta, no callbacks)."""
         self._check_device(x)

@@ -4,7 +4,8 @@ phonemizer — is absent from this image, so raw English text is refused with th
 
     python -m forwardtacotron_amd.gen_forward --checkpoint ckpt.pt \\
         [--input_phonemes "həloʊ wɜːld" | --input_tokens 12,40,7 | --sentences file] \\
-        [--alpha 1.0] [--amp 1.0] {griffinlim,melgan,hifigan}
+        [--alpha 1.0] [--amp 1.0] {griffinlim,melgan,hifigan,wavernn}
+        [--voc_checkpoint voc.pt | --voc_synthetic] [--target 11000] [--overlap 550]
 
 Per sentence, exactly like the reference loop (`gen_forward.py:106-134`): tokens (B = 1) ->
 `generate(x, alpha, pitch_function=lambda x: x * amp, energy_function=lambda x: x)` on the
@@ -12,9 +13,10 @@ HIP path -> `mel_post.cpu()` -> the vocoder's output file in model_outputs/:
   griffinlim  {name}.wav  DSP.griffinlim (HIP NNLS + Griffin-Lim) -> DSP.save_wav (16-bit PCM)
   melgan      {name}.mel  torch.save of the (1, n_mels, T) mel tensor
   hifigan     {name}.npy  np.save(..., allow_pickle=False) of the same array
-with name = f'{i}_forward_{tts_k}k_alpha{alpha}_amp{amp}_{vocoder}' (`:113`).  WaveRNN is out
-of scope and refused.  --synthetic runs the synthetic weights
-(tests / benchmarks without a checkpoint).
+  wavernn     {name}.wav  WaveRNN.generate(mels, batched=True, target, overlap, mu_law of the
+              vocoder's dsp config) on the HIP sample loop -> DSP.save_wav (`:78-80, :125-131`)
+with name = f'{i}_forward_{tts_k}k_alpha{alpha}_amp{amp}_{vocoder}' (`:113`).  --synthetic /
+--voc_synthetic run the synthetic weights (tests / benchmarks without a checkpoint).
 """
 from __future__ import annotations
 
@@ -56,14 +58,41 @@ def wav_name(i: int, tts_k: int, alpha: float, amp: float, vocoder: str) -> str:
     return f'{i}_forward_{tts_k}k_alpha{alpha}_amp{amp}_{vocoder}'
 
 
-def write_output(m: torch.Tensor, name: str, vocoder: str, out_path: Path, dsp=None) -> Path:
-    """`gen_forward.py:120-134` for one sentence: m is the host (1, n_mels, T) mel_post."""
+def load_wavernn(checkpoint_path: str):
+    """`gen_forward.py:30-37` (weights_only load)."""
+    from .wavernn import WaveRNN
+    print(f'Loading voc checkpoint {checkpoint_path}')
+    checkpoint = torch.load(checkpoint_path, map_location=torch.device('cpu'), weights_only=True)
+    config = checkpoint['config']
+    voc_model = WaveRNN.from_config(config)
+    voc_model.load_state_dict(checkpoint['model'])
+    print(f'Loaded model with step {voc_model.get_step()}')
+    return voc_model, config
+
+
+def synthetic_wavernn():
+    from .synthetic import default_config, load_synthetic
+    from .wavernn import WaveRNN
+    config = default_config()
+    return load_synthetic(WaveRNN.from_config(config), 0, 'wavernn'), config
+
+
+def write_output(m: torch.Tensor, name: str, vocoder: str, out_path: Path, dsp=None, voc=None,
+                 target: int = 11000, overlap: int = 550) -> Path:
+    """`gen_forward.py:120-134` for one sentence: m is the host (1, n_mels, T) mel_post;
+    voc = (WaveRNN model, its DSP) for the wavernn vocoder."""
     if vocoder == 'melgan':
         p = out_path / f'{name}.mel'
         torch.save(m, p)
     elif vocoder == 'hifigan':
         p = out_path / f'{name}.npy'
         np.save(p, m.numpy(), allow_pickle=False)
+    elif vocoder == 'wavernn':
+        p = out_path / f'{name}.wav'
+        voc_model, voc_dsp = voc
+        wav = voc_model.generate(mels=m, batched=True, target=target, overlap=overlap,
+                                 mu_law=voc_dsp.mu_law)
+        dsp.save_wav(wav, p)
     elif vocoder == 'griffinlim':
         p = out_path / f'{name}.wav'
         wav = dsp.griffinlim(m.squeeze().numpy())
@@ -104,10 +133,14 @@ def main(argv: Optional[Sequence[str]] = None) -> List[Path]:
     parser.add_argument('--amp', type=float, default=1.)
     parser.add_argument('--out', default='model_outputs')
     parser.add_argument('vocoder', choices=VOCODERS)
+    # the reference's `wavernn` sub-command options (gen_forward.py:54-57)
+    parser.add_argument('--voc_checkpoint', type=str, default=None,
+                        help='[string/path] Load in different WaveRNN weights')
+    parser.add_argument('--voc_synthetic', action='store_true', help='synthetic WaveRNN weights')
+    parser.add_argument('--overlap', '-o', default=550, type=int, help='[int] number of crossover samples')
+    parser.add_argument('--target', '-t', default=11_000, type=int,
+                        help='[int] number of samples in each batch index')
     args = parser.parse_args(argv)
-    if args.vocoder == 'wavernn':
-        raise SystemExit('wavernn: the WaveRNN vocoder is outside this build (SURVEY.md §8(f)); '
-                         'use griffinlim, melgan or hifigan')
     if args.checkpoint:
         tts_model, config = load_tts_model(args.checkpoint)
     elif args.synthetic:
@@ -116,6 +149,15 @@ def main(argv: Optional[Sequence[str]] = None) -> List[Path]:
         raise SystemExit('--checkpoint (or --synthetic) is required')
     from .dsp import DSP
     dsp = DSP.from_config(config)
+    voc = None
+    if args.vocoder == 'wavernn':
+        if args.voc_checkpoint:
+            voc_model, voc_config = load_wavernn(args.voc_checkpoint)
+        elif args.voc_synthetic:
+            voc_model, voc_config = synthetic_wavernn()
+        else:
+            raise SystemExit('wavernn: --voc_checkpoint (or --voc_synthetic) is required')
+        voc = (voc_model, DSP.from_config(voc_config))
     out_path = Path(args.out)
     out_path.mkdir(parents=True, exist_ok=True)
     if not torch.cuda.is_available():
@@ -123,6 +165,8 @@ def main(argv: Optional[Sequence[str]] = None) -> List[Path]:
     device = torch.device('cuda')
     tts_model.to(device)
     tts_model.eval()
+    if voc is not None:
+        voc[0].to(device)
     tts_k = tts_model.get_step() // 1000
     texts = read_inputs(args)
     pitch_function = lambda x: x * args.amp  # noqa: E731  (gen_forward.py:103)
@@ -135,7 +179,8 @@ def main(argv: Optional[Sequence[str]] = None) -> List[Path]:
         gen = tts_model.generate(x=x, alpha=args.alpha, pitch_function=pitch_function,
                                  energy_function=energy_function)
         m = gen['mel_post'].cpu()
-        written.append(write_output(m, name, args.vocoder, out_path, dsp))
+        written.append(write_output(m, name, args.vocoder, out_path, dsp, voc, args.target,
+                                    args.overlap))
     print('\n\nDone.\n')
     return written
 

@@ -274,6 +274,14 @@ class WaveRNN(Packed):
         with torch.no_grad():
             return ops.run_checked(run, dev)
 
+    def __prepare_scriptable__(self):
+        """`torch.jit.script(model)` (README.md:149-161 exports the reference this way) is not
+        possible here: the compute runs in libftmi.so through ctypes, which TorchScript
+        cannot call.  Fail with the reason instead of a TorchScript frontend error; the
+        scripted entry point's behaviour is available eagerly (`generate`)."""
+        raise RuntimeError(f'{type(self).__name__} runs on libftmi.so (HIP kernels called through '
+                           'ctypes) and cannot be compiled by torch.jit.script; call generate eagerly')
+
     def _fold_shape(self, total_len, n_items, batched, target, overlap):
         """(B, L) of the sample loop: fold_with_overlap's fold count (:320-331) or one row
         per utterance."""

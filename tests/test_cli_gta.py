@@ -60,7 +60,7 @@ def test_inputs(tmp_path):
     ns.input_text = 'Hello world'
     with pytest.raises(SystemExit):
         read_inputs(ns)
-    with pytest.raises(SystemExit):
+    with pytest.raises(SystemExit):  # wavernn needs --voc_checkpoint / --voc_synthetic
         main(['--synthetic', '--input_tokens', '1,2', 'wavernn'])
 
 

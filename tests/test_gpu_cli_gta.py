@@ -30,6 +30,13 @@ def test_cli_end_to_end(tmp_path, gpu_model):
     with wave.open(str(outs['griffinlim']), 'rb') as w:
         assert w.getframerate() == 22050 and w.getsampwidth() == 2
         assert w.getnframes() == 256 * (m.shape[2] - 1)  # librosa istft length, center=True
+    # the reference's `wavernn` sub-command (gen_forward.py:54-57, :125-131): batched
+    # WaveRNN generation of the same mel, wave_len = (T - 1) hop
+    (p,) = main(['--synthetic', '--input_tokens', ids, '--amp', '1.2', '--out', str(tmp_path),
+                 'wavernn', '--voc_synthetic', '--target', '4000', '--overlap', '200'])
+    assert p.name == '1_forward_0k_alpha1.0_amp1.2_wavernn.wav'
+    with wave.open(str(p), 'rb') as w:
+        assert w.getframerate() == 22050 and w.getnframes() == 256 * (m.shape[2] - 1)
 
 
 def test_gta_export(tmp_path, gpu_model, synth_sd):

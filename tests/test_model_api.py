@@ -110,3 +110,17 @@ def test_dsp_api_surface():
     np.testing.assert_allclose(d.denormalize(d.normalize(np.array([1e-7, 0.5]))), [1e-5, 0.5])
     with pytest.raises(RuntimeError):
         d.wav_to_mel(__import__('torch').zeros(4000))
+
+
+@pytest.mark.parametrize('kind', ['forward_tacotron', 'fast_pitch', 'wavernn'])
+def test_torchscript_export_fails_with_reason(kind):
+    """README.md:149-161 scripts the reference model; the HIP path cannot be scripted
+    (ctypes calls), and says so instead of a TorchScript frontend error."""
+    from forwardtacotron_amd.checkpoints import init_tts_model
+    from forwardtacotron_amd.synthetic import default_config
+    from forwardtacotron_amd.wavernn import WaveRNN
+    cfg = default_config()
+    cfg['tts_model'] = kind if kind != 'wavernn' else 'forward_tacotron'
+    m = WaveRNN.from_config(cfg) if kind == 'wavernn' else init_tts_model(cfg)
+    with pytest.raises(RuntimeError, match='cannot be compiled by torch.jit.script'):
+        torch.jit.script(m)
