@@ -189,8 +189,19 @@ struct Geo {
   static constexpr int SLOTS = NT / 8;
 };
 
+// Two instances (NI = 2): a GRU workgroup's idle-phase weights (W_hh1, W_hh2: 48 active
+// slots x 8 lanes x 32 floats each) live in LDS, [matrix][j][lane][4] so a wave's 16-B reads
+// are consecutive; only W_ih2a (on the sample chain) stays in VGPRs: 512 threads leave half
+// the registers of a one-instance workgroup.
+template <int NI>
+struct WlDims {
+  static constexpr int LANES = NI == 2 ? 6 * (WR_R / (WR_GRID / NI / 2)) * 8 : 0;  // 6 UG slots x 8
+  static constexpr int FLOATS = NI == 2 ? 2 * 8 * LANES * 4 : 1;
+};
+
 template <int NBV, int NI>
 struct WrShared {
+  float wl[WlDims<NI>::FLOATS];  // NI = 2: W_hh1 / W_hh2 of the GRU workgroup
   float vec[NBV * 512];          // the acquired vector (h1 / h2 / h1+h2 / y1 / y2)
   float part[3][Geo<NI>::SLOTS][NBV];  // per-slot partial sums of the products
   float partm[Geo<NI>::SLOTS][NBV];    // per-slot partial sums of the mel conditioning
@@ -439,6 +450,44 @@ __device__ __forceinline__ void matvec(const float (&w)[NJ * 4], const float *ve
   }
 }
 
+// the same product with the lane's weights read from LDS (wl: [j][lanes][4], this lane's
+// column), once per four-fold block
+template <int NJ, int JS, int LANES>
+__device__ __forceinline__ void matvec_lds(const float *wl, const float *vec, int kbase, int kl,
+                                           float *out, bool active, int B) {
+  const int lane = threadIdx.x < LANES ? threadIdx.x : 0;
+  for (int b = 0; b < B; b += 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NJ; j += 2) {
+      f32x4 h[2][4], w[2];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        w[jj] = *(const f32x4 *)&wl[((j + jj) * LANES + lane) * 4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          h[jj][q] = *(const f32x4 *)&vec[(b + q) * 512 + kbase + (j + jj) * JS + kl * 4];
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[q] = fmaf(w[jj].x, h[jj][q].x, acc[q]);
+          acc[q] = fmaf(w[jj].y, h[jj][q].y, acc[q]);
+          acc[q] = fmaf(w[jj].z, h[jj][q].z, acc[q]);
+          acc[q] = fmaf(w[jj].w, h[jj][q].w, acc[q]);
+        }
+      __builtin_amdgcn_sched_barrier(0x0006);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = sum8(acc[q]);
+    if (active && kl == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) out[b + q] = acc[q];
+    }
+  }
+}
+
 // mel conditioning: 80 = 8 lanes x 10, lane kl takes k = kl + 8 j; four folds per pass
 __device__ __forceinline__ void matvec_mel(const float (&w)[10], const float *melv, int kl, float *out,
                                            bool active, int B) {
@@ -515,7 +564,9 @@ __global__ __launch_bounds__(Geo<NI>::NT, 1) void wavernn_kernel(const WrParams 
     // inactive slots (s >= 6 UG) hold a valid row's weights: their sums are never stored
     const int rc = act ? r : 0;
     const int mrow = (rc / UG) * WR_R + u0 + rc % UG;
-    float w1[32], w2[32], w3[32], wmr[10];
+    constexpr bool WL = NI == 2;
+    constexpr int LANES = WlDims<NI>::LANES;
+    float w1[WL ? 1 : 32], w2[WL ? 1 : 32], w3[32], wmr[10];
     {
       // one base address per matrix, 16-B loads at immediate offsets (k = 64 j + 32 kp + 4 kl + e)
       const size_t off = (size_t)mrow * WR_R + kp * 32 + kl * 4;
@@ -525,9 +576,19 @@ __global__ __launch_bounds__(Geo<NI>::NT, 1) void wavernn_kernel(const WrParams 
         const f32x4 x1 = *(const f32x4 *)(a1 + j * 64), x2 = *(const f32x4 *)(a2 + j * 64),
                     x3 = *(const f32x4 *)(a3 + j * 64);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w1[4 * j + e] = x1[e], w2[4 * j + e] = x2[e], w3[4 * j + e] = x3[e];
+        for (int e = 0; e < 4; ++e) w3[4 * j + e] = x3[e];
+        if constexpr (WL) {
+          if (tid < LANES) {
+            *(f32x4 *)&sh.wl[(j * LANES + tid) * 4] = x1;
+            *(f32x4 *)&sh.wl[((8 + j) * LANES + tid) * 4] = x2;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w1[4 * j + e] = x1[e], w2[4 * j + e] = x2[e];
+        }
       }
     }
+    __syncthreads();
     {  // mel rows: slot s < 6 UG = (block s / 3 UG: G1 | Q, gate row s % 3 UG)
       const int sc = act ? s : 0;
       const int rr = sc % (3 * UG);
@@ -576,14 +637,20 @@ __global__ __launch_bounds__(Geo<NI>::NT, 1) void wavernn_kernel(const WrParams 
         mp.fetch(p, t + 1);
         fetch_cond(t + 1);
       }
-      matvec<8, 64>(w1, sh.vec, kp * 32, kl, sh.part[0][s], act, p.B);  // W_hh1 h1_{t-1}
+      if constexpr (WL)  // W_hh1 h1_{t-1}
+        matvec_lds<8, 64, LANES>(sh.wl, sh.vec, kp * 32, kl, sh.part[0][s], act, p.B);
+      else
+        matvec<8, 64>(w1, sh.vec, kp * 32, kl, sh.part[0][s], act, p.B);
       __syncthreads();
       WR_STAMP(0);
       if (t > 0) acquire_vec(p, sh, 1, t - 1, false);  // h2_{t-1}
       __syncthreads();
       WR_STAMP(1);
       if (sh.abort_flag) return;
-      matvec<8, 64>(w2, sh.vec, kp * 32, kl, sh.part[1][s], act, p.B);  // W_hh2 h2_{t-1}
+      if constexpr (WL)  // W_hh2 h2_{t-1}
+        matvec_lds<8, 64, LANES>(sh.wl + 8 * LANES * 4, sh.vec, kp * 32, kl, sh.part[1][s], act, p.B);
+      else
+        matvec<8, 64>(w2, sh.vec, kp * 32, kl, sh.part[1][s], act, p.B);
       matvec_mel(wmr, sh.melv, kl, sh.partm[s], act, p.B);
       // ---- the chain: s_{t-1} -------------------------------------------------------
       __syncthreads();
@@ -915,17 +982,17 @@ extern "C" int ftmi_wavernn(const ftmi_wavernn_args *a, ftmi_stream_t stream) {
   p.stamps = stamps_env;
   // two instances (each the whole pipeline on 128 workgroups, half the folds) whenever
   // there are two folds to share: the per-step hand-off latency is paid once for both
-  const int per_launch = WR_NBMAX * WR_NI_MAX;
+  const int per_launch = WR_NBMAX;  // NI = 2: 2 x 16 (the LDS holds the GRU weights)
   for (int f0 = 0; f0 < a->B; f0 += p.B) {
     p.fold0 = f0;
     p.B = a->B - f0 < per_launch ? a->B - f0 : per_launch;
-    // FTMI_WR_NI=2: two instances.  Measured slower (c2-size mel: 36.6 vs 32.9 us/step):
-    // at 512 threads a workgroup gets half the registers and the GRU weights spill
+    // two instances from two folds on (c2-size mel, 19 folds: 23.95 against 31.8 us/step
+    // with one); FTMI_WR_NI=1 forces one instance (A/B runs)
     static const int ni_env = [] {
       const char *v = getenv("FTMI_WR_NI");
-      return v ? atoi(v) : 1;
+      return v ? atoi(v) : 2;
     }();
-    const int ni = (p.B >= 2 && ni_env == 2) ? 2 : 1;
+    const int ni = (p.B >= 2 && ni_env != 1) ? 2 : 1;
     const int bi = (p.B + ni - 1) / ni;
     const int ncr = a->mol ? 1 : a->n_classes / (WR_GRID / ni / 2);
     hipError_t e = hipMemsetAsync(a->workspace, 0, (size_t)ftmi_wavernn_workspace_bytes(), s);
@@ -958,10 +1025,8 @@ extern "C" int ftmi_wavernn(const ftmi_wavernn_args *a, ftmi_stream_t stream) {
   }
       if (bi <= 8) {
         FTMI_WR_NCR(8)
-      } else if (bi <= 16) {
-        FTMI_WR_NCR(16)
       } else {
-        FTMI_WR_NCR(32)
+        FTMI_WR_NCR(16)
       }
 #undef FTMI_WR_NCR
     }
