@@ -1,7 +1,11 @@
 """Time the WaveRNN sample loop on the GPU (gen_forward.py's batched defaults: target 11000,
 overlap 550) for a mel of T frames; prints ms per call, us per step and samples/s."""
 import argparse
+import sys
 import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 import numpy as np
 import torch
