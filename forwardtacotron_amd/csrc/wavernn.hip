@@ -201,11 +201,13 @@ struct WlDims {
 
 template <int NBV, int NI>
 struct WrShared {
-  float wl[WlDims<NI>::FLOATS];  // NI = 2: W_hh1 / W_hh2 of the GRU workgroup
-  float vec[NBV * 512];          // the acquired vector (h1 / h2 / h1+h2 / y1 / y2)
+  // every member read with 16-B LDS accesses is 16-B aligned (a misaligned vec made the
+  // one-instance products 4x slower: wl is a single float there)
+  __attribute__((aligned(16))) float wl[WlDims<NI>::FLOATS];  // NI = 2: W_hh1 / W_hh2
+  __attribute__((aligned(16))) float vec[NBV * 512];  // the acquired vector (h1 / h2 / y1 / y2)
   float part[3][Geo<NI>::SLOTS][NBV];  // per-slot partial sums of the products
   float partm[Geo<NI>::SLOTS][NBV];    // per-slot partial sums of the mel conditioning
-  float melv[NBV * WR_NM];       // this step's mel rows
+  __attribute__((aligned(16))) float melv[NBV * WR_NM];  // this step's mel rows
   float sval[NBV];               // s_{t-1}
   unsigned long long stamp[12];  // diag phase sums (thread 0)
   int abort_flag;
@@ -285,7 +287,7 @@ __device__ __forceinline__ void acquire_sample(const WrParams &p, WrShared<NBV, 
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.xch, (short)0, 0x7FFFFFF0, 0x00020000);
   const unsigned want = step_tag(t);
   const int soff = (4 * XS_VEC + (t & 1) * WR_NBMAX * WR_NF * 2) * 4;
-  const int np = p.mol ? p.NC : Geo<NI>::NF;
+  const int np = p.mol ? p.NC : Geo<NI>::NF / 2;  // RAW: the fc3 half of the FC workgroups
   const int b = tid >> 3, part = tid & 7;
   constexpr int PER = Geo<NI>::NF / 16;
   u32x4 r[PER];
@@ -506,7 +508,7 @@ __device__ __forceinline__ void matvec_mel(const float (&w)[10], const float *me
   }
 }
 
-template <int NBV, int NCR, int NI>
+template <int NBV, int NI>
 __global__ __launch_bounds__(Geo<NI>::NT, 1) void wavernn_kernel(const WrParams p0) {
   using G = Geo<NI>;
   constexpr int NT = G::NT, UG = G::UG, FR = G::FR, NG = G::NG;
@@ -707,23 +709,34 @@ __global__ __launch_bounds__(Geo<NI>::NT, 1) void wavernn_kernel(const WrParams 
     }
   } else {
     // ================================= FC workgroup =====================================
+    // fc1: every FC workgroup, FR rows.  fc2 / fc3 on disjoint halves of the FC workgroups
+    // (2 FR rows each): an edge's price grows with its consumers, so y1 is read by half
+    // of them (the fc2 half) and y2 by the other half (fc3), not by all.
+    constexpr int HF = G::NF / 2, FR2 = 2 * FR;
     const int f = local - NG;
+    const bool fc2role = f < HF;
     const int r0 = f * FR;
-    const int r = s >> 3, kp = s & 7;  // FR rows x 8 k-parts
-    float wf1[8], wf2[8], wf3[8], wmr[10];
-    const int k3 = f * NCR + r;  // fc3 row of this slot
-    const bool act3 = r < NCR && k3 < p.NC;
+    const int r = s >> 3, kp = s & 7;      // fc1: FR rows x 8 k-parts (2 chunks per lane)
+    const int r2 = s >> 2, kp2 = s & 3;    // fc2 / fc3: FR2 rows x 4 k-parts (4 chunks)
+    const int q0 = (fc2role ? f : f - HF) * FR2;  // first fc2 (fc3) row of this workgroup
+    float wf1[8], wf23[16], wmr[10];
+    const bool act23 = fc2role || q0 + r2 < p.NC;
     {
-      const int koff = kp * 32 + kl * 4;  // k = 256 j + 32 kp + 4 kl + e
-      const float *a1 = p.w_fc1a + (size_t)(r0 + r) * WR_R + koff;
-      const float *a2 = p.w_fc2a + (size_t)(r0 + r) * WR_F + koff;
-      const float *a3 = p.w_fc3 + (size_t)(act3 ? k3 : 0) * WR_F + koff;
+      const float *a1 = p.w_fc1a + (size_t)(r0 + r) * WR_R + kp * 32 + kl * 4;  // k = 256 j + ..
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const f32x4 x1 = *(const f32x4 *)(a1 + j * 256), x2 = *(const f32x4 *)(a2 + j * 256),
-                    x3 = *(const f32x4 *)(a3 + j * 256);
+        const f32x4 x1 = *(const f32x4 *)(a1 + j * 256);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) wf1[4 * j + e] = x1[e], wf2[4 * j + e] = x2[e], wf3[4 * j + e] = x3[e];
+        for (int e = 0; e < 4; ++e) wf1[4 * j + e] = x1[e];
+      }
+      const float *a2 = fc2role ? p.w_fc2a + (size_t)(q0 + r2) * WR_F
+                                : p.w_fc3 + (size_t)(act23 ? q0 + r2 : 0) * WR_F;
+      a2 += kp2 * 32 + kl * 4;  // k = 128 j + 32 kp2 + 4 kl + e
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 x2 = *(const f32x4 *)(a2 + j * 128);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wf23[4 * j + e] = x2[e];
       }
     }
     const bool actm = s < FR;
@@ -732,17 +745,21 @@ __global__ __launch_bounds__(Geo<NI>::NT, 1) void wavernn_kernel(const WrParams 
 #pragma unroll
       for (int j = 0; j < 10; ++j) wmr[j] = am[8 * j];
     }
-    // cell thread (row cr, fold cb)
+    // cell threads: fc1 (row cr, fold cb); fc2 (row cr2, fold cb2)
     const bool cell = tid < FR * p.B;
     const int cr = tid % FR, cb = tid / FR;
+    const bool cell2 = fc2role && tid < FR2 * p.B;
+    const int cr2 = tid % FR2, cb2 = tid / FR2;
     const float vv1 = p.v1[r0 + cr];
     float rn = 0.f, sn = 0.f;
     auto fetch_cond = [&](int t) {
       if (cell) {
         const Pos ps = position(p, cb, t);
-        const float *crow = p.cond + (size_t)ps.cond_row * WR_COND;
-        rn = crow[6 * WR_R + r0 + cr];
-        sn = crow[6 * WR_R + WR_F + r0 + cr];
+        rn = p.cond[(size_t)ps.cond_row * WR_COND + 6 * WR_R + r0 + cr];
+      }
+      if (cell2) {
+        const Pos ps = position(p, cb2, t);
+        sn = p.cond[(size_t)ps.cond_row * WR_COND + 6 * WR_R + WR_F + q0 + cr2];
       }
     };
     MelPrefetch<NBV, NI> mp;
@@ -782,57 +799,60 @@ __global__ __launch_bounds__(Geo<NI>::NT, 1) void wavernn_kernel(const WrParams 
         const float pre = ((rc + sh.partm[cr][cb]) + vv1 * sh.sval[cb]) + acc;
         publish(p, 2, t, cb, r0 + cr, tagged(fmaxf(pre, 0.f), t));
       }
-      acquire_vec(p, sh, 2, t, false);  // y1
-      __syncthreads();
-      if (sh.abort_flag) return;
-      WR_STAMP(5);
-      matvec<2, 256>(wf2, sh.vec, kp * 32, kl, sh.part[1][s], true, p.B);
-      __syncthreads();
-      WR_STAMP(6);
-      if (cell) {
-        float acc = sh.part[1][cr * 8][cb];
+      if (fc2role) {
+        acquire_vec(p, sh, 2, t, false);  // y1
+        __syncthreads();
+        if (sh.abort_flag) return;
+        WR_STAMP(5);
+        matvec<4, 128>(wf23, sh.vec, kp2 * 32, kl, sh.part[1][s], true, p.B);
+        __syncthreads();
+        WR_STAMP(6);
+        if (cell2) {
+          float acc = sh.part[1][cr2 * 4][cb2];
 #pragma unroll
-        for (int i = 1; i < 8; ++i) acc += sh.part[1][cr * 8 + i][cb];
-        publish(p, 3, t, cb, r0 + cr, tagged(fmaxf(sc + acc, 0.f), t));
-      }
-      acquire_vec(p, sh, 3, t, false);  // y2
-      __syncthreads();
-      if (sh.abort_flag) return;
-      WR_STAMP(7);
-      matvec<2, 256>(wf3, sh.vec, kp * 32, kl, sh.part[2][s], act3, p.B);
-      __syncthreads();
-      WR_STAMP(8);
-      // ---- fc3 rows of this workgroup: logits and Gumbel scores (one thread per (row,
-      // fold): the Philox rounds and logs in parallel), then the draw's partial ----------
-      if (tid < NCR * p.B) {
-        const int rr = tid % NCR, b = tid / NCR, k = f * NCR + rr;
-        float z = -INFINITY;
-        if (k < p.NC) {
-          float l = sh.part[2][rr * 8][b];
-#pragma unroll
-          for (int i = 1; i < 8; ++i) l += sh.part[2][rr * 8 + i][b];
-          l = l + p.b_fc3[k];
-          if (p.logits) p.logits[((size_t)(p.fold0 + b) * p.L + t) * p.NC + k] = l;
-          if (p.mol) {
-            z = l;
-          } else {
-            const u32x4 w = philox((u32x4){(unsigned)t, (unsigned)(p.fold0 + b), (unsigned)(k >> 2), 0u},
-                                   p.k0, p.k1);
-            z = l - logf(-logf(u01(pword(w, k & 3))));
-          }
+          for (int i = 1; i < 4; ++i) acc += sh.part[1][cr2 * 4 + i][cb2];
+          publish(p, 3, t, cb2, q0 + cr2, tagged(fmaxf(sc + acc, 0.f), t));
         }
-        sh.partm[rr][b] = z;  // the mel partials of this step are consumed
-      }
-      __syncthreads();
-      if (tid < p.B && f * NCR < p.NC) {
-        float best = sh.partm[0][tid];
-        int bidx = f * NCR;
+      } else {
+        acquire_vec(p, sh, 3, t, false);  // y2
+        __syncthreads();
+        if (sh.abort_flag) return;
+        WR_STAMP(7);
+        matvec<4, 128>(wf23, sh.vec, kp2 * 32, kl, sh.part[2][s], act23, p.B);
+        __syncthreads();
+        WR_STAMP(8);
+        // ---- fc3 rows of this workgroup: logits and Gumbel scores (one thread per
+        // (row, fold): the Philox rounds and logs in parallel), then the draw's partial(s)
+        if (tid < FR2 * p.B) {
+          const int rr = tid % FR2, b = tid / FR2, k = q0 + rr;
+          float z = -INFINITY;
+          if (k < p.NC) {
+            float l = sh.part[2][rr * 4][b];
 #pragma unroll
-        for (int rr = 1; rr < NCR; ++rr)
-          if (sh.partm[rr][tid] > best) best = sh.partm[rr][tid], bidx = f * NCR + rr;
-        publish_z(p, t, tid, f, best, bidx);
+            for (int i = 1; i < 4; ++i) l += sh.part[2][rr * 4 + i][b];
+            l = l + p.b_fc3[k];
+            if (p.logits) p.logits[((size_t)(p.fold0 + b) * p.L + t) * p.NC + k] = l;
+            if (p.mol) {
+              publish_z(p, t, b, k, l, k);  // MOL: every logit is a granule of its own
+            } else {
+              const u32x4 w = philox((u32x4){(unsigned)t, (unsigned)(p.fold0 + b), (unsigned)(k >> 2), 0u},
+                                     p.k0, p.k1);
+              z = l - logf(-logf(u01(pword(w, k & 3))));
+            }
+          }
+          sh.partm[rr][b] = z;  // the mel partials of this step are consumed
+        }
+        __syncthreads();
+        if (!p.mol && tid < p.B) {  // RAW: the best (score, class) of these rows
+          float best = sh.partm[0][tid];
+          int bidx = q0;
+#pragma unroll
+          for (int rr = 1; rr < FR2; ++rr)
+            if (sh.partm[rr][tid] > best) best = sh.partm[rr][tid], bidx = q0 + rr;
+          publish_z(p, t, tid, f - HF, best, bidx);
+        }
+        WR_STAMP(9);
       }
-      WR_STAMP(9);
     }
   }
   if (stamping) {
@@ -951,9 +971,9 @@ extern "C" int ftmi_wavernn(const ftmi_wavernn_args *a, ftmi_stream_t stream) {
     return FTMI_E_ARG;
   if (a->rnn_dims != WR_R || a->fc_dims != WR_F || a->feat_dims != WR_NM || a->aux_dims != WR_NA)
     return FTMI_E_UNSUPPORTED;
-  // RAW: 2^bits classes spread over all 128 FC workgroups (1..4 rows each): bits 7..9
+  // RAW: 2^bits <= 512 classes (the fc3 rows of the FC workgroups' fc3 half)
   if (a->mol ? a->n_classes != 30
-             : (a->n_classes < WR_NF || a->n_classes > 4 * WR_NF || (a->n_classes & (a->n_classes - 1)) != 0))
+             : (a->n_classes < 2 || a->n_classes > WR_F || (a->n_classes & (a->n_classes - 1)) != 0))
     return FTMI_E_UNSUPPORTED;
   if (a->xin ? !a->logits : !a->samples) return FTMI_E_ARG;
   if (a->batched && a->fold_stride <= 0) return FTMI_E_ARG;
@@ -994,41 +1014,18 @@ extern "C" int ftmi_wavernn(const ftmi_wavernn_args *a, ftmi_stream_t stream) {
     }();
     const int ni = (p.B >= 2 && ni_env != 1) ? 2 : 1;
     const int bi = (p.B + ni - 1) / ni;
-    const int ncr = a->mol ? 1 : a->n_classes / (WR_GRID / ni / 2);
     hipError_t e = hipMemsetAsync(a->workspace, 0, (size_t)ftmi_wavernn_workspace_bytes(), s);
     if (e != hipSuccess) return (int)e;
-#define FTMI_WR_LAUNCH(NBV_, NCR_, NI_)                                                  \
-  hipLaunchKernelGGL((wavernn_kernel<NBV_, NCR_, NI_>), dim3(WR_GRID), dim3(WR_NT * NI_), 0, s, p)
+#define FTMI_WR_LAUNCH(NBV_, NI_)                                                         \
+  hipLaunchKernelGGL((wavernn_kernel<NBV_, NI_>), dim3(WR_GRID), dim3(WR_NT * NI_), 0, s, p)
     if (ni == 1) {
       p.B = p.B < WR_NBMAX ? p.B : WR_NBMAX;  // one instance: <= 32 folds per launch
-#define FTMI_WR_NCR1(NBV_)                         \
-  switch (ncr) {                                   \
-    case 1: FTMI_WR_LAUNCH(NBV_, 1, 1); break;     \
-    case 2: FTMI_WR_LAUNCH(NBV_, 2, 1); break;     \
-    default: FTMI_WR_LAUNCH(NBV_, 4, 1); break;    \
-  }
-      if (p.B <= 8) {
-        FTMI_WR_NCR1(8)
-      } else if (p.B <= 16) {
-        FTMI_WR_NCR1(16)
-      } else {
-        FTMI_WR_NCR1(32)
-      }
-#undef FTMI_WR_NCR1
+      if (p.B <= 8) FTMI_WR_LAUNCH(8, 1);
+      else if (p.B <= 16) FTMI_WR_LAUNCH(16, 1);
+      else FTMI_WR_LAUNCH(32, 1);
     } else {
-#define FTMI_WR_NCR(NBV_)                          \
-  switch (ncr) {                                   \
-    case 1: FTMI_WR_LAUNCH(NBV_, 1, 2); break;     \
-    case 2: FTMI_WR_LAUNCH(NBV_, 2, 2); break;     \
-    case 4: FTMI_WR_LAUNCH(NBV_, 4, 2); break;     \
-    default: FTMI_WR_LAUNCH(NBV_, 8, 2); break;    \
-  }
-      if (bi <= 8) {
-        FTMI_WR_NCR(8)
-      } else {
-        FTMI_WR_NCR(16)
-      }
-#undef FTMI_WR_NCR
+      if (bi <= 8) FTMI_WR_LAUNCH(8, 2);
+      else FTMI_WR_LAUNCH(16, 2);
     }
 #undef FTMI_WR_LAUNCH
     FTMI_CHECK_LAUNCH();
