@@ -13,6 +13,10 @@ them); `valid_frames_per_s` counts only each utterance's own frames.
   --config c2            configs[1]: batch 1, 120 phonemes
   --callbacks gen_forward  the callbacks gen_forward.py:103-104 passes
                          (pitch_function = lambda x: x * amp, energy_function = lambda x: x)
+  --vocoder griffinlim   configs[1] names the Griffin-Lim vocoder: a THIRD timed loop runs the
+                         whole gen_forward.py sentence step (generate, mel_post.cpu(),
+                         dsp.griffinlim -> numpy wav, :115-134) and reports it beside `value`
+                         as `with_vocoder` (batch > 1: DSP.griffinlim_batch on the device)
   --model fast_pitch     configs[4], "c5": FastPitch, batch 64, lengths U{50..200}
   --model wavernn        the `gen_forward.py wavernn` vocoder (no BASELINE
                          number): WaveRNN.generate of one c2-length mel (821 frames, synthetic
@@ -131,6 +135,8 @@ def main():
                     help='gen_forward: pitch_function = lambda x: x * amp, energy_function = '
                          'lambda x: x, as gen_forward.py:103-104 passes them')
     ap.add_argument('--amp', type=float, default=1.0, help='gen_forward.py --amp')
+    ap.add_argument('--vocoder', choices=['none', 'griffinlim'], default='none',
+                    help='griffinlim: also time generate + Griffin-Lim per step (gen_forward.py)')
     ap.add_argument('--no-host-loop', action='store_true',
                     help='skip the second (host-to-host, PCIe-inclusive) timed loop')
     args = ap.parse_args()
@@ -213,6 +219,34 @@ def main():
         torch.cuda.synchronize()
         barrier()
         host_elapsed = time.perf_counter() - h0
+    # Third loop (--vocoder griffinlim): the whole gen_forward.py sentence step — generate,
+    # mel_post.cpu(), DSP.griffinlim (HIP NNLS + 32 fast-GL iterations) -> numpy wav.
+    voc = None
+    if args.vocoder == 'griffinlim' and world == 1:
+        from forwardtacotron_amd.dsp import DSP
+        dsp = DSP.from_config(default_config())
+
+        def vstep():
+            o = gen(x_host.to(dev))
+            m = o['mel_post']
+            if m.size(0) == 1:
+                return dsp.griffinlim(m.cpu().squeeze(0).numpy()).shape[0]
+            w, n = dsp.griffinlim_batch(m)
+            w.cpu()
+            return int(n.sum().item()) if torch.is_tensor(n) else int(np.sum(n))
+        vstep()
+        torch.cuda.synchronize()
+        v0 = time.perf_counter()
+        nsamp = 0
+        for _ in range(args.steps):
+            nsamp += vstep()
+        torch.cuda.synchronize()
+        velapsed = time.perf_counter() - v0
+        voc = {'name': 'griffinlim', 'ms_per_step': round(velapsed / args.steps * 1e3, 3),
+               'mel_frames_per_s': round(frames / velapsed, 1),
+               'audio_samples_per_s': round(nsamp / velapsed, 1),
+               'what': 'generate() + mel_post D2H + DSP.griffinlim (numpy wav out) per step, '
+                       'as gen_forward.py:115-134 with the griffinlim vocoder'}
     # The timed steps replay the phoneme phase as a HIP graph (forward_tacotron.GRAPH), whose
     # kernels the per-launch probe cannot see: one more generate() with the phase eager,
     # after the timed region, gives their per-kernel times (the prenet bank, --kernels).
@@ -332,6 +366,8 @@ def main():
                                            'energy_function = lambda x: x')
         if prenet is not None:
             line['prenet_bank'] = prenet
+        if voc is not None:
+            line['with_vocoder'] = voc
         if world == 1 and not args.no_cpu_baseline:
             line['cpu_baseline'], line['parity'] = cpu_baseline(sd, x_np, out, args.model,
                                                                 cb_kind=args.callbacks, amp=args.amp)
