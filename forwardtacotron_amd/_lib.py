@@ -97,6 +97,7 @@ SIGNATURES = {
     'ftmi_griffinlim_stft': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P,
                                      P, P, c_float, c_int, P, P]),
     'ftmi_spec_mul': (c_int, [P, P, c_int64, P, P]),
+    'ftmi_unit_phases': (c_int, [P, c_int, c_int, c_int, P, P]),
     'ftmi_istft_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
     'ftmi_istft': (c_int, [P, c_int, c_int, P, c_int, c_int, P, P, P, P, P, c_int64, c_int64, P]),
     'ftmi_wr_stretch_conv': (c_int, [P, c_int64, c_int, c_int, c_int, c_int, P, P, c_int64, c_int,

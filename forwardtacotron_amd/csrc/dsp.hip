@@ -479,3 +479,31 @@ extern "C" int ftmi_spec_mul(const float *S, const void *angles, int64_t n, void
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
 }
+
+namespace {
+// librosa 0.7.2 griffinlim's initial phases, np.exp(2j * np.pi * u) with u = np.random.rand
+// (n_bins, T): float64 cos / sin of 6.283185307179586 * u (the imaginary part numpy forms),
+// rounded to complex64, written frame-major (B, T, n_bins) from the bin-major draws
+__global__ void unit_phase_kernel(const double *__restrict__ u, int32_t nb, int32_t T,
+                                  int64_t n, float2 *__restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bt = i / nb;            // (item, frame)
+    const int k = (int)(i - bt * nb);
+    const int64_t b = bt / T, t = bt - b * T;
+    const double y = 6.283185307179586 * u[(b * nb + k) * T + t];
+    out[i] = make_float2((float)cos(y), (float)sin(y));
+  }
+}
+}  // namespace
+
+extern "C" int ftmi_unit_phases(const double *u, int32_t B, int32_t n_bins, int32_t T,
+                                void *angles, ftmi_stream_t stream) {
+  if (!u || !angles || B <= 0 || n_bins <= 0 || T <= 0) return FTMI_E_ARG;
+  const int64_t n = (int64_t)B * n_bins * T;
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(unit_phase_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                     ftmi_hs(stream), u, n_bins, T, n, (float2 *)angles);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}

@@ -206,8 +206,15 @@ def mel_to_stft(plan: DspPlan, mel: torch.Tensor, frames: Optional[torch.Tensor]
 def griffinlim_from_stft(plan: DspPlan, S: torch.Tensor, angles: torch.Tensor, n_iter: int = 32,
                          frames: Optional[torch.Tensor] = None, momentum: float = 0.99) -> torch.Tensor:
     """librosa core.griffinlim (0.7.2 fast GL) of magnitudes S (B, F, nb) from initial unit
-    phases `angles` (B, F, nb) complex64 -> audio rows (B, hop*(F-1))."""
+    phases `angles` (B, F, nb) complex64 -> audio rows (B, hop*(F-1)).  (A HIP-graph replay of
+    this loop measured no faster at batch 1 — 5.98 vs 5.65 ms per gen_forward sentence step:
+    the kernels, not the launches, set the pace — so it stays eager.)"""
     _need_cuda(S, angles, frames)
+    return _gl_loop(plan, S, angles, n_iter, frames, momentum)
+
+
+def _gl_loop(plan: DspPlan, S: torch.Tensor, angles: torch.Tensor, n_iter: int,
+             frames: Optional[torch.Tensor], momentum: float) -> torch.Tensor:
     B, F, nb = S.shape
     dev = S.device
     X = torch.empty(B, F, nb, dtype=torch.complex64, device=dev)
@@ -327,11 +334,18 @@ class DSP:
         plan = self.plan(m.device)
         T = m.shape[-1]
         if angles is None:
+            # the reference's draw (librosa: np.random.rand(n_bins, T)); exp(2 pi i u) and the
+            # frame-major layout on the device (ftmi_unit_phases: the host exp of 420 k
+            # complex values took longer than the whole Griffin-Lim on the GPU)
             rng = np.random if random_state is None else np.random.RandomState(random_state)
-            angles = np.exp(2j * np.pi * rng.rand(plan.nb, T)).astype(np.complex64)
-        a = angles if isinstance(angles, torch.Tensor) else torch.from_numpy(
-            np.ascontiguousarray(np.asarray(angles, dtype=np.complex64).T))
-        a = a.to(m.device).reshape(1, T, plan.nb).contiguous()
+            u = torch.from_numpy(rng.rand(plan.nb, T)).to(m.device)
+            a = torch.empty(1, T, plan.nb, dtype=torch.complex64, device=m.device)
+            launch('ftmi_unit_phases', f'unit_phases[T={T}]', 0, 16.0 * plan.nb * T,
+                   u.data_ptr(), 1, plan.nb, T, a.data_ptr(), _stream())
+        else:
+            a = angles if isinstance(angles, torch.Tensor) else torch.from_numpy(
+                np.ascontiguousarray(np.asarray(angles, dtype=np.complex64).T))
+            a = a.to(m.device).reshape(1, T, plan.nb).contiguous()
         S = mel_to_stft(plan, m.float().reshape(1, plan.n_mels, T).contiguous(), iters=self.nnls_iters)
         wav = griffinlim_from_stft(plan, S, a, n_iter)[0]
         return wav if is_t else wav.cpu().numpy()
@@ -346,8 +360,10 @@ class DSP:
         plan = self.plan(mel.device)
         B, _, F = mel.shape
         fr = None if frames is None else frames.to(device=mel.device, dtype=torch.int32)
-        u = torch.rand(B, F, plan.nb, dtype=torch.float64, device=mel.device, generator=generator)
-        angles = torch.polar(torch.ones_like(u), 2 * np.pi * u).to(torch.complex64)
+        u = torch.rand(B, plan.nb, F, dtype=torch.float64, device=mel.device, generator=generator)
+        angles = torch.empty(B, F, plan.nb, dtype=torch.complex64, device=mel.device)
+        launch('ftmi_unit_phases', f'unit_phases[B={B},T={F}]', 0, 16.0 * B * plan.nb * F,
+               u.data_ptr(), B, plan.nb, F, angles.data_ptr(), _stream())
         S = mel_to_stft(plan, mel.float().contiguous(), fr, iters=self.nnls_iters)
         wav = griffinlim_from_stft(plan, S, angles, n_iter, fr)
         n = plan.hop * ((fr if fr is not None else torch.full((B,), F, device=mel.device)) - 1)

@@ -392,6 +392,13 @@ int ftmi_griffinlim_stft(const float *y, int64_t y_stride, int32_t B, int64_t L,
  * Griffin-Lim synthesis input for the initial phases.  n = number of bins in total. */
 int ftmi_spec_mul(const float *S, const void *angles, int64_t n, void *X, ftmi_stream_t stream);
 
+/* Griffin-Lim's random initial phases (librosa 0.7.2 core.griffinlim:
+ * np.exp(2j * np.pi * np.random.rand(n_bins, T))) from the host's uniform draws u (B, n_bins,
+ * T) float64, bin-major as numpy draws them: angles (B, T, n_bins) complex64, frame-major
+ * (float64 cos / sin, rounded to complex64).  ABI 11. */
+int ftmi_unit_phases(const double *u, int32_t B, int32_t n_bins, int32_t T, void *angles,
+                     ftmi_stream_t stream);
+
 /* librosa core.istft (center=True): per-frame fp64 irfft * window, overlap-added in frame
  * order with float32 rounding, divided by the window sum-square where > FLT_MIN, cropped
  * by n_fft/2.  Item b yields hop * (frames_b - 1) samples into y[b, :], zero-filled up to

@@ -140,3 +140,22 @@ def test_cpu_tensor_raises(dsp):
     from forwardtacotron_amd import dsp as G
     with pytest.raises(RuntimeError):
         G.mel_spectrogram(dsp.plan(), torch.zeros(1, 4000))
+
+
+def test_unit_phases_match_numpy_draw(dsp):
+    """ftmi_unit_phases == librosa's np.exp(2j * np.pi * u) rounded to complex64, transposed to
+    frame-major; and DSP.griffinlim(random_state=k) == griffinlim(angles=those phases)."""
+    from forwardtacotron_amd import _lib
+    plan = dsp.plan()
+    T = REF_MEL.shape[1]
+    u = np.random.RandomState(3).rand(plan.nb, T)
+    ref = np.exp(2j * np.pi * u).astype(np.complex64).T
+    a = torch.empty(1, T, plan.nb, dtype=torch.complex64, device='cuda')
+    ut = torch.from_numpy(u).cuda()
+    assert _lib.load().ftmi_unit_phases(ut.data_ptr(), 1, plan.nb, T, a.data_ptr(),
+                                        torch.cuda.current_stream().cuda_stream) == 0
+    np.testing.assert_array_equal(a[0].cpu().numpy(), ref)
+    w1 = dsp.griffinlim(REF_MEL, random_state=3)
+    w2 = dsp.griffinlim(REF_MEL, angles=np.exp(2j * np.pi * np.random.RandomState(3).rand(plan.nb, T)))
+    np.testing.assert_array_equal(w1, w2)
+
