@@ -252,8 +252,9 @@ class WaveRNN(Packed):
             a.samples = out.data_ptr()
         R, F = self.rnn_dims, self.fc_dims
         per_step = 2.0 * (3 * R * R * 3 + F * R + F * F + self.n_classes * F + (6 * R + F) * self.feat_dims)
+        # cond / ws / xin / m_up are freed on return: the caching allocator hands their blocks
+        # to later allocations of this stream only, which run after the kernel (stream order)
         ops.wavernn(a, B, L, per_step * B * L, dev)
-        keep = (cond, ws, rec, xin, m_up)  # noqa: F841  (alive until the launch is enqueued)
         return out
 
     def forward(self, x: torch.Tensor, mels: torch.Tensor) -> torch.Tensor:
