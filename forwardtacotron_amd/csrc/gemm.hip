@@ -1642,6 +1642,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
   const int kw = GW.k, padw = GW.pad, dp = pad - padw;  // slab row offset of this group's taps
   const int nsteps = nch * kw, hs = (nsteps + 1) / 2;
   const int s_begin = half ? hs : 0, s_end = half ? nsteps : hs;
+  // the epilogue's per-column parameters, requested now: their latency hides under the
+  // weight stream instead of opening the tail
+  const int ecol = col0 + fr < GW.N ? col0 + fr : GW.N - 1;
+  const bool fin = !half && col0 < GW.N;
+  const bool direct = !(p.split > 1 || p.force_part);
+  const float e_cs = fin ? GW.colscale[ecol] : 1.f;
+  const float e_bias = fin && direct && GW.bias ? GW.bias[ecol] : 0.f;
+  const float e_sc = fin && direct && GW.scale ? GW.scale[ecol] : 1.f;
+  const float e_sh = fin && direct && GW.scale ? GW.shift[ecol] : 0.f;
   f32x4 acc[8];
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) acc[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -1728,8 +1737,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     // lane (fr, fs) holds rows mi*16 + 4 fs + i of column col0 + fr
     const int col = col0 + fr;
     const bool cok = col < GW.N;
-    const float cs = GW.colscale[cok ? col : GW.N - 1];
-    if (p.split > 1 || p.force_part) {
+    const float cs = e_cs;
+    if (!direct) {
       float *part = p.part + (size_t)blockIdx.y * p.M * p.ldp + GW.ycol0;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
@@ -1742,9 +1751,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
           }
         }
     } else {
-      const float bias = GW.bias && cok ? GW.bias[col] : 0.f;
-      const float sc = GW.scale && cok ? GW.scale[col] : 1.f;
-      const float sh = GW.scale && cok ? GW.shift[col] : 0.f;
+      const float bias = e_bias, sc = e_sc, sh = e_sh;  // (unused for !cok columns)
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -1782,8 +1789,27 @@ __global__ __launch_bounds__(256) void skinny_finish_kernel(const GemmParams p) 
        idx += (int64_t)gridDim.x * (256 / L)) {  // the L lanes of an element iterate together
     const int row = (int)(idx / N), col = (int)(idx - (int64_t)row * N);
     const int64_t pi = (int64_t)row * p.ldp + G.ycol0 + col;
+    // eight / four splits' loads issued together, added in split order (the same sums as
+    // one by one)
     float v = 0.f;
-    for (int s = q; s < p.split; s += L) v += p.part[(size_t)s * total + pi];
+    int s = q;
+    for (; s + 7 * L < p.split; s += 8 * L) {
+      float a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = p.part[(size_t)(s + u * L) * total + pi];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += a[u];
+    }
+    for (; s + 3 * L < p.split; s += 4 * L) {
+      const float a0 = p.part[(size_t)s * total + pi], a1 = p.part[(size_t)(s + L) * total + pi];
+      const float a2 = p.part[(size_t)(s + 2 * L) * total + pi];
+      const float a3 = p.part[(size_t)(s + 3 * L) * total + pi];
+      v += a0;
+      v += a1;
+      v += a2;
+      v += a3;
+    }
+    for (; s < p.split; s += L) v += p.part[(size_t)s * total + pi];
     if constexpr (L == 4) {
       v += __shfl_xor(v, 1, 4);
       v += __shfl_xor(v, 2, 4);
@@ -1813,7 +1839,17 @@ __global__ __launch_bounds__(256) void skinny_highway_finish_kernel(const GemmPa
     const int c1 = (o >> 5) * 64 + (o & 31);
     const int64_t pi = (int64_t)row * p.ldp + c1;
     float v1 = 0.f, v2 = 0.f;
-    for (int s = 0; s < p.split; ++s) {
+    int s = 0;
+    for (; s + 1 < p.split; s += 2) {  // two splits' loads together, added in split order
+      const float a0 = p.part[(size_t)s * total + pi], b0 = p.part[(size_t)s * total + pi + 32];
+      const float a1 = p.part[(size_t)(s + 1) * total + pi];
+      const float b1 = p.part[(size_t)(s + 1) * total + pi + 32];
+      v1 += a0;
+      v2 += b0;
+      v1 += a1;
+      v2 += b1;
+    }
+    for (; s < p.split; ++s) {
       v1 += p.part[(size_t)s * total + pi];
       v2 += p.part[(size_t)s * total + pi + 32];
     }
