@@ -76,6 +76,10 @@ def wsplit(w, pre, mma=1):
     (2, 9, 32, 64, 16, True, False, False),     # slab kernel: k = 16 > T, every tap masked
     (4, 70, 64, 1536, 1, False, False, True),   # slab kernel, k = 1, many column tiles
     (1, 816, 1024, 80, 1, False, False, True),  # c2 lin: narrow linear, 816 rows (skinny)
+    # skinny finish: split counts that leave remainders after its 4- / 8-split load batches
+    (1, 40, 416, 64, 3, True, True, True),      # 7 splits (one lane per element: 4 + 3)
+    (1, 33, 1280, 96, 1, False, False, True),   # 20 splits (4 lanes per element: 4 + 1)
+    (1, 25, 2304, 128, 1, True, False, True),   # 36 splits (4 lanes per element: 8 + 1)
 ])
 @pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
 def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre, kernel, monkeypatch):
@@ -274,7 +278,8 @@ def test_conv_bank_skinny_schedules(K, Cin, B, T, balanced, rng, monkeypatch):
 
 @MMAS
 @pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
-@pytest.mark.parametrize('C,B,T', [(256, 3, 77), (128, 2, 300), (256, 1, 816)])
+@pytest.mark.parametrize('C,B,T', [(256, 3, 77), (128, 2, 300), (256, 1, 816),
+                                   (160, 1, 90)])  # skinny: 3 splits (2 + 1 in the finish)
 def test_highway(rng, mma, pre, kernel, C, B, T, monkeypatch):
     from forwardtacotron_amd.common_layers import HighwayNetwork
     slab_or_skip(kernel, mma, monkeypatch)
