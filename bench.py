@@ -82,7 +82,7 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 
 PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r2_pmc_traffic.json')        # c3
-PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r1c2_pmc_traffic.json')   # c2 (--config c2)
+PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r2c2_pmc_traffic.json')   # c2 (--config c2)
 
 
 def rocprof_name(label: str):
@@ -90,7 +90,11 @@ def rocprof_name(label: str):
     if label.startswith('rnn_bidir['):
         cell = 1 if label.startswith('rnn_bidir[lstm') else 0
         H = int(label.split('H=')[1].split(',')[0].rstrip(']'))
-        return f'rnn_bidir_kernel<{cell}, {H},'
+        B = int(label.split('B=')[1].split(',')[0])
+        # rnn.hip gemv_path: B <= 4 runs the exact-fp32 GEMV recurrence for these shapes
+        gemv = (os.environ.get('FTMI_RNN_GEMV', '1') != '0' and B <= 4
+                and ((cell == 1 and H == 512) or (cell == 0 and H in (64, 128, 256))))
+        return f'rnn_gemv_kernel<{cell}, {H},' if gemv else f'rnn_bidir_kernel<{cell}, {H},'
     return None
 
 
@@ -282,7 +286,11 @@ def main():
         s = dom['avg_ms'] / 1e3
         if dom['flops'] > 0:
             achieved = dom['flops'] / s / 1e12
-            if 'mma=2' in dom_label:
+            if (rocprof_name(dom_label) or '').startswith('rnn_gemv_kernel'):
+                peak, basis = PEAK_FP32_TFLOPS, ('fp32: at B <= 4 the recurrence is the exact-fp32 '
+                                                 'GEMV kernel (VALU FMAs; rnn.hip gemv_path), '
+                                                 'whatever mma the label requests')
+            elif 'mma=2' in dom_label:
                 peak, basis = PEAK_X3_TFLOPS, ('f16 dense MFMA 2.5 PF / 3 (fp32-level f16x3 split: 3 '
                                                'f16 products per fp32 product)')
             elif 'mma=1' in dom_label:

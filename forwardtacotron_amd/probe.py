@@ -38,7 +38,14 @@ class KernelProbe:
         """After a device sync: {label: dict(entry, launches, avg_ms, total_ms, flops, bytes)}."""
         out = OrderedDict()
         for label, evs in self.events.items():
-            ms = [s.elapsed_time(e) for s, e in evs]
+            ms = []
+            for s, e in evs:
+                try:
+                    ms.append(s.elapsed_time(e))
+                except RuntimeError:  # under rocprofv3 --pmc (serialised dispatch) some
+                    pass              # event pairs report no time: the run is for counters
+            if not ms:
+                continue
             name, flops, nbytes = self.meta[label]
             out[label] = {'entry': name, 'launches': len(ms), 'total_ms': sum(ms),
                           'avg_ms': sum(ms) / len(ms), 'flops': flops, 'bytes': nbytes}
