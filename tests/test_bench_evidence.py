@@ -1,0 +1,25 @@
+"""bench.py's roofline evidence lookup (CPU): each config's dominant recurrence maps to the
+kernel that actually runs (B <= 4: the exact-fp32 GEMV recurrence, rnn.hip gemv_path), and
+the committed PMC summaries hold exactly one such kernel."""
+import bench
+
+
+def test_rocprof_name_follows_the_gemv_rule(monkeypatch):
+    monkeypatch.delenv('FTMI_RNN_GEMV', raising=False)
+    assert bench.rocprof_name('rnn_bidir[lstm,B=1,T=816,H=512,mma=2]') == 'rnn_gemv_kernel<1, 512,'
+    assert bench.rocprof_name('rnn_bidir[gru,B=4,T=816,H=256,mma=2]') == 'rnn_gemv_kernel<0, 256,'
+    assert bench.rocprof_name('rnn_bidir[lstm,B=64,T=1368,H=512,mma=2]') == 'rnn_bidir_kernel<1, 512,'
+    assert bench.rocprof_name('rnn_bidir[gru,B=1,T=816,H=32,mma=2]') == 'rnn_bidir_kernel<0, 32,'
+    monkeypatch.setenv('FTMI_RNN_GEMV', '0')
+    assert bench.rocprof_name('rnn_bidir[lstm,B=1,T=816,H=512,mma=2]') == 'rnn_bidir_kernel<1, 512,'
+    assert bench.rocprof_name('conv1d[M=12800,N=256,K=1280,mma=2]') is None
+
+
+def test_committed_traffic_covers_the_dominant_kernels(monkeypatch):
+    monkeypatch.delenv('FTMI_RNN_GEMV', raising=False)
+    c3 = bench.pmc_traffic('rnn_bidir[lstm,B=64,T=1368,H=512,mma=2]', bench.PMC_PROFILE)
+    c2 = bench.pmc_traffic('rnn_bidir[lstm,B=1,T=816,H=512,mma=2]', bench.PMC_PROFILE_C2)
+    for t in (c3, c2):
+        assert t is not None and t['bytes_per_launch'] > 0
+    # c2: W_hh (8.4 MB) + phoneme-rate projections + y: no re-read of the weights per step
+    assert c2['bytes_per_launch'] < 2 * 8.4e6
