@@ -94,7 +94,13 @@ def rocprof_name(label: str):
         # rnn.hip gemv_path: B <= 4 runs the exact-fp32 GEMV recurrence for these shapes
         gemv = (os.environ.get('FTMI_RNN_GEMV', '1') != '0' and B <= 4
                 and ((cell == 1 and H == 512) or (cell == 0 and H in (64, 128, 256))))
-        return f'rnn_gemv_kernel<{cell}, {H},' if gemv else f'rnn_bidir_kernel<{cell}, {H},'
+        if gemv:
+            return f'rnn_gemv_kernel<{cell}, {H},'
+        # rnn.hip row_path: FTMI_RNN_ROW=1 runs the f16x3 recurrences of H 128 / 256 / 512
+        # on rnn_row_kernel
+        row = (os.environ.get('FTMI_RNN_ROW', '0') != '0' and 'mma=2' in label
+               and ((cell == 1 and H == 512) or (cell == 0 and H in (128, 256))))
+        return f'rnn_row_kernel<{cell}, {H},' if row else f'rnn_bidir_kernel<{cell}, {H},'
     return None
 
 
@@ -177,7 +183,9 @@ def main():
 
     if args.callbacks == 'gen_forward':  # gen_forward.py:103-104 (same objects every call)
         amp = args.amp
-        cb = dict(pitch_function=lambda v: v * amp, energy_function=lambda v: v)
+        # pure for the run's fixed amp: graph_safe, as the CLI marks them
+        cb = dict(pitch_function=ft_module.graph_safe(lambda v: v * amp),
+                  energy_function=ft_module.graph_safe(lambda v: v))
     else:
         cb = {}
     if world > 1:  # c4: one global batch sharded over the ranks (reference-identical result),
@@ -211,9 +219,29 @@ def main():
     kern = probe.summary()
 
     # Second loop, PCIe-inclusive, as gen_forward.py:111-120 runs a call: token ids H2D,
-    # generate(), mel_post D2H (.cpu()).  Reported beside `value`, never as it.
-    host_elapsed = None
+    # generate(), mel_post D2H — through pinned buffers, the D2H stream-ordered on a side
+    # stream (host_io.PinnedD2H) so it overlaps the next call's phoneme phase; every result
+    # is on the host when the loop's clock stops.  Reported beside `value`, never as it.
+    # A third loop times the serial form (pageable .cpu() per call, gen_forward.py:120).
+    host_elapsed = host_serial = None
     if not args.no_host_loop:
+        from forwardtacotron_amd.host_io import PinnedD2H
+        d2h = PinnedD2H(dev)
+        x_pin = x_host.pin_memory()
+        o = gen(x_pin.to(dev, non_blocking=True))  # the pinned ring's buffers, untimed
+        if o is not None:
+            d2h.submit(o['mel_post'])
+        d2h.synchronize()
+        barrier()
+        h0 = time.perf_counter()
+        for _ in range(args.steps):
+            o = gen(x_pin.to(dev, non_blocking=True))
+            if o is not None:
+                d2h.submit(o['mel_post'])
+        d2h.synchronize()
+        torch.cuda.synchronize()
+        barrier()
+        host_elapsed = time.perf_counter() - h0
         barrier()
         h0 = time.perf_counter()
         for _ in range(args.steps):
@@ -222,7 +250,7 @@ def main():
                 o['mel_post'].cpu()
         torch.cuda.synchronize()
         barrier()
-        host_elapsed = time.perf_counter() - h0
+        host_serial = time.perf_counter() - h0
     # Third loop (--vocoder griffinlim): the whole gen_forward.py sentence step — generate,
     # mel_post.cpu(), DSP.griffinlim (HIP NNLS + 32 fast-GL iterations) -> numpy wav.
     voc = None
@@ -265,10 +293,12 @@ def main():
         kern_all = probe_eager.summary()
 
     if world > 1:
-        t = torch.tensor([elapsed, host_elapsed or 0.0], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, host_elapsed or 0.0, host_serial or 0.0], device=dev,
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0].item())
         host_elapsed = float(t[1].item()) if host_elapsed is not None else None
+        host_serial = float(t[2].item()) if host_serial is not None else None
 
     if rank == 0:
         # dominant kernel = largest device time inside the timed region
@@ -367,8 +397,15 @@ def main():
             line['host_to_host'] = {
                 'value': round(frames / host_elapsed, 1), 'unit': 'mel-frames/s',
                 'ms_per_step': round(host_elapsed / args.steps * 1e3, 3),
-                'what': 'token ids H2D + generate() + mel_post D2H per step, as gen_forward.py:111-120 '
-                        '(PCIe-inclusive; `value` has the tokens resident in HBM)'}
+                'vs_value': round(elapsed / host_elapsed, 4),
+                'what': 'token ids H2D (pinned) + generate() + mel_post D2H per step into pinned '
+                        'host buffers, the D2H stream-ordered on a side stream and overlapping the '
+                        'next call (host_io.PinnedD2H); all results on the host at the clock stop '
+                        '(PCIe-inclusive; `value` has the tokens resident in HBM)',
+                'serial': {'value': round(frames / host_serial, 1),
+                           'ms_per_step': round(host_serial / args.steps * 1e3, 3),
+                           'what': 'pageable x.to(dev) + generate() + mel_post.cpu() per call, '
+                                   'serialised as gen_forward.py:111-120 writes it'}}
         if args.callbacks != 'identity':
             line['config']['callbacks'] = (f'gen_forward.py:103-104: pitch_function = lambda x: x * {args.amp}, '
                                            'energy_function = lambda x: x')
@@ -473,7 +510,7 @@ def cpu_baseline_wavernn(sd, cfg, mels_np, target, overlap, B, L, samples, steps
     sdt = wr.to_torch(sd)
     vcfg = dict(cfg['vocoder']['model'])
     info = _cpu_info()
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    torch.set_num_threads(baseline_threads())
     threads = torch.get_num_threads()
     torch.manual_seed(0)
     t0 = time.perf_counter()
@@ -511,6 +548,27 @@ def _cpu_info():
     return model, phys
 
 
+def _usable_cpus():
+    """CPUs this process may run on: its affinity mask, capped by a cgroup CPU quota (the
+    GPU box grants a share of the host: os.cpu_count() shows the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            quota, period = f.read().split()[:2]
+        if quota != 'max':
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def baseline_threads():
+    """BASELINE.md:48: torch.set_num_threads(<physical cores>) — capped by the CPUs the
+    process is actually granted (oversubscribing a quota only slows the baseline down)."""
+    _, phys = _cpu_info()
+    return max(1, min(phys or 1, _usable_cpus()))
+
+
 def cpu_baseline(sd, x_np, out, kind='forward_tacotron', cb_kind='identity', amp=1.0):
     """Time the torch-CPU restatement of the reference on the same batch (bounded: one call
     at the process's thread count), plus a 1-thread figure on a bounded sample of it."""
@@ -521,10 +579,14 @@ def cpu_baseline(sd, x_np, out, kind='forward_tacotron', cb_kind='identity', amp
         from oracle import ft_torch_cpu
     cb = {}
     if cb_kind == 'gen_forward':
-        cb = dict(pitch_function=lambda v: v * amp, energy_function=lambda v: v)
+        # pure for the run's fixed amp: graph_safe, as the CLI marks them
+        cb = dict(pitch_function=ft_module.graph_safe(lambda v: v * amp),
+                  energy_function=ft_module.graph_safe(lambda v: v))
     sdt = ft_torch_cpu.to_torch(sd)
     xt = torch.from_numpy(x_np)
-    threads = torch.get_num_threads()
+    threads_before = torch.get_num_threads()
+    threads = baseline_threads()
+    torch.set_num_threads(threads)
     ft_torch_cpu.generate(sdt, xt[:1, :20])  # warm the CPU kernels
     t0 = time.perf_counter()
     ref = ft_torch_cpu.generate(sdt, xt, **cb)
@@ -539,7 +601,7 @@ def cpu_baseline(sd, x_np, out, kind='forward_tacotron', cb_kind='identity', amp
         r1 = ft_torch_cpu.generate(sdt, x1, **cb)
         dt1 = time.perf_counter() - t0
     finally:
-        torch.set_num_threads(threads)
+        torch.set_num_threads(threads_before)
     f1 = r1['mel_post'].size(0) * r1['mel_post'].size(2)
     got = out['mel_post'].float().cpu().numpy()
     r = ref['mel_post'].numpy()
@@ -551,6 +613,9 @@ def cpu_baseline(sd, x_np, out, kind='forward_tacotron', cb_kind='identity', amp
     base = {'value': round(frames / dt, 1), 'unit': 'mel-frames/s', 'cores': threads,
             'kind': 'port',
             'threads_used': threads, 'cpu_model': cpu_model, 'host_physical_cores': phys,
+            'usable_cpus': _usable_cpus(), 'os_cpu_count': os.cpu_count(),
+            'threads_rule': 'min(host physical cores, CPUs granted to the process: affinity '
+                            'and cgroup quota) (BASELINE.md:48)',
             'value_1thread': round(f1 / dt1, 1),
             'sample': f'one generate() of the same batch ({x_np.shape[0]} x {x_np.shape[1]} phonemes, '
                       f'T_mel {r.shape[2]}) with oracle/{ft_torch_cpu.__name__.split(".")[-1]}.py '

@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 11
+ABI_VERSION = 12
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 

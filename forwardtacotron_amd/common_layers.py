@@ -218,6 +218,9 @@ class BiRNN(Packed):
         super().__init__()
         self.cell = 0 if cell == 'gru' else 1
         self.input_size, self.hidden = fin, hidden
+        # the recurrence runs alone and may spread over every CU (ops.rnn_bidir `spread`);
+        # set by the owner for the decoder-side recurrences only
+        self.spread = False
         gh = (3 if self.cell == 0 else 4) * hidden
         b = 1.0 / math.sqrt(hidden)
         for sfx in ('', '_reverse'):
@@ -260,7 +263,7 @@ class BiRNN(Packed):
         _, b_in, b_hh, w_hh, _ = self.packed_weights()
         return ops.rnn_bidir(self.cell, xp, self.hidden, w_hh, b_hh, T=T, index=index,
                              xp_zero=b_in if index is not None else None, lengths=lengths,
-                             pad_value=pad_value)
+                             pad_value=pad_value, spread=self.spread)
 
     def forward(self, x: torch.Tensor):
         """(B, T, In) -> ((B, T, 2H), None) like nn.GRU/LSTM(batch_first=True) without h0."""

@@ -127,6 +127,7 @@ struct RnnParams {
   const float *w_ih;
   const float *b_ih;
   unsigned spin_limit;  // bound of every spin (g_spin_limit at launch)
+  int psleep;  // s_sleep(1) count before a step's first h poll (FTMI_RNN_PSLEEP; valid results)
   int diag;  // timing experiments only (FTMI_RNN_DIAG, results invalid when set): bit 0 =
              // input projections from one L2-hot row, bit 1 = no hand-off waits,
              // bit 2 = no drain
@@ -190,7 +191,7 @@ __device__ __forceinline__ void report_timeout(const RnnParams &p) {
 
 constexpr int FUSE_CIN = 256;  // input width of the fused-projection instances
 
-template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false>
+template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false, bool CST = false>
 __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(const RnnParams p) {
   constexpr bool X6 = MODE != 0;  // 16x16x32 fragment layout (bf16x6 and f16x3)
   constexpr bool H3 = MODE == 2;
@@ -212,6 +213,10 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   // FUSE (f16x3 GRU, several workgroups per group): each wave also multiplies its quarter of
   // the input channels by W_ih; the partial gate inputs go through the same LDS reduction
   static_assert(!FUSE || (H3 && CELL == 0 && !LOCAL), "fused input projection: f16x3 GRU");
+  // CST: the compute waves store their own tagged h chunks right after the cell update (each
+  // wave's 16 chunks are its own cells: CPT == 1), the comm wave only the y rows — barrier C
+  // and the comm wave's stage read leave the h hand-off's critical path
+  static_assert(!CST || (H3 && !LOCAL && CPT == 1 && U == 16), "compute-wave h stores");
   constexpr int KWI = FUSE ? FUSE_CIN / WK : 32;  // input channels per wave
   constexpr int KSI = KWI / 32;                   // their 32-deep k-steps
   constexpr int RR = FUSE ? 2 * R : R;            // reduction rows: W_hh h [+ W_ih x]
@@ -335,7 +340,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         const int soff = (t & 1) * hxp;
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int i = 0; i < FPL; ++i) {
+        for (int i = 0; i < (CST ? 0 : FPL); ++i) {
           // every sequence slot of the chunk, the batch tail's too: consumers check the tags
           // of all 16 columns of their fragments
           const u32x4 v = *(const u32x4 *)&hstage[(lane + 64 * i) * 4];
@@ -461,6 +466,15 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.hx, (short)0, 0x7FFFFFF0, 0x00020000);
   const unsigned hoff = (unsigned)((gglob * slab + wk * NL * 256 + lane * 4) * 4);
   const int hx_par = p.ngroups_total * slab * 4;  // bytes between the two parity halves
+  unsigned cst_off = 0;  // CST: the exchange offset of stage chunk 16 wave + lane
+  if constexpr (CST) {
+    const int f = 16 * wave + (lane & 15);
+    const int bl = f / (U / 4), rem = f % (U / 4), plane = rem & 1;
+    const int k0 = u0 + (rem >> 1) * 8;
+    const int kwv = k0 / KW, r = k0 % KW, q = r % 32;
+    const int ln = (q >> 3) * 16 + bl;
+    cst_off = (unsigned)((gglob * 16 * H * 2 + ((kwv * NL + (r / 32) * 2 + plane) * 64 + ln) * 8) * 2);
+  }
 
   // input projections (independent of h), fetched two steps ahead through register rings
   // of three sets; with the LengthRegulator map the frame's source row index is fetched a
@@ -591,6 +605,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       // accesses are single-copy atomic, so a torn 16-byte store only delays the read;
       // every load of the exchange buffer is sc1 (L2-served).
       const int soff = ((t - 1) & 1) * hx_par;
+      for (int i = 0; i < p.psleep; ++i) __builtin_amdgcn_s_sleep(1);
       // fp32 words carry the tag in bit 0; f16 pairs in bits 0 and 16 (both halves)
       const unsigned tmask = HSPLIT ? 0x00010001u : 1u;
       const bool want1 = h_tag(t - 1) != 0u;  // uniform
@@ -789,6 +804,20 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         const int c = bl * U + cu[j];
         if constexpr (!HSPLIT) hstage[c] = hn;
         ystage[c] = yout;
+      }
+    }
+    if constexpr (CST) {
+      // this wave's cells (sequences 4 wave .. 4 wave + 3, all 16 units) are the stage's
+      // chunks 16 wave .. 16 wave + 15: read back (same wave, LDS in order) and store
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane < 16) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = *(const u32x4 *)&hstage[(16 * wave + lane) * 4];
+        if (xcd_mode)
+          __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, cst_off, (t & 1) * hx_par, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, cst_off, (t & 1) * hx_par, 16);
       }
     }
     STAMP(4);
@@ -1045,6 +1074,292 @@ __global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * GV_KSEG) void rnn_gem
   }
 }
 
+// ---- row-owning f16x3 recurrence (opt-in, FTMI_RNN_ROW=1; see row_path) ----------------
+// One WAVE owns 4 hidden units: its 16-row W_hh tile is ordered (unit, gate) = (lc / 4,
+// lc % 4), so the 16x16x32 MFMA accumulator of lane (ls, lc) holds the gate sums of unit ls
+// for sequence lc — the cell update runs on the accumulators (no K-split partials, no LDS
+// reduction) and each lane stores its own tagged h (f16 head | scaled f16 tail, one 32-bit
+// word) into the exchange buffer: no comm wave, no staging.  Each wave holds the full K of
+// its rows (H / 4 VGPRs of f16 head + tail).  The group's h_{t-1} is acquired ONCE per
+// workgroup — each wave polls a quarter of it (step tags, as rnn_bidir_kernel) — and written
+// into an LDS B-fragment image the four waves share: ONE barrier per step.
+// NBL live sequences per group (16, 8 or 4; the MFMA's other columns are dead): the h bytes a
+// workgroup acquires per step scale with NBL, the MFMA work per wave does not, so a smaller
+// NBL spreads a small-H recurrence over more CUs at a lower per-step latency.
+// Exchange layout of a group: [H/4 unit quads][NBL sequences][4 units] u32 words; a wave's
+// 64 (or 4 NBL) stores of one step are one contiguous run.
+template <int CELL, int H, int NBL>
+__global__ __launch_bounds__(256, 1) void rnn_row_kernel(const RnnParams p) {
+  constexpr int G = CELL ? 4 : 3;
+  constexpr int U = 16;            // units per workgroup (4 per wave)
+  constexpr int BPG = H / U;
+  constexpr int KS = H / 32;       // 32-deep k-steps of the contraction
+  constexpr int KSW = KS / 4;      // k-steps whose h each wave acquires
+  constexpr int SLAB = H * NBL;    // u32 words of one group's h
+  static_assert(KS % 4 == 0 && BPG >= 2 && BPG <= FLAGS_PER_GROUP && 16 % NBL == 0, "shape");
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  __shared__ u32x4 hl[2][KS][2][64];  // [step parity][k-step][head, tail][lane]
+  __shared__ int s_abort, s_group, s_bi, s_mode;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ls = lane >> 4, lc = lane & 15;
+
+  // ---- group assignment: the census of rnn_bidir_kernel ---------------------------------
+  if (tid == 0) {
+    int mode = 0, group = blockIdx.x % p.ngroups, bi = blockIdx.x / p.ngroups, abort = 0;
+    if (p.xcd_local) {
+      const unsigned x = xcc_id();
+      const unsigned slot = __hip_atomic_fetch_add(p.ws + WS_CENSUS + x * CNT_PAD, 1u,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(p.ws + WS_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!poll_ge(p.ws + WS_ARRIVE, gridDim.x, p.spin_limit)) {
+        abort = 1;
+        report_timeout(p);
+      } else if (p.ngroups % 8 == 0 || (int)gridDim.x == 8 * BPG) {
+        const int gpx = p.ngroups % 8 == 0 ? p.ngroups / 8 : 1;
+        const unsigned per = (unsigned)gpx * BPG;
+        bool balanced = true;
+        for (int i = 0; i < 8; ++i)
+          balanced &= __hip_atomic_load(p.ws + WS_CENSUS + i * CNT_PAD, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT) == per;
+        if (balanced) {
+          mode = 1;
+          group = (int)(x * gpx + slot / BPG);
+          bi = (int)(slot % BPG);
+        }
+      }
+    }
+    s_mode = mode;
+    s_group = group;
+    s_bi = bi;
+    s_abort = abort;
+  }
+  __syncthreads();
+  if (s_abort) return;
+  if (s_group >= p.ngroups || s_bi >= BPG) return;  // surplus workgroups of a padded grid
+  const int group = s_group, bi = s_bi;
+  const bool xcd_mode = s_mode == 1;
+  const int dir = group & 1;
+  const int chunk = p.chunk0 + (group >> 1);
+  const int gglob = p.chunk0 * 2 + group;
+  const int u0 = bi * U;
+
+  // ---- W_hh tile -> f16 head / scaled tail A-fragments (row lc = unit lc/4, gate lc%4;
+  // the GRU's fourth gate row is zero) ------------------------------------------------------
+  f16x8 wh[KS], wt[KS];
+  bool wbad = false;
+  {
+    const int gate = lc & 3, unit = u0 + 4 * wave + (lc >> 2);
+    const bool gl = gate < G;
+    const float *src = p.w_hh + (size_t)dir * (G * H) * H +
+                       (size_t)((gl ? gate : 0) * H + unit) * H + 8 * ls;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const f32x4 a = *(const f32x4 *)(src + ks * 32);
+      const f32x4 b = *(const f32x4 *)(src + ks * 32 + 4);
+      float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = gl ? v[e] : 0.f;
+        wbad |= !(__builtin_fabsf(v[e]) <= 65504.f);
+      }
+      split2h8(v, wh[ks], wt[ks]);
+    }
+  }
+  if (wbad && p.status) atomicOr(p.status, 2u);
+
+  // ---- the cell of this lane: unit cu of the workgroup, sequence lc of the group ---------
+  const int cu = 4 * wave + ls;
+  const int b = chunk * NBL + lc;
+  const bool live = lc < NBL;  // the MFMA column carries a sequence of this group
+  const bool cvalid = live && b < p.B;
+  const int bsafe = cvalid ? b : 0;
+  float hstate = 0.f, cstate = 0.f, bhh[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) bhh[g] = (CELL == 0) ? p.b_hh[dir * G * H + g * H + u0 + cu] : 0.f;
+  const int len = (p.lengths && cvalid) ? p.lengths[b] : p.T;
+  const int32_t *iptr = p.index ? p.index + (size_t)bsafe * p.T : (const int32_t *)p.ws;
+  const size_t brow = (size_t)bsafe * p.T_src;
+  const float *xcol = p.xp + dir * G * H + u0 + cu;
+  const float *zcol = (p.index ? p.xp_zero : p.xp) + dir * G * H + u0 + cu;
+  auto frame = [&](int t) { return dir ? (p.T - 1 - t) : t; };
+  auto load_idx = [&](int t) -> int { return iptr[p.index ? frame(t < p.T ? t : p.T - 1) : 0]; };
+  auto load_gx = [&](int t, int ir, float (&g)[G]) {
+    const int tt = frame(t < p.T ? t : p.T - 1);
+    const int src = p.index ? ir : tt;
+    const float *row = src >= 0 ? xcol + (brow + src) * p.xp_stride : zcol;
+    if (p.diag & 1) row = zcol;  // timing experiment: L2-hot rows
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) g[gi] = row[gi * H];
+  };
+
+  // ---- exchange addresses ----------------------------------------------------------------
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.hx, (short)0, 0x7FFFFFF0, 0x00020000);
+  const int par_bytes = p.ngroups_total * SLAB * 4;
+  const unsigned gbase = (unsigned)gglob * SLAB * 4u;
+  // producer: word ((quad * NBL + seq) * 4 + unit in quad), quad = (u0 + 4 wave) / 4
+  const unsigned st_off = gbase + (unsigned)((((bi * 4 + wave) * NBL + lc) * 4 + ls) * 4);
+  // consumer: k-step ks = wave * KSW + j needs quads 8 ks + 2 ls and 8 ks + 2 ls + 1 of
+  // sequence lc (dead columns read a live sequence's words: valid addresses, ignored)
+  const int lcl = live ? lc : lc % NBL;
+  unsigned ld_off[KSW];
+#pragma unroll
+  for (int j = 0; j < KSW; ++j)
+    ld_off[j] = gbase + (unsigned)((((wave * KSW + j) * 8 + 2 * ls) * NBL + lcl) * 16);
+
+  float g0[G], g1[G], g2[G];
+  int i0 = load_idx(0), i1 = load_idx(1);
+  load_gx(0, i0, g0);
+  load_gx(1, i1, g1);
+  int i2 = load_idx(2);
+
+  auto step = [&](int t, const float (&gx)[G], float (&gnext)[G], int inext, int &iload) -> bool {
+    const int tt = frame(t);
+    // ---- acquire this wave's quarter of h_{t-1} (tags in bits 0 and 16 of every word) ----
+    u32x4 hr[2 * KSW];
+    if (t == 0) {
+#pragma unroll
+      for (int i = 0; i < 2 * KSW; ++i) hr[i] = (u32x4){0u, 0u, 0u, 0u};
+    } else {
+      const int soff = ((t - 1) & 1) * par_bytes;
+      const bool want1 = h_tag(t - 1) != 0u;
+      for (unsigned spins = 0;; ++spins) {
+        // a compiler memory barrier: without it the loop (no store on its path) lets LICM
+        // hoist the loads out and spin on the first values
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < KSW; ++j) {
+          hr[2 * j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ld_off[j], soff, 16);
+          hr[2 * j + 1] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ld_off[j] + NBL * 16, soff, 16);
+        }
+        bool fresh;
+        if (want1) {
+          u32x4 a = hr[0];
+#pragma unroll
+          for (int i = 1; i < 2 * KSW; ++i) a &= hr[i];
+          fresh = ((a.x & a.y & a.z & a.w) & 0x00010001u) == 0x00010001u;
+        } else {
+          u32x4 o = hr[0];
+#pragma unroll
+          for (int i = 1; i < 2 * KSW; ++i) o |= hr[i];
+          fresh = ((o.x | o.y | o.z | o.w) & 0x00010001u) == 0u;
+        }
+        if (__all(fresh || !live) || (p.diag & 2)) break;
+        if (spins > p.spin_limit) {
+          if (lane == 0) {
+            s_abort = 1;
+            report_timeout(p);
+          }
+          break;
+        }
+      }
+    }
+    // ---- B-fragment image: heads / tails of units 32 ks + 8 ls + (0..7), sequence lc ----
+#pragma unroll
+    for (int j = 0; j < KSW; ++j) {
+      const u32x4 a = hr[2 * j], c = hr[2 * j + 1];
+      u32x4 hh, ht;
+      hh.x = __builtin_amdgcn_perm(a.y, a.x, 0x05040100u);
+      hh.y = __builtin_amdgcn_perm(a.w, a.z, 0x05040100u);
+      hh.z = __builtin_amdgcn_perm(c.y, c.x, 0x05040100u);
+      hh.w = __builtin_amdgcn_perm(c.w, c.z, 0x05040100u);
+      ht.x = __builtin_amdgcn_perm(a.y, a.x, 0x07060302u);
+      ht.y = __builtin_amdgcn_perm(a.w, a.z, 0x07060302u);
+      ht.z = __builtin_amdgcn_perm(c.y, c.x, 0x07060302u);
+      ht.w = __builtin_amdgcn_perm(c.w, c.z, 0x07060302u);
+      if (!live) hh = ht = (u32x4){0u, 0u, 0u, 0u};
+      hl[t & 1][wave * KSW + j][0][lane] = hh;
+      hl[t & 1][wave * KSW + j][1][lane] = ht;
+    }
+    __syncthreads();
+    if (s_abort) return false;  // a wave timed out acquiring h_{t-1}
+    load_gx(t + 2, inext, gnext);  // the projections two steps ahead (independent of h)
+    iload = load_idx(t + 3);
+
+    // ---- W_hh h over the whole K: big = W_h h_h, sml = W_t h_h + W_h h_t ---------------
+    f32x4 big = {0.f, 0.f, 0.f, 0.f}, sml = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const f16x8 hh = __builtin_bit_cast(f16x8, hl[t & 1][ks][0][lane]);
+      const f16x8 ht = __builtin_bit_cast(f16x8, hl[t & 1][ks][1][lane]);
+      sml = __builtin_amdgcn_mfma_f32_16x16x32_f16(wt[ks], hh, sml, 0, 0, 0);
+      sml = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ks], ht, sml, 0, 0, 0);
+      big = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ks], hh, big, 0, 0, 0);
+    }
+    // ---- cell update on the accumulators: element e = gate e of unit cu, sequence lc ----
+    float gs[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gs[e] = fmaf(sml[e], H3_UNSCALE, big[e]);
+    float hn;
+    if (CELL == 0) {
+      const float r = fast_sigmoid(gx[0] + (gs[0] + bhh[0]));
+      const float z = fast_sigmoid(gx[1] + (gs[1] + bhh[1]));
+      const float n = fast_tanh(gx[2] + r * (gs[2] + bhh[G - 1]));
+      hn = n + z * (hstate - n);
+    } else {
+      const float ig = fast_sigmoid(gs[0] + gx[0]);
+      const float fg = fast_sigmoid(gs[1] + gx[1]);
+      const float gg = fast_tanh(gs[2] + gx[2]);
+      const float og = fast_sigmoid(gs[3] + gx[G - 1]);
+      cstate = fg * cstate + ig * gg;
+      hn = og * fast_tanh(cstate);
+    }
+    if (tt >= len) {  // packed-sequence padding: reverse direction restarts from zero
+      hn = 0.f;
+      cstate = 0.f;
+    }
+    hstate = hn;
+    // tagged f16 head and scaled tail (tail taken after the head's tag bit is set), as
+    // rnn_bidir_kernel's pre-split exchange; the state and the output stay exact fp32
+    const unsigned short tg = (unsigned short)h_tag(t);
+    const unsigned short h16 =
+        (unsigned short)((__builtin_bit_cast(unsigned short, (_Float16)hn) & 0xFFFEu) | tg);
+    const unsigned short t16 = (unsigned short)(
+        (__builtin_bit_cast(unsigned short,
+                            (_Float16)((hn - (float)__builtin_bit_cast(_Float16, h16)) * H3_SCALE)) &
+         0xFFFEu) | tg);
+    if (live) {
+      const unsigned word = (unsigned)h16 | ((unsigned)t16 << 16);
+      if (xcd_mode)  // stays in this XCD's L2, read back by same-XCD sc1 loads
+        __builtin_amdgcn_raw_buffer_store_b32(word, rsrc, st_off, (t & 1) * par_bytes, 0);
+      else  // write-through (sc1)
+        __builtin_amdgcn_raw_buffer_store_b32(word, rsrc, st_off, (t & 1) * par_bytes, 16);
+    }
+    if (cvalid)
+      p.y[((size_t)b * p.T + tt) * p.y_stride + dir * H + u0 + cu] = tt >= len ? p.pad_value : hn;
+    return true;
+  };
+
+  for (int t = 0; t < p.T; t += 3) {
+    if (!step(t, g0, g2, i2, i0)) break;
+    if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1)) break;
+    if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2)) break;
+  }
+}
+
+template <int CELL, int H, int NBL>
+int launch_row(RnnParams p, int max_blocks, hipStream_t s) {
+  constexpr int BPG = H / 16;
+  const int nchunks = (p.B + NBL - 1) / NBL;
+  p.ngroups_total = 2 * nchunks;
+  const int max_groups = (max_blocks / BPG) & ~1;
+  if (max_groups < 2) return FTMI_E_UNSUPPORTED;
+  for (int c0 = 0; c0 < nchunks; c0 += max_groups / 2) {
+    const int nc = (nchunks - c0) < max_groups / 2 ? (nchunks - c0) : max_groups / 2;
+    p.chunk0 = c0;
+    p.ngroups = 2 * nc;
+    if (c0 > 0) {  // the census words are per launch
+      hipError_t e = hipMemsetAsync(p.ws + WS_CENSUS, 0, (WS_FLAGS - WS_CENSUS) * 4, s);
+      if (e != hipSuccess) return (int)e;
+    }
+    int nblk = p.ngroups * BPG;
+    if (p.xcd_local && p.ngroups < 8 && 8 * BPG <= max_blocks) nblk = 8 * BPG;
+    hipLaunchKernelGGL((rnn_row_kernel<CELL, H, NBL>), dim3(nblk), dim3(256), 0, s, p);
+    FTMI_CHECK_LAUNCH();
+  }
+  return FTMI_OK;
+}
+
 template <int CELL, int H, int U>
 int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
   constexpr int BPG = H / U;
@@ -1068,7 +1383,7 @@ int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
   return FTMI_OK;
 }
 
-template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false>
+template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false, bool CST = false>
 int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
   constexpr int BPG = H / U;
   int max_groups = (max_blocks / BPG) & ~1;
@@ -1090,7 +1405,7 @@ int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
     int nblk = p.ngroups * BPG;
     if (BPG > 1 && pad_env && p.xcd_local && p.ngroups < 8 && 8 * BPG <= max_blocks)
       nblk = 8 * BPG;
-    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, FUSE>), dim3(nblk),
+    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, FUSE, CST>), dim3(nblk),
                        dim3(BPG == 1 ? 256 : 320), 0, s, p);
     FTMI_CHECK_LAUNCH();
   }
@@ -1139,9 +1454,43 @@ static int rnn_units(int cell, int H, int mma) {
   return 16;
 }
 
+// FTMI_RNN_ROW=1: the f16x3 recurrences of H = 128 / 256 / 512 run on rnn_row_kernel (opt-in:
+// measured slower than rnn_bidir_kernel at c3 — LSTM 1.84-1.87 against 1.65-1.73 us/step,
+// postnet GRU 1.30-1.34 against 1.26 — its shared LDS h image makes the MFMA phase LDS-bound,
+// 4 waves x 32 KB of fragment reads per step; read per call: tests switch it)
+static bool row_path(int cell, int H, int mma) {
+  const char *v = getenv("FTMI_RNN_ROW");
+  const int env = v ? atoi(v) : 0;
+  return env && mma == 2 && ((cell == 1 && H == 512) || (cell == 0 && (H == 128 || H == 256)));
+}
+// live sequences per group of rnn_row_kernel: 16, or with FTMI_RNN_SPREAD the smallest of
+// 4 / 8 whose groups all fit the device at once (fewer h bytes per workgroup and step);
+// FTMI_RNN_NB (4, 8, 16) forces it
+static int row_nbl(int B, int H, bool spread, int maxb) {
+  const char *v = getenv("FTMI_RNN_NB");
+  if (v && (atoi(v) == 4 || atoi(v) == 8 || atoi(v) == 16)) return atoi(v);
+  if (!spread) return 16;
+  for (int nbl = 4; nbl <= 8; nbl *= 2)
+    if (2 * ((B + nbl - 1) / nbl) * (H / 16) <= maxb) return nbl;
+  return 16;
+}
+
 extern "C" int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t mma) {
   if (B <= 0 || H <= 0 || H % 16 != 0) return 0;
+  const bool spread = (mma & FTMI_RNN_SPREAD) != 0;
+  mma &= 0xFF;
   if (gemv_path(cell, B, H)) return (xcd_local_env() ? 8 : 2) * (H / 16);  // launch_gemv
+  if (row_path(cell, H, mma)) {  // launch_row
+    const int maxb = device_cu_count(), bpg = H / 16;
+    const int nbl = row_nbl(B, H, spread, maxb);
+    const int max_groups = (maxb / bpg) & ~1;
+    if (max_groups < 2) return 0;
+    const int nchunks = (B + nbl - 1) / nbl;
+    const int ngroups = 2 * (nchunks < max_groups / 2 ? nchunks : max_groups / 2);
+    int nblk = ngroups * bpg;
+    if (xcd_local_env() && ngroups < 8 && 8 * bpg <= maxb) nblk = 8 * bpg;
+    return nblk;
+  }
   const int bpg = H / rnn_units(cell, H, mma);
   const int maxb = device_cu_count();
   const int max_groups = (maxb / bpg) & ~1;
@@ -1206,6 +1555,11 @@ static int rnn_setup(RnnParams &p, int B, int T, int H, int cell, const float *w
     return v ? atoi(v) : 0;
   }();
   p.diag = diag_env;
+  static const int psleep_env = [] {
+    const char *v = getenv("FTMI_RNN_PSLEEP");
+    return v ? atoi(v) : 0;
+  }();
+  p.psleep = psleep_env;
   return FTMI_OK;
 }
 
@@ -1217,6 +1571,8 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
                               ftmi_stream_t stream) {
   if (!xp || !w_hh || !y || !sync) return FTMI_E_ARG;
   if (B <= 0 || T <= 0 || H <= 0 || T_src <= 0) return FTMI_E_ARG;
+  const bool spread = (mma & FTMI_RNN_SPREAD) != 0;
+  mma &= ~FTMI_RNN_SPREAD;
   if (mma < 0 || mma > 2) return FTMI_E_ARG;
   if (cell == 0 && !b_hh) return FTMI_E_ARG;
   if (index && !xp_zero) return FTMI_E_ARG;
@@ -1242,6 +1598,19 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
     if (H == 128) return launch_gemv<0, 128, 16>(p, maxb, s);
     return launch_gemv<0, 64, 16>(p, maxb, s);
   }
+  if (row_path(cell, H, mma)) {
+    const int nbl = row_nbl(B, H, spread, maxb);
+#define FTMI_ROW_NB(CELL_, H_)                                         \
+  switch (nbl) {                                                       \
+    case 4: return launch_row<CELL_, H_, 4>(p, maxb, s);               \
+    case 8: return launch_row<CELL_, H_, 8>(p, maxb, s);               \
+    default: return launch_row<CELL_, H_, 16>(p, maxb, s);             \
+  }
+    if (cell == 1) FTMI_ROW_NB(1, 512)
+    if (H == 256) FTMI_ROW_NB(0, 256)
+    FTMI_ROW_NB(0, 128)
+#undef FTMI_ROW_NB
+  }
 #define FTMI_RNN_MODES(CELL_, H_, U_, WKX_, WKF_)                                   \
   switch (mma) {                                                                    \
     case 2: return launch_rnn<CELL_, H_, U_, WKX_, 2>(p, nchunks, maxb, s);          \
@@ -1261,6 +1630,23 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   if (cell == 0 && H == 128) FTMI_RNN_MODES(0, 128, 16, 4, 4)
   // H = 256 / 512: 16 units per workgroup (32 units measured 1.84 against 1.19 us/step for
   // the H = 256 GRU; the LSTM's W_hh slice does not fit the VGPRs at 32 units)
+  // FTMI_RNN_WK=2 (timing experiments): the LSTM with a 2-way K split (two row halves per
+  // workgroup) on the f16x3 path instead of 4
+  static const int wk_env = [] {
+    const char *v = getenv("FTMI_RNN_WK");
+    return v ? atoi(v) : 4;
+  }();
+  // FTMI_RNN_CSTORE=1 (A/B): compute-wave h stores (rnn_bidir_kernel CST; read per call)
+  const char *cst_v = getenv("FTMI_RNN_CSTORE");
+  const int cst_env = cst_v ? atoi(cst_v) : 0;
+  if (cst_env && mma == 2 && cell == 1 && H == 512)
+    return launch_rnn<1, 512, 16, 4, 2, false, true>(p, nchunks, maxb, s);
+  if (cst_env && mma == 2 && cell == 0 && (H == 256 || H == 128)) {
+    if (H == 256) return launch_rnn<0, 256, 16, 4, 2, false, true>(p, nchunks, maxb, s);
+    return launch_rnn<0, 128, 16, 4, 2, false, true>(p, nchunks, maxb, s);
+  }
+  if (wk_env == 2 && mma == 2 && cell == 1 && H == 512)
+    return launch_rnn<1, 512, 16, 2, 2>(p, nchunks, maxb, s);
   if (cell == 0 && H == 256) FTMI_RNN_MODES(0, 256, 16, 4, 4)
   if (cell == 1 && H == 512) FTMI_RNN_MODES(1, 512, 16, 4, 4)
 #undef FTMI_RNN_MODES

@@ -38,6 +38,21 @@ def _identity(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def graph_safe(fn: Callable[[torch.Tensor], torch.Tensor]) -> Callable[[torch.Tensor], torch.Tensor]:
+    """Mark a pitch / energy callback as safe to capture in the phoneme-phase HIP graph: a
+    pure function of its tensor argument made of device-side torch ops, whose behaviour
+    does not change between calls (no Python-side state it reads changes: closure
+    variables, attributes, scalars).  gen_forward.py's `lambda x: x * amp` is, for the run's
+    fixed `amp`.  An unmarked callback runs eagerly on every call, as the reference calls
+    it (`models/forward_tacotron.py:258-261`); returns fn."""
+    fn._ftmi_graph_safe = True
+    return fn
+
+
+def _graphable(fn) -> bool:
+    return fn is _identity or getattr(fn, '_ftmi_graph_safe', False) is True
+
+
 # generate() replays the phoneme phase as a HIP graph (captured per (device, x shape, alpha,
 # callbacks), see _phoneme_graph) when the phase is launch-bound: B*T <= GRAPH_MAX_TOKENS.
 # Measured: c2 (B = 1, T = 120) 4.18 -> 3.57 ms/step; c3 (B = 64, T = 200) 9.20 -> 9.58, the
@@ -149,6 +164,9 @@ class ForwardTacotron(nn.Module):
                             num_highways=postnet_num_highways, dropout=postnet_dropout)
         self.post_proj = LinearParams(2 * postnet_dims, n_mels, bias=False)
         self.n_mels = n_mels
+        # the decoder-side recurrences run alone on the device: they may spread over every
+        # CU (the phoneme phase's four GRUs share it and keep the compact form)
+        self.lstm.spread = self.postnet.rnn.spread = True
 
     def __repr__(self):
         num_params = sum([np.prod(p.size()) for p in self.parameters()])
@@ -300,11 +318,12 @@ class ForwardTacotron(nn.Module):
         Keyed on (device, x shape, alpha, the callbacks' identity, matrix paths); a key is
         captured the SECOND time it is seen (a one-off shape — gen_forward.py's sentences
         of different lengths — stays eager: capture costs ~3 eager phases).  The callbacks
-        are captured with the phase, so they must be device-side torch ops whose effect
-        does not change between calls (gen_forward.py's `lambda x: x * amp` is); set
-        FTMI_GRAPH=0 (or forward_tacotron.GRAPH = False) for callbacks with host-side
-        effects.  A capture that fails (a callback that syncs or leaves the device) marks
-        the key eager for good.
+        are captured with the phase, so only the default identity and callbacks marked
+        `graph_safe` (pure device-side torch ops whose effect does not change between calls,
+        as gen_forward.py's `lambda x: x * amp`) get here; generate() runs any other
+        callback eagerly.  FTMI_GRAPH=0 (or forward_tacotron.GRAPH = False) turns capture
+        off.  A capture that fails (a callback that syncs or leaves the device) marks the
+        key eager for good.
         Static buffers: x is copied in, dur / pitch / energy are cloned out (they go back to
         the caller); enc, the offsets and the LSTM input projection are consumed by this
         call's decoder — the next replay waits for the decoder's completion event
@@ -452,7 +471,10 @@ class ForwardTacotron(nn.Module):
             self.eval()
         self._check_device(x)
 
-        graph = GRAPH and batch is None and x.numel() <= GRAPH_MAX_TOKENS
+        # only callbacks known to be pure are captured (graph_safe): a replay would freeze any
+        # Python-side state an arbitrary callback reads
+        graph = (GRAPH and batch is None and x.numel() <= GRAPH_MAX_TOKENS
+                 and _graphable(pitch_function) and _graphable(energy_function))
 
         def run():
             with torch.no_grad():

@@ -2,10 +2,14 @@
 ids onward (the text frontend — `utils/text/cleaners.py`: unidecode, inflect, espeak via
 phonemizer — is absent from this image, so raw English text is refused with that reason).
 
-    python -m forwardtacotron_amd.gen_forward --checkpoint ckpt.pt \\
+    python -m forwardtacotron_amd.gen_forward [--checkpoint ckpt.pt | --config config.yaml] \\
         [--input_phonemes "həloʊ wɜːld" | --input_tokens 12,40,7 | --sentences file] \\
         [--alpha 1.0] [--amp 1.0] {griffinlim,melgan,hifigan,wavernn}
+    python -m forwardtacotron_amd.gen_forward ... wavernn \\
         [--voc_checkpoint voc.pt | --voc_synthetic] [--target 11000] [--overlap 550]
+
+Without --checkpoint the checkpoint is found from --config like the reference
+(`gen_forward.py:68-72`: checkpoints/{tts_model_id}.forward/latest_model.pt).
 
 Per sentence, exactly like the reference loop (`gen_forward.py:106-134`): tokens (B = 1) ->
 `generate(x, alpha, pitch_function=lambda x: x * amp, energy_function=lambda x: x)` on the
@@ -102,8 +106,22 @@ def write_output(m: torch.Tensor, name: str, vocoder: str, out_path: Path, dsp=N
     return p
 
 
+RAW_TEXT_HINT = ('needs the reference text frontend (utils/text/cleaners.py: unidecode + '
+                 'phonemizer/espeak), absent here: pass --input_phonemes, --input_tokens or a '
+                 '--sentences file of phonemised lines')
+
+
+def _looks_raw(line: str) -> bool:
+    """Uppercase ASCII letters or digits never occur in the cleaner's phonemised output
+    (espeak IPA is lower case, numbers are spelled out): such a line is raw text."""
+    return any(('A' <= c <= 'Z') or c.isdigit() for c in line)
+
+
 def read_inputs(args) -> List[List[int]]:
-    """Token id lists, one per sentence."""
+    """Token id lists, one per sentence.  Phonemised input only: the reference cleans raw
+    text first (`gen_forward.py:86,109`), which needs espeak — raw text is refused with that
+    reason, never tokenised as if it were phonemes."""
+    from .text.symbols import phonemes
     from .text.tokenizer import Tokenizer
     tok = Tokenizer()
     if args.input_tokens:
@@ -111,50 +129,86 @@ def read_inputs(args) -> List[List[int]]:
     if args.input_phonemes:
         return [tok(args.input_phonemes)]
     if args.input_text:
-        raise SystemExit('--input_text needs the reference text frontend (utils/text/cleaners.py: '
-                         'unidecode + phonemizer/espeak), absent here: pass --input_phonemes or '
-                         '--input_tokens')
+        raise SystemExit('--input_text ' + RAW_TEXT_HINT)
+    # the reference reads sentences.txt (raw text, gen_forward.py:92-94); here a file of
+    # phonemised lines (--sentences, default the reference's file name)
     path = Path(args.sentences)
-    with open(path, 'r', encoding='utf-8') as f:  # gen_forward.py:93-94 (phonemised lines)
-        return [tok(line.strip()) for line in f if line.strip()]
+    with open(path, 'r', encoding='utf-8') as f:
+        lines = [line.strip() for line in f if line.strip()]
+    known = set(phonemes)
+    for i, line in enumerate(lines, 1):
+        if _looks_raw(line):
+            raise SystemExit(f'{path}:{i} looks like raw text ({line[:40]!r}); it ' + RAW_TEXT_HINT)
+        skipped = sorted(set(line) - known)
+        if skipped:  # the reference Tokenizer drops them too (utils/text/tokenizer.py)
+            print(f'warning: {path}:{i}: symbols outside the phoneme set skipped: {skipped}')
+    return [tok(line) for line in lines]
 
 
-def main(argv: Optional[Sequence[str]] = None) -> List[Path]:
+def checkpoint_from_config(config_path: str) -> Path:
+    """`gen_forward.py:68-72`: without --checkpoint, the latest forward checkpoint of the
+    config's tts_model_id — Paths(...).forward_checkpoints / 'latest_model.pt', i.e.
+    checkpoints/{tts_model_id}.forward/latest_model.pt under the directory the CLI runs from
+    (the reference resolves it under its repository root, where it is run from).  The config
+    is read with yaml.safe_load (the reference: FullLoader)."""
+    import yaml
+    with open(config_path, 'r', encoding='utf-8') as f:
+        config = yaml.safe_load(f)
+    return Path.cwd() / 'checkpoints' / f"{config['tts_model_id']}.forward" / 'latest_model.pt'
+
+
+def build_parser() -> argparse.ArgumentParser:
+    """The reference's grammar (`gen_forward.py:43-61`): top-level options, then the vocoder
+    as a sub-command; `wavernn` takes --overlap / --target / --voc_checkpoint.  Additions:
+    phonemised / token input, --synthetic / --voc_synthetic weights, --out."""
     parser = argparse.ArgumentParser(description='TTS Generator (MI355X HIP path)')
-    parser.add_argument('--input_text', '-i', default=None, type=str)
+    parser.add_argument('--input_text', '-i', default=None, type=str,
+                        help='[string] raw text (refused: needs the espeak text frontend)')
     parser.add_argument('--input_phonemes', default=None, type=str,
                         help='phonemised sentence (what the reference cleaner produces)')
     parser.add_argument('--input_tokens', default=None, type=str, help='comma-separated token ids')
     parser.add_argument('--sentences', default='sentences.txt',
-                        help='file of phonemised sentences, one per line')
-    parser.add_argument('--checkpoint', type=str, default=None)
+                        help='file of PHONEMISED sentences, one per line (raw text is refused)')
+    parser.add_argument('--checkpoint', type=str, default=None,
+                        help='[string/path] path to .pt model file.')
+    parser.add_argument('--config', metavar='FILE', default='config.yaml',
+                        help='The config containing all hyperparams. Only used if no checkpoint is set.')
     parser.add_argument('--synthetic', action='store_true', help='synthetic weights, no checkpoint')
     parser.add_argument('--alpha', type=float, default=1.)
     parser.add_argument('--amp', type=float, default=1.)
     parser.add_argument('--out', default='model_outputs')
-    parser.add_argument('vocoder', choices=VOCODERS)
-    # the reference's `wavernn` sub-command options (gen_forward.py:54-57)
-    parser.add_argument('--voc_checkpoint', type=str, default=None,
-                        help='[string/path] Load in different WaveRNN weights')
-    parser.add_argument('--voc_synthetic', action='store_true', help='synthetic WaveRNN weights')
-    parser.add_argument('--overlap', '-o', default=550, type=int, help='[int] number of crossover samples')
-    parser.add_argument('--target', '-t', default=11_000, type=int,
-                        help='[int] number of samples in each batch index')
-    args = parser.parse_args(argv)
-    if args.checkpoint:
-        tts_model, config = load_tts_model(args.checkpoint)
-    elif args.synthetic:
+    subparsers = parser.add_subparsers(dest='vocoder')
+    wr_parser = subparsers.add_parser('wavernn')
+    wr_parser.add_argument('--overlap', '-o', default=550, type=int,
+                           help='[int] number of crossover samples')
+    wr_parser.add_argument('--target', '-t', default=11_000, type=int,
+                           help='[int] number of samples in each batch index')
+    wr_parser.add_argument('--voc_checkpoint', type=str,
+                           help='[string/path] Load in different WaveRNN weights')
+    wr_parser.add_argument('--voc_synthetic', action='store_true', help='synthetic WaveRNN weights')
+    for name in ('griffinlim', 'melgan', 'hifigan'):
+        subparsers.add_parser(name)
+    return parser
+
+
+def main(argv: Optional[Sequence[str]] = None) -> List[Path]:
+    args = build_parser().parse_args(argv)
+    if args.vocoder not in VOCODERS:  # gen_forward.py:65-66
+        raise SystemExit("Please provide a valid vocoder! Choices: ['griffinlim', 'wavernn', "
+                         "'melgan', 'hifigan']")
+    if args.synthetic:
         tts_model, config = synthetic_tts_model()
     else:
-        raise SystemExit('--checkpoint (or --synthetic) is required')
+        checkpoint = args.checkpoint or checkpoint_from_config(args.config)
+        tts_model, config = load_tts_model(str(checkpoint))
     from .dsp import DSP
     dsp = DSP.from_config(config)
     voc = None
     if args.vocoder == 'wavernn':
-        if args.voc_checkpoint:
-            voc_model, voc_config = load_wavernn(args.voc_checkpoint)
-        elif args.voc_synthetic:
+        if args.voc_synthetic:
             voc_model, voc_config = synthetic_wavernn()
+        elif args.voc_checkpoint:
+            voc_model, voc_config = load_wavernn(args.voc_checkpoint)
         else:
             raise SystemExit('wavernn: --voc_checkpoint (or --voc_synthetic) is required')
         voc = (voc_model, DSP.from_config(voc_config))
@@ -169,8 +223,13 @@ def main(argv: Optional[Sequence[str]] = None) -> List[Path]:
         voc[0].to(device)
     tts_k = tts_model.get_step() // 1000
     texts = read_inputs(args)
-    pitch_function = lambda x: x * args.amp  # noqa: E731  (gen_forward.py:103)
-    energy_function = lambda x: x  # noqa: E731  (gen_forward.py:104)
+    # gen_forward.py:103-104; amp is fixed for the run, so the lambdas are pure (graph_safe:
+    # the phoneme phase may replay them from a HIP graph)
+    from .forward_tacotron import graph_safe
+    pitch_function = graph_safe(lambda x: x * args.amp)
+    energy_function = graph_safe(lambda x: x)
+    from .host_io import PinnedD2H
+    d2h = PinnedD2H(device, depth=1)  # pinned D2H: the drop-in for .cpu() (gen_forward.py:120)
     written = []
     for i, ids in enumerate(texts, 1):
         print(f'\n| Generating {i}/{len(texts)}')
@@ -178,9 +237,9 @@ def main(argv: Optional[Sequence[str]] = None) -> List[Path]:
         name = wav_name(i, tts_k, args.alpha, args.amp, args.vocoder)
         gen = tts_model.generate(x=x, alpha=args.alpha, pitch_function=pitch_function,
                                  energy_function=energy_function)
-        m = gen['mel_post'].cpu()
-        written.append(write_output(m, name, args.vocoder, out_path, dsp, voc, args.target,
-                                    args.overlap))
+        m = d2h.fetch(gen['mel_post'])
+        written.append(write_output(m, name, args.vocoder, out_path, dsp, voc,
+                                    getattr(args, 'target', 11000), getattr(args, 'overlap', 550)))
     print('\n\nDone.\n')
     return written
 

@@ -98,16 +98,23 @@ def run_checked(fn, device, reduce=None):
     reused).  reduce(word) -> word combines the status over ranks (sharded generation)
     before the decision."""
     st = status_word(device)
-    st.zero_()
-    out = fn()
-    s = st if reduce is None else reduce(st)
-    w = int(s.item())
-    if w & STATUS_RNN_TIMEOUT:
-        raise RnnTimeout('a recurrence workgroup timed out waiting for its group (not all '
-                         'workgroups co-resident): the result is invalid')
+
+    def attempt():
+        st.zero_()
+        res = fn()
+        s = st if reduce is None else reduce(st)
+        w = int(s.item())
+        if w & STATUS_RNN_TIMEOUT:
+            raise RnnTimeout('a recurrence workgroup timed out waiting for its group (not all '
+                             'workgroups co-resident): the result is invalid')
+        return res, w
+
+    out, w = attempt()
     if w and not _FORCED:
+        # the rerun is checked like the first pass (a timeout there raises too; its range
+        # bits cannot recur on the range-unlimited paths)
         with exact_paths():
-            out = fn()
+            out, _ = attempt()
     return out
 
 
@@ -459,6 +466,9 @@ def highway_stack(x: torch.Tensor, pre_split: torch.Tensor, C: int, hw_splits, b
     return y, h
 
 
+RNN_SPREAD = 0x100  # include/ftmi.h FTMI_RNN_SPREAD
+
+
 def rnn_blocks(cell: int, B: int, H: int, mma: Optional[int] = None) -> int:
     """Persistent workgroups one ftmi_rnn_bidir launch occupies (ftmi_rnn_blocks)."""
     m = _rnn_mma() if mma is None else mma
@@ -469,12 +479,16 @@ def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Opt
               T: Optional[int] = None, index: Optional[torch.Tensor] = None,
               xp_zero: Optional[torch.Tensor] = None, lengths: Optional[torch.Tensor] = None,
               pad_value: float = 0.0, check: bool = False,
-              ws: Optional[torch.Tensor] = None, mma: Optional[int] = None) -> torch.Tensor:
+              ws: Optional[torch.Tensor] = None, mma: Optional[int] = None,
+              spread: bool = False) -> torch.Tensor:
     """Bidirectional GRU (cell=0) / LSTM (cell=1) recurrence -> (B, T, 2H).
 
     xp: (B, T_src, 2*G*H) input projections; index: (B, T) int32 frame -> row map.
     check=True synchronises and raises RnnTimeout if a workgroup gave up waiting.
     mma: matrix path of W_hh h (default RNN_MMA; exact_paths() forces fp32).
+    spread: FTMI_RNN_SPREAD — the recurrence may occupy every CU (fewer sequences per
+    workgroup group, lower step latency); only for a recurrence that runs alone (the
+    decoder LSTM, the postnet GRU), never beside other persistent recurrences.
     """
     mma = (_rnn_mma() if mma is None or _FORCED else mma)
     if lengths is not None:  # host-side lengths (as pack_padded_sequence takes) are fine
@@ -497,7 +511,8 @@ def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Opt
            4.0 * (B * T * 2 * G * H + 2 * G * H * H + B * T * 2 * H),
            cell, B, T, H, xp.data_ptr(), xs, T_src, _ptr(index), _ptr(xp_zero),
            w_hh.data_ptr(), _ptr(b_hh), _ptr(lengths), float(pad_value), y.data_ptr(), y.stride(1),
-           int(mma), status_word(xp.device).data_ptr(), ws.data_ptr(), _stream())
+           int(mma) | (RNN_SPREAD if spread else 0), status_word(xp.device).data_ptr(),
+           ws.data_ptr(), _stream())
     if check:
         torch.cuda.current_stream().synchronize()
         off = int(lib.ftmi_rnn_error_offset(B)) // 4

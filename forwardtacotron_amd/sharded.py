@@ -96,11 +96,13 @@ def gather_rows_to(t: torch.Tensor, sizes: List[int], dst: int = 0, group=None) 
     """Gather along dim 0 to rank `dst` only (result collection: one copy of the output,
     not one per rank); returns the concatenation on `dst`, None elsewhere."""
     world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    rank = dist.get_rank(group)  # dst is a rank WITHIN the group, like this one
     dev = _coll_device(group, t.device)
     src = _padded(t, max(sizes), dev)
     bufs = [torch.empty_like(src) for _ in range(world)] if rank == dst else None
-    dist.gather(src, bufs, dst=dst, group=group)
+    # dist.gather takes the destination as a GLOBAL rank
+    gdst = dst if group is None else dist.get_global_rank(group, dst)
+    dist.gather(src, bufs, dst=gdst, group=group)
     if rank != dst:
         return None
     return torch.cat([b[:s] for b, s in zip(bufs, sizes)], 0).to(t.device)

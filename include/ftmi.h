@@ -64,7 +64,7 @@ enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
        FTMI_BANK_Y_SPLIT = 2, /* with FTMI_BANK_POOL: y as f16x3 split rows of K*Cout */
        FTMI_BANK_X_SPLIT = 4  /* x given as f16x3 split rows of Cin (FTMI_MMA_F16X3) */ };
 
-/* ABI version; bumped on any signature change (11: the WaveRNN vocoder entry points). */
+/* ABI version; bumped on any signature change (12: FTMI_RNN_SPREAD flag of ftmi_rnn_bidir / ftmi_rnn_blocks). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
@@ -260,7 +260,10 @@ int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, int32_t Cp, 
  * y:    (B, T, 2H) rows with y_stride.
  * mma:  matrix path of W_hh h: FTMI_MMA_F16X3 (default; W_hh split in-kernel, bit 1 of
  *     *status set if an entry exceeds the f16 range — rerun with FTMI_MMA_BF16X6),
- *     FTMI_MMA_BF16X6 or FTMI_MMA_F32.  status: optional device word.
+ *     FTMI_MMA_BF16X6 or FTMI_MMA_F32.  status: optional device word.  ABI 12: OR
+ *     FTMI_RNN_SPREAD into mma to let the call spread a small-H recurrence over the whole
+ *     device (fewer sequences per workgroup group: lower step latency, more workgroups —
+ *     for a recurrence that runs alone; ftmi_rnn_blocks takes the same flag).
  * sync: 16-byte aligned device workspace of ftmi_rnn_workspace_bytes() bytes (zeroed by
  *     the call; holds the arrival counters and the h exchange buffer).  After the stream
  *     has completed, the 32-bit word at byte offset ftmi_rnn_error_offset() is non-zero if
@@ -268,6 +271,7 @@ int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, int32_t Cp, 
  *     event sets FTMI_STATUS_RNN_TIMEOUT in *status.
  * Supported H: GRU 64, 128, 256; LSTM 512 (the ForwardTacotron config).
  * ---------------------------------------------------------------------------------- */
+enum { FTMI_RNN_SPREAD = 0x100 };
 int64_t ftmi_rnn_workspace_bytes(int32_t B, int32_t H, int32_t cell);
 int64_t ftmi_rnn_error_offset(int32_t B);
 /* Workgroups the (first) launch of ftmi_rnn_bidir(cell, B, H, mma) occupies: each is

@@ -114,3 +114,13 @@ def test_workspace_sizes():
     assert lib.ftmi_rnn_workspace_bytes(64, 512, 1) > 0
     assert lib.ftmi_rnn_workspace_bytes(0, 512, 1) == 0
     assert lib.ftmi_rnn_error_offset(64) % 4 == 0
+
+
+def test_build_id_tracks_flags():
+    """a build with extra compile flags carries another id than the default build
+    (so _lib.load refuses it as the package library), and the default id is the sources'."""
+    from forwardtacotron_amd._srchash import source_hash
+    from forwardtacotron_amd.build import build_id
+    assert build_id() == source_hash() == _lib.load().ftmi_build_id().decode()
+    assert build_id(['-DFTMI_X=1']) != build_id()
+    assert build_id(['-DFTMI_X=1']).startswith(source_hash() + '+')

@@ -64,6 +64,65 @@ def test_inputs(tmp_path):
         main(['--synthetic', '--input_tokens', '1,2', 'wavernn'])
 
 
+def test_raw_sentence_file_refused(tmp_path, capsys):
+    """a sentences file of raw English (what the reference's sentences.txt holds)
+    is refused with the reason, never tokenised as phonemes; symbols outside the phoneme
+    set are reported (and dropped, as the reference Tokenizer drops them)."""
+    import argparse
+    from forwardtacotron_amd.gen_forward import read_inputs
+    f = tmp_path / 'sentences.txt'
+    f.write_text('President Trump met with other leaders at the Group of 20 conference.\n',
+                 encoding='utf-8')
+    ns = argparse.Namespace(input_tokens=None, input_phonemes=None, input_text=None,
+                            sentences=str(f))
+    with pytest.raises(SystemExit, match='raw text'):
+        read_inputs(ns)
+    f.write_text('həloʊ "wɜːld"\n', encoding='utf-8')
+    (ids,) = read_inputs(ns)
+    assert 'outside the phoneme set' in capsys.readouterr().out
+    from forwardtacotron_amd.text.tokenizer import Tokenizer
+    assert ids == Tokenizer()('həloʊ wɜːld')
+
+
+def test_parser_grammar_matches_reference():
+    """gen_forward.py:43-61: top-level options, then the vocoder sub-command; only
+    `wavernn` takes --overlap / --target / --voc_checkpoint (defaults 550 / 11000)."""
+    from forwardtacotron_amd.gen_forward import build_parser
+    p = build_parser()
+    a = p.parse_args(['--alpha', '1.5', '--amp', '0.8', 'wavernn', '--voc_checkpoint', 'v.pt',
+                      '-t', '9000'])
+    assert (a.vocoder, a.alpha, a.amp, a.voc_checkpoint, a.target, a.overlap) == \
+        ('wavernn', 1.5, 0.8, 'v.pt', 9000, 550)
+    assert p.parse_args(['griffinlim']).vocoder == 'griffinlim'
+    assert p.parse_args([]).vocoder is None
+    assert p.parse_args(['hifigan']).config == 'config.yaml'
+    with pytest.raises(SystemExit):  # sub-command options belong to wavernn only
+        p.parse_args(['griffinlim', '--target', '5'])
+
+
+def test_checkpoint_from_config(tmp_path, monkeypatch):
+    """gen_forward.py:68-72: no --checkpoint -> Paths(...).forward_checkpoints /
+    'latest_model.pt' of the config's tts_model_id, loaded like an explicit checkpoint."""
+    from forwardtacotron_amd import gen_forward as G
+    from forwardtacotron_amd.checkpoints import save_checkpoint
+    from forwardtacotron_amd.synthetic import default_config
+    cfg = tmp_path / 'config.yaml'
+    cfg.write_text("tts_model_id: 'my_tts'\ndata_path: 'data/'\n", encoding='utf-8')
+    monkeypatch.chdir(tmp_path)
+    path = G.checkpoint_from_config(str(cfg))
+    assert path == tmp_path / 'checkpoints' / 'my_tts.forward' / 'latest_model.pt'
+    model, _ = G.synthetic_tts_model()
+    path.parent.mkdir(parents=True)
+    save_checkpoint(model, None, default_config(), path)
+    loaded = []
+    monkeypatch.setattr(G, 'load_tts_model', lambda p: loaded.append(p) or G.synthetic_tts_model())
+    with pytest.raises(SystemExit, match='GPU'):  # CPU container: stops at the device check
+        G.main(['--config', str(cfg), '--input_tokens', '1,2', 'hifigan'])
+    assert loaded == [str(path)]
+    with pytest.raises(SystemExit, match='valid vocoder'):
+        G.main(['--synthetic', '--input_tokens', '1,2'])
+
+
 def test_checkpoint_roundtrip(tmp_path):
     """save_checkpoint -> gen_forward.load_tts_model (weights_only) restores the weights."""
     from forwardtacotron_amd.checkpoints import save_checkpoint

@@ -136,6 +136,81 @@ def test_griffinlim_batch_lengths(dsp):
     assert not wb[1, 256 * 24:].any()
 
 
+# ---- BASELINE sizes: c2's 821-frame mel, a c3-length batch of 64 ----
+C2_FRAMES = 821  # BASELINE configs[1] (gen_forward.py, B = 1, T = 120 -> T_mel 821)
+
+
+def _speechlike_mel(frames, seed):
+    """A log-mel of a noisy harmonic signal (the reference's wav_to_mel on the oracle)."""
+    y = audio(256 * (frames - 1), seed)
+    return D.wav_to_mel(y)[:, :frames]
+
+
+def test_griffinlim_from_stft_c2_length(dsp):
+    """The 32-iteration GL loop at the c2 length (821 frames) vs the oracle on identical
+    magnitudes and initial phases."""
+    from forwardtacotron_amd import dsp as G
+    y = audio(256 * (C2_FRAMES - 1), 11)
+    S = np.abs(D.stft(y)).astype(np.float32)
+    assert S.shape == (513, C2_FRAMES)
+    ang = D.random_angles(S.shape, 6)
+    ref = D.griffinlim_from_stft(S, ang, n_iter=32)
+    got = G.griffinlim_from_stft(dsp.plan(), torch.from_numpy(np.ascontiguousarray(S.T)).cuda()[None],
+                                 torch.from_numpy(np.ascontiguousarray(ang.T)).cuda()[None], 32)
+    got = got[0].cpu().numpy()
+    assert got.shape == ref.shape == (256 * (C2_FRAMES - 1),)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-4 * np.abs(ref).max())
+
+
+def test_mel_to_stft_c2_length(dsp):
+    """NNLS at the c2 length: the GPU solution's objective over all 821 frames, and per
+    127-frame block (librosa's block structure) against the reference's L-BFGS-B on the
+    first two blocks (the oracle is seconds per block)."""
+    from forwardtacotron_amd import dsp as G
+    mel = _speechlike_mel(C2_FRAMES, 12)
+    M = np.exp(mel).astype(np.float32)
+    A = D.mel_filters(22050, 1024, 80, 0, 8000).astype(np.float32)
+    S = G.mel_to_stft(dsp.plan(), torch.from_numpy(mel).cuda()[None])[0].cpu().numpy().T
+    assert S.shape == (513, C2_FRAMES) and (S >= 0).all()
+    obj = lambda x, m: np.linalg.norm(A.astype(np.float64) @ x - m)  # noqa: E731
+    x0 = np.clip(np.linalg.lstsq(A, M, rcond=None)[0], 0, None)  # the clipped LS start
+    assert obj(S, M) <= obj(x0, M)
+    for s in (0, 127):
+        ref = D.nnls(A, M[:, s:s + 127])
+        blk = S[:, s:s + 127]
+        assert obj(blk, M[:, s:s + 127]) <= obj(ref, M[:, s:s + 127]) * 1.01 + 1e-7 * np.linalg.norm(M[:, s:s + 127])
+
+
+def test_griffinlim_batch_c3_lengths(dsp):
+    """griffinlim_batch on a B = 64 batch of c3-like lengths (frame counts spread up to
+    1368) == each item on its own with the same initial phases (bit for bit), the padded
+    tail of each row zero."""
+    from forwardtacotron_amd import dsp as G
+    plan = dsp.plan()
+    B, F = 64, 1368
+    rng = np.random.Generator(np.random.PCG64(13))
+    frames_np = np.sort(rng.integers(350, F + 1, B))[::-1].copy()
+    frames_np[0] = F
+    base = _speechlike_mel(F, 14)
+    mels = np.stack([np.roll(base, 37 * b, axis=1) for b in range(B)]).astype(np.float32)
+    frames = torch.from_numpy(frames_np.astype(np.int32)).cuda()
+    md = torch.from_numpy(mels).cuda()
+    S = G.mel_to_stft(plan, md, frames)
+    g = torch.Generator(device='cuda')
+    g.manual_seed(3)
+    u = torch.rand(B, F, plan.nb, dtype=torch.float64, device='cuda', generator=g)
+    ang = torch.polar(torch.ones_like(u), u * 6.283185307179586).to(torch.complex64)
+    wb = G.griffinlim_from_stft(plan, S, ang, 32, frames)
+    assert wb.shape == (B, 256 * (F - 1))
+    for b in list(range(0, B, 9)) + [B - 1]:
+        f = int(frames_np[b])
+        Sb = G.mel_to_stft(plan, md[b:b + 1, :, :f].contiguous())
+        np.testing.assert_array_equal(Sb[0].cpu().numpy(), S[b, :f].cpu().numpy())
+        wi = G.griffinlim_from_stft(plan, Sb, ang[b:b + 1, :f].contiguous(), 32)
+        np.testing.assert_array_equal(wb[b, :256 * (f - 1)].cpu().numpy(), wi[0].cpu().numpy())
+        assert not wb[b, 256 * (f - 1):].any()
+
+
 def test_cpu_tensor_raises(dsp):
     from forwardtacotron_amd import dsp as G
     with pytest.raises(RuntimeError):

@@ -39,20 +39,40 @@ def rng():
 # (mma, pre-split weights): fp32 MFMA, bf16x6 splitting both operands per call, bf16x6
 # with the weights split once by ftmi_split_weights, f16x3 on ftmi_split_weights_f16
 # planes (the model's default path)
-MMAS = pytest.mark.parametrize('mma,pre', [(0, False), (1, False), (1, True), (2, True)],
-                               ids=['f32', 'bf16x6', 'bf16x6-presplit', 'f16x3'])
+MMA_CELLS = [(0, False, 'f32'), (1, False, 'bf16x6'), (1, True, 'bf16x6-presplit'),
+             (2, True, 'f16x3')]
+MMAS = pytest.mark.parametrize('mma,pre', [c[:2] for c in MMA_CELLS], ids=[c[2] for c in MMA_CELLS])
+KERNELS = ('tiled', 'slab', 'skinny')
 
 
-def slab_or_skip(kernel, mma, monkeypatch, M=None, N=None):
+def kernel_applies(kernel, mma, M=None, N=None):
     """'skinny': the default choice (the weight-streaming skinny kernel for M <= 256 rows,
-    the slab kernel above); 'slab': the f16x3 slab kernel for every eligible shape
-    (FTMI_GEMM_SKINNY=0); 'tiled': the 128 x 128 tiled kernels only (FTMI_GEMM_SLAB_MIN
-    above any shape here, skinny off)."""
+    the slab kernel above); 'slab': the f16x3 slab kernel for every eligible shape; 'tiled':
+    the 128 x 128 tiled kernels only.  slab / skinny are f16x3 kernels; the skinny kernel
+    takes M <= 256 rows (narrow single-group linears: M <= 1024)."""
     if kernel in ('slab', 'skinny') and mma != 2:
-        pytest.skip(f'the {kernel} kernel is an f16x3 kernel')
+        return False
+    if kernel == 'skinny' and M is not None and M > 256 and not (N is not None and N <= 128 and M <= 1024):
+        return False
+    return True
+
+
+def gemm_cases(shapes, rows=lambda s: None, cols=lambda s: None, ids=None):
+    """pytest params (*shape, mma, pre, kernel) of the APPLICABLE cells only (no runtime
+    skips: a real skip stays visible)."""
+    out = []
+    for i, shape in enumerate(shapes):
+        sid = ids[i] if ids else '-'.join(str(v) for v in shape)
+        for mma, pre, mid in MMA_CELLS:
+            for kernel in KERNELS:
+                if kernel_applies(kernel, mma, rows(shape), cols(shape)):
+                    out.append(pytest.param(*shape, mma, pre, kernel, id=f'{sid}-{mid}-{kernel}'))
+    return out
+
+
+def use_kernel(kernel, monkeypatch):
+    """Route the GEMM family to `kernel` (see kernel_applies)."""
     if kernel == 'skinny':
-        if M is not None and M > 256 and not (N is not None and N <= 128 and M <= 1024):
-            pytest.skip('the skinny kernel takes M <= 256 rows (narrow linears: M <= 1024)')
         return
     monkeypatch.setenv('FTMI_GEMM_SKINNY', '0')
     if kernel == 'tiled':
@@ -64,8 +84,7 @@ def wsplit(w, pre, mma=1):
     return ops.presplit_for(w, mma) if pre else None
 
 
-@MMAS
-@pytest.mark.parametrize('B,T,Cin,N,k,relu,bn,bias', [
+CONV_SHAPES = [
     (2, 37, 64, 256, 5, True, True, False),     # SeriesPredictor conv 1
     (3, 50, 256, 256, 5, True, True, False),    # SeriesPredictor conv 2/3
     (2, 129, 512, 80, 1, False, False, True),   # lin-like (N tail)
@@ -80,10 +99,13 @@ def wsplit(w, pre, mma=1):
     (1, 40, 416, 64, 3, True, True, True),      # 7 splits (one lane per element: 4 + 3)
     (1, 33, 1280, 96, 1, False, False, True),   # 20 splits (4 lanes per element: 4 + 1)
     (1, 25, 2304, 128, 1, True, False, True),   # 36 splits (4 lanes per element: 8 + 1)
-])
-@pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
+]
+
+
+@pytest.mark.parametrize('B,T,Cin,N,k,relu,bn,bias,mma,pre,kernel',
+                         gemm_cases(CONV_SHAPES, rows=lambda s: s[0] * s[1], cols=lambda s: s[3]))
 def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre, kernel, monkeypatch):
-    slab_or_skip(kernel, mma, monkeypatch, B * T, N)
+    use_kernel(kernel, monkeypatch)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
@@ -102,11 +124,9 @@ def test_conv1d(B, T, Cin, N, k, relu, bn, bias, rng, mma, pre, kernel, monkeypa
     close(host(y), ref.transpose(0, 2, 1))
 
 
-@MMAS
-@pytest.mark.parametrize('Cin', [128, 1024])
-@pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
+@pytest.mark.parametrize('Cin,mma,pre,kernel', gemm_cases([(128,), (1024,)], rows=lambda s: 90))
 def test_conv1d_maxpool_residual_transposed(rng, mma, pre, Cin, kernel, monkeypatch):
-    slab_or_skip(kernel, mma, monkeypatch, 90)
+    use_kernel(kernel, monkeypatch)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     B, T, N = 2, 45, 80
@@ -126,7 +146,7 @@ def test_conv1d_maxpool_residual_transposed(rng, mma, pre, Cin, kernel, monkeypa
 def test_conv1d_c2_proj1_maxpool(rng, kernel, monkeypatch):
     """BASELINE config c2 (B = 1, T = 120): the prenet proj1 shape (Cin = 16 x 256, k = 3,
     maxpool fused, ReLU then BN) — 64 channel splits on the skinny kernel."""
-    slab_or_skip(kernel, 2, monkeypatch, 120)
+    use_kernel(kernel, monkeypatch)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     B, T, Cin, N = 1, 120, 4096, 256
@@ -153,12 +173,12 @@ def test_conv1d_strided_input_view(rng, mma, pre):
     close(host(y), full[:, :, C:] @ w.T)
 
 
-@MMAS
-@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 2, 41), (8, 80, 2, 150), (5, 48, 3, 270),
-                                     (16, 256, 1, 120), (3, 80, 2, 128)])
-@pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
+@pytest.mark.parametrize('K,Cin,B,T,mma,pre,kernel',
+                         gemm_cases([(16, 256, 2, 41), (8, 80, 2, 150), (5, 48, 3, 270),
+                                     (16, 256, 1, 120), (3, 80, 2, 128)],
+                                    rows=lambda s: s[2] * s[3]))
 def test_conv_bank(K, Cin, B, T, rng, mma, pre, kernel, monkeypatch):
-    slab_or_skip(kernel, mma, monkeypatch, B * T)
+    use_kernel(kernel, monkeypatch)
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     C = 256
@@ -276,13 +296,12 @@ def test_conv_bank_skinny_schedules(K, Cin, B, T, balanced, rng, monkeypatch):
     close(host(y), ref.transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
 
 
-@MMAS
-@pytest.mark.parametrize('kernel', ['tiled', 'slab', 'skinny'])
-@pytest.mark.parametrize('C,B,T', [(256, 3, 77), (128, 2, 300), (256, 1, 816),
-                                   (160, 1, 90)])  # skinny: 3 splits (2 + 1 in the finish)
+@pytest.mark.parametrize('C,B,T,mma,pre,kernel',
+                         gemm_cases([(256, 3, 77), (128, 2, 300), (256, 1, 816),
+                                     (160, 1, 90)]))  # skinny: 3 splits (2 + 1 in the finish)
 def test_highway(rng, mma, pre, kernel, C, B, T, monkeypatch):
     from forwardtacotron_amd.common_layers import HighwayNetwork
-    slab_or_skip(kernel, mma, monkeypatch)
+    use_kernel(kernel, monkeypatch)
     hw = HighwayNetwork(C)
     sd = {'W1.weight': rng.normal(0, 1 / 16, (C, C)), 'W1.bias': rng.normal(0, .1, C),
           'W2.weight': rng.normal(0, 1 / 16, (C, C)), 'W2.bias': rng.normal(0, .1, C)}
@@ -439,19 +458,22 @@ def _rnn_module(cell, fin, H, rng):
 
 
 RNN_MMAS = pytest.mark.parametrize('rnn_mma', [2, 1, 0], ids=['f16x3', 'bf16x6', 'f32'])
+# fused: the input projection inside the recurrence (ftmi_gru_bidir_fused) exists on the
+# f16x3 path for H 128 / 256 only — only those cells are generated
+GRU_CASES = [pytest.param(H, B, T, m, f, id=f'{"fused" if f else "two-call"}-{H}-{B}-{T}-{mid}')
+             for H, B, T in [(64, 3, 40), (128, 2, 33), (256, 5, 60), (256, 17, 9)]
+             for m, mid in ((2, 'f16x3'), (1, 'bf16x6'), (0, 'f32'))
+             for f in (True, False) if not f or (m == 2 and H in (128, 256))]
 
 
-@RNN_MMAS
-@pytest.mark.parametrize('H,B,T', [(64, 3, 40), (128, 2, 33), (256, 5, 60), (256, 17, 9)])
-@pytest.mark.parametrize('fused', [True, False], ids=['fused', 'two-call'])
+@pytest.mark.parametrize('H,B,T,rnn_mma,fused', GRU_CASES)
 def test_gru_bidir(H, B, T, rng, rnn_mma, fused, monkeypatch):
     """fused: the input projection inside the recurrence (ftmi_gru_bidir_fused, f16x3,
     H 128 / 256); two-call: ftmi_conv1d + ftmi_rnn_bidir."""
     from forwardtacotron_amd import ops
     monkeypatch.setattr(ops, 'RNN_MMA', rnn_mma)
     monkeypatch.setattr(ops, 'FUSED_GRU', fused)
-    if fused and not ops.gru_fused_ok(H, 256):
-        pytest.skip('no fused form for this shape / path')
+    assert not fused or ops.gru_fused_ok(H, 256)
     m, sd = _rnn_module('gru', 256, H, rng)
     x = rng.normal(0, 1, (B, T, 256)).astype(np.float32)
     ref = O.gru_bidir(sd, 'r', x, np.float32)
@@ -468,21 +490,35 @@ def test_lstm_bidir(rng, rnn_mma, monkeypatch):
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize('cell,H,B,T', [('lstm', 512, 1, 23), ('lstm', 512, 17, 12),
-                                        ('lstm', 512, 64, 9), ('gru', 256, 1, 31),
-                                        ('gru', 256, 64, 7), ('gru', 256, 130, 5),
-                                        ('gru', 128, 20, 14), ('gru', 64, 64, 11),
-                                        ('gru', 64, 1, 40)])
-def test_rnn_f16x3_kernels(cell, H, B, T, rng, monkeypatch):
+F16X3_SHAPES = [('lstm', 512, 1, 23), ('lstm', 512, 17, 12), ('lstm', 512, 64, 9),
+                ('gru', 256, 1, 31), ('gru', 256, 64, 7), ('gru', 256, 130, 5),
+                ('gru', 128, 20, 14), ('gru', 64, 64, 11), ('gru', 64, 1, 40)]
+# kernel variants: rnn_row_kernel (H 128 / 256 / 512) with 16 / 8 / 4 live sequences per
+# group and with the spread choice, rnn_bidir_kernel (the default) and its compute-wave h-store
+# form (FTMI_RNN_CSTORE=1); H = 64 always runs rnn_bidir_kernel — only the applicable cells
+# are generated
+ROW_VARIANTS = ['row16', 'row8', 'row4', 'spread', 'legacy', 'cstore']
+F16X3_CASES = [pytest.param(*shape, v, id=f'{shape[0]}{shape[1]}-B{shape[2]}-{v}')
+               for shape in F16X3_SHAPES
+               for v in (ROW_VARIANTS if shape[1] >= 128 else ['legacy'])]
+
+
+@pytest.mark.parametrize('cell,H,B,T,variant', F16X3_CASES)
+def test_rnn_f16x3_kernels(cell, H, B, T, variant, rng, monkeypatch):
     """The f16x3 recurrence over batch sizes that exercise one chunk (B = 1: padded grid,
     one group per XCD), a partial chunk, whole XCDs (B = 64: 8 groups), several launches'
-    worth of groups (B = 130) — against the numpy oracle.  (B <= 4 normally takes the GEMV
-    kernel: switched off here.)"""
+    worth of groups (B = 130) — against the numpy oracle, on every kernel variant.  (B <= 4
+    normally takes the GEMV kernel: switched off here.)"""
     from forwardtacotron_amd import ops
     monkeypatch.setattr(ops, 'RNN_MMA', 2)
     monkeypatch.setenv('FTMI_RNN_GEMV', '0')
+    monkeypatch.setenv('FTMI_RNN_ROW', '0' if variant in ('legacy', 'cstore') else '1')
+    monkeypatch.setenv('FTMI_RNN_CSTORE', '1' if variant == 'cstore' else '0')
+    if variant.startswith('row'):
+        monkeypatch.setenv('FTMI_RNN_NB', variant[3:])
     fin = 512 if cell == 'lstm' else 256
     m, sd = _rnn_module(cell, fin, H, rng)
+    m.spread = variant == 'spread'
     x = rng.normal(0, 1, (B, T, fin)).astype(np.float32)
     ref = (O.lstm_bidir if cell == 'lstm' else O.gru_bidir)(sd, 'r', x, np.float32)
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
@@ -520,16 +556,21 @@ def test_rnn_f16_weight_range_guard(rng, monkeypatch):
     assert int(st.item()) & 2
 
 
-def test_lstm_through_lr_index_and_lengths(rng):
+@pytest.mark.parametrize('B,variant', [(2, 'gemv'), (9, 'row16'), (9, 'row4'), (9, 'legacy')])
+def test_lstm_through_lr_index_and_lengths(B, variant, rng, monkeypatch):
     """LSTM reading phoneme-rate projections through the LR index map == LSTM over the
-    expanded sequence; with lengths it reproduces pack_padded / pad_packed semantics."""
+    expanded sequence; with lengths it reproduces pack_padded / pad_packed semantics (B = 2:
+    the GEMV kernel; B = 9: the row kernel with 16 / 4 live sequences per group, legacy)."""
     from forwardtacotron_amd import ops
+    monkeypatch.setenv('FTMI_RNN_ROW', '0' if variant == 'legacy' else '1')
+    if variant.startswith('row'):
+        monkeypatch.setenv('FTMI_RNN_NB', variant[3:])
     m, sd = _rnn_module('lstm', 512, 512, rng)
-    B, T = 2, 11
+    T = 11
     x = rng.normal(0, 1, (B, T, 512)).astype(np.float32)
     dur = rng.uniform(-0.5, 5.0, (B, T)).astype(np.float32)
     xe, _ = O.length_regulator(x, dur)
-    lens = np.array([xe.shape[1], xe.shape[1] - 5])
+    lens = np.array([xe.shape[1] - (5 * b) % 13 for b in range(B)])
     ref = O.lstm_bidir(sd, 'r', xe, np.float32, lengths=lens, pad_value=-11.5129)
     d = dev(dur)
     off, tot, _ = ops.duration_counts(d, apply_fill=False)

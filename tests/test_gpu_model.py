@@ -6,6 +6,8 @@ Bounds (north star: mel frames within 1e-4 fp32, LengthRegulator bit-exact):
   mean |mel_post - ref| < 1e-4, mean |mel - ref| < 1e-4, max |.| < 2e-3 (|mel| ~ 5),
   durations to 1e-5 and LengthRegulator counts identical (=> identical T_mel).
 """
+import contextlib
+
 import numpy as np
 import pytest
 import torch
@@ -216,7 +218,8 @@ def test_graph_with_user_callbacks(gpu_model, monkeypatch):
     from forwardtacotron_amd import forward_tacotron as FT
     g = load_golden('gen_callbacks')
     x = torch.from_numpy(g['x']).cuda()
-    kw = dict(alpha=1.2, pitch_function=lambda p: p * 2.0 + 0.1, energy_function=lambda e: e - 0.05)
+    kw = dict(alpha=1.2, pitch_function=FT.graph_safe(lambda p: p * 2.0 + 0.1),
+              energy_function=FT.graph_safe(lambda e: e - 0.05))
     monkeypatch.setattr(FT, 'GRAPH', False)
     eager = gpu_model.generate(x, **kw)
     monkeypatch.setattr(FT, 'GRAPH', True)
@@ -227,6 +230,71 @@ def test_graph_with_user_callbacks(gpu_model, monkeypatch):
         for k in ('mel', 'mel_post', 'dur', 'pitch', 'energy'):
             assert torch.equal(o[k], eager[k]), k
     check(outs[-1], g)
+
+
+def test_unmarked_callback_follows_python_state(gpu_model, monkeypatch):
+    """a callback not marked graph_safe runs eagerly on every call, so Python-side
+    state it reads (a closure variable here) is seen by each call, as the reference calls
+    it; a graph_safe-marked one is captured (and would replay the captured value)."""
+    from forwardtacotron_amd import forward_tacotron as FT
+    g = load_golden('gen_b3')
+    x = torch.from_numpy(g['x']).cuda()
+    monkeypatch.setattr(FT, 'GRAPH', True)
+    _fresh_graphs(gpu_model)
+    amp = [1.0]
+    fn = lambda p: p * amp[0]  # noqa: E731
+    outs = []
+    for a in (1.0, 1.0, 1.5, 0.5):  # eager, (would-be) capture, replays
+        amp[0] = a
+        outs.append(gpu_model.generate(x, pitch_function=fn))
+    assert not gpu_model.__dict__.get('_ftmi_graphs')  # nothing captured
+    monkeypatch.setattr(FT, 'GRAPH', False)
+    for a, o in zip((1.0, 1.0, 1.5, 0.5), outs):
+        amp[0] = a
+        ref = gpu_model.generate(x, pitch_function=fn)
+        for k in ('pitch', 'mel_post'):
+            assert torch.equal(o[k], ref[k]), (a, k)
+    assert not torch.equal(outs[2]['pitch'], outs[3]['pitch'])
+    # marked graph_safe: captured on the second sighting
+    monkeypatch.setattr(FT, 'GRAPH', True)
+    _fresh_graphs(gpu_model)
+    safe = FT.graph_safe(lambda p: p * 1.25)
+    for _ in range(3):
+        gpu_model.generate(x, pitch_function=safe)
+    assert len(gpu_model.__dict__['_ftmi_graphs']) == 1
+
+
+def test_range_guard_rerun_is_checked(monkeypatch, synth_sd):
+    """the exact-path rerun triggered by a range bit is status-checked like the
+    first pass — a recurrence timeout during the rerun raises RnnTimeout (spin bound 1 in
+    the rerun only)."""
+    from forwardtacotron_amd import _lib, ops
+    from forwardtacotron_amd import forward_tacotron as FT
+    from forwardtacotron_amd.synthetic import default_config
+    sd = dict(synth_sd)
+    sd['embedding.weight'] = sd['embedding.weight'] * np.float32(1e5)  # range bit, pass 1
+    m = FT.ForwardTacotron.from_config(default_config())
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.cuda().eval()
+    x = torch.from_numpy(load_golden('gen_b3')['x']).cuda()
+    monkeypatch.setattr(FT, 'GRAPH', False)
+    lib = _lib.load()
+    orig = ops.exact_paths
+
+    @contextlib.contextmanager
+    def exact_with_spin_1():
+        with orig():
+            lib.ftmi_set_rnn_spin_limit(1)
+            try:
+                yield
+            finally:
+                torch.cuda.synchronize()
+                lib.ftmi_set_rnn_spin_limit(0)
+
+    monkeypatch.setattr(ops, 'exact_paths', exact_with_spin_1)
+    with pytest.raises(ops.RnnTimeout):
+        m.generate(x)
+    torch.cuda.synchronize()
 
 
 def test_graph_sees_new_weights(gpu_model, synth_sd, monkeypatch):

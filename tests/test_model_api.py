@@ -124,3 +124,37 @@ def test_torchscript_export_fails_with_reason(kind):
     m = WaveRNN.from_config(cfg) if kind == 'wavernn' else init_tts_model(cfg)
     with pytest.raises(RuntimeError, match='cannot be compiled by torch.jit.script'):
         torch.jit.script(m)
+
+
+def test_run_checked_checks_the_rerun(monkeypatch):
+    """the exact-path rerun after a range bit is status-checked like the first
+    pass (a timeout there raises RnnTimeout; reduce applies to it too); a clean rerun
+    returns the rerun's output."""
+    from forwardtacotron_amd import ops
+    st = torch.zeros(1, dtype=torch.int32)
+    monkeypatch.setattr(ops, 'status_word', lambda device: st)
+
+    def pass_bits(*bits):
+        calls = []
+
+        def fn():
+            calls.append(ops.forced_exact())
+            st.fill_(bits[len(calls) - 1])
+            return len(calls)
+        return fn, calls
+
+    fn, calls = pass_bits(1, ops.STATUS_RNN_TIMEOUT)
+    with pytest.raises(ops.RnnTimeout):
+        ops.run_checked(fn, 'cpu')
+    assert calls == [False, True]
+    fn, calls = pass_bits(2, 0)
+    assert ops.run_checked(fn, 'cpu') == 2 and calls == [False, True]
+    fn, calls = pass_bits(0)
+    assert ops.run_checked(fn, 'cpu') == 1 and calls == [False]
+    # a reduce (sharded generation) sees the rerun's word as well
+    seen = []
+    fn, calls = pass_bits(1, 0)
+    red = lambda w: (seen.append(int(w)), torch.full_like(w, ops.STATUS_RNN_TIMEOUT if len(seen) == 2 else int(w)))[1]  # noqa: E731
+    with pytest.raises(ops.RnnTimeout):
+        ops.run_checked(fn, 'cpu', reduce=red)
+    assert seen == [1, 0]

@@ -190,3 +190,29 @@ def test_generate_sharded_gpu_matches_single_call(tmp_path):
     assert got.shape == ref.shape
     np.testing.assert_allclose(got, ref, atol=1e-4, rtol=1e-5)
     np.testing.assert_array_equal(O.duration_counts(dg), O.duration_counts(dr))
+
+
+def _subgroup_gather(rank, world, port):
+    from forwardtacotron_amd import sharded as S
+    _init(rank, world, port)
+    try:
+        sub = dist.new_group([1, 2])  # every rank creates it; global rank 0 is not a member
+        if rank in (1, 2):
+            rows = torch.full((rank, 3), float(rank))
+            sizes, _ = S.shard_sizes(rows.size(0), 0, sub, rows.device)
+            assert sizes == [1, 2]
+            got = S.gather_rows_to(rows, sizes, dst=0, group=sub)
+            if rank == 1:  # rank 0 OF THE GROUP = global rank 1
+                assert torch.equal(got, torch.tensor([[1.] * 3, [2.] * 3, [2.] * 3]))
+            else:
+                assert got is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_to_subgroup_without_global_rank0():
+    """gather_rows_to's dst is a rank within the group; with a subgroup that
+    excludes global rank 0 the rows land on the group's rank 0 (dist.gather is given the
+    matching global rank)."""
+    mp.spawn(_subgroup_gather, args=(3, _port()), nprocs=3, join=True)
