@@ -1551,7 +1551,10 @@ __device__ unsigned long long ftmi_skinny_stamps[4096 * 8];
   } while (0)
 #endif
 
-template <bool MAXPOOL, bool BANK = false>
+// DIAG (timing experiments only, FTMI_SKINNY_DIAG on the bank schedule; results invalid):
+// bit 0 = the A fragments read once before the loop (no LDS reads in it), bit 1 = no MFMAs
+// (the loaded weights feed one VALU add), bit 2 = every weight load from one L2-hot line
+template <bool MAXPOOL, bool BANK = false, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmParams p) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[SK_CPB * 2 * SK_AIMG];
   SKSTAMP(0);
@@ -1679,7 +1682,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     auto loadB = [&](int s, f16x8 &b0, f16x8 &b1) {
       const int j = s / nch, c = s - j * nch;
       const int ch = (c_begin + c) * 32 + fs * 8;
-      const int off = j * Cin + (ch < Cin ? ch : 0);  // Cin % 16 == 0: wholly in or out
+      const int off = (DIAG & 4) ? fs * 8 : j * Cin + (ch < Cin ? ch : 0);  // Cin % 16 == 0
       b0 = *(const f16x8 *)(w0 + off);
       b1 = *(const f16x8 *)(w0 + plane + off);
     };
@@ -1689,6 +1692,14 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     // per-step vmcnt waits 21.7 / 18.5 us, an 8-step ring 23.5 / 20.6, against 21.1 / 15.8
     // for this form: the waves are not bound by the weight-load latency alone.)
     f16x8 rb0[SK_PF], rb1[SK_PF];
+    f16x8 dh[(DIAG & 1) ? 8 : 1], dt[(DIAG & 1) ? 8 : 1];
+    if constexpr (DIAG & 1) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        dh[mi] = *(const f16x8 *)(lds + (mi * 16 + fr) * SL_P + fs * 8);
+        dt[mi] = *(const f16x8 *)(lds + SK_AIMG + (mi * 16 + fr) * SL_P + fs * 8);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < SK_PF; ++u) loadB(min(s_begin + u, s_end - 1), rb0[u], rb1[u]);
     for (int s0 = s_begin; s0 < s_end; s0 += SK_PF) {
@@ -1701,21 +1712,30 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
           f16x8 ah[8], at[8];
 #pragma unroll
           for (int mi = 0; mi < 8; ++mi) {
-            const bool ok = (vmask[mi] >> j) & 1u;
-            const int o = (ok ? mi * 16 + fr + j + dp : SK_ZROW) * SL_P + fs * 8;
-            ah[mi] = *(const f16x8 *)(Ab + o);
-            at[mi] = *(const f16x8 *)(Ab + SK_AIMG + o);
+            if constexpr (DIAG & 1) {
+              ah[mi] = dh[mi];
+              at[mi] = dt[mi];
+            } else {
+              const bool ok = (vmask[mi] >> j) & 1u;
+              const int o = (ok ? mi * 16 + fr + j + dp : SK_ZROW) * SL_P + fs * 8;
+              ah[mi] = *(const f16x8 *)(Ab + o);
+              at[mi] = *(const f16x8 *)(Ab + SK_AIMG + o);
+            }
           }
           const f16x8 z = {};
           const bool bok = s < s_end && (c_begin + c) * 32 + fs * 8 < Cin;
           const f16x8 b0 = bok ? rb0[u] : z, b1 = bok ? rb1[u] : z;
           const f16x8 bh = b0 * (_Float16)(1.0f / H3_SCALE);
+          if constexpr (DIAG & 2) {
+            acc[0][0] += (float)bh[0] + (float)b1[0] + (float)ah[u & 7][0] + (float)at[u & 7][0];
+          } else {
 #pragma unroll
-          for (int mi = 0; mi < 8; ++mi) acc[mi] = mma16(at[mi], bh, acc[mi]);  // small terms first
+            for (int mi = 0; mi < 8; ++mi) acc[mi] = mma16(at[mi], bh, acc[mi]);  // small terms first
 #pragma unroll
-          for (int mi = 0; mi < 8; ++mi) acc[mi] = mma16(ah[mi], b1, acc[mi]);
+            for (int mi = 0; mi < 8; ++mi) acc[mi] = mma16(ah[mi], b1, acc[mi]);
 #pragma unroll
-          for (int mi = 0; mi < 8; ++mi) acc[mi] = mma16(ah[mi], b0, acc[mi]);
+            for (int mi = 0; mi < 8; ++mi) acc[mi] = mma16(ah[mi], b0, acc[mi]);
+          }
         }
         // refill the slot in place (a copy of a pending load would wait for it)
         loadB(min(s + SK_PF, s_end - 1), rb0[u], rb1[u]);
@@ -2369,7 +2389,17 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
   for (int i = 0; bank && i < q.ngroups; ++i) bank = q.g[i].k == q.ngroups - i;
   if (bank) {
     dim3 grid(MT * (q.ngroups / 2) * (q.g[0].N / 32), q.split), block(512);
-    hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true>), grid, block, 0, s, q);
+    const char *dg = getenv("FTMI_SKINNY_DIAG");  // timing experiments (results invalid)
+    switch (dg ? atoi(dg) : 0) {
+#define FTMI_SK_DIAG(D_)                                                                   \
+  case D_:                                                                                 \
+    hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true, D_>), grid, block, 0, s, q); \
+    break;
+      FTMI_SK_DIAG(1) FTMI_SK_DIAG(2) FTMI_SK_DIAG(3) FTMI_SK_DIAG(4) FTMI_SK_DIAG(7)
+#undef FTMI_SK_DIAG
+      default:
+        hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true>), grid, block, 0, s, q);
+    }
   } else {
     dim3 grid(MT * q.ngroups * NT, q.split), block(512);
     if (maxpool)

@@ -133,6 +133,21 @@ struct RnnParams {
              // bit 2 = no drain
 };
 
+// workspace: [control: err, census, flags, counters][hx: 2 * 2*nchunks * 16*H floats], sized
+// for chunks of 8 sequences: the most groups any kernel form runs (a spread GRU on
+// rnn_bidir_kernel: 8 live sequences per group in the same 16-column slab format)
+constexpr int WS_CHUNK = 8;
+static int64_t ws_chunks(int64_t B) { return (B + WS_CHUNK - 1) / WS_CHUNK; }
+static int64_t ctl_bytes(int64_t nchunks) {
+  return (WS_GROUPS_OF((int)(2 * nchunks)) + 2 * nchunks * CNT_PAD) * (int64_t)sizeof(unsigned);
+}
+
+// host-side guard before a launch: the exchange words a kernel form indexes (2 parities x
+// ngroups_total slabs of slab_words) fit the exchange region of the workspace for (B, H)
+static bool hx_fits(const RnnParams &p, int H, int64_t slab_words) {
+  return 2 * (int64_t)p.ngroups_total * slab_words <= 2 * (2 * ws_chunks(p.B)) * NB * (int64_t)H;
+}
+
 __device__ __forceinline__ float fast_sigmoid(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
 }
@@ -191,7 +206,11 @@ __device__ __forceinline__ void report_timeout(const RnnParams &p) {
 
 constexpr int FUSE_CIN = 256;  // input width of the fused-projection instances
 
-template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false, bool CST = false>
+// NBL: live sequences per group (16, or 8 to spread a recurrence over twice the groups: every
+// workgroup then acquires and stores half the h bytes per step; the MFMA columns past NBL are
+// dead)
+template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false, bool CST = false,
+          int NBL = NB>
 __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(const RnnParams p) {
   constexpr bool X6 = MODE != 0;  // 16x16x32 fragment layout (bf16x6 and f16x3)
   constexpr bool H3 = MODE == 2;
@@ -217,6 +236,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   // wave's 16 chunks are its own cells: CPT == 1), the comm wave only the y rows — barrier C
   // and the comm wave's stage read leave the h hand-off's critical path
   static_assert(!CST || (H3 && !LOCAL && CPT == 1 && U == 16), "compute-wave h stores");
+  static_assert(NBL == NB || (NBL == 8 && !LOCAL && !FUSE), "live sequences per group");
   constexpr int KWI = FUSE ? FUSE_CIN / WK : 32;  // input channels per wave
   constexpr int KSI = KWI / 32;                   // their 32-deep k-steps
   constexpr int RR = FUSE ? 2 * R : R;            // reduction rows: W_hh h [+ W_ih x]
@@ -304,9 +324,9 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         const int f = lane + 64 * i;
         {  // y: float4 f = 4 units of one sequence
           const int bl = f / (U / 4);
-          yb[i] = chunk * NB + bl;
+          yb[i] = chunk * NBL + bl;
           k0s[i] = u0 + (f % (U / 4)) * 4;
-          ok[i] = yb[i] < p.B;
+          ok[i] = bl < NBL && yb[i] < p.B;
         }
         if constexpr (H3) {  // h: 16-B chunk f = (seq, 8 units, plane) of f16 halves
           const int bl = f / (U / 4), rem = f % (U / 4), plane = rem & 1;
@@ -344,6 +364,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
           // every sequence slot of the chunk, the batch tail's too: consumers check the tags
           // of all 16 columns of their fragments
           const u32x4 v = *(const u32x4 *)&hstage[(lane + 64 * i) * 4];
+          if (NBL != NB && (lane + 64 * i) / (U / 4) >= NBL) continue;  // dead sequence
           if (xcd_mode)  // stays in this XCD's L2, read back by same-XCD sc1 loads
             __builtin_amdgcn_raw_buffer_store_b128(v, rs, hofs[i], soff, 0);
           else  // write-through (sc1)
@@ -426,7 +447,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   if (wbad && p.status) atomicOr(p.status, 2u);
 
   // ---- per-thread cells: cell c = tid + 256*j -> (unit u = c % U, seq b = c / U) ------
-  int cu[CPT], cb[CPT], len[CPT], hxo[CPT];
+  int cu[CPT], cb[CPT], cbl[CPT], len[CPT], hxo[CPT];
   bool cvalid[CPT];
   float hstate[CPT], cstate[CPT], bhh[CPT][G], bih[FUSE ? CPT : 1][G];
 #pragma unroll
@@ -434,8 +455,9 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
     const int c = tid + 256 * j;
     cu[j] = c % U;
     const int bl = c / U;
-    cb[j] = chunk * NB + bl;
-    cvalid[j] = cb[j] < p.B;
+    cbl[j] = bl;
+    cb[j] = chunk * NBL + bl;
+    cvalid[j] = bl < NBL && cb[j] < p.B;
     hstate[j] = 0.f;
     cstate[j] = 0.f;
     len[j] = (p.lengths && cvalid[j]) ? p.lengths[cb[j]] : p.T;
@@ -600,6 +622,10 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         hv[4 * i + 3] = v.w;
       }
     } else {
+      if constexpr (NBL != NB) {  // dead columns multiply zeros
+#pragma unroll
+        for (int i = 0; i < NL; ++i) hr[i] = (u32x4){0u, 0u, 0u, 0u};
+      }
       // Tagged acquire: every exchanged h value carries h_tag(step) in its mantissa LSB;
       // re-load until this wave's whole K range carries the tag of h_{t-1}.  4-byte
       // accesses are single-copy atomic, so a torn 16-byte store only delays the read;
@@ -609,10 +635,12 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       // fp32 words carry the tag in bit 0; f16 pairs in bits 0 and 16 (both halves)
       const unsigned tmask = HSPLIT ? 0x00010001u : 1u;
       const bool want1 = h_tag(t - 1) != 0u;  // uniform
+      const bool hlive = (lane & 15) < NBL;  // this lane's h column is a live sequence
       for (unsigned spins = 0;; ++spins) {
 #pragma unroll
         for (int i = 0; i < NL; ++i)
-          hr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + i * 1024, soff, 16);
+          if (NBL == NB || hlive)
+            hr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + i * 1024, soff, 16);
         // every tag equals want iff (want 1) the AND of all words has the tag bits set,
         // (want 0) their OR has none: a 3-input reduction instead of a test per word
         bool fresh;
@@ -627,7 +655,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
           for (int i = 1; i < NL; ++i) o |= hr[i];
           fresh = ((o.x | o.y | o.z | o.w) & tmask) == 0u;
         }
-        if (__all(fresh) || (p.diag & 2)) break;
+        if (__all(fresh || !hlive) || (p.diag & 2)) break;
         if (spins > p.spin_limit) {
           if (lane == 0) {
             s_abort = 1;
@@ -733,7 +761,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
     // cell update
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
-      const int bl = cb[j] - chunk * NB;
+      const int bl = cbl[j];
       float gs[G], gi[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
@@ -811,7 +839,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       // chunks 16 wave .. 16 wave + 15: read back (same wave, LDS in order) and store
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      if (lane < 16) {
+      if (lane < 16 && (16 * wave + lane) / (U / 4) < NBL) {  // live sequences only
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 v = *(const u32x4 *)&hstage[(16 * wave + lane) * 4];
         if (xcd_mode)
@@ -1342,6 +1370,7 @@ int launch_row(RnnParams p, int max_blocks, hipStream_t s) {
   constexpr int BPG = H / 16;
   const int nchunks = (p.B + NBL - 1) / NBL;
   p.ngroups_total = 2 * nchunks;
+  if (!hx_fits(p, H, (int64_t)H * NBL)) return FTMI_E_SHAPE;  // never index past the workspace
   const int max_groups = (max_blocks / BPG) & ~1;
   if (max_groups < 2) return FTMI_E_UNSUPPORTED;
   for (int c0 = 0; c0 < nchunks; c0 += max_groups / 2) {
@@ -1383,8 +1412,14 @@ int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
   return FTMI_OK;
 }
 
-template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false, bool CST = false>
+template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false, bool CST = false,
+          int NBL = NB>
 int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
+  if (NBL != NB) {  // chunks of NBL sequences (the caller counted chunks of NB)
+    nchunks = (p.B + NBL - 1) / NBL;
+    p.ngroups_total = 2 * nchunks;
+  }
+  if (!hx_fits(p, H, (int64_t)NB * H)) return FTMI_E_SHAPE;  // never index past the workspace
   constexpr int BPG = H / U;
   int max_groups = (max_blocks / BPG) & ~1;
   if (max_groups < 2) return FTMI_E_UNSUPPORTED;
@@ -1405,7 +1440,7 @@ int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
     int nblk = p.ngroups * BPG;
     if (BPG > 1 && pad_env && p.xcd_local && p.ngroups < 8 && 8 * BPG <= max_blocks)
       nblk = 8 * BPG;
-    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, FUSE, CST>), dim3(nblk),
+    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, FUSE, CST, NBL>), dim3(nblk),
                        dim3(BPG == 1 ? 256 : 320), 0, s, p);
     FTMI_CHECK_LAUNCH();
   }
@@ -1475,6 +1510,24 @@ static int row_nbl(int B, int H, bool spread, int maxb) {
   return 16;
 }
 
+// FTMI_RNN_CSTORE=0 (read per call) keeps the comm wave's h stores: measured at c3, the
+// compute waves' own stores take the postnet GRU 1.315 -> 1.116 us/step, the LSTM 1.55 ->
+// 1.535 (barrier C and the stage read leave the hand-off's critical path)
+static bool cst_enabled() {
+  const char *v = getenv("FTMI_RNN_CSTORE");
+  return !(v && atoi(v) == 0);
+}
+// live sequences per group of a spread f16x3 GRU on rnn_bidir_kernel: 8 when twice the groups
+// still fit the device at once (the c3 postnet GRU: 256 instead of 128 workgroups, half the h
+// bytes per workgroup and step); FTMI_RNN_NB=16 keeps 16 (read per call)
+static int legacy_nbl(int cell, int B, int H, int mma, bool spread, int maxb) {
+  const char *v = getenv("FTMI_RNN_NB");
+  if (!spread || mma != 2 || cell != 0 || (H != 256 && H != 128) || !cst_enabled() ||
+      (v && atoi(v) == 16))
+    return NB;
+  return 2 * ((B + 7) / 8) * (H / 16) <= maxb ? 8 : NB;
+}
+
 extern "C" int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t mma) {
   if (B <= 0 || H <= 0 || H % 16 != 0) return 0;
   const bool spread = (mma & FTMI_RNN_SPREAD) != 0;
@@ -1495,24 +1548,21 @@ extern "C" int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t m
   const int maxb = device_cu_count();
   const int max_groups = (maxb / bpg) & ~1;
   if (max_groups < 2) return 0;
-  const int nchunks = (B + NB - 1) / NB;
+  const int nbl = legacy_nbl(cell, B, H, mma, spread, maxb);
+  const int nchunks = (B + nbl - 1) / nbl;
   const int ngroups = 2 * (nchunks < max_groups / 2 ? nchunks : max_groups / 2);
   int nblk = ngroups * bpg;
   if (bpg > 1 && ngroups < 8 && 8 * bpg <= maxb) nblk = 8 * bpg;  // launch_rnn's padding
   return nblk;
 }
 
-// workspace: [control: err, census, flags, counters][hx: 2 * 2*nchunks * 16*H floats]
-static int64_t ctl_bytes(int64_t nchunks) {
-  return (WS_GROUPS_OF((int)(2 * nchunks)) + 2 * nchunks * CNT_PAD) * (int64_t)sizeof(unsigned);
-}
-
 extern "C" int64_t ftmi_rnn_workspace_bytes(int32_t B, int32_t H, int32_t cell) {
   (void)cell;
   if (B <= 0 || H <= 0) return 0;
-  const int64_t nchunks = (B + NB - 1) / NB;
+  const int64_t nchunks = ws_chunks(B);
   return ctl_bytes(nchunks) + 2 * (2 * nchunks) * NB * (int64_t)H * (int64_t)sizeof(float);
 }
+
 
 extern "C" uint32_t ftmi_set_rnn_spin_limit(uint32_t limit) {
   const unsigned prev = g_spin_limit;
@@ -1532,7 +1582,7 @@ static int rnn_setup(RnnParams &p, int B, int T, int H, int cell, const float *w
                      int64_t y_stride, uint32_t *status, void *sync, hipStream_t s,
                      int &nchunks) {
   nchunks = (B + NB - 1) / NB;
-  const int64_t ctl = ctl_bytes(nchunks);
+  const int64_t ctl = ctl_bytes(ws_chunks(B));
   const int64_t wsb = ftmi_rnn_workspace_bytes(B, H, cell);
   hipError_t e = hipMemsetAsync(sync, 0, (size_t)wsb, s);
   if (e != hipSuccess) return (int)e;
@@ -1636,14 +1686,16 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
     const char *v = getenv("FTMI_RNN_WK");
     return v ? atoi(v) : 4;
   }();
-  // FTMI_RNN_CSTORE=1 (A/B): compute-wave h stores (rnn_bidir_kernel CST; read per call)
-  const char *cst_v = getenv("FTMI_RNN_CSTORE");
-  const int cst_env = cst_v ? atoi(cst_v) : 0;
-  if (cst_env && mma == 2 && cell == 1 && H == 512)
-    return launch_rnn<1, 512, 16, 4, 2, false, true>(p, nchunks, maxb, s);
-  if (cst_env && mma == 2 && cell == 0 && (H == 256 || H == 128)) {
-    if (H == 256) return launch_rnn<0, 256, 16, 4, 2, false, true>(p, nchunks, maxb, s);
-    return launch_rnn<0, 128, 16, 4, 2, false, true>(p, nchunks, maxb, s);
+  // f16x3, 16 units per workgroup: the compute waves store their own h (CST) and a spread
+  // GRU runs 8 live sequences per group (legacy_nbl)
+  if (mma == 2 && cst_enabled() && ((cell == 1 && H == 512) || (cell == 0 && (H == 256 || H == 128)))) {
+    const bool nb8 = legacy_nbl(cell, B, H, mma, spread, maxb) == 8;
+    if (cell == 1) return launch_rnn<1, 512, 16, 4, 2, false, true>(p, nchunks, maxb, s);
+    if (H == 256)
+      return nb8 ? launch_rnn<0, 256, 16, 4, 2, false, true, 8>(p, nchunks, maxb, s)
+                 : launch_rnn<0, 256, 16, 4, 2, false, true>(p, nchunks, maxb, s);
+    return nb8 ? launch_rnn<0, 128, 16, 4, 2, false, true, 8>(p, nchunks, maxb, s)
+               : launch_rnn<0, 128, 16, 4, 2, false, true>(p, nchunks, maxb, s);
   }
   if (wk_env == 2 && mma == 2 && cell == 1 && H == 512)
     return launch_rnn<1, 512, 16, 2, 2>(p, nchunks, maxb, s);

@@ -12,24 +12,43 @@ from oracle import ft_oracle as O
 pytestmark = pytest.mark.gpu
 
 
-def test_cli_end_to_end(tmp_path, gpu_model):
+def test_cli_end_to_end(tmp_path, gpu_model, synth_sd):
+    from forwardtacotron_amd import dsp as G
     from forwardtacotron_amd.gen_forward import main
+    from forwardtacotron_amd.synthetic import default_config
+    from oracle import dsp_oracle as D
+    from oracle import ft_torch_cpu as TC
     ids = '12,40,7,88,23,5,61,19,33,2,77,45'
     outs = {}
     for voc in ('hifigan', 'melgan', 'griffinlim'):
+        np.random.seed(7)  # the griffinlim vocoder draws its phases from np.random (librosa)
         (p,) = main(['--synthetic', '--input_tokens', ids, '--amp', '1.2', '--out',
                      str(tmp_path), voc])
         assert p.name.startswith('1_forward_0k_alpha1.0_amp1.2_' + voc)
         outs[voc] = p
     m = np.load(outs['hifigan'], allow_pickle=False)
     assert torch.equal(torch.load(outs['melgan'], weights_only=True), torch.from_numpy(m))
-    x = torch.tensor([[int(v) for v in ids.split(',')]]).cuda()
-    ref = gpu_model.generate(x, pitch_function=lambda v: v * 1.2)['mel_post'].cpu().numpy()
+    x = torch.tensor([[int(v) for v in ids.split(',')]])
+    ref = gpu_model.generate(x.cuda(), pitch_function=lambda v: v * 1.2)['mel_post'].cpu().numpy()
     assert m.shape == ref.shape == (1, 80, ref.shape[2])
     assert np.abs(m - ref).max() < 1e-5
+    # the written mel against the torch-CPU restatement of the reference (gen_forward.py's
+    # callbacks): the north-star bar, mean |d| < 1e-4
+    cpu = TC.generate(TC.to_torch(synth_sd), x, pitch_function=lambda v: v * 1.2)['mel_post'].numpy()
+    assert cpu.shape == m.shape and np.abs(m - cpu).mean() < 1e-4, np.abs(m - cpu).mean()
+    # the .wav: 16-bit PCM of Griffin-Lim on the same seeded phases as the oracle's
+    # librosa-0.7.2 iteration (np.random.seed(7) -> rand(513, T)), over the device NNLS
+    # magnitudes (the NNLS minimiser itself is checked by its objective, test_gpu_dsp.py)
     with wave.open(str(outs['griffinlim']), 'rb') as w:
         assert w.getframerate() == 22050 and w.getsampwidth() == 2
         assert w.getnframes() == 256 * (m.shape[2] - 1)  # librosa istft length, center=True
+        pcm = np.frombuffer(w.readframes(w.getnframes()), dtype='<i2').astype(np.float64) / 32767
+    T = m.shape[2]
+    plan = G.DSP.from_config(default_config()).plan()
+    S = G.mel_to_stft(plan, torch.from_numpy(m).cuda())[0].cpu().numpy().T
+    ang = np.exp(2j * np.pi * np.random.RandomState(7).rand(513, T)).astype(np.complex64)
+    wref = D.griffinlim_from_stft(S, ang, n_iter=32)
+    assert np.abs(pcm - wref).max() <= 1e-4 * np.abs(wref).max() + 1.0 / 32767, np.abs(pcm - wref).max()
     # the reference's `wavernn` sub-command (gen_forward.py:54-57, :125-131): batched
     # WaveRNN generation of the same mel, wave_len = (T - 1) hop
     (p,) = main(['--synthetic', '--input_tokens', ids, '--amp', '1.2', '--out', str(tmp_path),

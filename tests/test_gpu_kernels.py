@@ -493,14 +493,15 @@ def test_lstm_bidir(rng, rnn_mma, monkeypatch):
 F16X3_SHAPES = [('lstm', 512, 1, 23), ('lstm', 512, 17, 12), ('lstm', 512, 64, 9),
                 ('gru', 256, 1, 31), ('gru', 256, 64, 7), ('gru', 256, 130, 5),
                 ('gru', 128, 20, 14), ('gru', 64, 64, 11), ('gru', 64, 1, 40)]
-# kernel variants: rnn_row_kernel (H 128 / 256 / 512) with 16 / 8 / 4 live sequences per
-# group and with the spread choice, rnn_bidir_kernel (the default) and its compute-wave h-store
-# form (FTMI_RNN_CSTORE=1); H = 64 always runs rnn_bidir_kernel — only the applicable cells
-# are generated
-ROW_VARIANTS = ['row16', 'row8', 'row4', 'spread', 'legacy', 'cstore']
+# kernel variants: rnn_row_kernel (H 128 / 256 / 512, FTMI_RNN_ROW=1) with 16 / 8 / 4 live
+# sequences per group and with the spread choice; rnn_bidir_kernel (the default: compute-wave
+# h stores), with the comm wave's h stores (FTMI_RNN_CSTORE=0), and spread (GRU: 8 live
+# sequences per group); H = 64 always runs rnn_bidir_kernel — only the applicable cells are
+# generated
+ROW_VARIANTS = ['row16', 'row8', 'row4', 'rowspread', 'default', 'comm', 'spread']
 F16X3_CASES = [pytest.param(*shape, v, id=f'{shape[0]}{shape[1]}-B{shape[2]}-{v}')
                for shape in F16X3_SHAPES
-               for v in (ROW_VARIANTS if shape[1] >= 128 else ['legacy'])]
+               for v in (ROW_VARIANTS if shape[1] >= 128 else ['default'])]
 
 
 @pytest.mark.parametrize('cell,H,B,T,variant', F16X3_CASES)
@@ -512,13 +513,13 @@ def test_rnn_f16x3_kernels(cell, H, B, T, variant, rng, monkeypatch):
     from forwardtacotron_amd import ops
     monkeypatch.setattr(ops, 'RNN_MMA', 2)
     monkeypatch.setenv('FTMI_RNN_GEMV', '0')
-    monkeypatch.setenv('FTMI_RNN_ROW', '0' if variant in ('legacy', 'cstore') else '1')
-    monkeypatch.setenv('FTMI_RNN_CSTORE', '1' if variant == 'cstore' else '0')
-    if variant.startswith('row'):
+    monkeypatch.setenv('FTMI_RNN_ROW', '1' if variant.startswith('row') else '0')
+    monkeypatch.setenv('FTMI_RNN_CSTORE', '0' if variant == 'comm' else '1')
+    if variant in ('row16', 'row8', 'row4'):
         monkeypatch.setenv('FTMI_RNN_NB', variant[3:])
     fin = 512 if cell == 'lstm' else 256
     m, sd = _rnn_module(cell, fin, H, rng)
-    m.spread = variant == 'spread'
+    m.spread = variant in ('rowspread', 'spread')
     x = rng.normal(0, 1, (B, T, fin)).astype(np.float32)
     ref = (O.lstm_bidir if cell == 'lstm' else O.gru_bidir)(sd, 'r', x, np.float32)
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
@@ -556,13 +557,13 @@ def test_rnn_f16_weight_range_guard(rng, monkeypatch):
     assert int(st.item()) & 2
 
 
-@pytest.mark.parametrize('B,variant', [(2, 'gemv'), (9, 'row16'), (9, 'row4'), (9, 'legacy')])
+@pytest.mark.parametrize('B,variant', [(2, 'gemv'), (9, 'row16'), (9, 'row4'), (9, 'default')])
 def test_lstm_through_lr_index_and_lengths(B, variant, rng, monkeypatch):
     """LSTM reading phoneme-rate projections through the LR index map == LSTM over the
     expanded sequence; with lengths it reproduces pack_padded / pad_packed semantics (B = 2:
     the GEMV kernel; B = 9: the row kernel with 16 / 4 live sequences per group, legacy)."""
     from forwardtacotron_amd import ops
-    monkeypatch.setenv('FTMI_RNN_ROW', '0' if variant == 'legacy' else '1')
+    monkeypatch.setenv('FTMI_RNN_ROW', '1' if variant.startswith('row') else '0')
     if variant.startswith('row'):
         monkeypatch.setenv('FTMI_RNN_NB', variant[3:])
     m, sd = _rnn_module('lstm', 512, 512, rng)
