@@ -100,6 +100,9 @@ struct GemmParams {
   // y_split_c > 0 = the pool_out epilogue writes y as split rows of y_split_c channels
   int x_split;
   int y_split_c;
+  // skinny conv bank (FTMI_BANK_LAST): per-tile arrival counters (zero between launches);
+  // the last split block of a tile sums the splits and finishes it (no finish launch)
+  unsigned *tile_cnt;
   GemmGroup g[MAX_GROUPS];
 };
 
@@ -1554,7 +1557,8 @@ __device__ unsigned long long ftmi_skinny_stamps[4096 * 8];
 // DIAG (timing experiments only, FTMI_SKINNY_DIAG on the bank schedule; results invalid):
 // bit 0 = the A fragments read once before the loop (no LDS reads in it), bit 1 = no MFMAs
 // (the loaded weights feed one VALU add), bit 2 = every weight load from one L2-hot line
-template <bool MAXPOOL, bool BANK = false, int DIAG = 0>
+// LAST (BANK, split > 1): the tile's last split block finishes it (see conv_bank_qb_kernel)
+template <bool MAXPOOL, bool BANK = false, int DIAG = 0, bool LAST = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmParams p) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[SK_CPB * 2 * SK_AIMG];
   SKSTAMP(0);
@@ -1767,7 +1771,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
           const int row = m0 + mi * 16 + 4 * fs + i;
           if (cok && row < p.M) {
             bad |= !__builtin_isfinite(acc[mi][i]);
-            part[(size_t)row * p.ldp + col] = acc[mi][i] * cs;
+            if constexpr (LAST)  // write-through: the last arriver reads it with sc1 loads
+              __hip_atomic_store(part + (size_t)row * p.ldp + col, acc[mi][i] * cs,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+              part[(size_t)row * p.ldp + col] = acc[mi][i] * cs;
           }
         }
     } else {
@@ -1792,6 +1800,267 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     }
   }
   SKSTAMP(3);
+  if constexpr (LAST && BANK) {  // the tile = this block's (pair, two column sets)
+    __shared__ int s_last;
+    if (p.split > 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores done
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(p.tile_cnt + blockIdx.x, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == (unsigned)p.split - 1;
+        if (s_last)  // every split block has added: zero for the next launch
+          __hip_atomic_store(p.tile_cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (s_last) {
+        // element e = (row, unit, column): 16 lanes read one unit's 64-B row piece; units
+        // (group of the pair, column set) as the waves' cw
+        const int rows = min(SK_BM, p.M - m0);
+        for (int e = threadIdx.x; e < rows * 64; e += 512) {
+          const int colf = e & 15, uu = (e >> 4) & 3, row = m0 + (e >> 6);
+          const int g = (uu >> 1) ? p.ngroups - 1 - gi : gi;
+          const GemmGroup &GF = p.g[g];
+          const int c = (nt + (uu & 1)) * 16 + colf;
+          if (c >= GF.N) continue;
+          const float *src = p.part + (size_t)row * p.ldp + GF.ycol0 + c;
+          float v = 0.f;
+          for (int sp = 0; sp < p.split; ++sp)
+            v += __hip_atomic_load(src + (size_t)sp * p.M * p.ldp, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          bad |= !__builtin_isfinite(v);
+          if (GF.bias) v += GF.bias[c];
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (GF.scale) v = v * GF.scale[c] + GF.shift[c];
+          if (p.y) p.y[(int64_t)row * p.y_stride + GF.ycol0 + c] = v;
+        }
+      }
+    }
+  }
+  if (bad && p.status) atomicOr(p.status, 1u);
+}
+
+// ---- the c2 conv bank, quarter-balanced (FTMI_BANK_QB, default on) ---------------------
+// The BANK schedule of conv_gemm_skinny_kernel gives a block the group pair (k, K + 1 - k)
+// and two 16-column sets, but a wave only one (unit, half): the heavy group's waves run k
+// steps, the light group's K + 1 - k, so on each SIMD one wave is left alone for most of the
+// loop and the block waits for it at the end.  Here every wave takes one QUARTER of the step
+// range of a heavy unit AND one quarter of the light unit of the same column set: all 8
+// waves run (K + 1) / 4 steps.  The four quarters of a unit meet in LDS (summed in quarter
+// order: deterministic) and all 8 waves share the tail stores (wave w: unit w / 2, row
+// fragments 4 (w % 2) .. + 4).  Slab, per-step loop and epilogue are the skinny kernel's.
+// LAST: the split blocks publish their partial sums write-through (sc1) and bump the tile's
+// arrival counter after every storing wave's vmcnt(0) wait and a barrier; the block whose add
+// returns split - 1 resets the counter, reads the split partials with sc1 loads in split order
+// (deterministic) and applies the epilogue — MI355X_MICROARCH.md "Valid forms", first row of
+// the sc1 table (agent-scope atomic add, the last adder told by its return value).
+constexpr int QB_RED = 4 * 4 * 8 * 64;  // f32x4 [unit][quarter][row fragment][lane]
+
+template <bool LAST>
+__global__ __launch_bounds__(512, 1) void conv_bank_qb_kernel(const GemmParams p) {
+  __shared__ __attribute__((aligned(16))) f32x4 red[QB_RED];  // 128 KB; the slab aliases it
+  _Float16 *const lds = (_Float16 *)red;
+  static_assert(SK_CPB * 2 * SK_AIMG * sizeof(_Float16) <= sizeof(red), "slab alias");
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const int MT = (p.M + SK_BM - 1) / SK_BM, NC = p.g[0].N / 16;
+  const int bid = blockIdx.x, mt = bid % MT, v = bid / MT;
+  const int gi = (2 * v) / NC;  // the pair's heavier group (k = K - gi): its slab
+  const int nt = (2 * v) % NC;  // first of the block's two 16-column sets
+  const GemmGroup &G = p.g[gi];
+  const int m0 = mt * SK_BM, k = G.k, pad = G.pad, Cin = p.Cin;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fs = lane >> 4;
+  const int nch_all = (Cin + 31) / 32;
+  const int c_begin = blockIdx.y * p.kc_per;
+  const int nch = min(nch_all - c_begin, p.kc_per);
+  const int SR = SK_BM + k - 1;
+
+  // ---- prologue: the slab of this block's chunks (as conv_gemm_skinny_kernel) -------------
+  constexpr int SK_ASLOTS = (SK_CPB * SK_SR * 8 + 511) / 512;
+  const int nitems = nch * SR * 8;
+  f32x4 av[SK_ASLOTS];
+#pragma unroll
+  for (int i = 0; i < SK_ASLOTS; ++i) {
+    const int idx = tid + 512 * i;
+    av[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
+    const int ch = (c_begin + c) * 32 + seg * 4;
+    if (idx < nitems && ch < Cin) {
+      int m = m0 - pad + sr;
+      m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);
+      av[i] = *(const f32x4 *)(p.x + (int64_t)m * p.x_stride + ch);
+    }
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < SK_ASLOTS; ++i) {
+    const int idx = tid + 512 * i;
+    if (idx >= nitems) break;
+    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
+    const f32x4 x = av[i];
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+    f16x4 h, t;
+    split2h(x, h, t);
+    _Float16 *dst = lds + c * 2 * SK_AIMG + sr * SL_P + seg * 4;
+    *(f16x4 *)dst = h;
+    *(f16x4 *)(dst + SK_AIMG) = t;
+  }
+  if (tid < SK_CPB * 2 * (SL_P / 8)) {
+    const int img = tid / (SL_P / 8), part = tid % (SL_P / 8);
+    *(u32x4 *)(lds + img * SK_AIMG + SK_ZROW * SL_P + part * 8) = (u32x4){0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+  bool bad = !(amax <= 65504.f);
+
+  // ---- wave w: column set w & 1, quarter w >> 1 of the heavy and of the light unit ------
+  const int cset = wave & 1, q = wave >> 1;
+  const int col0 = (nt + cset) * 16;
+  f32x4 acc[2][8];
+  auto run_unit = [&](int gw, f32x4 (&a)[8]) {
+    const GemmGroup &GW = p.g[gw];
+    const int kw = GW.k, padw = GW.pad, dp = pad - padw;
+    const int nsteps = nch * kw;
+    const int s_begin = (nsteps * q) >> 2, s_end = (nsteps * (q + 1)) >> 2;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) a[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (col0 >= GW.N || s_end <= s_begin) return;  // wave-uniform
+    unsigned vmask[8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int m = m0 + mi * 16 + fr;
+      unsigned msk = 0;
+      if (m < p.M) {
+        const int t = m % p.T;
+        const int lo = max(padw - t, 0), hi = min(p.T - 1 + padw - t, kw - 1);
+        if (lo <= hi) msk = (2u << hi) - (1u << lo);
+      }
+      vmask[mi] = msk;
+    }
+    const int n = col0 + fr < GW.N ? col0 + fr : GW.N - 1;
+    const _Float16 *w0 = (const _Float16 *)GW.w3 + (int64_t)n * GW.Kpad;
+    const int64_t plane = (int64_t)GW.N * GW.Kpad;
+    auto loadB = [&](int s, f16x8 &b0, f16x8 &b1) {
+      const int j = s / nch, c = s - j * nch;
+      const int ch = (c_begin + c) * 32 + fs * 8;
+      const int off = j * Cin + (ch < Cin ? ch : 0);
+      b0 = *(const f16x8 *)(w0 + off);
+      b1 = *(const f16x8 *)(w0 + plane + off);
+    };
+    f16x8 rb0[SK_PF], rb1[SK_PF];
+#pragma unroll
+    for (int u = 0; u < SK_PF; ++u) loadB(min(s_begin + u, s_end - 1), rb0[u], rb1[u]);
+    for (int s0 = s_begin; s0 < s_end; s0 += SK_PF) {
+#pragma unroll
+      for (int u = 0; u < SK_PF; ++u) {
+        const int s = s0 + u;
+        const int sl = min(s, s_end - 1), j = sl / nch, c = sl - j * nch;
+        const _Float16 *Ab = lds + c * 2 * SK_AIMG;
+        f16x8 ah[8], at[8];
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+          const bool ok = (vmask[mi] >> j) & 1u;
+          const int o = (ok ? mi * 16 + fr + j + dp : SK_ZROW) * SL_P + fs * 8;
+          ah[mi] = *(const f16x8 *)(Ab + o);
+          at[mi] = *(const f16x8 *)(Ab + SK_AIMG + o);
+        }
+        const f16x8 z = {};
+        const bool bok = s < s_end && (c_begin + c) * 32 + fs * 8 < Cin;
+        const f16x8 b0 = bok ? rb0[u] : z, b1 = bok ? rb1[u] : z;
+        const f16x8 bh = b0 * (_Float16)(1.0f / H3_SCALE);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) a[mi] = mma16(at[mi], bh, a[mi]);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) a[mi] = mma16(ah[mi], b1, a[mi]);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) a[mi] = mma16(ah[mi], b0, a[mi]);
+        loadB(min(s + SK_PF, s_end - 1), rb0[u], rb1[u]);
+      }
+    }
+  };
+  run_unit(__builtin_amdgcn_readfirstlane(gi), acc[0]);
+  run_unit(__builtin_amdgcn_readfirstlane(p.ngroups - 1 - gi), acc[1]);
+
+  // ---- the four quarters of each unit meet in LDS (the slab is dead after the barrier) ---
+  __syncthreads();
+#pragma unroll
+  for (int g2 = 0; g2 < 2; ++g2)
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) red[(((2 * cset + g2) * 4 + q) * 8 + mi) * 64 + lane] = acc[g2][mi];
+  __syncthreads();
+  // wave w finishes unit u = w >> 1 (column set u >> 1, heavy / light u & 1), fragments
+  // 4 (w & 1) .. + 4
+  const int u = wave >> 1, mlo = (wave & 1) * 4;
+  const int gw = __builtin_amdgcn_readfirstlane((u & 1) ? p.ngroups - 1 - gi : gi);
+  const GemmGroup &GW = p.g[gw];
+  const int ucol = (nt + (u >> 1)) * 16 + fr;
+  const bool cok = ucol < GW.N;
+  const int ec = cok ? ucol : GW.N - 1;
+  const float cs = GW.colscale[ec];
+  const bool direct = !(p.split > 1 || p.force_part);
+  const float bias = direct && GW.bias ? GW.bias[ec] : 0.f;
+  const float sc = direct && GW.scale ? GW.scale[ec] : 1.f;
+  const float sh = direct && GW.scale ? GW.shift[ec] : 0.f;
+#pragma unroll
+  for (int mj = 0; mj < 4; ++mj) {
+    const int mi = mlo + mj;
+    f32x4 v4 = red[((u * 4 + 0) * 8 + mi) * 64 + lane];
+    v4 += red[((u * 4 + 1) * 8 + mi) * 64 + lane];
+    v4 += red[((u * 4 + 2) * 8 + mi) * 64 + lane];
+    v4 += red[((u * 4 + 3) * 8 + mi) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + mi * 16 + 4 * fs + i;
+      if (!cok || row >= p.M) continue;
+      bad |= !__builtin_isfinite(v4[i]);
+      if (!direct) {
+        float *dst = p.part + (size_t)blockIdx.y * p.M * p.ldp + (size_t)row * p.ldp + GW.ycol0 + ucol;
+        if constexpr (LAST)  // write-through: the last arriver reads it with sc1 loads
+          __hip_atomic_store(dst, v4[i] * cs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          *dst = v4[i] * cs;
+      } else {
+        float y = v4[i] * cs + bias;
+        if (p.relu) y = fmaxf(y, 0.f);
+        if (GW.scale) y = y * sc + sh;
+        if (p.y) p.y[(int64_t)row * p.y_stride + GW.ycol0 + ucol] = y;
+      }
+    }
+  }
+  if constexpr (LAST) {
+    __shared__ int s_last;
+    if (p.split > 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores done
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(p.tile_cnt + blockIdx.x, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == (unsigned)p.split - 1;
+        if (s_last)  // every split block has added: zero for the next launch
+          __hip_atomic_store(p.tile_cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (s_last) {
+        // element e = (row, unit, column): 16 consecutive lanes read one unit's 64-B row piece
+        const int rows = min(SK_BM, p.M - m0);
+        for (int e = tid; e < rows * 64; e += 512) {
+          const int col = e & 15, uu = (e >> 4) & 3, row = m0 + (e >> 6);
+          const int g = (uu & 1) ? p.ngroups - 1 - gi : gi;
+          const GemmGroup &GF = p.g[g];
+          const int c = (nt + (uu >> 1)) * 16 + col;
+          if (c >= GF.N) continue;
+          const float *src = p.part + (size_t)row * p.ldp + GF.ycol0 + c;
+          float v = 0.f;
+          for (int sp = 0; sp < p.split; ++sp)
+            v += __hip_atomic_load(src + (size_t)sp * p.M * p.ldp, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          if (GF.bias) v += GF.bias[c];
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (GF.scale) v = v * GF.scale[c] + GF.shift[c];
+          if (p.y) p.y[(int64_t)row * p.y_stride + GF.ycol0 + c] = v;
+        }
+      }
+    }
+  }
   if (bad && p.status) atomicOr(p.status, 1u);
 }
 
@@ -2390,7 +2659,23 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
   if (bank) {
     dim3 grid(MT * (q.ngroups / 2) * (q.g[0].N / 32), q.split), block(512);
     const char *dg = getenv("FTMI_SKINNY_DIAG");  // timing experiments (results invalid)
-    switch (dg ? atoi(dg) : 0) {
+    // FTMI_BANK_QB=1: the quarter-balanced kernel (opt-in: measured slower, 27-29 against
+    // 24-25 us for the c2 prenet bank + finish)
+    const char *qb = getenv("FTMI_BANK_QB");
+    const bool qbk = qb && atoi(qb) == 1 && !(dg && atoi(dg) != 0) && !q.yt && !q.residual;
+    const bool last = q.tile_cnt && q.split > 1 && (int)grid.x <= FTMI_BANK_COUNTERS &&
+                      !q.yt && !q.residual && !(dg && atoi(dg) != 0);
+    if (last) {  // finished in-kernel by each tile's last split block: no finish launch
+      if (qbk)
+        hipLaunchKernelGGL(conv_bank_qb_kernel<true>, grid, block, 0, s, q);
+      else
+        hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true, 0, true>), grid, block, 0, s, q);
+      FTMI_CHECK_LAUNCH();
+      return FTMI_OK;
+    }
+    if (qbk)
+      hipLaunchKernelGGL(conv_bank_qb_kernel<false>, grid, block, 0, s, q);
+    else switch (dg ? atoi(dg) : 0) {
 #define FTMI_SK_DIAG(D_)                                                                   \
   case D_:                                                                                 \
     hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true, D_>), grid, block, 0, s, q); \
@@ -2649,7 +2934,9 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
   p.y = y;
   p.y_stride = y_stride;
   p.status = status;
-  if (pool_out & ~(FTMI_BANK_POOL | FTMI_BANK_Y_SPLIT | FTMI_BANK_X_SPLIT)) return FTMI_E_ARG;
+  if (pool_out & ~(FTMI_BANK_POOL | FTMI_BANK_Y_SPLIT | FTMI_BANK_X_SPLIT | FTMI_BANK_LAST))
+    return FTMI_E_ARG;
+  if ((pool_out & FTMI_BANK_LAST) && (split_k <= 1 || !split_ws)) return FTMI_E_ARG;
   p.pool_out = pool_out & FTMI_BANK_POOL;
   if (pool_out & FTMI_BANK_Y_SPLIT) {  // split output rows need the pooled epilogue
     if (!p.pool_out) return FTMI_E_UNSUPPORTED;
@@ -2690,6 +2977,10 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
   if (split_k > 1) {
     p.split_req = split_k;
     p.part = split_ws;
+    if (pool_out & FTMI_BANK_LAST) {  // tile counters first, then the partial sums
+      p.tile_cnt = (unsigned *)split_ws;
+      p.part = split_ws + FTMI_BANK_COUNTERS;
+    }
   }
   return launch(p, EPI_CONV, false, tile0, mma, ftmi_hs(stream));
 }

@@ -112,9 +112,11 @@ def run_checked(fn, device, reduce=None):
     out, w = attempt()
     if w and not _FORCED:
         # the rerun is checked like the first pass (a timeout there raises too; its range
-        # bits cannot recur on the range-unlimited paths)
+        # bits cannot recur on the range-unlimited paths); afterwards the word shows the
+        # bits that caused it, as the call's record
         with exact_paths():
             out, _ = attempt()
+        st.fill_(w)
     return out
 
 
@@ -373,18 +375,44 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
     M = B * T
     flops = 2.0 * M * Cout * Cin * K * (K + 1) / 2
     mma, wsp = _gemm_mma(mma, w_split)
-    sk, part = 0, None
+    sk, part, last = 0, None, 0
     if not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
         sk = _skinny_split(Cin)  # weight-streaming kernel: partial sums, finished in order
-        part = torch.empty(sk * M * K * Cout, device=x.device, dtype=_f32)
+        if os.environ.get('FTMI_BANK_LAST', '1') != '0':
+            # tile counters + partials, finished in-kernel by each tile's last split block
+            part, last = _bank_workspace(sk * M * K * Cout, x.device), BANK_LAST
+        else:
+            part = torch.empty(sk * M * K * Cout, device=x.device, dtype=_f32)
     launch('ftmi_conv_bank_split', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}'
            f'{",pool" if pool else ""}{",split" if split_out else ""}{",xsplit" if x_split else ""}]',
            flops, 4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
            x.data_ptr(), xs, B, T, Cin, w.data_ptr(), wsp, K, Cout,
            scale.data_ptr(), shift.data_ptr(), y.data_ptr(), y.stride(1), mma,
            status_word(x.device).data_ptr(), sk, _ptr(part),
-           int(pool) | (2 * int(split_out)) | (4 * int(x_split)), _stream())
+           int(pool) | (2 * int(split_out)) | (4 * int(x_split)) | last, _stream())
     return y
+
+
+BANK_LAST, BANK_COUNTERS = 8, 4096  # include/ftmi.h FTMI_BANK_LAST, FTMI_BANK_COUNTERS
+_BANK_WS = {}
+
+
+def _bank_workspace(n_part: int, device) -> torch.Tensor:
+    """The FTMI_BANK_LAST workspace of the current stream: BANK_COUNTERS tile counters (zero
+    once; every launch leaves them zero) followed by n_part floats of partial sums.  One per
+    (device, stream) — launches on one stream are ordered, so they may share it — kept alive
+    for graph replays that captured its address; grown (a new zeroed buffer) when too small."""
+    stream = torch.cuda.current_stream(device)
+    key = (torch.device(device), stream.cuda_stream)
+    t = _BANK_WS.get(key)
+    if t is None or t.numel() < BANK_COUNTERS + n_part:
+        if t is not None:  # the old buffer may still be in use by queued work
+            _BANK_OLD.append(t)
+        t = _BANK_WS[key] = torch.zeros(BANK_COUNTERS + n_part, device=device, dtype=_f32)
+    return t
+
+
+_BANK_OLD = []  # superseded workspaces (kept: a captured graph may still replay them)
 
 
 def split_rows(x: torch.Tensor) -> torch.Tensor:

@@ -62,7 +62,15 @@ enum { FTMI_STATUS_F16_RANGE = 1, FTMI_STATUS_WHH_RANGE = 2, FTMI_STATUS_RNN_TIM
 /* ftmi_conv_bank_split pool_out flags (ABI 10; 0 / 1 keep their ABI 9 meaning) */
 enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
        FTMI_BANK_Y_SPLIT = 2, /* with FTMI_BANK_POOL: y as f16x3 split rows of K*Cout */
-       FTMI_BANK_X_SPLIT = 4  /* x given as f16x3 split rows of Cin (FTMI_MMA_F16X3) */ };
+       FTMI_BANK_X_SPLIT = 4, /* x given as f16x3 split rows of Cin (FTMI_MMA_F16X3) */
+       FTMI_BANK_LAST = 8     /* ABI 12, with split_k > 1: split_ws starts with
+                                 FTMI_BANK_COUNTERS 32-bit tile counters, zeroed once by the
+                                 caller and left zero by every launch; the partial sums follow.
+                                 The weight-streaming bank then finishes in-kernel (each tile's
+                                 last split block sums the splits in order) instead of a second
+                                 launch.  One workspace per stream: concurrent launches must not
+                                 share the counters. */ };
+enum { FTMI_BANK_COUNTERS = 4096 };
 
 /* ABI version; bumped on any signature change (12: FTMI_RNN_SPREAD flag of ftmi_rnn_bidir / ftmi_rnn_blocks). */
 int ftmi_abi_version(void);

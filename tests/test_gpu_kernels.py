@@ -220,6 +220,32 @@ def test_conv_bank_pooled(K, Cin, B, T, rng, monkeypatch):
     close(yp, O.maxpool_k2_s1_p1(ref).transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
 
 
+def test_conv_bank_last_arriver_counters(rng):
+    """FTMI_BANK_LAST: every launch leaves the tile counters zero, so banks of different
+    split counts sharing the stream's workspace (prenet: 4 splits, postnet: 2) and repeated
+    calls give bit-identical results."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+
+    def bank(K, Cin, T):
+        C = 256
+        x = dev(rng.normal(0, 1, (1, T, Cin)).astype(np.float32))
+        ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
+        wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
+        w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
+        sc = dev(rng.uniform(0.5, 1.5, K * C).astype(np.float32))
+        sh = dev(rng.normal(0, 0.1, K * C).astype(np.float32))
+        return lambda: ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3)
+
+    pre, post = bank(16, 256, 120), bank(8, 80, 100)
+    a0, b0 = host(pre()), host(post())
+    for _ in range(3):
+        assert np.array_equal(host(pre()), a0)
+        assert np.array_equal(host(post()), b0)
+    key = (torch.device('cuda', torch.cuda.current_device()), torch.cuda.current_stream().cuda_stream)
+    assert not ops._BANK_WS[key][:ops.BANK_COUNTERS].any()  # counters back to zero
+
+
 def split_rows_host(v):
     """The f16x3 split rows of include/ftmi.h (per row C heads, then C scaled tails)."""
     h = v.astype(np.float16)
@@ -273,16 +299,22 @@ def test_split_rows_bank_to_proj1(K, Cin, B, T, split_k, rng, monkeypatch):
         ops.conv1d(ys, w1, 3, 1, mma=0, x_split=True)
 
 
-@pytest.mark.parametrize('balanced', ['1', '0'])
+@pytest.mark.parametrize('schedule', ['pairs', 'pairs-finish', 'quarters', 'quarters-finish', 'groups'])
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (8, 80, 1, 100), (4, 64, 2, 50),
                                      (16, 256, 2, 100)])
-def test_conv_bank_skinny_schedules(K, Cin, B, T, balanced, rng, monkeypatch):
-    """The weight-streaming bank at batch-1 sizes on both block schedules
-    (FTMI_BANK_BALANCED: group pairs (k, K + 1 - k) per block, or one group per block),
-    f16x3, against the numpy oracle."""
+def test_conv_bank_skinny_schedules(K, Cin, B, T, schedule, rng, monkeypatch):
+    """The weight-streaming bank at batch-1 sizes on every block schedule: group pairs
+    (k, K + 1 - k) per block with one (unit, half) per wave (the default), the same with each
+    wave on a quarter of a heavy and of a light unit (conv_bank_qb_kernel, FTMI_BANK_QB=1),
+    one group per block (FTMI_BANK_BALANCED=0); each with the in-kernel last-arriver finish
+    (FTMI_BANK_LAST, default) or the finish launch; f16x3, against the numpy oracle."""
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
-    monkeypatch.setenv('FTMI_BANK_BALANCED', balanced)
+    monkeypatch.setenv('FTMI_BANK_BALANCED', '0' if schedule == 'groups' else '1')
+    monkeypatch.setenv('FTMI_BANK_QB', '1' if schedule.startswith('quarters') else '0')
+    # the tile's last split block finishes in-kernel (FTMI_BANK_LAST, default), or *-finish:
+    # the separate finish launch
+    monkeypatch.setenv('FTMI_BANK_LAST', '0' if schedule.endswith('-finish') else '1')
     C = 256
     x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
     ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]

@@ -149,6 +149,7 @@ def test_run_checked_checks_the_rerun(monkeypatch):
     assert calls == [False, True]
     fn, calls = pass_bits(2, 0)
     assert ops.run_checked(fn, 'cpu') == 2 and calls == [False, True]
+    assert int(st.item()) == 2  # the word keeps the bits that caused the rerun
     fn, calls = pass_bits(0)
     assert ops.run_checked(fn, 'cpu') == 1 and calls == [False]
     # a reduce (sharded generation) sees the rerun's word as well

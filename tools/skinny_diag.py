@@ -38,13 +38,25 @@ def main():
     sc = torch.ones(K * C, device='cuda')
     sh = torch.zeros(K * C, device='cuda')
     wbytes = 4.0 * C * C * K * (K + 1) / 2
+    diags = sys.argv[2].split(',') if len(sys.argv) > 2 else ['0', '1', '2', '3', '4', '7']
     for _ in range(rounds):
-        for d in ('0', '1', '2', '3', '4', '7'):
+        for qb, last in (('0', '1'), ('0', '0'), ('1', '1'), ('1', '0')):
+            os.environ['FTMI_BANK_QB'] = qb
+            os.environ['FTMI_BANK_LAST'] = last
+            os.environ['FTMI_SKINNY_DIAG'] = '0'
+            t = timed(lambda: ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3))
+            print(f'FTMI_BANK_QB={qb} FTMI_BANK_LAST={last}: bank+finish {t:6.1f} us  '
+                  f'({wbytes / t / 1e3:6.0f} GB/s of weights)', flush=True)
+        os.environ['FTMI_BANK_LAST'] = '0'
+        os.environ['FTMI_BANK_QB'] = '0'
+        for d in diags:
+            if d == '0':
+                continue
             os.environ['FTMI_SKINNY_DIAG'] = d
             t = timed(lambda: ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3))
-            print(f'diag {d}: bank+finish {t:6.1f} us  ({wbytes / t / 1e6:6.0f} GB/s of weights)',
-                  flush=True)
+            print(f'diag {d} (pairs kernel): bank+finish {t:6.1f} us', flush=True)
     os.environ['FTMI_SKINNY_DIAG'] = '0'
+    os.environ.pop('FTMI_BANK_QB')
 
 
 if __name__ == '__main__':

@@ -1,5 +1,8 @@
 """Summarise a rocprofv3 --kernel-trace CSV: per-kernel totals and the timeline of the last
-generate() step (start offset, duration, overlap).  usage: python tools/timeline.py <dir>"""
+generate() step (start offset, duration, overlap).  usage: python tools/timeline.py <dir>
+[marker]: with a marker (a kernel-name substring launched once per step, e.g.
+duration_counts_kernel for FastPitch) the window between its last two launches is shown
+instead of the ForwardTacotron LSTM-based step."""
 import csv, glob, sys
 from collections import defaultdict
 
@@ -10,6 +13,20 @@ for r in rows:
 rows.sort(key=lambda r: r['s'])
 name = lambda r: r['Kernel_Name'].replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0][:70]
 # steps: the LSTM kernel marks each generate(); take the window between the last two
+if len(sys.argv) > 2:
+    marks = [i for i, r in enumerate(rows) if sys.argv[2] in r['Kernel_Name']]
+    a, b = marks[-2], marks[-1]
+    t0 = rows[a]['s']
+    print(f'window between the last two {sys.argv[2]}: {b - a} kernels, '
+          f'wall {(rows[b]["s"] - t0) / 1e6:.3f} ms')
+    tot = defaultdict(float)
+    for r in rows[a:b]:
+        tot[name(r)] += (r['e'] - r['s']) / 1e3
+    for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:25]:
+        print(f'   {v:9.1f} us  {k}')
+    for r in rows[a:b]:
+        print(f'   {(r["s"] - t0) / 1e3:9.1f} us  +{(r["e"] - r["s"]) / 1e3:8.1f} us  q{r.get("Queue_Id", "?"):>3}  {name(r)}')
+    sys.exit(0)
 marks = [i for i, r in enumerate(rows) if 'rnn_bidir_kernel<1' in r['Kernel_Name']]
 if len(marks) >= 2:
     # the step = from the first kernel after the previous LSTM's postnet to this LSTM's tail
