@@ -283,6 +283,7 @@ def main():
     # kernels the per-launch probe cannot see: one more generate() with the phase eager,
     # after the timed region, gives their per-kernel times (the prenet bank, --kernels).
     kern_all = kern
+    from forwardtacotron_amd import fast_pitch as fp_module
     if (world == 1 and args.model == 'forward_tacotron' and ft_module.GRAPH
             and x.numel() <= ft_module.GRAPH_MAX_TOKENS):
         ft_module.GRAPH = False
@@ -290,6 +291,13 @@ def main():
             gen(x)
             torch.cuda.synchronize()
         ft_module.GRAPH = True
+        kern_all = probe_eager.summary()
+    elif world == 1 and args.model == 'fast_pitch' and fp_module.FP_GRAPH:
+        fp_module.FP_GRAPH = False
+        with KernelProbe() as probe_eager:
+            gen(x)
+            torch.cuda.synchronize()
+        fp_module.FP_GRAPH = True
         kern_all = probe_eager.summary()
 
     if world > 1:

@@ -1605,9 +1605,13 @@ static int rnn_setup(RnnParams &p, int B, int T, int H, int cell, const float *w
     return v ? atoi(v) : 0;
   }();
   p.diag = diag_env;
+  // s_sleep(1) count before a step's first h poll (rnn_bidir_kernel): the first poll then
+  // lands after the producers' stores instead of a round trip before them.  Interleaved A/B
+  // at c3 (tools/rnn_env_ab.py, two boxes): 3 -> LSTM 1.55 -> 1.52-1.54, postnet GRU 1.32 ->
+  // 1.27 us/step; 6 made the LSTM slower again (1.58-1.61)
   static const int psleep_env = [] {
     const char *v = getenv("FTMI_RNN_PSLEEP");
-    return v ? atoi(v) : 0;
+    return v ? atoi(v) : 3;
   }();
   p.psleep = psleep_env;
   return FTMI_OK;

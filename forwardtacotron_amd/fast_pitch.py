@@ -15,6 +15,7 @@ layers, final LayerNorm.
 from __future__ import annotations
 
 import math
+import os
 from pathlib import Path
 from typing import Any, Callable, Dict, Optional, Union
 
@@ -24,7 +25,14 @@ import torch.nn as nn
 
 from . import ops
 from .common_layers import Conv1dParams, LengthRegulator, LinearParams, Packed, pack_conv, presplit
-from .forward_tacotron import Embedding
+from .forward_tacotron import Embedding, _graphable, _identity
+
+# generate() replays the phoneme phase (three predictors, the prenet, the duration counts:
+# ~160 launches over four streams) as a HIP graph, captured on the second sighting of a
+# (device, x shape, alpha, callbacks) key; callbacks must be the identity or graph_safe
+# (forward_tacotron.graph_safe).  FTMI_FP_GRAPH=0 keeps it eager.
+FP_GRAPH = os.environ.get('FTMI_FP_GRAPH', '1') != '0'
+FP_GRAPH_CACHE = 8
 from .text.symbols import phonemes
 
 
@@ -270,49 +278,131 @@ class FastPitch(nn.Module):
     def generate(self,
                  x: torch.Tensor,
                  alpha=1.0,
-                 pitch_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x,
-                 energy_function: Callable[[torch.Tensor], torch.Tensor] = lambda x: x,
+                 pitch_function: Callable[[torch.Tensor], torch.Tensor] = _identity,
+                 energy_function: Callable[[torch.Tensor], torch.Tensor] = _identity,
                  batch=None) -> Dict[str, torch.Tensor]:
         """`models/fast_pitch.py:286-303`: predictors without masks; the prenet on side
         streams overlaps the duration path and its one host sync (T_mel).  `batch`: a
         sharded.GlobalBatch when x is one rank's shard of a larger batch.  Runs under the
         f16x3 range guard (ops.run_checked)."""
-        self.eval()
+        if self.training:  # the module-tree walk of eval() is host time on every call
+            self.eval()
         self._check_device(x)
         return ops.run_checked(
             lambda: self._generate(x, alpha, pitch_function, energy_function, batch), x.device,
             reduce=None if batch is None else batch.status)
 
+    def _phase(self, x, alpha, pitch_function, energy_function, batch=None, capture=False):
+        """The phoneme phase: the prenet on a side stream beside the pitch / energy
+        predictors, the duration predictor and counts on the caller's stream, then the
+        pitch / energy projections added to the prenet output.  Returns (dur_hat, pitch_hat,
+        energy_hat, h, offsets, T_mel); capture=True (graph capture): no host sync, the T_mel
+        slot holds max(totals) on the device."""
+        main = torch.cuda.current_stream(x.device)
+        s_pitch, s_energy, s_prenet = self._side_streams(x.device)
+        for s in (s_pitch, s_energy, s_prenet):
+            s.wait_stream(main)
+        len_mask = x == 0
+        with torch.cuda.stream(s_prenet):
+            h = self.prenet.embed(x, self.embedding.weight.detach())
+            h = self.prenet.layers_cl(h, len_mask)
+        with torch.cuda.stream(s_pitch):
+            pitch_hat = pitch_function(self.pitch_pred.forward_bt(x).unsqueeze(1))
+        with torch.cuda.stream(s_energy):
+            energy_hat = energy_function(self.energy_pred.forward_bt(x).unsqueeze(1))
+        dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
+        if batch is None:
+            offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=True)
+            T_mel = totals.max() if capture else int(totals.max().item())
+        else:
+            offsets, totals = batch.duration_counts(dur_hat)
+            T_mel = batch.t_mel(totals)
+        for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat), (s_prenet, h),
+                     (s_prenet, len_mask)):
+            main.wait_stream(s)
+            if not capture:
+                t.record_stream(main)
+        wp, bp, we, be = self._series_proj_weights()
+        ops.series_proj_add(h, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
+                            self.energy_strength)
+        return dur_hat, pitch_hat, energy_hat, h, offsets, T_mel
+
+    def _weights_key(self):
+        """(data_ptr, _version) of every parameter and buffer (ForwardTacotron._weights_key)."""
+        return tuple((t.data_ptr(), t._version) for m in self.modules()
+                     for d in (m._parameters, m._buffers) for t in d.values() if t is not None)
+
+    def _phase_graph(self, x, alpha, pitch_fn, energy_fn):
+        """The phoneme phase as a HIP graph (ForwardTacotron._phoneme_graph's protocol): a
+        key is captured the second time it is seen; x is copied into the static input; dur /
+        pitch / energy are cloned out; h and the offsets are consumed by this call's decoder
+        (the next replay waits for the decoder's completion event); a weights change drops
+        the captured phases.  Returns ((dur, pitch, energy, h, offsets, T_mel), entry) or
+        None (run the eager phase)."""
+        cache = self.__dict__.setdefault('_ftmi_graphs', {})
+        seen = self.__dict__.setdefault('_ftmi_graph_seen', {})
+        key = (x.device, tuple(x.shape), float(alpha), pitch_fn, energy_fn, ops.MMA)
+        ent = cache.pop(key, None)
+        fresh = False
+        if ent is None:
+            n = seen.get(key, 0)
+            if n < 0:
+                return None
+            if len(seen) >= 64 * FP_GRAPH_CACHE:
+                seen.clear()
+            seen[key] = n + 1
+            if n == 0:
+                return None
+            wkey = self._weights_key()
+            sx = x.clone()
+            try:
+                self._phase(sx, alpha, pitch_fn, energy_fn, capture=True)  # warm-up
+                torch.cuda.synchronize(x.device)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    outs = self._phase(sx, alpha, pitch_fn, energy_fn, capture=True)
+            except Exception:  # pylint: disable=broad-except
+                torch.cuda.synchronize(x.device)
+                seen[key] = -1
+                return None
+            ent = {'g': g, 'sx': sx, 'outs': outs, 'wkey': wkey, 'done': torch.cuda.Event()}
+            ent['done'].record(torch.cuda.current_stream(x.device))
+            fresh = True
+            while len(cache) >= FP_GRAPH_CACHE:
+                cache.pop(next(iter(cache)))
+        cache[key] = ent
+        main = torch.cuda.current_stream(x.device)
+        main.wait_event(ent['done'])
+        ent['sx'].copy_(x)
+        ent['g'].replay()
+        if not fresh and self._weights_key() != ent['wkey']:
+            main.synchronize()
+            cache.clear()
+            return None
+        dur_hat, pitch_hat, energy_hat, h, offsets, tmax = ent['outs']
+        t_host = torch.empty((), dtype=tmax.dtype, pin_memory=True)
+        t_host.copy_(tmax, non_blocking=True)
+        t_ready = torch.cuda.Event()
+        t_ready.record(main)
+        dur_hat, pitch_hat, energy_hat = dur_hat.clone(), pitch_hat.clone(), energy_hat.clone()
+        t_ready.synchronize()
+        return (dur_hat, pitch_hat, energy_hat, h, offsets, int(t_host)), ent
+
     def _generate(self, x, alpha, pitch_function, energy_function, batch):
         with torch.no_grad():
-            main = torch.cuda.current_stream(x.device)
-            s_pitch, s_energy, s_prenet = self._side_streams(x.device)
-            for s in (s_pitch, s_energy, s_prenet):
-                s.wait_stream(main)
-            len_mask = x == 0
-            with torch.cuda.stream(s_prenet):
-                h = self.prenet.embed(x, self.embedding.weight.detach())
-                h = self.prenet.layers_cl(h, len_mask)
-            with torch.cuda.stream(s_pitch):
-                pitch_hat = pitch_function(self.pitch_pred.forward_bt(x).unsqueeze(1))
-            with torch.cuda.stream(s_energy):
-                energy_hat = energy_function(self.energy_pred.forward_bt(x).unsqueeze(1))
-            dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
-            if batch is None:
-                offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=True)
-                T_mel = int(totals.max().item())
-            else:
-                offsets, totals = batch.duration_counts(dur_hat)
-                T_mel = batch.t_mel(totals)
-            for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat), (s_prenet, h),
-                         (s_prenet, len_mask)):
-                main.wait_stream(s)
-                t.record_stream(main)
-            wp, bp, we, be = self._series_proj_weights()
-            ops.series_proj_add(h, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
-                                self.energy_strength)
+            phase = ent = None
+            if (FP_GRAPH and batch is None and not ops.forced_exact()
+                    and _graphable(pitch_function) and _graphable(energy_function)):
+                r = self._phase_graph(x, alpha, pitch_function, energy_function)
+                if r is not None:
+                    phase, ent = r
+            if phase is None:
+                phase = self._phase(x, alpha, pitch_function, energy_function, batch)
+            dur_hat, pitch_hat, energy_hat, h, offsets, T_mel = phase
             index = ops.lr_index(offsets, T_mel)
             mel = self._decode(h, index)
+            if ent is not None:  # the decoder has consumed the graph's static buffers
+                ent['done'].record(torch.cuda.current_stream(x.device))
             return {'mel': mel, 'mel_post': mel, 'dur': dur_hat,
                     'pitch': pitch_hat, 'energy': energy_hat}
 

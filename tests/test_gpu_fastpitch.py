@@ -162,3 +162,32 @@ def test_batch64_against_oracle(fp_model):
     assert mel.shape == ref['mel'].shape
     d = np.abs(mel - ref['mel'])
     assert d.mean() < 2e-5 and d.max() < 1e-3
+
+
+def test_graph_phase_matches_eager(fp_model, monkeypatch):
+    """generate() replays FastPitch's phoneme phase as a HIP graph (captured on the second
+    call of a shape): identical (bit for bit) to the eager phase across replays with new
+    tokens of the same shape; the returned dur / pitch / energy are not graph buffers; an
+    unmarked callback is never captured."""
+    from forwardtacotron_amd import fast_pitch as FPM
+    m, _ = fp_model
+    g = load_golden('fp_gen_b3')
+    x1 = dev(g['x'])
+    x2 = x1.clone()
+    x2[x2 > 0] = (x2[x2 > 0] * 7) % 133 + 1
+    monkeypatch.setattr(FPM, 'FP_GRAPH', False)
+    eager = [m.generate(x) for x in (x1, x2)]
+    monkeypatch.setattr(FPM, 'FP_GRAPH', True)
+    for k in ('_ftmi_graphs', '_ftmi_graph_seen'):
+        m.__dict__.pop(k, None)
+    graph = [m.generate(x) for x in (x1, x2, x1, x2)]  # eager, capture, replay, replay
+    assert len(m.__dict__['_ftmi_graphs']) == 1
+    assert graph[1]['dur'].data_ptr() != graph[3]['dur'].data_ptr()
+    for e, gr in ((eager[0], graph[0]), (eager[1], graph[1]), (eager[0], graph[2]),
+                  (eager[1], graph[3])):
+        for k in ('mel', 'dur', 'pitch', 'energy'):
+            assert torch.equal(e[k], gr[k]), k
+    fn = lambda p: p * 1.1  # noqa: E731  (not graph_safe)
+    for _ in range(3):
+        m.generate(x1, pitch_function=fn)
+    assert len(m.__dict__['_ftmi_graphs']) == 1
