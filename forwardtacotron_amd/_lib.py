@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 12
+ABI_VERSION = 13
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -69,6 +69,8 @@ SIGNATURES = {
     'ftmi_split_rows': (c_int, [P, c_int64, c_int64, c_int, P, c_int64, P, P]),
     'ftmi_split_weights_f16': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_split_weights_f16_frag': (c_int, [P, c_int64, c_int64, P, P]),
+    'ftmi_panel_proj': (c_int, [P, c_int64, c_int64, c_int, P, c_int, P, P, c_int64, P, P,
+                                c_float, P, c_int64, P, P]),
     'ftmi_rnn_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
     'ftmi_rnn_error_offset': (c_int64, [c_int]),
     'ftmi_rnn_blocks': (c_int, [c_int, c_int, c_int, c_int]),

@@ -2323,13 +2323,9 @@ __device__ __forceinline__ void hs_step(f32x4 (&acc)[4][NI], const _Float16 *Ah,
 // kept rolled and the steps fenced by sched barriers: otherwise the compiler hoists further
 // loads and LDS reads across steps and spills).
 template <int NI>
-__device__ __forceinline__ void hs_gemm(f32x4 (&acc)[4][NI], const _Float16 *Ah,
-                                        const _Float16 *At, const _Float16 *const (&bp)[NI],
-                                        int64_t plane, int nks, int fr, int fs) {
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+__device__ __forceinline__ void hs_gemm_acc(f32x4 (&acc)[4][NI], const _Float16 *Ah,
+                                            const _Float16 *At, const _Float16 *const (&bp)[NI],
+                                            int64_t plane, int nks, int fr, int fs) {
   // three register sets in a ring: the loads of k-step ks + 3 are issued right after step
   // ks consumed its set (one step of look-ahead left the L2 latency exposed: the MFMAs of a
   // step are ~800 cycles per wave, a loaded L2 round trip is more)
@@ -2359,6 +2355,17 @@ __device__ __forceinline__ void hs_gemm(f32x4 (&acc)[4][NI], const _Float16 *Ah,
     load(z0, z1, ks + 5);
     __builtin_amdgcn_sched_barrier(0);
   }
+}
+
+template <int NI>
+__device__ __forceinline__ void hs_gemm(f32x4 (&acc)[4][NI], const _Float16 *Ah,
+                                        const _Float16 *At, const _Float16 *const (&bp)[NI],
+                                        int64_t plane, int nks, int fr, int fs) {
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  hs_gemm_acc<NI>(acc, Ah, At, bp, plane, nks, fr, fs);
 }
 
 __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackParams p) {
@@ -2501,6 +2508,212 @@ __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackPara
           }
       }
     }
+  }
+  if (!(amax <= 65504.f) && p.status) atomicOr(p.status, 1u);
+}
+
+// ---- row-panel projection: y = [LayerNorm](x W^T + b [+ residual]) --------------------
+// The k = 1 contractions of a FastPitch FFT block (models/fast_pitch.py:56-91, the
+// reference's FFTBlock): self_attn.in_proj (K = d, N = 3d), out_proj + residual -> norm1
+// (K = N = d) and conv2 (k = 1) + residual -> norm2 (K = d_fft, N = d).  At d = 256 these are
+// short-K or narrow-N GEMMs: the 256 x 128 slab tiles run them at 90-170 TF/s, prologue and
+// epilogue bound, and each LayerNorm is one more read + write of the rows.  Here a workgroup
+// owns 64 rows: their channels are staged once per 256-channel chunk into an f16 head /
+// scaled tail LDS image (the highway stack's layout and k-step code, hs_gemm_acc), the 8
+// waves sweep 256-column panels (wave = 32 columns, B fragments from the L2-resident
+// fragment-major planes), and the epilogue applies colscale and bias into an LDS row tile,
+// then adds the residual and — for a 256-column output — runs the LayerNorm one wave per
+// row with layernorm_kernel<4>'s arithmetic, writing each row once with coalesced stores.
+// Per k-step, product and epilogue rounding the slab kernel's order: the projection
+// values are bit-identical to conv1d's.  HBM per row: K floats in, N out (+ N residual).
+constexpr int PP_BM = 64;
+constexpr int PP_KC = HS_C;    // channels per staged chunk
+constexpr int PP_TP = HS_C + 4;  // floats per LDS tile row (conflict-free fragment stores)
+
+struct PanelParams {
+  const float *x;
+  int64_t x_stride;
+  int M, K, kpad, N;
+  const _Float16 *w;  // split_weights_f16_frag planes [3][N/16][kpad/32][64][8]
+  const float *cs;    // their column scales
+  const float *bias;
+  const float *res;
+  int64_t res_stride;
+  const float *ln_g, *ln_b;  // LayerNorm over the N = 256 columns (null: none)
+  float eps;
+  float *y;
+  int64_t y_stride;
+  unsigned *status;
+};
+
+// Persistent over row tiles (grid = min(tiles, CUs)): the next job's channels (the next
+// chunk, or the next tile's first) are loaded into registers right after the current chunk
+// is staged, so their HBM latency hides behind this chunk's MFMAs (the residual rows of a
+// panel are issued at once ahead of its tile writes); one workgroup per CU (136 KB LDS).
+__global__ __launch_bounds__(512) void panel_proj_kernel(const PanelParams p) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * HS_IMG];   // head | tail
+  __shared__ __attribute__((aligned(16))) float tile[PP_BM * PP_TP];  // finished panel rows
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fs = lane >> 4;
+  // column block of this wave, rotated per workgroup (highway_stack_kernel: spreads the
+  // concurrent B reads of one XCD over different weight lines)
+  const int cb = (wave + (blockIdx.x >> 3)) & 7;
+  const int ntiles = (p.M + PP_BM - 1) / PP_BM;
+  const int nch = (p.kpad + PP_KC - 1) / PP_KC, nq = p.N / HS_C;
+  const bool ln = p.ln_g != nullptr;
+  float amax = 0.f;
+  f32x4 ra[8];  // one job's channels: rows wave + 8 u, channels c0 + 4 lane .. + 3
+  auto load_job = [&](int t, int c) {
+    const int c0 = c * PP_KC, kc = min(PP_KC, p.kpad - c0);
+    const float *xb = p.x + (int64_t)(t * PP_BM + wave) * p.x_stride + c0 + 4 * lane;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ra[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (4 * lane < kc && t * PP_BM + wave + 8 * u < p.M && c0 + 4 * lane < p.K)
+        ra[u] = *(const f32x4 *)(xb + (int64_t)8 * u * p.x_stride);
+    }
+  };
+  auto store_job = [&](int c) {  // ra -> the LDS image (f16 head / scaled tail)
+    if (4 * lane >= min(PP_KC, p.kpad - c * PP_KC)) return;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const f32x4 v = ra[u];
+      amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      f16x4 hh, tt;
+      split2h(v, hh, tt);
+      const int o = (wave + 8 * u) * HS_P + 4 * lane;
+      *(f16x4 *)(lds + o) = hh;
+      *(f16x4 *)(lds + HS_IMG + o) = tt;
+    }
+  };
+  // the residual of panel q, in the row pass's layout: LN — wave w rows 8w + u, columns
+  // lane + 64 j (rv[u][j]); plain — rows w + 8u, columns 4 lane .. + 3 (rv[u] as a float4)
+  float rv[8][4];
+  auto load_res = [&](int t, int q) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int row = t * PP_BM + (ln ? 8 * wave + u : wave + 8 * u);
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (p.res && row < p.M) {
+        const float *rr = p.res + (int64_t)row * p.res_stride + HS_C * q;
+        if (ln) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = rr[lane + 64 * j];
+        } else {
+          v = *(const f32x4 *)(rr + 4 * lane);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rv[u][j] = v[j];
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  load_job(t, 0);
+#pragma unroll 1
+  for (;; ) {
+#pragma unroll 1
+    for (int q = 0; q < nq; ++q) {
+      f32x4 acc[4][2];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+      for (int c = 0; c < nch; ++c) {
+        if (nch > 1 || q == 0) {  // one chunk: staged once for every panel
+          __syncthreads();        // every wave is past its reads of the image
+          store_job(c);
+          __syncthreads();
+          // the next job's channels, in flight during this chunk's MFMAs
+          if (c + 1 < nch)
+            load_job(t, c + 1);
+          else if (nch > 1 && q + 1 < nq)
+            load_job(t, 0);
+          else if (t + (int)gridDim.x < ntiles)
+            load_job(t + gridDim.x, 0);
+        }
+        const _Float16 *bp[2];
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          bp[ni] = p.w + (int64_t)((HS_C * q + 32 * cb + 16 * ni) >> 4) * (p.kpad / 32) * 512 +
+                   lane * 8 + 512 * (PP_KC / 32) * c;
+        hs_gemm_acc<2>(acc, lds, lds + HS_IMG, bp, (int64_t)p.N * p.kpad,
+                       min(PP_KC, p.kpad - c * PP_KC) / 32, fr, fs);
+      }
+      // ---- epilogue, the slab kernel's rounding order: t = acc colscale (+ bias) into the
+      // LDS row tile, then row passes: (+ residual), [LayerNorm], coalesced stores
+      load_res(t, q);  // in flight during the tile writes and the barrier
+      if (q > 0) __syncthreads();  // the previous panel's row pass is done with the tile
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int col = HS_C * q + 32 * cb + 16 * ni + fr;
+        const float cs = p.cs[col], b = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+#pragma clang fp contract(off)
+            float v = acc[mi][ni][i] * cs;
+            if (p.bias) v += b;
+            tile[(16 * mi + 4 * fs + i) * PP_TP + 32 * cb + 16 * ni + fr] = v;
+          }
+      }
+      __syncthreads();
+      const int m0 = t * PP_BM;
+      if (!ln) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int r = wave + 8 * u, row = m0 + r;
+          if (row >= p.M) continue;
+          f32x4 v = *(const f32x4 *)(tile + r * PP_TP + 4 * lane);
+          if (p.res) v += (f32x4){rv[u][0], rv[u][1], rv[u][2], rv[u][3]};
+          *(f32x4 *)(p.y + (int64_t)row * p.y_stride + HS_C * q + 4 * lane) = v;
+        }
+      } else {  // one wave per row: layernorm_kernel<4>'s arithmetic (fp64 sums, same order)
+        float gm[4], bt[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          gm[j] = p.ln_g[lane + 64 * j];
+          bt[j] = p.ln_b[lane + 64 * j];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int r = 8 * wave + u, row = m0 + r;
+          if (row >= p.M) break;
+          float v[4];
+          double sm = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] = tile[r * PP_TP + lane + 64 * j];
+            if (p.res) v[j] += rv[u][j];
+            sm += v[j];
+          }
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o);
+          const double mean = sm / HS_C;
+          double sq = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const double d = (double)v[j] - mean;
+            sq += d * d;
+          }
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+          const float rstd = (float)(1.0 / sqrt(sq / HS_C + (double)p.eps));
+          const float meanf = (float)mean;
+          const float nb = -(rstd * meanf);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+#pragma clang fp contract(off)
+            p.y[(int64_t)row * p.y_stride + lane + 64 * j] = (v[j] * rstd + nb) * gm[j] + bt[j];
+          }
+        }
+      }
+    }
+    t += gridDim.x;
+    if (t >= ntiles) break;
   }
   if (!(amax <= 65504.f) && p.status) atomicOr(p.status, 1u);
 }
@@ -3092,6 +3305,52 @@ extern "C" int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, i
   p.status = status;
   const unsigned blocks = (unsigned)((M + HS_BM - 1) / HS_BM);
   hipLaunchKernelGGL(highway_stack_kernel, dim3(blocks), dim3(512), 0, ftmi_hs(stream), p);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_panel_proj(const float *x, int64_t x_stride, int64_t M, int32_t K,
+                               const void *w_split_frag, int32_t N, const float *bias,
+                               const float *residual, int64_t res_stride, const float *ln_gamma,
+                               const float *ln_beta, float eps, float *y, int64_t y_stride,
+                               uint32_t *status, ftmi_stream_t stream) {
+  if (!x || !w_split_frag || !y || M < 0 || K <= 0 || N <= 0) return FTMI_E_ARG;
+  if (!ln_gamma != !ln_beta) return FTMI_E_ARG;
+  if (K % 4 || N % HS_C || (ln_gamma && N != HS_C) || M > INT32_MAX) return FTMI_E_SHAPE;
+  if (x_stride < K || y_stride < N || (residual && res_stride < N)) return FTMI_E_SHAPE;
+  if (!ftmi_aligned16(x) || (x_stride & 3) || !ftmi_aligned16(w_split_frag)) return FTMI_E_ALIGN;
+  // the rows of x are re-read after other workgroups' rows of y are written (chunks,
+  // panels): no aliasing; y may alias the residual (each element read before its write)
+  if ((const float *)x == y) return FTMI_E_ARG;
+  if (M == 0) return FTMI_OK;
+  PanelParams p = {};
+  p.x = x;
+  p.x_stride = x_stride;
+  p.M = (int)M;
+  p.K = K;
+  p.kpad = (K + X6_BK - 1) / X6_BK * X6_BK;
+  p.N = N;
+  p.w = (const _Float16 *)w_split_frag;
+  p.cs = f16_colscale(w_split_frag, N, K);
+  p.bias = bias;
+  p.res = residual;
+  p.res_stride = res_stride;
+  p.ln_g = ln_gamma;
+  p.ln_b = ln_beta;
+  p.eps = eps;
+  p.y = y;
+  p.y_stride = y_stride;
+  p.status = status;
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  const int64_t tiles = (M + PP_BM - 1) / PP_BM;
+  const unsigned blocks = (unsigned)(tiles < cus ? tiles : cus);
+  hipLaunchKernelGGL(panel_proj_kernel, dim3(blocks), dim3(512), 0, ftmi_hs(stream), p);
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
 }

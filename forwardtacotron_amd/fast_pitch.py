@@ -108,15 +108,45 @@ class FFTBlock(Packed):
                 (w1, self.conv1.bias.detach().contiguous(), presplit(w1)),
                 (w2, self.conv2.bias.detach().contiguous(), presplit(w2)))
 
+    def _panel_pack(self):
+        """Fragment-major f16x3 planes of in_proj, out_proj and (kernel 1) conv2 — the
+        operands of ops.panel_proj — cached like every pack (rebuilt with the params)."""
+        key = self._pack_key()
+        cache = self.__dict__.get('_ftmi_panel')
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                (wi, _, _), (wo, _, _), _, (w2, _, _) = self.packed_weights()
+                f16 = ops.split_weights_f16
+                cache = (key, (f16(wi, frag=True), f16(wo, frag=True),
+                               f16(w2, frag=True) if self.k2 == 1 else None))
+            self.__dict__['_ftmi_panel'] = cache
+        return cache[1]
+
     def forward_cl(self, x: torch.Tensor, kpm: Optional[torch.Tensor] = None) -> torch.Tensor:
         (wi, bi, si), (wo, bo, so), (w1, b1, s1), (w2, b2, s2) = self.packed_weights()
-        qkv, _ = ops.conv1d(x, wi, 1, 0, bias=bi, w_split=si)
+        d = x.size(2)
+        ln1 = (self.norm1.weight.detach(), self.norm1.bias.detach(), self.norm1.eps)
+        ln2 = (self.norm2.weight.detach(), self.norm2.bias.detach(), self.norm2.eps)
+        # the k = 1 projections with their residual add + LayerNorm as row-panel launches
+        # (ops.panel_proj) where the f16x3 path is in force and d fits its 256-column panels;
+        # the slab GEMM + layernorm launches otherwise (same projection values)
+        panel = ops.panel_ok(d, d, True, si)
+        fi, fo, f2 = self._panel_pack() if panel else (None, None, None)
+        if panel:
+            qkv = ops.panel_proj(x, fi, 3 * d, bias=bi)
+        else:
+            qkv, _ = ops.conv1d(x, wi, 1, 0, bias=bi, w_split=si)
         a = ops.attention(qkv, self.heads, kpm)
         del qkv
-        h, _ = ops.conv1d(a, wo, 1, 0, bias=bo, residual=x, w_split=so)
+        if panel:
+            h = ops.panel_proj(a, fo, d, bias=bo, residual=x, ln=ln1)
+        else:
+            h, _ = ops.conv1d(a, wo, 1, 0, bias=bo, residual=x, w_split=so)
+            h = self.norm1.forward_cl(h, out=h)
         del a
-        h = self.norm1.forward_cl(h, out=h)
         f, _ = ops.conv1d(h, w1, self.k1, self.k1 // 2, bias=b1, relu=True, w_split=s1)
+        if panel and f2 is not None and ops.panel_ok(f.size(2), d, True, s2):
+            return ops.panel_proj(f, f2, d, bias=b2, residual=h, ln=ln2, out=h)
         y, _ = ops.conv1d(f, w2, self.k2, self.k2 // 2, bias=b2, residual=h, w_split=s2)
         del f
         return self.norm2.forward_cl(y, out=y)

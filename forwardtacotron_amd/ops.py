@@ -378,7 +378,7 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
     sk, part, last = 0, None, 0
     if not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
         sk = _skinny_split(Cin)  # weight-streaming kernel: partial sums, finished in order
-        if os.environ.get('FTMI_BANK_LAST', '1') != '0':
+        if os.environ.get('FTMI_BANK_LAST', '0') != '0':
             # tile counters + partials, finished in-kernel by each tile's last split block
             part, last = _bank_workspace(sk * M * K * Cout, x.device), BANK_LAST
         else:
@@ -492,6 +492,49 @@ def highway_stack(x: torch.Tensor, pre_split: torch.Tensor, C: int, hw_splits, b
            _ptr(h), h.stride(1) if h is not None else 0, status_word(x.device).data_ptr(),
            _stream())
     return y, h
+
+
+PANEL_N = 256  # gemm.hip panel_proj_kernel: output columns per panel (LayerNorm width)
+
+
+def panel_ok(K: int, N: int, ln: bool, split) -> bool:
+    """Whether `panel_proj` applies: the f16x3 path is in force (not inside exact_paths()),
+    the weight has its fragment-major f16 planes, and the shape fits the kernel
+    (FTMI_PANEL=0 keeps the slab GEMM + LayerNorm launches)."""
+    if os.environ.get('FTMI_PANEL', '1') == '0' or (_FORCED and _FORCED[-1][0] != 2):
+        return False
+    if not _FORCED and MMA != 2:
+        return False
+    return (split is not None and split.dtype == torch.uint8 and K % 4 == 0
+            and N % PANEL_N == 0 and (N == PANEL_N or not ln))
+
+
+def panel_proj(x: torch.Tensor, w_frag: torch.Tensor, N: int, bias: Optional[torch.Tensor] = None,
+               residual: Optional[torch.Tensor] = None, ln=None,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = [LayerNorm](x W^T + bias [+ residual]) in one launch (`ftmi_panel_proj`): the k = 1
+    projections of a FastPitch FFT block (models/fast_pitch.py:56-91) with their residual
+    add and norm.  x: (B, T, K) channels-last; w_frag: split_weights_f16(W, frag=True);
+    ln: (gamma, beta, eps) or None.  out may be the residual (in place), never x."""
+    _dev(x, w_frag, bias, residual)
+    B, T, K, xs = _rows(x)
+    M = B * T
+    y = out if out is not None else torch.empty(B, T, N, device=x.device, dtype=_f32)
+    rs = 0
+    if residual is not None:
+        if tuple(residual.shape) != (B, T, N):
+            raise ValueError(f'residual shape {tuple(residual.shape)} != {(B, T, N)}')
+        rs = _rows(residual)[3]
+    if tuple(y.shape) != (B, T, N):
+        raise ValueError(f'out shape {tuple(y.shape)} != {(B, T, N)}')
+    _rows(y)
+    g, b, eps = ln if ln is not None else (None, None, 0.0)
+    launch('ftmi_panel_proj', f'panel_proj[M={M},K={K},N={N}{",ln" if ln is not None else ""}]',
+           2.0 * M * N * K, 4.0 * M * (K + N * (2 if residual is not None else 1)),
+           x.data_ptr(), xs, M, K, w_frag.data_ptr(), N, _ptr(bias), _ptr(residual), rs,
+           _ptr(g), _ptr(b), float(eps), y.data_ptr(), y.stride(1),
+           status_word(x.device).data_ptr(), _stream())
+    return y
 
 
 RNN_SPREAD = 0x100  # include/ftmi.h FTMI_RNN_SPREAD

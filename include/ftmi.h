@@ -72,7 +72,7 @@ enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
                                  share the counters. */ };
 enum { FTMI_BANK_COUNTERS = 4096 };
 
-/* ABI version; bumped on any signature change (12: FTMI_RNN_SPREAD flag of ftmi_rnn_bidir / ftmi_rnn_blocks). */
+/* ABI version; bumped on any signature change (13: ftmi_panel_proj). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
@@ -455,6 +455,24 @@ int ftmi_lr_posenc(const float *x, int64_t x_stride, int32_t B, int32_t T, int32
  * biased variance, y = (x*rstd - rstd*mean)*gamma + beta.  C <= 1024; y may alias x. */
 int ftmi_layernorm(const float *x, int64_t x_stride, int64_t M, int32_t C, const float *gamma,
                    const float *beta, float eps, float *y, int64_t y_stride, ftmi_stream_t stream);
+
+/* Row-panel projection (ABI 13) — the k = 1 contractions of a FastPitch FFT block
+ * (models/fast_pitch.py:56-91: self_attn in_proj, out_proj + residual -> norm1, conv2 with
+ * kernel 1 + residual -> norm2) with their epilogue in one launch:
+ *   v = x W^T + bias (+ residual);   y = ln_gamma ? LayerNorm(v) : v
+ * (nn.LayerNorm over the N columns: biased variance, eps, y = (v*rstd - rstd*mean)*gamma +
+ * beta as ftmi_layernorm).  x: M rows of K floats (K % 4 == 0, 16-B aligned, x_stride % 4
+ * == 0); w_split_frag: ftmi_split_weights_f16_frag of W [N][K]; N % 256 == 0, N == 256 with
+ * LayerNorm; bias, residual (M x N, res_stride), ln_gamma / ln_beta (both or neither):
+ * nullable.  y (M x N, y_stride) must not alias x; it may alias residual.  f16x3 arithmetic:
+ * the projection values are bit-identical to ftmi_conv1d's on FTMI_MMA_F16X3 with the same
+ * planes in row-major order; status bit 0 (optional word) when |x| > 65504 (rerun
+ * unfused on FTMI_MMA_F32). */
+int ftmi_panel_proj(const float *x, int64_t x_stride, int64_t M, int32_t K,
+                    const void *w_split_frag, int32_t N, const float *bias,
+                    const float *residual, int64_t res_stride, const float *ln_gamma,
+                    const float *ln_beta, float eps, float *y, int64_t y_stride,
+                    uint32_t *status, ftmi_stream_t stream);
 
 /* nn.MultiheadAttention self-attention core (FFTBlock.forward :76-79; torch
  * multi_head_attention_forward math path): per batch b and head h,

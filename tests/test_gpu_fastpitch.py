@@ -191,3 +191,23 @@ def test_graph_phase_matches_eager(fp_model, monkeypatch):
     for _ in range(3):
         m.generate(x1, pitch_function=fn)
     assert len(m.__dict__['_ftmi_graphs']) == 1
+
+
+def test_panel_path_matches_unfused(fp_model, monkeypatch):
+    """The FFT blocks' row-panel launches (ops.panel_proj: in_proj, out_proj + norm1, conv2
+    + norm2) against the slab GEMM + layernorm launches (FTMI_PANEL=0).  The projections agree
+    bit for bit wherever the unfused GEMM runs unsplit (test_gpu_kernels.py::test_panel_proj);
+    at these row counts the unfused conv2 (K = 1024) sums split-K partials, so the bound is
+    the fp32 summation-order one."""
+    from forwardtacotron_amd.synthetic import synthetic_tokens
+    m, _ = fp_model
+    x = dev(synthetic_tokens(4, 80, seed=5, min_len=70))
+    outs = {}
+    for v in ('0', '1'):
+        monkeypatch.setenv('FTMI_PANEL', v)
+        outs[v] = {k: host(t) for k, t in m.generate(x).items() if k in ('mel', 'dur', 'pitch', 'energy')}
+    d = np.abs(outs['0']['mel'] - outs['1']['mel'])
+    assert d.max() < 1e-4 and d.mean() < 5e-6, (d.max(), d.mean())
+    np.testing.assert_array_equal(FP.duration_counts(outs['0']['dur']), FP.duration_counts(outs['1']['dur']))
+    for k in ('pitch', 'energy'):
+        np.testing.assert_allclose(outs['0'][k], outs['1'][k], atol=1e-5)

@@ -406,6 +406,75 @@ def test_highway_stack_range_guard(rng):
         assert bool(int(st.item()) & 1) == bad
 
 
+PANEL_CASES = [  # (B, T, K, N, residual, ln): FFTBlock in_proj, out_proj + norm1, conv2 + norm2
+    (4, 900, 256, 768, False, False),
+    (4, 900, 256, 256, True, True),
+    (4, 900, 1024, 256, True, True),
+    (2, 333, 96, 512, True, False),  # K not a multiple of 32 (zero-padded k-step), 2 panels
+    (1, 37, 256, 256, True, True),    # one partial row tile
+]
+
+
+@pytest.mark.parametrize('B,T,K,N,res,ln', PANEL_CASES)
+def test_panel_proj(rng, monkeypatch, B, T, K, N, res, ln):
+    """ftmi_panel_proj (FastPitch FFT-block projections, fast_pitch.py:56-91) vs a float64
+    numpy oracle of x W^T + b (+ residual) (-> LayerNorm) within the f16x3 bound, and vs the
+    unfused slab conv1d + layernorm launches bit for bit (same k-step / product / epilogue
+    order) where the unfused GEMM runs unsplit, within 1e-5 where it sums split-K partials."""
+    from forwardtacotron_amd import ops
+    monkeypatch.setenv('FTMI_GEMM_SKINNY', '0')
+    x = rng.normal(0, 1, (B, T, K)).astype(np.float32)
+    w = (rng.normal(0, 1, (N, K)) / np.sqrt(K)).astype(np.float32)
+    b = rng.normal(0, 0.1, N).astype(np.float32)
+    r = rng.normal(0, 1, (B, T, N)).astype(np.float32) if res else None
+    g = rng.normal(1, 0.2, N).astype(np.float32)
+    bt = rng.normal(0, 0.2, N).astype(np.float32)
+    wd = dev(w)
+    lnp = (dev(g), dev(bt), 1e-5) if ln else None
+    y = ops.panel_proj(dev(x), ops.split_weights_f16(wd, frag=True), N, bias=dev(b),
+                       residual=dev(r) if res else None, ln=lnp)
+    ref = x.reshape(-1, K).astype(np.float64) @ w.astype(np.float64).T + b
+    if res:
+        ref = ref + r.reshape(-1, N)
+    if ln:
+        mu = ref.mean(1, keepdims=True)
+        ref = (ref - mu) / np.sqrt(((ref - mu) ** 2).mean(1, keepdims=True) + 1e-5) * g + bt
+    close(host(y).reshape(-1, N), ref, rtol=1e-5, atol=1e-5)
+    yu, _ = ops.conv1d(dev(x), wd, 1, 0, bias=dev(b), residual=dev(r) if res else None,
+                       w_split=ops.split_weights_f16(wd))
+    if ln:
+        yu = ops.layernorm(yu, lnp[0], lnp[1], 1e-5, out=yu)
+    if B * T > 256 and ops._split_k(B * T, N, K, 2, True, K) == 1:
+        np.testing.assert_array_equal(host(y), host(yu))
+    else:  # the unfused side sums split-K partials there (skinny kernel / slab split)
+        close(host(y), host(yu), rtol=1e-5, atol=1e-5)
+
+
+def test_panel_proj_in_place_and_range_guard(rng):
+    """out may alias the residual (FFTBlock's norm2 step writes over h); |x| > 65504 sets
+    status bit 0."""
+    from forwardtacotron_amd import ops
+    x = rng.normal(0, 1, (2, 300, 256)).astype(np.float32)
+    w = dev((rng.normal(0, 1, (256, 256)) / 16).astype(np.float32))
+    wf = ops.split_weights_f16(w, frag=True)
+    r = dev(rng.normal(0, 1, (2, 300, 256)).astype(np.float32))
+    ln = (torch.ones(256, device='cuda'), torch.zeros(256, device='cuda'), 1e-5)
+    ref = ops.panel_proj(dev(x), wf, 256, residual=r, ln=ln)
+    got = ops.panel_proj(dev(x), wf, 256, residual=r, ln=ln, out=r)
+    assert got.data_ptr() == r.data_ptr()
+    np.testing.assert_array_equal(host(got), host(ref))
+    with pytest.raises(Exception):
+        xd = dev(x)
+        ops.panel_proj(xd, wf, 256, out=xd[..., :256])  # y aliasing x: refused
+    st = ops.status_word('cuda')
+    for bad in (False, True):
+        if bad:
+            x[1, 17, 5] = 7e4
+        st.zero_()
+        ops.panel_proj(dev(x), wf, 256)
+        assert bool(int(st.item()) & 1) == bad
+
+
 def test_split_weights_exact(rng):
     """The three bf16 pieces sum back to the fp32 weights exactly; K padding is zero."""
     from forwardtacotron_amd import ops
