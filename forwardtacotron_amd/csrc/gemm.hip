@@ -2064,212 +2064,6 @@ __global__ __launch_bounds__(512, 1) void conv_bank_qb_kernel(const GemmParams p
   if (bad && p.status) atomicOr(p.status, 1u);
 }
 
-// ---- the c2 conv bank without a channel split (FTMI_BANK_CS, default for M <= 128) --------
-// The skinny bank above splits the 256 input channels over 4 blocks per tile, so every tile
-// pays a partial-sum round trip (8 MB of fp32 partials written, a finish launch reading them)
-// and its blocks a ~10 k-cycle tail.  Here a block owns a unit = (group pair (k, K + 1 - k),
-// one 16-column set of each group) for ALL input channels and one RM-row tile: the whole
-// slab (RM + K - 1 rows x Cin, f16 head / scaled tail) is staged once, the 8 waves split the
-// unit's (tap, chunk) steps between them (step q = wave + 8 i, chunks fastest: at Cin = 256
-// wave w streams chunk w of every tap, so waves 2i / 2i + 1 read the two halves of each
-// 128-B weight line together), their partial sums meet in LDS in wave order
-// (deterministic) and the block applies colscale, ReLU and the BN affine itself: no
-// partials, no finish launch.  Every pair has k + (K + 1 - k) = K + 1 taps, so every wave of
-// every block runs the same (K + 1) nch / 8 steps.  At M = 120 (B = 1, T = 120): 128 units x
-// 2 row tiles = 256 blocks, one per CU; the two row tiles of a unit have the same
-// blockIdx.x % 8 (one XCD under round-robin dispatch), so the second tile's weight reads are
-// served by that XCD's L2 — placement only ever affects speed.  The weight fragments run
-// CS_PF steps ahead in a register ring that is filled before the slab is staged, so the first
-// HBM latency overlaps the slab's L2 reads.
-#ifndef BANK_CS_PF
-#define BANK_CS_PF 8
-#endif
-constexpr int CS_PF = BANK_CS_PF;
-constexpr int CS_MAXCH = 8;  // 32-channel chunks staged: Cin <= 256
-constexpr int CS_MMAX = 128;
-
-template <int MI>  // row fragments per block: RM = 16 MI rows
-__global__ __launch_bounds__(512, 1) void conv_bank_cs_kernel(const GemmParams p) {
-  constexpr int RM = MI * 16;
-  constexpr int SRM = RM + SL_MAXK - 1;
-  constexpr int AIMG = (SRM + 1) * SL_P;  // halves per (chunk, plane) image; row SRM is zero
-  constexpr int SLAB_BYTES = CS_MAXCH * 2 * AIMG * 2;
-  constexpr int RED_BYTES = 8 * 2 * MI * 64 * 16;  // f32x4 [wave][unit][mi][lane]
-  constexpr int LDS_BYTES = SLAB_BYTES > RED_BYTES ? SLAB_BYTES : RED_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-  _Float16 *const lds = (_Float16 *)smem;
-  f32x4 *const red = (f32x4 *)smem;  // aliases the slab after the loop
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const int MT = (p.M + RM - 1) / RM, NC = p.g[0].N / 16;
-  const int units = (p.ngroups / 2) * NC;
-  const int bid = blockIdx.x;
-  int u, mt;
-  if (units % 8 == 0) {  // the row tiles of a unit 8 blocks apart
-    const int grp = bid / (8 * MT), r = bid - grp * 8 * MT;
-    mt = r >> 3;
-    u = grp * 8 + (r & 7);
-  } else {
-    mt = bid % MT;
-    u = bid / MT;
-  }
-  const int gi = u / NC, cset = u - gi * NC;
-  const int gl = p.ngroups - 1 - gi;
-  const GemmGroup &GH = p.g[gi];  // the pair's heavy group (k = K - gi): its slab
-  const GemmGroup &GL = p.g[gl];
-  const int m0 = mt * RM, kh = GH.k, padh = GH.pad, kl = GL.k, dpl = padh - GL.pad;
-  const int Cin = p.Cin, nch = Cin >> 5;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fs = lane >> 4;
-  const int col = cset * 16 + fr;  // < N (N % 16 == 0: host check)
-
-  // ---- this wave's steps q = wave + 8 i over the unit's (group, tap, chunk) list ----------
-  const int QH = nch * kh, Q = QH + nch * kl;
-  const int ns = Q > wave ? (Q - wave + 7) >> 3 : 0;  // 0 for some waves when Q < 8
-  const _Float16 *wh = (const _Float16 *)GH.w3 + (int64_t)col * GH.Kpad + fs * 8;
-  const _Float16 *wl = (const _Float16 *)GL.w3 + (int64_t)col * GL.Kpad + fs * 8;
-  const int64_t planeh = (int64_t)GH.N * GH.Kpad, planel = (int64_t)GL.N * GL.Kpad;
-  auto loadB = [&](int i, f16x8 &b0, f16x8 &b1) {
-    const int q = min(wave + 8 * max(min(i, ns - 1), 0), Q - 1);  // clamped: always in range
-    const bool hv = q < QH;
-    const int qq = hv ? q : q - QH, j = qq / nch, c = qq - j * nch;
-    const _Float16 *src = (hv ? wh : wl) + j * Cin + c * 32;
-    b0 = *(const f16x8 *)src;
-    b1 = *(const f16x8 *)(src + (hv ? planeh : planel));
-  };
-  f16x8 rb0[CS_PF], rb1[CS_PF];
-#pragma unroll
-  for (int i = 0; i < CS_PF; ++i) loadB(i, rb0[i], rb1[i]);
-  // the epilogue's per-column parameters, requested now (their latency hides in the loop)
-  const float cs_h = GH.colscale[col], cs_l = GL.colscale[col];
-
-  // ---- prologue: the slab (every chunk), one float4 of 4 channels per item ----------------
-  constexpr int ASLOTS = (CS_MAXCH * SRM * 8 + 511) / 512;
-  const int SR = RM + kh - 1, nitems = nch * SR * 8;
-  f32x4 av[ASLOTS];
-#pragma unroll
-  for (int i = 0; i < ASLOTS; ++i) {
-    const int idx = tid + 512 * i;
-    av[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
-    if (idx < nitems) {
-      int m = m0 - padh + sr;
-      m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
-      av[i] = *(const f32x4 *)(p.x + (int64_t)m * p.x_stride + c * 32 + seg * 4);
-    }
-  }
-  float amax = 0.f;
-#pragma unroll
-  for (int i = 0; i < ASLOTS; ++i) {
-    const int idx = tid + 512 * i;
-    if (idx >= nitems) break;
-    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
-    const f32x4 x = av[i];
-    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
-    f16x4 h, t;
-    split2h(x, h, t);
-    _Float16 *dst = lds + c * 2 * AIMG + sr * SL_P + seg * 4;
-    *(f16x4 *)dst = h;
-    *(f16x4 *)(dst + AIMG) = t;
-  }
-  if (tid < nch * 2 * (SL_P / 8)) {  // the zero row of every (chunk, plane) image
-    const int img = tid / (SL_P / 8), part = tid % (SL_P / 8);
-    *(u32x4 *)(lds + img * AIMG + SRM * SL_P + part * 8) = (u32x4){0u, 0u, 0u, 0u};
-  }
-  bool bad = !(amax <= 65504.f);
-  // per-row tap masks of both groups: bit j set iff frame t + j - pad lies in the sequence
-  unsigned mh[MI], ml[MI];
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi) {
-    const int m = m0 + mi * 16 + fr;
-    unsigned a = 0, b = 0;
-    if (m < p.M) {
-      const int t = m % p.T;
-      int lo = max(padh - t, 0), hi = min(p.T - 1 + padh - t, kh - 1);
-      if (lo <= hi) a = (2u << hi) - (1u << lo);
-      lo = max(GL.pad - t, 0), hi = min(p.T - 1 + GL.pad - t, kl - 1);
-      if (lo <= hi) b = (2u << hi) - (1u << lo);
-    }
-    mh[mi] = a;
-    ml[mi] = b;
-  }
-  __syncthreads();
-
-  f32x4 acch[MI], accl[MI];
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi) acch[mi] = accl[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int i0 = 0; i0 < ns; i0 += CS_PF) {
-#pragma unroll
-    for (int v = 0; v < CS_PF; ++v) {
-      const int i = i0 + v;
-      const int q = wave + 8 * min(i, ns - 1);
-      const bool hv = q < QH;  // wave-uniform
-      const int qq = hv ? q : q - QH, j = qq / nch, c = qq - j * nch;
-      const _Float16 *Ab = lds + c * 2 * AIMG;
-      const int dr = hv ? j : j + dpl;
-      f16x8 ah[MI], at[MI];
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const bool ok = (((hv ? mh[mi] : ml[mi]) >> j) & 1u) != 0;
-        const int o = (ok ? mi * 16 + fr + dr : SRM) * SL_P + fs * 8;
-        ah[mi] = *(const f16x8 *)(Ab + o);
-        at[mi] = *(const f16x8 *)(Ab + AIMG + o);
-      }
-      const f16x8 z = {};
-      const bool live = i < ns;  // ring steps past the end multiply zeros
-      const f16x8 b0 = live ? rb0[v] : z, b1 = live ? rb1[v] : z;
-      const f16x8 bh = b0 * (_Float16)(1.0f / H3_SCALE);
-      if (hv) {
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) acch[mi] = mma16(at[mi], bh, acch[mi]);  // small terms first
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) acch[mi] = mma16(ah[mi], b1, acch[mi]);
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) acch[mi] = mma16(ah[mi], b0, acch[mi]);
-      } else {
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) accl[mi] = mma16(at[mi], bh, accl[mi]);
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) accl[mi] = mma16(ah[mi], b1, accl[mi]);
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) accl[mi] = mma16(ah[mi], b0, accl[mi]);
-      }
-      loadB(i + CS_PF, rb0[v], rb1[v]);  // refill the slot in place
-    }
-  }
-
-  // ---- the 8 waves' partial sums meet in LDS (the slab is dead after the barrier) ---------
-  __syncthreads();
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi) {
-    red[((wave * 2 + 0) * MI + mi) * 64 + lane] = acch[mi];
-    red[((wave * 2 + 1) * MI + mi) * 64 + lane] = accl[mi];
-  }
-  __syncthreads();
-  // thread t finishes slot t = (unit uu, fragment mi, lane): 4 rows of one column
-  for (int t = tid; t < 2 * MI * 64; t += 512) {
-    const int uu = t / (MI * 64), mi = (t >> 6) % MI, ln = t & 63;
-    f32x4 v4 = red[(uu * MI + mi) * 64 + ln];
-#pragma unroll
-    for (int w = 1; w < 8; ++w) v4 += red[((w * 2 + uu) * MI + mi) * 64 + ln];
-    const GemmGroup &GW = uu ? GL : GH;
-    const int c = cset * 16 + (ln & 15);
-    const float cs = uu ? __shfl(cs_l, ln) : __shfl(cs_h, ln);  // lane ln & 15 holds column c
-    const float bias = GW.bias ? GW.bias[c] : 0.f;
-    const float sc = GW.scale ? GW.scale[c] : 1.f, sh = GW.scale ? GW.shift[c] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = m0 + mi * 16 + 4 * (ln >> 4) + i;
-      if (row >= p.M) continue;
-      bad |= !__builtin_isfinite(v4[i]);
-      float y = v4[i] * cs + bias;
-      if (p.relu) y = fmaxf(y, 0.f);
-      if (GW.scale) y = y * sc + sh;
-      p.y[(int64_t)row * p.y_stride + GW.ycol0 + c] = y;
-    }
-  }
-  if (bad && p.status) atomicOr(p.status, 1u);
-}
-
 // sum of the skinny kernel's split partials + the conv epilogue; blockIdx.y is the group
 // (uniform: its parameters stay scalar loads).  L = 4 lanes share an element when there
 // are many splits (L = 1 below 8): lane q adds splits q, q + L, ... in order and xor-
@@ -3131,33 +2925,6 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
   return FTMI_OK;
 }
 
-// conv_bank_cs_kernel: a CBHG bank (groups k = K .. 1, even K, equal 16-column-multiple
-// widths) of at most CS_MMAX rows and Cin <= 256 (a multiple of 32), plain epilogue;
-// FTMI_BANK_CS=0 (read per call) keeps the channel-split skinny kernel
-static bool bank_cs_ok(const GemmParams &p, int epi, bool maxpool) {
-  const char *e = getenv("FTMI_BANK_CS");
-  if (e && atoi(e) == 0) return false;
-  if (epi != EPI_CONV || maxpool || p.ngroups < 2 || p.ngroups % 2 || p.To != p.T) return false;
-  if (p.M <= 0 || p.M > CS_MMAX || p.Cin % 32 || p.Cin > CS_MAXCH * 32) return false;
-  if (!p.y || p.yt || p.residual || p.x_split || p.pool_out || p.y_split_c) return false;
-  for (int i = 0; i < p.ngroups; ++i)
-    if (p.g[i].k != p.ngroups - i || p.g[i].N != p.g[0].N || p.g[i].N % 16 || !p.g[i].w3 ||
-        !p.g[i].colscale)
-      return false;
-  return true;
-}
-
-static int launch_bank_cs(const GemmParams &p, hipStream_t s) {
-  const int units = (p.ngroups / 2) * (p.g[0].N / 16);
-  if (p.M <= 64) {
-    hipLaunchKernelGGL(conv_bank_cs_kernel<2>, dim3(units * ((p.M + 31) / 32)), dim3(512), 0, s, p);
-  } else {
-    hipLaunchKernelGGL(conv_bank_cs_kernel<4>, dim3(units * ((p.M + 63) / 64)), dim3(512), 0, s, p);
-  }
-  FTMI_CHECK_LAUNCH();
-  return FTMI_OK;
-}
-
 int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hipStream_t s) {
   if (nblocks <= 0) return FTMI_OK;
   dim3 grid(nblocks), block(256);
@@ -3178,7 +2945,6 @@ int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hip
     if (!(mma == 2 && presplit && !maxpool && slab_ok(p, epi))) return FTMI_E_UNSUPPORTED;
     return launch_slab(p, epi, false, s);
   }
-  if (mma == 2 && presplit && bank_cs_ok(p, epi, maxpool)) return launch_bank_cs(p, s);
   if (mma == 2 && presplit && skinny_ok(p, epi)) return launch_skinny(p, epi, maxpool, s);
   if (p.ngroups > 1 && p.split_req > 1) {  // a bank split only serves the skinny kernel
     GemmParams q = p;

@@ -149,18 +149,6 @@ def _skinny(mma: int, T: int, To: int, Cin: int, k: int, M: int, N: Optional[int
             and Cin % 16 == 0 and k <= 16 and rows_ok)
 
 
-BANK_CS_MMAX = 128  # gemm.hip CS_MMAX
-
-
-def _bank_cs(mma: int, wsp, M: int, K: int, Cin: int, Cout: int) -> bool:
-    """Whether a conv bank takes conv_bank_cs_kernel (gemm.hip bank_cs_ok): f16x3, at most
-    128 rows, Cin a multiple of 32 up to 256, even K, 16-column groups — one block per
-    (group pair, column set, row tile) over every input channel, no split partials."""
-    return (os.environ.get('FTMI_BANK_CS', '1') != '0' and mma == 2 and wsp is not None
-            and 0 < M <= BANK_CS_MMAX and Cin % 32 == 0 and Cin <= 256 and K >= 2
-            and K % 2 == 0 and Cout % 16 == 0)
-
-
 def _skinny_split(Cin: int) -> int:
     """Channel split of the skinny kernel: two 32-channel chunks per block."""
     nch = -(-Cin // 32)
@@ -388,9 +376,7 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
     flops = 2.0 * M * Cout * Cin * K * (K + 1) / 2
     mma, wsp = _gemm_mma(mma, w_split)
     sk, part, last = 0, None, 0
-    if not pool and not x_split and _bank_cs(mma, wsp, M, K, Cin, Cout):
-        pass  # gemm.hip conv_bank_cs_kernel: all channels per block, no partial sums
-    elif not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
+    if not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
         sk = _skinny_split(Cin)  # weight-streaming kernel: partial sums, finished in order
         if os.environ.get('FTMI_BANK_LAST', '0') != '0':
             # tile counters + partials, finished in-kernel by each tile's last split block

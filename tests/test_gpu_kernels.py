@@ -227,7 +227,6 @@ def test_conv_bank_last_arriver_counters(rng, monkeypatch):
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     monkeypatch.setenv('FTMI_BANK_LAST', '1')
-    monkeypatch.setenv('FTMI_BANK_CS', '0')  # the prenet bank on the channel-split kernel
 
     def bank(K, Cin, T):
         C = 256
@@ -301,23 +300,19 @@ def test_split_rows_bank_to_proj1(K, Cin, B, T, split_k, rng, monkeypatch):
         ops.conv1d(ys, w1, 3, 1, mma=0, x_split=True)
 
 
-@pytest.mark.parametrize('schedule', ['cs', 'pairs', 'pairs-finish', 'quarters', 'quarters-finish', 'groups'])
+@pytest.mark.parametrize('schedule', ['pairs', 'pairs-finish', 'quarters', 'quarters-finish', 'groups'])
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (8, 80, 1, 100), (4, 64, 2, 50),
                                      (16, 256, 2, 64), (16, 256, 1, 37), (2, 32, 1, 128),
                                      (16, 256, 1, 129)])
 def test_conv_bank_skinny_schedules(K, Cin, B, T, schedule, rng, monkeypatch):
-    """The weight-streaming bank at batch-1 sizes on every block schedule: 'cs' = one block
-    per (group pair, column set, row tile) over every input channel (conv_bank_cs_kernel, the
-    default for M <= 128 and Cin % 32 == 0: 64-row tiles, 32-row tiles at M <= 64, sequences
-    starting inside a tile at B = 2; Cin = 80 and M = 129 fall back to the split kernel);
-    the channel-split kernel (FTMI_BANK_CS=0) with group pairs (k, K + 1 - k) per block and
-    one (unit, half) per wave, the same with each wave on a quarter of a heavy and of a light
-    unit (conv_bank_qb_kernel, FTMI_BANK_QB=1), one group per block (FTMI_BANK_BALANCED=0);
-    each with the in-kernel last-arriver finish (FTMI_BANK_LAST=1) or the finish launch;
-    f16x3, against the numpy oracle."""
+    """The weight-streaming bank at batch-1 sizes on every block schedule: group pairs
+    (k, K + 1 - k) per block with one (unit, half) per wave (the default), the same with each
+    wave on a quarter of a heavy and of a light unit (conv_bank_qb_kernel, FTMI_BANK_QB=1),
+    one group per block (FTMI_BANK_BALANCED=0); each with the in-kernel last-arriver finish
+    (FTMI_BANK_LAST=1) or the finish launch; f16x3, against the numpy oracle.  M = 129: two
+    row tiles, the second with one row."""
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
-    monkeypatch.setenv('FTMI_BANK_CS', '1' if schedule == 'cs' else '0')
     monkeypatch.setenv('FTMI_BANK_BALANCED', '0' if schedule == 'groups' else '1')
     monkeypatch.setenv('FTMI_BANK_QB', '1' if schedule.startswith('quarters') else '0')
     # the tile's last split block finishes in-kernel (FTMI_BANK_LAST, default), or *-finish:
