@@ -1554,6 +1554,62 @@ __device__ unsigned long long ftmi_skinny_stamps[4096 * 8];
   } while (0)
 #endif
 
+// The last split block of a bank tile (FTMI_BANK_LAST) finishes it: the tile = rows m0 ..
+// m0 + 127 of the four units (group gi / its pair partner, column sets nt, nt + 1).  Item =
+// (row, unit, 4 columns); every thread issues the write-through-stored partials of ALL its
+// items and splits (16-B sc1 loads, clamped so no load is conditional) before it adds any,
+// so the reducer pays about one round trip instead of one per element and split; the
+// splits are added in split order (the finish kernel's sums, bit for bit).
+__device__ __forceinline__ bool bank_last_reduce(const GemmParams &p, int gi, int nt, int m0) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int IT = SK_BM * 16 / 512, SPL = 4;  // items per thread, splits per load batch
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.part, (short)0, 0x7FFFFFF0, 0x00020000);
+  const int rows = min(SK_BM, p.M - m0);
+  bool bad = false;
+  f32x4 v[IT];
+  int off[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    v[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int e = threadIdx.x + 512 * i, r = min(e >> 4, rows - 1), uu = (e >> 2) & 3;
+    const int g = (uu >> 1) ? p.ngroups - 1 - gi : gi;
+    const int c = min((nt + (uu & 1)) * 16 + (e & 3) * 4, p.g[g].N - 4);
+    off[i] = ((m0 + r) * p.ldp + p.g[g].ycol0 + c) * 4;  // bytes; < 2^31 (host check)
+  }
+  const int sb = p.M * p.ldp * 4;  // bytes per split
+  for (int s0 = 0; s0 < p.split; s0 += SPL) {
+    u32x4 r[IT][SPL];
+#pragma unroll
+    for (int i = 0; i < IT; ++i)
+#pragma unroll
+      for (int k = 0; k < SPL; ++k)
+        r[i][k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[i], min(s0 + k, p.split - 1) * sb, 16);
+#pragma unroll
+    for (int i = 0; i < IT; ++i)
+#pragma unroll
+      for (int k = 0; k < SPL; ++k)
+        if (s0 + k < p.split) v[i] += __builtin_bit_cast(f32x4, r[i][k]);
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = threadIdx.x + 512 * i, uu = (e >> 2) & 3;
+    const int g = (uu >> 1) ? p.ngroups - 1 - gi : gi;
+    const GemmGroup &GF = p.g[g];
+    const int c0 = (nt + (uu & 1)) * 16 + (e & 3) * 4, row = m0 + (e >> 4);
+    if ((e >> 4) >= rows || c0 >= GF.N) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float y = v[i][q];
+      bad |= !__builtin_isfinite(y);
+      if (GF.bias) y += GF.bias[c0 + q];
+      if (p.relu) y = fmaxf(y, 0.f);
+      if (GF.scale) y = y * GF.scale[c0 + q] + GF.shift[c0 + q];
+      p.y[(int64_t)row * p.y_stride + GF.ycol0 + c0 + q] = y;
+    }
+  }
+  return bad;
+}
+
 // DIAG (timing experiments only, FTMI_SKINNY_DIAG on the bank schedule; results invalid):
 // bit 0 = the A fragments read once before the loop (no LDS reads in it), bit 1 = no MFMAs
 // (the loaded weights feed one VALU add), bit 2 = every weight load from one L2-hot line
@@ -1813,28 +1869,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
           __hip_atomic_store(p.tile_cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
-      if (s_last) {
-        // element e = (row, unit, column): 16 lanes read one unit's 64-B row piece; units
-        // (group of the pair, column set) as the waves' cw
-        const int rows = min(SK_BM, p.M - m0);
-        for (int e = threadIdx.x; e < rows * 64; e += 512) {
-          const int colf = e & 15, uu = (e >> 4) & 3, row = m0 + (e >> 6);
-          const int g = (uu >> 1) ? p.ngroups - 1 - gi : gi;
-          const GemmGroup &GF = p.g[g];
-          const int c = (nt + (uu & 1)) * 16 + colf;
-          if (c >= GF.N) continue;
-          const float *src = p.part + (size_t)row * p.ldp + GF.ycol0 + c;
-          float v = 0.f;
-          for (int sp = 0; sp < p.split; ++sp)
-            v += __hip_atomic_load(src + (size_t)sp * p.M * p.ldp, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-          bad |= !__builtin_isfinite(v);
-          if (GF.bias) v += GF.bias[c];
-          if (p.relu) v = fmaxf(v, 0.f);
-          if (GF.scale) v = v * GF.scale[c] + GF.shift[c];
-          if (p.y) p.y[(int64_t)row * p.y_stride + GF.ycol0 + c] = v;
-        }
-      }
+      if (s_last) bad |= bank_last_reduce(p, gi, nt, m0);
     }
   }
   if (bad && p.status) atomicOr(p.status, 1u);
@@ -2039,26 +2074,7 @@ __global__ __launch_bounds__(512, 1) void conv_bank_qb_kernel(const GemmParams p
           __hip_atomic_store(p.tile_cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
-      if (s_last) {
-        // element e = (row, unit, column): 16 consecutive lanes read one unit's 64-B row piece
-        const int rows = min(SK_BM, p.M - m0);
-        for (int e = tid; e < rows * 64; e += 512) {
-          const int col = e & 15, uu = (e >> 4) & 3, row = m0 + (e >> 6);
-          const int g = (uu & 1) ? p.ngroups - 1 - gi : gi;
-          const GemmGroup &GF = p.g[g];
-          const int c = (nt + (uu >> 1)) * 16 + col;
-          if (c >= GF.N) continue;
-          const float *src = p.part + (size_t)row * p.ldp + GF.ycol0 + c;
-          float v = 0.f;
-          for (int sp = 0; sp < p.split; ++sp)
-            v += __hip_atomic_load(src + (size_t)sp * p.M * p.ldp, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-          if (GF.bias) v += GF.bias[c];
-          if (p.relu) v = fmaxf(v, 0.f);
-          if (GF.scale) v = v * GF.scale[c] + GF.shift[c];
-          if (p.y) p.y[(int64_t)row * p.y_stride + GF.ycol0 + c] = v;
-        }
-      }
+      if (s_last) bad |= bank_last_reduce(p, gi, nt, m0);
     }
   }
   if (bad && p.status) atomicOr(p.status, 1u);
@@ -2877,7 +2893,8 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
     const char *qb = getenv("FTMI_BANK_QB");
     const bool qbk = qb && atoi(qb) == 1 && !(dg && atoi(dg) != 0) && !q.yt && !q.residual;
     const bool last = q.tile_cnt && q.split > 1 && (int)grid.x <= FTMI_BANK_COUNTERS &&
-                      !q.yt && !q.residual && !(dg && atoi(dg) != 0);
+                      !q.yt && !q.residual && q.y && !(dg && atoi(dg) != 0) &&
+                      (int64_t)q.split * q.M * q.ldp * 4 < INT32_MAX;  // reducer byte offsets
     if (last) {  // finished in-kernel by each tile's last split block: no finish launch
       if (qbk)
         hipLaunchKernelGGL(conv_bank_qb_kernel<true>, grid, block, 0, s, q);
