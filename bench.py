@@ -121,6 +121,31 @@ def pmc_traffic(label: str, path: str = PMC_PROFILE):
             'source': os.path.relpath(path, ROOT)}
 
 
+def time_prenet_bank(model, x, reps: int = 20) -> float:
+    """ms per call of the prenet CBHG conv bank exactly as generate() issues it (same
+    operand, packed weights, pooled / split-output choice), back to back on torch's stream
+    (bank kernel + the split finish launch: the whole fused Conv1d+ReLU+BN bank)."""
+    from forwardtacotron_amd import ops
+    cb = model.prenet
+    h = ops.embedding(x, model.embedding.weight.detach())
+    bank_w, scale, shift, _, bank3, _ = cb.packed_weights()
+    pooled = ops.bank_pools(h, cb.K, cb.channels, w_split=bank3)
+
+    def call():
+        return ops.conv_bank(h, bank_w, cb.K, cb.channels, scale, shift, w_split=bank3,
+                             pool=pooled, split_out=pooled and ops.SPLIT_ROWS)
+    for _ in range(3):
+        call()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(reps):
+        call()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -300,6 +325,9 @@ def main():
         fp_module.FP_GRAPH = True
         kern_all = probe_eager.summary()
 
+    prenet_bank_ms = (time_prenet_bank(model, x) if world == 1 and args.model == 'forward_tacotron'
+                      else None)
+
     if world > 1:
         t = torch.tensor([elapsed, host_elapsed or 0.0, host_serial or 0.0], device=dev,
                          dtype=torch.float64)
@@ -361,16 +389,20 @@ def main():
         prenet = None
         if pre:
             lab, v = pre[0]
-            s_ = v['avg_ms'] / 1e3
-            prenet = {'kernel': lab, 'avg_launch_ms': round(v['avg_ms'], 4),
+            ms = prenet_bank_ms if prenet_bank_ms is not None else v['avg_ms']
+            s_ = ms / 1e3
+            prenet = {'kernel': lab, 'avg_launch_ms': round(ms, 4),
                       'hbm_achieved_GBs': round(v['bytes'] / s_ / 1e9, 1), 'hbm_peak_GBs': PEAK_HBM_GBS,
                       'hbm_frac': round(v['bytes'] / s_ / 1e9 / PEAK_HBM_GBS, 4),
                       'algorithmic_bytes': v['bytes'],
                       'mfma_achieved_TFLOPs': round(v['flops'] / s_ / 1e12, 2),
                       'mfma_frac': round(v['flops'] / s_ / 1e12 / PEAK_X3_TFLOPS, 4),
-                      'measured': ('HIP events, one eager generate() after the timed steps '
-                                   '(which replay the phoneme phase as a HIP graph)'
-                                   if kern_all is not kern else 'HIP events, timed steps')}
+                      'measured': ('HIP events around 20 back-to-back calls of the bank as generate() '
+                                   'issues it (bank kernel + the split finish launch where the '
+                                   'channel-split kernel runs; weights cache-warm as in a generate() '
+                                   'loop) on the same embedded tokens, after the timed steps'
+                                   if prenet_bank_ms is not None else 'HIP events, timed steps'),
+                      'eager_single_call_ms': round(v['avg_ms'], 4)}
         value = frames / elapsed
         # valid frames: frames of the non-pad phonemes (the rest of B * T_mel is padding)
         tok = (x_np != 0) if world == 1 else None
