@@ -1066,6 +1066,100 @@ constexpr int SL_AIMG = (SL_SR + 1) * SL_P;         // halves per (buffer, plane
 constexpr int SL_BIMG = SL_BN * SL_P;               // halves per (buffer, plane) B image
 constexpr int SL_TP = SL_BN + 4;                    // floats per row of the epilogue tile
 
+// The slab kernels' epilogue: the finished fp32 tile [SL_BM][SL_TP] (colscale applied) in
+// LDS -> split-K partials, or bias / ReLU / BN / residual (conv: plain, transposed or pooled
+// rows, optionally as f16x3 split rows), or the highway gating.  Every store moves 16 B.
+template <int EPI, int NTHR>
+__device__ __forceinline__ void slab_epilogue(const GemmParams &p, const GemmGroup &G,
+                                              float *tile, int m0, int n0, int tid) {
+  const int rows = min(SL_BM, p.M - m0);
+  const int ncols = min(SL_BN, G.N - n0);  // a multiple of 4 (slab_ok)
+
+  if (p.split > 1) {  // raw partial sums; splitk_epilogue_kernel finishes
+    float *part = p.part + (size_t)blockIdx.y * p.M * G.N;
+    for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
+      const int r = idx >> 5, c = (idx & 31) * 4;
+      if (r < rows && c < ncols)
+        *(f32x4 *)(part + (size_t)(m0 + r) * G.N + n0 + c) = *(const f32x4 *)(tile + r * SL_TP + c);
+    }
+    return;
+  }
+  if constexpr (EPI == EPI_CONV) {
+    if (p.pool_out) {  // finish every row in the tile, then store max(row - 1, row)
+      for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
+        const int r = idx >> 5, c = (idx & 31) * 4;
+        if (r >= rows || c >= ncols) continue;
+        const int col = n0 + c;
+        f32x4 v = *(const f32x4 *)(tile + r * SL_TP + c);
+        if (G.bias) v += *(const f32x4 *)(G.bias + col);
+        if (p.relu) v = fmax4(v, (f32x4){0.f, 0.f, 0.f, 0.f});
+        if (G.scale) v = v * *(const f32x4 *)(G.scale + col) + *(const f32x4 *)(G.shift + col);
+        *(f32x4 *)(tile + r * SL_TP + c) = v;
+      }
+      __syncthreads();
+      float ymax = 0.f;
+      for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
+        const int r = idx >> 5, c = (idx & 31) * 4;
+        if (r == 0 || r >= rows || c >= ncols) continue;
+        const int row = m0 + r, col = n0 + c;
+        f32x4 v = *(const f32x4 *)(tile + r * SL_TP + c);
+        if (row % p.T > 0) v = fmax4(v, *(const f32x4 *)(tile + (r - 1) * SL_TP + c));
+        if (p.y_split_c) {  // split rows for the next f16x3 GEMM (proj1), range-checked here
+          ymax = fmaxf(ymax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          f16x4 h, t;
+          split2h(v, h, t);
+          _Float16 *yr = (_Float16 *)(p.y + (int64_t)row * p.y_stride) + G.ycol0 + col;
+          *(f16x4 *)yr = h;
+          *(f16x4 *)(yr + p.y_split_c) = t;
+        } else {
+          *(f32x4 *)(p.y + (int64_t)row * p.y_stride + G.ycol0 + col) = v;
+        }
+      }
+      if (!(ymax <= 65504.f) && p.status) atomicOr(p.status, 1u);
+      return;
+    }
+    for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
+      const int r = idx >> 5, c = (idx & 31) * 4;
+      if (r >= rows || c >= ncols) continue;
+      const int row = m0 + r, col = n0 + c;
+      f32x4 v = *(const f32x4 *)(tile + r * SL_TP + c);
+      if (G.bias) v += *(const f32x4 *)(G.bias + col);
+      if (p.relu) v = fmax4(v, (f32x4){0.f, 0.f, 0.f, 0.f});
+      if (G.scale) v = v * *(const f32x4 *)(G.scale + col) + *(const f32x4 *)(G.shift + col);
+      if (p.residual) v += *(const f32x4 *)(p.residual + (int64_t)row * p.res_stride + col);
+      if (p.y) *(f32x4 *)(p.y + (int64_t)row * p.y_stride + G.ycol0 + col) = v;
+      if (p.yt) *(f32x4 *)(tile + r * SL_TP + c) = v;  // finished values for the yt pass
+    }
+    if (p.yt) {  // (B, N, To) copy: consecutive lanes take consecutive frames
+      __syncthreads();
+      for (int idx = tid; idx < SL_BM * SL_BN; idx += NTHR) {
+        const int r = idx & (SL_BM - 1), c = idx / SL_BM;
+        if (r >= rows || c >= ncols) continue;
+        const int row = m0 + r, b = row / p.To, t = row - b * p.To;
+        p.yt[((int64_t)b * p.yt_channels + G.ycol0 + n0 + c) * p.To + t] = tile[r * SL_TP + c];
+      }
+    }
+  } else {
+    // highway: packed 32-column blocks [W1 | W2] per 64 GEMM columns; GEMM columns
+    // q*64 + h (W1) and q*64 + 32 + h (W2) of the tile give output column n0/2 + q*32 + h
+    for (int idx = tid; idx < SL_BM * (SL_BN / 8); idx += NTHR) {
+      const int r = idx >> 4, o = (idx & 15) * 4, q = o >> 5, h = o & 31;
+      if (r >= rows || q * 64 >= ncols) continue;
+      const int row = m0 + r, col = n0 / 2 + o;
+      const f32x4 x1 = *(const f32x4 *)(tile + r * SL_TP + q * 64 + h) + *(const f32x4 *)(p.b1 + col);
+      const f32x4 x2 = *(const f32x4 *)(tile + r * SL_TP + q * 64 + 32 + h) + *(const f32x4 *)(p.b2 + col);
+      const f32x4 xin = *(const f32x4 *)(p.x + (int64_t)row * p.x_stride + col);
+      f32x4 out;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g = ftmi_sigmoid(x2[e]);
+        out[e] = highway_mix(g, x1[e], xin[e]);
+      }
+      *(f32x4 *)(p.y + (int64_t)row * p.y_stride + col) = out;
+    }
+  }
+}
+
 // WS (warp-specialised, 768 threads): waves 0-7 only read fragments and issue MFMAs; waves
 // 8-11 do all staging (global loads, the slab's f16 split, LDS stores), so the staging VALU
 // and load waits never sit in the MFMA waves' instruction streams.  !WS: all 8 waves do both.
@@ -1416,92 +1510,295 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
     __syncthreads();
   }
   if (bad && p.status) atomicOr(p.status, 1u);
-  const int rows = min(SL_BM, p.M - m0);
-  const int ncols = min(SL_BN, G.N - n0);  // a multiple of 4 (slab_ok)
+  slab_epilogue<EPI, NTHR>(p, G, tile, m0, n0, tid);
+}
 
-  if (p.split > 1) {  // raw partial sums; splitk_epilogue_kernel finishes
-    float *part = p.part + (size_t)blockIdx.y * p.M * G.N;
-    for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
-      const int r = idx >> 5, c = (idx & 31) * 4;
-      if (r < rows && c < ncols)
-        *(f32x4 *)(part + (size_t)(m0 + r) * G.N + n0 + c) = *(const f32x4 *)(tile + r * SL_TP + c);
-    }
-    return;
+// ---- slab kernel with fragment prefetch (default for single-group k = 1 GEMMs) ----------
+// The slab kernel above stalls at the top of every step: the step's B plane is stored just
+// before the barrier, so every wave issues its 16 fragment reads after it and waits for them
+// (PMC at the c5 k9 FFN conv, warp-specialised form: MFMA busy 59 %, waves parked in waitcnt /
+// barrier 41 % of their cycles).  Here the fragments of step s + 1 are read DURING step s,
+// into a second register set, while the MFMAs of step s run: the B planes are triple-buffered
+// (B(s + 2) is stored in iteration s, so B(s + 1) is visible one barrier earlier) and so is
+// the slab (chunk c is stored in iteration c k - 2).  The LDS images drop the 96-B padded
+// pitch for unpadded 64-B rows whose 16-B segments are XOR-swizzled by row bit 2
+// (segment s of row r at s ^ 2 ((r >> 2) & 1)): conflict-free ds_read_b128 fragment reads for
+// 16 consecutive rows from any first row (every tap shift), 3 + 3 buffers in 150 KB.
+// 512 threads: every wave multiplies and stages (the register budget of the warp-specialised
+// 768-thread form cannot hold two fragment sets).  Bit-identical to conv_gemm_slab_kernel
+// (same MFMA order and operands).  Measured (tools/slabp_ab.py, c3 / c5 shapes): k = 1
+// GEMMs 6-10 % faster than the 512-thread slab kernel; multi-tap convs and banks 0-6 %
+// SLOWER than the warp-specialised one: the staging (slab split, addresses) now sits in
+// the MFMA waves' instruction stream, ~200 VALU per 48 MFMAs per step, which the MFMA
+// issue shadow cannot absorb — the LDS wait it removes was not the only cost.
+constexpr int SP_ROW = 32;                     // halves per LDS row (32 channels, no pad)
+constexpr int SP_AIMG = (SL_SR + 1) * SP_ROW;  // halves per (buffer, plane) slab image
+constexpr int SP_BIMG = SL_BN * SP_ROW;        // halves per (buffer, plane) B image
+constexpr int SP_NBUF = 3;
+__device__ __forceinline__ int sp_off(int r, int seg) {  // half offset of (row, 16-B segment)
+  return r * SP_ROW + ((seg ^ (((r >> 2) & 1) << 1)) << 3);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void conv_gemm_slabp_kernel(const GemmParams p) {
+  constexpr int NTHR = 512;
+  constexpr int ASLOTS = (SL_SR * 8 + NTHR - 1) / NTHR;  // 4-channel slab items per thread
+  constexpr int BSLOTS = 1024 / NTHR;                    // 16-B B items per thread and step
+  __shared__ __attribute__((aligned(16))) _Float16 lds[SP_NBUF * 2 * SP_AIMG + SP_NBUF * 2 * SP_BIMG];
+  static_assert(SL_BM * SL_TP * 4 <= sizeof(lds), "epilogue tile");
+  _Float16 *const lds_a = lds;
+  _Float16 *const lds_b = lds + SP_NBUF * 2 * SP_AIMG;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  // tile order: conv_gemm_slab_kernel's (XCD-aware)
+  const int TS = p.pool_out ? SL_BM - 1 : SL_BM;
+  const int MT = (p.M + TS - 1) / TS, NT = p.g[0].ntiles, VT = p.ngroups * NT;
+  const int bid = blockIdx.x, s8 = bid >> 3, q8 = s8 / VT;
+  int mt = q8 * 8 + (bid & 7), v8 = s8 - q8 * VT;
+  if (MT < 8) {
+    mt = bid % MT;
+    v8 = bid / MT;
   }
-  if constexpr (EPI == EPI_CONV) {
-    if (p.pool_out) {  // finish every row in the tile, then store max(row - 1, row)
-      for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
-        const int r = idx >> 5, c = (idx & 31) * 4;
-        if (r >= rows || c >= ncols) continue;
-        const int col = n0 + c;
-        f32x4 v = *(const f32x4 *)(tile + r * SL_TP + c);
-        if (G.bias) v += *(const f32x4 *)(G.bias + col);
-        if (p.relu) v = fmax4(v, (f32x4){0.f, 0.f, 0.f, 0.f});
-        if (G.scale) v = v * *(const f32x4 *)(G.scale + col) + *(const f32x4 *)(G.shift + col);
-        *(f32x4 *)(tile + r * SL_TP + c) = v;
-      }
-      __syncthreads();
-      float ymax = 0.f;
-      for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
-        const int r = idx >> 5, c = (idx & 31) * 4;
-        if (r == 0 || r >= rows || c >= ncols) continue;
-        const int row = m0 + r, col = n0 + c;
-        f32x4 v = *(const f32x4 *)(tile + r * SL_TP + c);
-        if (row % p.T > 0) v = fmax4(v, *(const f32x4 *)(tile + (r - 1) * SL_TP + c));
-        if (p.y_split_c) {  // split rows for the next f16x3 GEMM (proj1), range-checked here
-          ymax = fmaxf(ymax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-          f16x4 h, t;
-          split2h(v, h, t);
-          _Float16 *yr = (_Float16 *)(p.y + (int64_t)row * p.y_stride) + G.ycol0 + col;
-          *(f16x4 *)yr = h;
-          *(f16x4 *)(yr + p.y_split_c) = t;
-        } else {
-          *(f32x4 *)(p.y + (int64_t)row * p.y_stride + G.ycol0 + col) = v;
-        }
-      }
-      if (!(ymax <= 65504.f) && p.status) atomicOr(p.status, 1u);
-      return;
-    }
-    for (int idx = tid; idx < SL_BM * (SL_BN / 4); idx += NTHR) {
-      const int r = idx >> 5, c = (idx & 31) * 4;
-      if (r >= rows || c >= ncols) continue;
-      const int row = m0 + r, col = n0 + c;
-      f32x4 v = *(const f32x4 *)(tile + r * SL_TP + c);
-      if (G.bias) v += *(const f32x4 *)(G.bias + col);
-      if (p.relu) v = fmax4(v, (f32x4){0.f, 0.f, 0.f, 0.f});
-      if (G.scale) v = v * *(const f32x4 *)(G.scale + col) + *(const f32x4 *)(G.shift + col);
-      if (p.residual) v += *(const f32x4 *)(p.residual + (int64_t)row * p.res_stride + col);
-      if (p.y) *(f32x4 *)(p.y + (int64_t)row * p.y_stride + G.ycol0 + col) = v;
-      if (p.yt) *(f32x4 *)(tile + r * SL_TP + c) = v;  // finished values for the yt pass
-    }
-    if (p.yt) {  // (B, N, To) copy: consecutive lanes take consecutive frames
-      __syncthreads();
-      for (int idx = tid; idx < SL_BM * SL_BN; idx += NTHR) {
-        const int r = idx & (SL_BM - 1), c = idx / SL_BM;
-        if (r >= rows || c >= ncols) continue;
-        const int row = m0 + r, b = row / p.To, t = row - b * p.To;
-        p.yt[((int64_t)b * p.yt_channels + G.ycol0 + n0 + c) * p.To + t] = tile[r * SL_TP + c];
-      }
-    }
-  } else {
-    // highway: packed 32-column blocks [W1 | W2] per 64 GEMM columns; GEMM columns
-    // q*64 + h (W1) and q*64 + 32 + h (W2) of the tile give output column n0/2 + q*32 + h
-    for (int idx = tid; idx < SL_BM * (SL_BN / 8); idx += NTHR) {
-      const int r = idx >> 4, o = (idx & 15) * 4, q = o >> 5, h = o & 31;
-      if (r >= rows || q * 64 >= ncols) continue;
-      const int row = m0 + r, col = n0 / 2 + o;
-      const f32x4 x1 = *(const f32x4 *)(tile + r * SL_TP + q * 64 + h) + *(const f32x4 *)(p.b1 + col);
-      const f32x4 x2 = *(const f32x4 *)(tile + r * SL_TP + q * 64 + 32 + h) + *(const f32x4 *)(p.b2 + col);
-      const f32x4 xin = *(const f32x4 *)(p.x + (int64_t)row * p.x_stride + col);
-      f32x4 out;
+  const int gi = v8 / NT, nt = v8 - gi * NT;
+  if (mt >= MT) return;
+  const GemmGroup &G = p.g[gi];
+  const int m0 = p.pool_out ? mt * TS - 1 : mt * SL_BM, n0 = nt * SL_BN;
+  const int k = G.k, pad = G.pad, Cin = p.Cin;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int fr = lane & 15, fs = lane >> 4;
+  int nch = (Cin + 31) / 32, c_begin = 0;
+  if (p.split > 1) {
+    c_begin = blockIdx.y * p.kc_per;
+    nch = min(nch - c_begin, p.kc_per);
+  }
+  const int nsteps = nch * k;
+
+  // ---- slab staging: item i = (slab row tid / 8 + 64 i, 8-B granule tid & 7 = 4 channels);
+  // 32 lanes store 4 whole 64-B rows (all 64 banks once) -----------------------------------
+  const int SR = SL_BM + k - 1;
+  const int g8 = tid & 7, sr0 = tid >> 3;
+  unsigned aoff[ASLOTS];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float g = ftmi_sigmoid(x2[e]);
-        out[e] = highway_mix(g, x1[e], xin[e]);
+  for (int i = 0; i < ASLOTS; ++i) {
+    int mp = m0 - pad + sr0 + 64 * i;
+    mp = mp < 0 ? 0 : (mp >= p.M ? p.M - 1 : mp);  // clamped rows only feed masked taps
+    aoff[i] = (unsigned)mp * (unsigned)p.x_stride;
+  }
+  const unsigned cbase = (unsigned)c_begin * 32u, aseg = (unsigned)g8 * 4u;
+  const unsigned a_last = (unsigned)(nch - 1) * 32u;
+  unsigned ach = 0;
+  struct ARaw {
+    f32x4 v[ASLOTS];
+    bool ok;
+  };
+  auto loadA = [&](ARaw &r) {
+    const unsigned ch = cbase + (ach < a_last ? ach : a_last) + aseg;
+    r.ok = ch < (unsigned)Cin;
+    const unsigned o = r.ok ? ch : 0u;
+    if (p.x_split) {  // split rows: 4 heads + the same 4 tails in one register
+#pragma unroll
+      for (int i = 0; i < ASLOTS; ++i) {
+        const _Float16 *xr = (const _Float16 *)(p.x + aoff[i]) + o;
+        const u32x2 h = *(const u32x2 *)xr, t = *(const u32x2 *)(xr + Cin);
+        r.v[i] = __builtin_bit_cast(f32x4, ((u32x4){h.x, h.y, t.x, t.y}));
       }
-      *(f32x4 *)(p.y + (int64_t)row * p.y_stride + col) = out;
+    } else {
+#pragma unroll
+      for (int i = 0; i < ASLOTS; ++i) r.v[i] = *(const f32x4 *)(p.x + aoff[i] + o);
+    }
+    ach += 32;
+  };
+  float amax = 0.f;
+  auto storeA = [&](const ARaw &r, int buf) {
+    _Float16 *dst = lds_a + buf * 2 * SP_AIMG;
+#pragma unroll
+    for (int i = 0; i < ASLOTS; ++i) {
+      const int sr = sr0 + 64 * i;
+      if (sr >= SR) continue;
+      const int o = sp_off(sr, g8 >> 1) + (g8 & 1) * 4;
+      if (p.x_split) {
+        u32x4 b = __builtin_bit_cast(u32x4, r.v[i]);
+        if (!r.ok) b = (u32x4){0u, 0u, 0u, 0u};
+        *(u32x2 *)(dst + o) = (u32x2){b.x, b.y};
+        *(u32x2 *)(dst + SP_AIMG + o) = (u32x2){b.z, b.w};
+        continue;
+      }
+      const f32x4 v = sel4(r.ok, r.v[i]);
+      amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      f16x4 h, t;
+      split2h(v, h, t);
+      *(f16x4 *)(dst + o) = h;
+      *(f16x4 *)(dst + SP_AIMG + o) = t;
+    }
+  };
+
+  // ---- B: item = (plane, row n, 16-B segment = 8 channels) -------------------------------
+  const _Float16 *w16 = (const _Float16 *)G.w3;
+  const _Float16 *bsrc[BSLOTS];
+  int bdst[BSLOTS];
+#pragma unroll
+  for (int i = 0; i < BSLOTS; ++i) {
+    const int idx = tid + NTHR * i, pl = idx >> 9, rem = idx & 511, nl = rem >> 2, seg = rem & 3;
+    const int n = n0 + nl < G.N ? n0 + nl : G.N - 1;
+    bsrc[i] = w16 + ((int64_t)pl * G.N + n) * G.Kpad + seg * 8;
+    bdst[i] = pl * SP_BIMG + sp_off(nl, seg);
+  }
+  struct BRaw {
+    u32x4 v[BSLOTS];
+    bool ok;
+  };
+  int bj = 0, bc = 0;  // tap / chunk of the next B load
+  auto loadB = [&](BRaw &rb) {
+    const bool in = bc < nch;
+    const int ch = (int)cbase + (in ? bc : nch - 1) * 32 + (tid & 3) * 8;
+    rb.ok = ch < Cin;
+    const int off = (in ? bj : k - 1) * Cin + (rb.ok ? ch - (tid & 3) * 8 : 0);
+#pragma unroll
+    for (int i = 0; i < BSLOTS; ++i) rb.v[i] = *(const u32x4 *)(bsrc[i] + off);
+    if (++bj == k) {
+      bj = 0;
+      ++bc;
+    }
+  };
+  auto storeB = [&](const BRaw &rb, int buf) {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < BSLOTS; ++i)
+      *(u32x4 *)(lds_b + buf * 2 * SP_BIMG + bdst[i]) = rb.ok ? rb.v[i] : z;
+  };
+
+  unsigned vmask[4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + wm * 64 + mi * 16 + fr;
+    unsigned msk = 0;
+    if (m >= 0 && m < p.M) {
+      const int t = m % p.T;
+      const int lo = max(pad - t, 0), hi = min(p.T - 1 + pad - t, k - 1);
+      if (lo <= hi) msk = (2u << hi) - (1u << lo);
+    }
+    vmask[mi] = msk;
+  }
+
+  struct Frag {
+    f16x8 ah[4], at[4], b0[4], b1[4];
+  };
+  auto read_frags = [&](Frag &f, int c, int j, int bbuf) {
+    const _Float16 *Ab = lds_a + (c % SP_NBUF) * 2 * SP_AIMG;
+    const _Float16 *Bb = lds_b + bbuf * 2 * SP_BIMG;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const bool ok = (vmask[mi] >> j) & 1u;
+      const int o = sp_off(ok ? wm * 64 + mi * 16 + fr + j : SL_ZROW, fs);
+      f.ah[mi] = *(const f16x8 *)(Ab + o);
+      f.at[mi] = *(const f16x8 *)(Ab + SP_AIMG + o);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int o = sp_off(wn * 64 + ni * 16 + fr, fs);
+      f.b0[ni] = *(const f16x8 *)(Bb + o);
+      f.b1[ni] = *(const f16x8 *)(Bb + SP_BIMG + o);
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto mfma_frags = [&](const Frag &f) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const f16x8 bh = f.b0[ni] * (_Float16)(1.0f / H3_SCALE);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {  // small terms first
+        f32x4 c = acc[mi][ni];
+        c = mma16(f.at[mi], bh, c);
+        c = mma16(f.ah[mi], f.b1[ni], c);
+        c = mma16(f.ah[mi], f.b0[ni], c);
+        acc[mi][ni] = c;
+      }
+    }
+  };
+
+  // ---- prologue: slab 0 (and 1 when k == 1), B steps 0 and 1; loads of B 2 / 3, slab next --
+  if (tid < SP_NBUF * 2 * (SP_ROW / 8)) {  // the zero rows of every slab buffer and plane
+    const int img = tid / (SP_ROW / 8), part = tid % (SP_ROW / 8);
+    *(u32x4 *)(lds_a + img * SP_AIMG + SL_ZROW * SP_ROW + part * 8) = (u32x4){0u, 0u, 0u, 0u};
+  }
+  ARaw ra;
+  BRaw rb0, rb1;
+  loadA(ra);
+  loadB(rb0);
+  loadB(rb1);
+  storeA(ra, 0);
+  storeB(rb0, 0);
+  storeB(rb1, 1);
+  loadB(rb0);  // step 2
+  loadB(rb1);  // step 3
+  int next_a = 1;  // next chunk whose slab is stored (in iteration next_a * k - 2)
+  if (nch > 1) {
+    loadA(ra);
+    if (k == 1) {
+      storeA(ra, 1);
+      next_a = 2;
+      if (nch > 2) loadA(ra);
     }
   }
+  __syncthreads();
+  Frag f0, f1;
+  read_frags(f0, 0, 0, 0);
+  int c1 = k == 1 ? 1 : 0, j1 = k == 1 ? 0 : 1;  // chunk / tap of step s + 1
+  auto iter = [&](int s, BRaw &rbs, Frag &cur, Frag &nxt) {
+    if (s + 2 < nsteps) {
+      storeB(rbs, (s + 2) % SP_NBUF);
+      loadB(rbs);  // step s + 4 (clamped)
+    }
+    if (next_a < nch && s == next_a * k - 2) {
+      storeA(ra, next_a % SP_NBUF);
+      if (++next_a < nch) loadA(ra);
+    }
+    // fragments of step s + 1 (clamped at the end: a harmless re-read) under the MFMAs of s
+    const bool more = s + 1 < nsteps;
+    read_frags(nxt, more ? c1 : nch - 1, more ? j1 : k - 1, (more ? s + 1 : s) % SP_NBUF);
+    mfma_frags(cur);
+    __syncthreads();
+    if (++j1 == k) {
+      j1 = 0;
+      ++c1;
+    }
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    iter(s, rb0, f0, f1);
+    if (s + 1 >= nsteps) break;
+    iter(s + 1, rb1, f1, f0);
+  }
+  bool bad = !(amax <= 65504.f);
+  // colscale, range guard, then the tile through LDS (every wave is past its reads)
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int col = n0 + wn * 64 + ni * 16 + fr;
+    const float cs = G.colscale[col < G.N ? col : G.N - 1];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wm * 64 + mi * 16 + 4 * fs + i;
+        bad |= col < G.N && row < p.M && !__builtin_isfinite(acc[mi][ni][i]);
+        acc[mi][ni][i] *= cs;
+      }
+  }
+  float *tile = (float *)lds;
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        tile[(wm * 64 + mi * 16 + 4 * fs + i) * SL_TP + wn * 64 + ni * 16 + fr] = acc[mi][ni][i];
+  __syncthreads();
+  if (bad && p.status) atomicOr(p.status, 1u);
+  slab_epilogue<EPI, NTHR>(p, G, tile, m0, n0, tid);
 }
 
 // ---- skinny kernel: few output rows (M <= SK_MMAX, e.g. batch 1), the weight stream binds --
@@ -2796,6 +3093,17 @@ static bool slab_ws(const GemmParams &p) {
   return v < 0 ? (p.g[0].k > 1 || p.ngroups > 1) : v != 0;
 }
 
+// The fragment-prefetch slab kernel for single-group k = 1 GEMMs (LSTM / GRU input
+// projections: 6-10 % faster than the 512-thread slab kernel); multi-tap convolutions and
+// banks keep the warp-specialised kernel (the prefetch kernel stages in its MFMA waves,
+// ~200 VALU per 48 MFMAs, and measured 4-6 % slower there: DESIGN.md section 4).
+// FTMI_SLAB_PF (read per call): 0 = never, 1 = every slab launch without input pooling.
+static bool slab_pf_enabled(const GemmParams &p) {
+  const char *e = getenv("FTMI_SLAB_PF");
+  if (e) return atoi(e) != 0;
+  return p.ngroups == 1 && p.g[0].k == 1;
+}
+
 static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s) {
   GemmParams q = p;
   const int nch = (q.Cin + 31) / 32;
@@ -2814,7 +3122,12 @@ static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s
   const int MT = (q.M + TS - 1) / TS;
   const int nblk = (MT < 8 ? MT : (MT + 7) / 8 * 8) * q.ngroups * q.g[0].ntiles;  // whole XCD rounds
   dim3 grid(nblk, q.split), block(512);
-  if (slab_ws(q)) {
+  if (!maxpool && slab_pf_enabled(q)) {
+    if (epi == EPI_HIGHWAY)
+      hipLaunchKernelGGL(conv_gemm_slabp_kernel<EPI_HIGHWAY>, grid, block, 0, s, q);
+    else
+      hipLaunchKernelGGL(conv_gemm_slabp_kernel<EPI_CONV>, grid, block, 0, s, q);
+  } else if (slab_ws(q)) {
     block = dim3(768);
     if (epi == EPI_HIGHWAY)
       hipLaunchKernelGGL((conv_gemm_slab_kernel<EPI_HIGHWAY, false, true>), grid, block, 0, s, q);

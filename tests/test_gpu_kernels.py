@@ -757,3 +757,78 @@ def test_series_proj_add_and_rowdot(rng):
     b = np.array([0.3], np.float32)
     h = rng.normal(0, 1, (B, T, 128)).astype(np.float32)
     close(host(ops.rowdot(dev(h), dev(w), dev(b), 1.3)), (h @ w + b[0]) / np.float32(1.3))
+
+
+# ---------------------------------------------------------------- slab kernel prefetch
+# conv_gemm_slabp_kernel (FTMI_SLAB_PF=1, default) reads the fragments of step s + 1 during
+# step s from swizzled, triple-buffered LDS images; its MFMAs run in the same order on the
+# same operands as conv_gemm_slab_kernel (FTMI_SLAB_PF=0), so every output is BIT-identical.
+SLABP_CASES = [  # B, T, Cin, N, k, residual, transposed-out
+    (2, 300, 256, 256, 5, False, False),   # predictor conv
+    (3, 301, 96, 200, 7, True, True),      # ragged rows / columns, residual, (B, N, T) copy
+    (2, 700, 256, 1024, 9, False, False),  # FastPitch FFN conv1 (k = 9)
+    (2, 9, 32, 64, 16, False, False),      # k = 16 > T: every tap masked for some rows
+    (4, 70, 64, 1536, 1, False, False),    # k = 1: the slab of chunk 1 stored in the prologue
+    (2, 200, 80, 256, 3, True, False),     # Cin = 80: a partial last chunk
+    (1, 600, 512, 384, 2, False, False),   # even k
+]
+
+
+@pytest.mark.parametrize('B,T,Cin,N,k,res,tr', SLABP_CASES)
+def test_slab_prefetch_bit_identical(B, T, Cin, N, k, res, tr, rng, monkeypatch):
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    monkeypatch.setenv('FTMI_GEMM_SKINNY', '0')
+    x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
+    w = rng.normal(0, 1 / np.sqrt(Cin * k), (N, Cin, k)).astype(np.float32)
+    b = rng.normal(0, 0.1, N).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, N).astype(np.float32)
+    sh = rng.normal(0, 0.1, N).astype(np.float32)
+    r = rng.normal(0, 1, (B, T, N)).astype(np.float32)
+    wp = pack_conv(torch.from_numpy(w)).cuda()
+    w3 = ops.presplit_for(wp, 2)
+    outs = []
+    for pf in ('1', '0'):
+        monkeypatch.setenv('FTMI_SLAB_PF', pf)
+        yt = torch.empty(B, N, T, device='cuda') if tr else None
+        y, _ = ops.conv1d(dev(x), wp, k, k // 2, bias=dev(b), relu=True, bn=(dev(sc), dev(sh)),
+                          residual=dev(r) if res else None, out_t=yt, mma=2, w_split=w3)
+        outs.append((host(y), host(yt) if tr else None))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    if tr:
+        np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    ref = np.maximum(O.conv1d(x.transpose(0, 2, 1), w, k // 2, b)[:, :, :T], 0)
+    ref = ref * sc[None, :, None] + sh[None, :, None]
+    if res:
+        ref = ref + r.transpose(0, 2, 1)
+    close(outs[0][0], ref.transpose(0, 2, 1))
+
+
+@pytest.mark.parametrize('split_k', [1, 3])
+def test_slab_prefetch_split_k_and_pooled_bank(split_k, rng, monkeypatch):
+    """The prefetch kernel's split-K partials (3 splits over 8 chunks: 3 + 3 + 2) and the
+    pooled bank epilogue with split-row output are bit-identical to the previous kernel's."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    monkeypatch.setenv('FTMI_GEMM_SKINNY', '0')
+    B, T, Cin, N, k = 2, 300, 256, 256, 3
+    x = dev(rng.normal(0, 1, (B, T, Cin)).astype(np.float32))
+    w = pack_conv(torch.from_numpy(rng.normal(0, 0.05, (N, Cin, k)).astype(np.float32))).cuda()
+    w3 = ops.presplit_for(w, 2)
+    K, C, Cb = 8, 256, 80
+    xb = dev(rng.normal(0, 1, (B, T, Cb)).astype(np.float32))
+    ws = [rng.normal(0, 1 / np.sqrt(Cb * kk), (C, Cb, kk)).astype(np.float32) for kk in range(1, K + 1)]
+    wb = torch.cat([pack_conv(torch.from_numpy(v)).reshape(-1) for v in ws]).cuda()
+    wb3 = ops.split_bank_weights(wb, K, Cb, C, 2)
+    bsc = dev(rng.uniform(0.5, 1.5, K * C).astype(np.float32))
+    bsh = dev(rng.normal(0, 0.1, K * C).astype(np.float32))
+    monkeypatch.setattr(ops, '_split_k', lambda *a, **kw: split_k)
+    outs = []
+    for pf in ('1', '0'):
+        monkeypatch.setenv('FTMI_SLAB_PF', pf)
+        y, _ = ops.conv1d(x, w, k, k // 2, relu=True, mma=2, w_split=w3)
+        assert ops.bank_pools(xb, K, C, w_split=wb3)
+        yb = ops.conv_bank(xb, wb, K, C, bsc, bsh, mma=2, w_split=wb3, pool=True, split_out=True)
+        outs.append((host(y), host(yb)))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])

@@ -13,6 +13,7 @@ SHAPES = {  # name: (kind, B, T, Cin, N, k, maxpool)
     'pre.proj1': ('conv', 64, 200, 4096, 256, 3, True),
     'pred.conv': ('conv', 64, 200, 256, 256, 5, False),
     'pre.bank': ('bank', 64, 200, 256, 16),
+    'fp.conv1': ('conv', 64, 1400, 256, 1024, 9, False),
 }
 ap = argparse.ArgumentParser()
 ap.add_argument('shape')
