@@ -81,8 +81,8 @@ PEAK_X3_TFLOPS = PEAK_BF16_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 
-PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r2_pmc_traffic.json')        # c3
-PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r2c2_pmc_traffic.json')   # c2 (--config c2)
+PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r3_pmc_traffic.json')        # c3
+PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r3c2_pmc_traffic.json')   # c2 (--config c2)
 
 
 def rocprof_name(label: str):
