@@ -268,6 +268,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const float *__restrict_
 // of *status (the caller reruns on the fp32 kernel).
 constexpr int AH_W = 8;    // waves (x 16 queries) per workgroup of the f16x3 kernel
 constexpr int AH_KT = 64;  // keys per tile
+constexpr float AH_LAZY = 8.f;  // lazy running max: P <= e^8 between moves of the max
 
 // PRE: K and V come pre-split from attn_split_kv_kernel (kv: f16 planes K head, K tail
 // [B*H][Tp][HD] and V head, V tail transposed [B*H][HD][Tp]): the tile staging is a copy, the
@@ -323,6 +324,14 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
       hd[e] = hh;
       tl[e] = (_Float16)((v[e] - (float)hh) * TS);
     }
+  };
+
+  // P in [0, e^AH_LAZY]: split without the range guard (packed conversions)
+  auto split8p = [&](const f32x4 a, const f32x4 c, f16x8 &hd, f16x8 &tl) {
+    typedef float f32x8 __attribute__((ext_vector_type(8)));
+    const f32x8 v = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+    hd = __builtin_convertvector(v, f16x8);
+    tl = __builtin_convertvector((v - __builtin_convertvector(hd, f32x8)) * TS, f16x8);
   };
 
   // A fragments of this wave's 16 query rows (lane: row c16, d = 32 ks + 8 g + j), scaled by
@@ -462,14 +471,23 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
         big = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[ks], kh, big, 0, 0, 0);
       }
       s[n] = big + sm * TU;
-      // mask: keys past T or flagged in key_padding_mask -> -inf
-      const int key = k0 + n * 16 + c16;
-      const bool dead = key >= T || (kpm && kpm[(int64_t)b * T + key]);
-      if (dead)
+      // mask: keys past T or flagged in key_padding_mask -> -inf (only a tile that reaches
+      // past T, or with a mask, has any: a uniform branch)
+      if (k0 + AH_KT > T || kpm) {
+        const int key = k0 + n * 16 + c16;
+        const bool dead = key >= T || (kpm && kpm[(int64_t)b * T + key]);
+        if (dead)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) s[n][i] = -INFINITY;
+          for (int i = 0; i < 4; ++i) s[n][i] = -INFINITY;
+      }
     }
-    // ---- online softmax per row (rows 4g+i; the 16 lanes of group g hold its columns)
+    // ---- online softmax per row (rows 4g+i; the 16 lanes of group g hold its columns) with
+    // a lazy running max: m moves only when a row's tile max exceeds it by more than
+    // AH_LAZY (so P = exp(s - m) <= e^AH_LAZY, far inside the f16 range of the P split), and
+    // the O rescale runs only on tiles where some row of the wave moved it — the same
+    // softmax, exp(s - m) / sum exp(s - m) for whichever m, up to rounding
+    bool moved = false;
+    float alpha[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float mx = s[0][i];
@@ -477,24 +495,33 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
       for (int n = 1; n < NB; ++n) mx = fmaxf(mx, s[n][i]);
 #pragma unroll
       FTMI_ROW16(fmaxf, mx);
-      const float mn = fmaxf(m[i], mx);
-      const float alpha = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f((m[i] - mn) * LOG2E);
+      const bool up = mx > m[i] + AH_LAZY;  // false while the row has only masked keys
+      const float mn = up ? mx : m[i];
+      alpha[i] = up ? __builtin_amdgcn_exp2f((m[i] - mn) * LOG2E) : 1.f;  // exp2(-inf) = 0
+      moved |= up;
+      // P = 2^(s log2e - m log2e): one FMA per score; a row without a live key yet has
+      // m = -inf and only -inf scores: P = 0
+      const float off = mn == -INFINITY ? 0.f : -mn * LOG2E;
       float ps = 0.f;
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
-        const float pv = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((s[n][i] - mn) * LOG2E);
+        const float pv = __builtin_amdgcn_exp2f(fmaf(s[n][i], LOG2E, off));
         s[n][i] = pv;
         ps += pv;
       }
 #pragma unroll
       FTMI_ROW16(add2, ps);
-      l[i] = l[i] * alpha + ps;
+      l[i] = l[i] * alpha[i] + ps;
       m[i] = mn;
+    }
+    if (__any(moved)) {
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        ob[n][i] *= alpha;
-        osm[n][i] *= alpha;
-      }
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          ob[n][i] *= alpha[i];
+          osm[n][i] *= alpha[i];
+        }
     }
     // ---- P (C layout) -> this wave's LDS rows -> A layout (row c16, keys 32 kk + 8 g ..)
     float *P = Ps[wave];
@@ -508,7 +535,7 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
       f16x8 ph, pt;
       const f32x4 a = *(const f32x4 *)&P[c16 * PP + 32 * kk + 8 * g];
       const f32x4 c = *(const f32x4 *)&P[c16 * PP + 32 * kk + 8 * g + 4];
-      split8(a, c, ph, pt);
+      split8p(a, c, ph, pt);
       // ---- O += P V
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
