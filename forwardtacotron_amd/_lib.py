@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 13
+ABI_VERSION = 14
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -92,6 +92,10 @@ SIGNATURES = {
     'ftmi_layernorm': (c_int, [P, c_int64, c_int64, c_int, P, P, c_float, P, c_int64, P]),
     'ftmi_attention': (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
                                c_float, P, c_int64, c_int, P, P, c_int64, P]),
+    'ftmi_panel_proj_qkv': (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, P, c_int, P,
+                                    c_int64, P, c_int64, P, P]),
+    'ftmi_attention_kv': (c_int, [P, c_int64, c_int, c_int, c_int, c_int, P, c_float, P, c_int64,
+                                  P, P, c_int64, P]),
     'ftmi_attention_workspace_bytes': (c_int64, [c_int, c_int, c_int, c_int]),
     'ftmi_stft': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P, P, P]),
     'ftmi_mel_spectrogram': (c_int, [P, c_int64, c_int, c_int64, P, c_int, c_int, P, P, c_int, P,

@@ -2857,6 +2857,11 @@ struct PanelParams {
   float *y;
   int64_t y_stride;
   unsigned *status;
+  // ftmi_panel_proj_qkv: panels 1 and 2 (K, V of the in_proj output) go to the attention
+  // workspace as f16 head / scaled tail planes instead of y (ftmi_attention's layout: K
+  // [B*H][Tp][hd], V transposed [B*H][hd][Tp]); rows are (b, key) = (row / T, row % T)
+  _Float16 *kv;
+  int T, H, hd, Tp;
 };
 
 // Persistent over row tiles (grid = min(tiles, CUs)): the next job's channels (the next
@@ -2975,7 +2980,59 @@ __global__ __launch_bounds__(512) void panel_proj_kernel(const PanelParams p) {
       }
       __syncthreads();
       const int m0 = t * PP_BM;
-      if (!ln) {
+      if (p.kv && q >= 1) {  // K / V panel -> split planes (the attention split pass's values)
+        const int64_t plane = (int64_t)(p.M / p.T) * p.H * p.Tp * p.hd;
+        float amax = 0.f;
+        if (q == 1) {  // K rows: lane = 4 consecutive columns of one head
+          const int c = 4 * lane, hh = c / p.hd, d = c - hh * p.hd;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int r = wave + 8 * u, row = m0 + r;
+            if (row >= p.M) continue;
+            const int b = row / p.T, key = row - b * p.T;
+            const f32x4 v = *(const f32x4 *)(tile + r * PP_TP + c);
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+            f16x4 h4, t4;
+            split2h(v, h4, t4);
+            const int64_t o = ((int64_t)(b * p.H + hh) * p.Tp + key) * p.hd + d;
+            *(f16x4 *)(p.kv + o) = h4;
+            *(f16x4 *)(p.kv + plane + o) = t4;
+          }
+        } else {  // V^T: a thread takes 4 consecutive keys (rows) of one column, 8 B per plane
+          // where they are 4 aligned keys of one sequence; a wave-instruction covers 16
+          // columns x 4 row quads (conflict-free LDS reads at the 260-float pitch)
+          for (int e = tid; e < HS_C * (PP_BM / 4); e += 512) {
+            const int l = e & 63, wv = e >> 6;
+            const int c = (wv & 15) * 16 + (l & 15), r0 = ((wv >> 4) * 4 + (l >> 4)) * 4;
+            const int hh = c / p.hd, d = c - hh * p.hd;
+            const int row0 = m0 + r0, b0 = row0 / p.T, key0 = row0 - b0 * p.T;
+            f32x4 v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = tile[(r0 + i) * PP_TP + c];
+            if (row0 + 3 < p.M && key0 + 3 < p.T && (key0 & 3) == 0) {
+              amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+              f16x4 h4, t4;
+              split2h(v, h4, t4);
+              const int64_t o = 2 * plane + ((int64_t)(b0 * p.H + hh) * p.hd + d) * p.Tp + key0;
+              *(f16x4 *)(p.kv + o) = h4;
+              *(f16x4 *)(p.kv + o + plane) = t4;
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int row = row0 + i;
+                if (row >= p.M) break;
+                const int b = row / p.T, key = row - b * p.T;
+                amax = fmaxf(amax, fabsf(v[i]));
+                const _Float16 h1 = (_Float16)v[i];
+                const int64_t o = 2 * plane + ((int64_t)(b * p.H + hh) * p.hd + d) * p.Tp + key;
+                p.kv[o] = h1;
+                p.kv[o + plane] = (_Float16)((v[i] - (float)h1) * H3_SCALE);
+              }
+            }
+          }
+        }
+        if (!(amax <= 65504.f) && p.status) atomicOr(p.status, 1u);
+      } else if (!ln) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int r = wave + 8 * u, row = m0 + r;
@@ -3639,6 +3696,58 @@ extern "C" int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, i
   return FTMI_OK;
 }
 
+static int panel_launch(PanelParams &p, int64_t M, hipStream_t stream) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  const int64_t tiles = (M + PP_BM - 1) / PP_BM;
+  const unsigned blocks = (unsigned)(tiles < cus ? tiles : cus);
+  hipLaunchKernelGGL(panel_proj_kernel, dim3(blocks), dim3(512), 0, stream, p);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_panel_proj_qkv(const float *x, int64_t x_stride, int32_t B, int32_t T,
+                                   int32_t K, const void *w_split_frag, int32_t d,
+                                   const float *bias, int32_t heads, float *q_out,
+                                   int64_t q_stride, void *kv_workspace, int64_t workspace_bytes,
+                                   uint32_t *status, ftmi_stream_t stream) {
+  if (!x || !w_split_frag || !q_out || !kv_workspace || B <= 0 || T <= 0 || K <= 0) return FTMI_E_ARG;
+  if (d != HS_C || heads <= 0 || d % heads) return FTMI_E_SHAPE;
+  const int hd = d / heads;
+  if (hd != 64 && hd != 128) return FTMI_E_UNSUPPORTED;
+  const int64_t M = (int64_t)B * T;
+  if (K % 4 || M > INT32_MAX || x_stride < K || q_stride < d) return FTMI_E_SHAPE;
+  if (workspace_bytes < ftmi_attention_workspace_bytes(B, T, heads, hd)) return FTMI_E_SHAPE;
+  if (!ftmi_aligned16(x) || (x_stride & 3) || !ftmi_aligned16(w_split_frag) ||
+      !ftmi_aligned16(q_out) || (q_stride & 3) || !ftmi_aligned16(kv_workspace))
+    return FTMI_E_ALIGN;
+  if ((const float *)x == q_out) return FTMI_E_ARG;
+  PanelParams p = {};
+  p.x = x;
+  p.x_stride = x_stride;
+  p.M = (int)M;
+  p.K = K;
+  p.kpad = (K + X6_BK - 1) / X6_BK * X6_BK;
+  p.N = 3 * d;
+  p.w = (const _Float16 *)w_split_frag;
+  p.cs = f16_colscale(w_split_frag, 3 * d, K);
+  p.bias = bias;
+  p.y = q_out;
+  p.y_stride = q_stride;
+  p.status = status;
+  p.kv = (_Float16 *)kv_workspace;
+  p.T = T;
+  p.H = heads;
+  p.hd = hd;
+  p.Tp = (T + 63) / 64 * 64;
+  return panel_launch(p, M, ftmi_hs(stream));
+}
+
 extern "C" int ftmi_panel_proj(const float *x, int64_t x_stride, int64_t M, int32_t K,
                                const void *w_split_frag, int32_t N, const float *bias,
                                const float *residual, int64_t res_stride, const float *ln_gamma,
@@ -3671,18 +3780,7 @@ extern "C" int ftmi_panel_proj(const float *x, int64_t x_stride, int64_t M, int3
   p.y = y;
   p.y_stride = y_stride;
   p.status = status;
-  static const int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n > 0 ? n : 256;
-  }();
-  const int64_t tiles = (M + PP_BM - 1) / PP_BM;
-  const unsigned blocks = (unsigned)(tiles < cus ? tiles : cus);
-  hipLaunchKernelGGL(panel_proj_kernel, dim3(blocks), dim3(512), 0, ftmi_hs(stream), p);
-  FTMI_CHECK_LAUNCH();
-  return FTMI_OK;
+  return panel_launch(p, M, ftmi_hs(stream));
 }
 
 extern "C" int64_t ftmi_split_weights_f16_bytes(int64_t N, int64_t K) {

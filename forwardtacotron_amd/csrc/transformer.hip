@@ -670,6 +670,29 @@ extern "C" int64_t ftmi_attention_workspace_bytes(int32_t B, int32_t T, int32_t 
   return 4 * (int64_t)B * H * Tp * head_dim * 2;
 }
 
+extern "C" int ftmi_attention_kv(const float *q, int64_t row_stride, int32_t B, int32_t T,
+                                 int32_t H, int32_t head_dim, const uint8_t *key_padding_mask,
+                                 float qscale, float *out, int64_t out_stride, uint32_t *status,
+                                 const void *kv_workspace, int64_t workspace_bytes,
+                                 ftmi_stream_t stream) {
+  if (!q || !out || !kv_workspace || B <= 0 || T <= 0 || H <= 0) return FTMI_E_ARG;
+  if (head_dim != 64 && head_dim != 128) return FTMI_E_UNSUPPORTED;
+  if (workspace_bytes < ftmi_attention_workspace_bytes(B, T, H, head_dim)) return FTMI_E_SHAPE;
+  if (!ftmi_aligned16(q) || (row_stride & 3) || !ftmi_aligned16(kv_workspace)) return FTMI_E_ALIGN;
+  const int nq = (T + 16 * AH_W - 1) / (16 * AH_W), Tp = (T + 63) / 64 * 64;
+  const dim3 g1((unsigned)(nq * B * H)), b1(64 * AH_W);
+  const _Float16 *kv = (const _Float16 *)kv_workspace;
+  const hipStream_t s = ftmi_hs(stream);
+  if (head_dim == 64)
+    hipLaunchKernelGGL((attention_h3_kernel<64, true>), g1, b1, 0, s, q, row_stride, B, T, H, 0,
+                       0, 0, key_padding_mask, qscale, out, out_stride, status, kv, Tp);
+  else
+    hipLaunchKernelGGL((attention_h3_kernel<128, true>), g1, b1, 0, s, q, row_stride, B, T, H, 0,
+                       0, 0, key_padding_mask, qscale, out, out_stride, status, kv, Tp);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
 extern "C" int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, int32_t T,
                               int32_t H, int32_t head_dim, int32_t q_off, int32_t k_off,
                               int32_t v_off, const uint8_t *key_padding_mask, float qscale,

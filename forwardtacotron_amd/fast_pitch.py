@@ -132,12 +132,18 @@ class FFTBlock(Packed):
         # the slab GEMM + layernorm launches otherwise (same projection values)
         panel = ops.panel_ok(d, d, True, si)
         fi, fo, f2 = self._panel_pack() if panel else (None, None, None)
-        if panel:
-            qkv = ops.panel_proj(x, fi, 3 * d, bias=bi)
+        if panel and ops.kv_fused_ok(x.size(1), d, self.heads, si):
+            # the attention's K / V split folded into in_proj (no split pass)
+            q, kv = ops.panel_proj_qkv(x, fi, d, self.heads, bias=bi)
+            a = ops.attention_kv(q, kv, self.heads, kpm)
+            del q
         else:
-            qkv, _ = ops.conv1d(x, wi, 1, 0, bias=bi, w_split=si)
-        a = ops.attention(qkv, self.heads, kpm)
-        del qkv
+            if panel:
+                qkv = ops.panel_proj(x, fi, 3 * d, bias=bi)
+            else:
+                qkv, _ = ops.conv1d(x, wi, 1, 0, bias=bi, w_split=si)
+            a = ops.attention(qkv, self.heads, kpm)
+            del qkv
         if panel:
             h = ops.panel_proj(a, fo, d, bias=bo, residual=x, ln=ln1)
         else:

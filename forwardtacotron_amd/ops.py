@@ -537,6 +537,70 @@ def panel_proj(x: torch.Tensor, w_frag: torch.Tensor, N: int, bias: Optional[tor
     return y
 
 
+_KV_WS = {}
+
+
+def _kv_workspace(nbytes: int, device) -> torch.Tensor:
+    """The attention K / V plane workspace of the current stream (ftmi_panel_proj_qkv /
+    ftmi_attention_kv): zeroed once at allocation — the planes' pad keys T..Tp-1 are never
+    written and must stay finite — then reused by every call on the stream (stream order
+    separates the layers' uses); grown when too small."""
+    stream = torch.cuda.current_stream(device)
+    key = (torch.device(device), stream.cuda_stream)
+    t = _KV_WS.get(key)
+    if t is None or t.numel() < nbytes:
+        if t is not None:
+            _KV_OLD.append(t)  # may still be read by queued work
+        t = _KV_WS[key] = torch.zeros(nbytes, device=device, dtype=torch.uint8)
+    return t
+
+
+_KV_OLD = []
+
+
+def kv_fused_ok(T: int, d: int, heads: int, w_frag) -> bool:
+    """Whether FastPitch's in_proj + attention take ftmi_panel_proj_qkv + ftmi_attention_kv
+    (the split pass folded into the projection): f16x3 in force, the attention would
+    presplit (T > 384), d = 256, head_dim 64 / 128.  FTMI_KV_FUSED=0 turns it off."""
+    return (os.environ.get('FTMI_KV_FUSED', '1') != '0' and panel_ok(d, 3 * d, False, w_frag)
+            and ATTN_PRESPLIT and T > 384 and d == PANEL_N and d % heads == 0
+            and d // heads in (64, 128))
+
+
+def panel_proj_qkv(x: torch.Tensor, w_frag: torch.Tensor, d: int, heads: int,
+                   bias: Optional[torch.Tensor] = None):
+    """in_proj with the attention's K / V split folded in (`ftmi_panel_proj_qkv`): returns
+    (q rows (B, T, d), the K / V plane workspace) for attention_kv."""
+    _dev(x, w_frag, bias)
+    B, T, K, xs = _rows(x)
+    q = torch.empty(B, T, d, device=x.device, dtype=_f32)
+    nws = int(_lib.load().ftmi_attention_workspace_bytes(B, T, heads, d // heads))
+    ws = _kv_workspace(nws, x.device)
+    launch('ftmi_panel_proj_qkv', f'panel_proj[M={B * T},K={K},N={3 * d},qkv]',
+           2.0 * B * T * 3 * d * K, 4.0 * B * T * (K + d) + 2.0 * nws / 4 * 2,
+           x.data_ptr(), xs, B, T, K, w_frag.data_ptr(), d, _ptr(bias), heads, q.data_ptr(),
+           q.stride(1), ws.data_ptr(), nws, status_word(x.device).data_ptr(), _stream())
+    return q, ws
+
+
+def attention_kv(q: torch.Tensor, ws: torch.Tensor, heads: int,
+                 key_padding_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """attention on Q rows with K / V from panel_proj_qkv's workspace (`ftmi_attention_kv`)."""
+    _dev(q, ws, key_padding_mask)
+    B, T, d, rs = _rows(q)
+    hd = d // heads
+    out = torch.empty(B, T, d, device=q.device, dtype=_f32)
+    kpm = None
+    if key_padding_mask is not None:
+        kpm = key_padding_mask.to(torch.uint8).contiguous()
+    launch('ftmi_attention_kv', f'attention[B={B},T={T},H={heads},hd={hd},mma=2,kv]',
+           4.0 * B * heads * T * T * hd, 4.0 * (B * T * d * 2),
+           q.data_ptr(), rs, B, T, heads, hd, _ptr(kpm), float(np.float32(np.sqrt(1.0 / hd))),
+           out.data_ptr(), out.stride(1), status_word(q.device).data_ptr(), ws.data_ptr(),
+           ws.numel(), _stream())
+    return out
+
+
 RNN_SPREAD = 0x100  # include/ftmi.h FTMI_RNN_SPREAD
 
 

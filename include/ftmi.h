@@ -72,7 +72,7 @@ enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
                                  share the counters. */ };
 enum { FTMI_BANK_COUNTERS = 4096 };
 
-/* ABI version; bumped on any signature change (13: ftmi_panel_proj). */
+/* ABI version; bumped on any signature change (14: ftmi_panel_proj_qkv, ftmi_attention_kv). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
@@ -492,6 +492,27 @@ int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, int32_t T, i
                    const uint8_t *key_padding_mask, float qscale, float *out,
                    int64_t out_stride, int32_t mma, uint32_t *status, void *workspace,
                    int64_t workspace_bytes, ftmi_stream_t stream);
+
+/* ABI 14: the attention split pass folded into the in_proj projection.
+ * ftmi_panel_proj_qkv = ftmi_panel_proj of self_attn.in_proj (models/fast_pitch.py:76; W
+ * [3d][K], d = 256, no residual / LayerNorm) on B*T rows that writes only the Q third as fp32
+ * rows (q_out, q_stride >= d) and K / V into kv_workspace (>= ftmi_attention_workspace_bytes
+ * (B, T, heads, d / heads) bytes) as the f16 head / scaled-tail planes ftmi_attention's split
+ * pass would write for the same values (K [B*heads][Tp][hd], V [B*heads][hd][Tp], Tp = T
+ * rounded up to 64; keys T..Tp-1 are never written and must hold finite values: zero the
+ * workspace once at allocation — later calls only ever store finite values into it).
+ * ftmi_attention_kv = ftmi_attention (f16x3) with Q rows q (row_stride) and K / V taken from
+ * such a workspace: no split pass.  The pair computes exactly what ftmi_panel_proj +
+ * ftmi_attention with a workspace compute (bit-identical); |value| > 65504 sets status bit 0. */
+int ftmi_panel_proj_qkv(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t K,
+                        const void *w_split_frag, int32_t d, const float *bias, int32_t heads,
+                        float *q_out, int64_t q_stride, void *kv_workspace,
+                        int64_t workspace_bytes, uint32_t *status, ftmi_stream_t stream);
+int ftmi_attention_kv(const float *q, int64_t row_stride, int32_t B, int32_t T, int32_t H,
+                      int32_t head_dim, const uint8_t *key_padding_mask, float qscale,
+                      float *out, int64_t out_stride, uint32_t *status,
+                      const void *kv_workspace, int64_t workspace_bytes,
+                      ftmi_stream_t stream);
 
 
 /* ---- WaveRNN vocoder (models/fatchord_version.py; gen_forward.py `wavernn`) -------------

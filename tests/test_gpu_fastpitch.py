@@ -211,3 +211,34 @@ def test_panel_path_matches_unfused(fp_model, monkeypatch):
     np.testing.assert_array_equal(FP.duration_counts(outs['0']['dur']), FP.duration_counts(outs['1']['dur']))
     for k in ('pitch', 'energy'):
         np.testing.assert_allclose(outs['0'][k], outs['1'][k], atol=1e-5)
+
+
+@pytest.mark.parametrize('B,T,H,kpm', [(3, 500, 2, False), (2, 451, 4, True), (1, 900, 2, False)])
+def test_kv_fused_in_proj_bit_identical(B, T, H, kpm):
+    """ftmi_panel_proj_qkv + ftmi_attention_kv (the attention's K / V split folded into
+    in_proj, FTMI_KV_FUSED) against ftmi_panel_proj + ftmi_attention with its split pass:
+    bit-identical Q rows and attention outputs; the pad keys of the stream's reused
+    workspace (zeroed at allocation, then holding earlier calls' planes) stay finite."""
+    from forwardtacotron_amd import ops
+    g = torch.Generator().manual_seed(B * T)
+    d = 256
+    x = torch.randn(B, T, d, generator=g).cuda()
+    w = (torch.randn(3 * d, d, generator=g) / 16).cuda()
+    b = (torch.randn(3 * d, generator=g) / 10).cuda()
+    mask = None
+    if kpm:
+        lens = torch.randint(T // 2, T + 1, (B,), generator=g)
+        mask = (torch.arange(T)[None, :] >= lens[:, None]).cuda()
+    wf = ops.split_weights_f16(w, frag=True)
+    qkv = ops.panel_proj(x, wf, 3 * d, bias=b)
+    ref = ops.attention(qkv, H, mask, mma=2, presplit=True)
+    q, kv = ops.panel_proj_qkv(x, wf, d, H, bias=b)
+    got = ops.attention_kv(q, kv, H, mask)
+    torch.cuda.synchronize()
+    assert torch.equal(q, qkv[:, :, :d])
+    assert torch.equal(got, ref)
+    hd, Tp = d // H, -(-T // 64) * 64
+    planes = kv[:4 * B * H * Tp * hd * 2].view(torch.float16).view(4, B * H, -1)
+    if Tp > T:  # pad keys of K [bh][Tp][hd] and of V^T [bh][hd][Tp] are finite
+        assert torch.isfinite(planes[:2].view(2, B * H, Tp, hd)[:, :, T:]).all()
+        assert torch.isfinite(planes[2:].view(2, B * H, hd, Tp)[:, :, :, T:]).all()
