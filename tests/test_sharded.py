@@ -216,3 +216,31 @@ def test_gather_to_subgroup_without_global_rank0():
     excludes global rank 0 the rows land on the group's rank 0 (dist.gather is given the
     matching global rank)."""
     mp.spawn(_subgroup_gather, args=(3, _port()), nprocs=3, join=True)
+
+
+@pytest.mark.gpu
+def test_generate_sharded_rccl_single_rank():
+    """The nccl (= RCCL) branch of the protocol on the device: one rank, so every collective
+    (the state broadcast, the global T / fill-rule / T_mel all-reduces on device tensors, the
+    shard-size all-gather and the rank-0 gather) runs through RCCL on one MI355X; the result
+    equals the unsharded HIP generate (one shard = the whole batch)."""
+    from forwardtacotron_amd import sharded as S
+    from forwardtacotron_amd.forward_tacotron import ForwardTacotron
+    from forwardtacotron_amd.synthetic import default_config, load_synthetic, synthetic_tokens
+    dev = torch.device('cuda', torch.cuda.current_device())
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{_port()}', rank=0,
+                            world_size=1, device_id=dev)
+    try:
+        assert dist.get_backend() == 'nccl' and S._coll_device(None, dev) == dev
+        m = load_synthetic(ForwardTacotron.from_config(default_config()), 0).cuda().eval()
+        S.broadcast_state(m, src=0)
+        x = torch.from_numpy(synthetic_tokens(5, 37, seed=4, min_len=9)).cuda()
+        out = S.generate_sharded(m, x, gather='rank0')
+        ref = m.generate(x)
+        torch.cuda.synchronize()
+        assert torch.equal(out['dur'], ref['dur'])
+        for k in ('mel_post', 'mel', 'pitch', 'energy'):
+            np.testing.assert_allclose(out[k].cpu().numpy(), ref[k].cpu().numpy(), atol=1e-6,
+                                       rtol=0, err_msg=k)
+    finally:
+        dist.destroy_process_group()
