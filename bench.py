@@ -286,8 +286,9 @@ def main():
         def vstep():
             o = gen(x_host.to(dev))
             m = o['mel_post']
-            if m.size(0) == 1:
-                return dsp.griffinlim(m.cpu().squeeze(0).numpy()).shape[0]
+            if m.size(0) == 1:  # as forwardtacotron_amd.gen_forward: D2H, GL from the device mel
+                m.cpu()
+                return dsp.griffinlim(m[0]).cpu().numpy().shape[0]
             w, n = dsp.griffinlim_batch(m)
             w.cpu()
             return int(n.sum().item()) if torch.is_tensor(n) else int(np.sum(n))
@@ -303,7 +304,9 @@ def main():
                'mel_frames_per_s': round(frames / velapsed, 1),
                'audio_samples_per_s': round(nsamp / velapsed, 1),
                'what': 'generate() + mel_post D2H + DSP.griffinlim (numpy wav out) per step, '
-                       'as gen_forward.py:115-134 with the griffinlim vocoder'}
+                       'as gen_forward.py:115-134 with the griffinlim vocoder (as forwardtacotron_'
+                       'amd.gen_forward: the mel fetched to the host, Griffin-Lim started from the '
+                       'device copy; the NNLS runs while the host draws the initial phases)'}
     # The timed steps replay the phoneme phase as a HIP graph (forward_tacotron.GRAPH), whose
     # kernels the per-launch probe cannot see: one more generate() with the phase eager,
     # after the timed region, gives their per-kernel times (the prenet bank, --kernels).

@@ -323,22 +323,38 @@ class DSP:
         t = torch.from_numpy(np.ascontiguousarray(y, dtype=np.float32)).cuda()[None]
         return mel_spectrogram(self.plan(t.device), t, log_norm=normalize)[0].cpu().numpy()
 
-    def griffinlim(self, mel, n_iter: int = 32, angles=None, random_state=None):
+    def draw_uniforms(self, T: int, random_state=None) -> np.ndarray:
+        """The U[0, 1) draw behind griffinlim's initial phases for a T-frame mel, taken from
+        the reference's stream (librosa: np.random.rand(n_bins, T), or RandomState
+        (random_state)).  Drawn ahead — e.g. while the GPU still decodes the mel, as
+        gen_forward does — and passed as griffinlim(..., uniforms=u), it is the same draw in
+        the same stream order."""
+        rng = np.random if random_state is None else np.random.RandomState(random_state)
+        return rng.rand(self.n_fft // 2 + 1, T)
+
+    def griffinlim(self, mel, n_iter: int = 32, angles=None, random_state=None, uniforms=None):
         """exp -> mel_to_stft (NNLS) -> fast Griffin-Lim (32 iterations, momentum 0.99).
         numpy (n_mels, T) -> numpy wav of hop * (T - 1) samples.  The initial phases are
         exp(2 pi i U[0,1)) drawn like librosa (np.random, or RandomState(random_state)),
-        shape (n_bins, T); pass `angles` to fix them."""
+        shape (n_bins, T); pass `uniforms` (draw_uniforms) to use a draw made ahead, or
+        `angles` to fix the phases."""
         is_t = isinstance(mel, torch.Tensor)
         m = mel if is_t else torch.from_numpy(np.ascontiguousarray(mel, dtype=np.float32)).cuda()
         _need_cuda(m)
         plan = self.plan(m.device)
         T = m.shape[-1]
+        # the NNLS magnitudes first: queued on the device, they run while the host draws the
+        # initial phases below (the draw does not depend on them)
+        S = mel_to_stft(plan, m.float().reshape(1, plan.n_mels, T).contiguous(), iters=self.nnls_iters)
         if angles is None:
             # the reference's draw (librosa: np.random.rand(n_bins, T)); exp(2 pi i u) and the
             # frame-major layout on the device (ftmi_unit_phases: the host exp of 420 k
             # complex values took longer than the whole Griffin-Lim on the GPU)
-            rng = np.random if random_state is None else np.random.RandomState(random_state)
-            u = torch.from_numpy(rng.rand(plan.nb, T)).to(m.device)
+            if uniforms is None:
+                uniforms = self.draw_uniforms(T, random_state)
+            if tuple(np.shape(uniforms)) != (plan.nb, T):
+                raise ValueError(f'uniforms of shape {np.shape(uniforms)}, expected {(plan.nb, T)}')
+            u = torch.from_numpy(np.ascontiguousarray(uniforms, dtype=np.float64)).to(m.device)
             a = torch.empty(1, T, plan.nb, dtype=torch.complex64, device=m.device)
             launch('ftmi_unit_phases', f'unit_phases[T={T}]', 0, 16.0 * plan.nb * T,
                    u.data_ptr(), 1, plan.nb, T, a.data_ptr(), _stream())
@@ -346,7 +362,6 @@ class DSP:
             a = angles if isinstance(angles, torch.Tensor) else torch.from_numpy(
                 np.ascontiguousarray(np.asarray(angles, dtype=np.complex64).T))
             a = a.to(m.device).reshape(1, T, plan.nb).contiguous()
-        S = mel_to_stft(plan, m.float().reshape(1, plan.n_mels, T).contiguous(), iters=self.nnls_iters)
         wav = griffinlim_from_stft(plan, S, a, n_iter)[0]
         return wav if is_t else wav.cpu().numpy()
 

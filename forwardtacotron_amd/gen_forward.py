@@ -82,9 +82,10 @@ def synthetic_wavernn():
 
 
 def write_output(m: torch.Tensor, name: str, vocoder: str, out_path: Path, dsp=None, voc=None,
-                 target: int = 11000, overlap: int = 550) -> Path:
+                 target: int = 11000, overlap: int = 550, mel_dev=None) -> Path:
     """`gen_forward.py:120-134` for one sentence: m is the host (1, n_mels, T) mel_post;
-    voc = (WaveRNN model, its DSP) for the wavernn vocoder."""
+    voc = (WaveRNN model, its DSP) for the wavernn vocoder; mel_dev: the same mel still on
+    the device (griffinlim then starts from it instead of copying m back)."""
     if vocoder == 'melgan':
         p = out_path / f'{name}.mel'
         torch.save(m, p)
@@ -99,7 +100,8 @@ def write_output(m: torch.Tensor, name: str, vocoder: str, out_path: Path, dsp=N
         dsp.save_wav(wav, p)
     elif vocoder == 'griffinlim':
         p = out_path / f'{name}.wav'
-        wav = dsp.griffinlim(m.squeeze().numpy())
+        wav = (dsp.griffinlim(m.squeeze().numpy()) if mel_dev is None
+               else dsp.griffinlim(mel_dev.reshape(mel_dev.shape[-2:])).cpu().numpy())
         dsp.save_wav(wav, p)
     else:
         raise ValueError(f'unsupported vocoder {vocoder!r}')
@@ -239,7 +241,8 @@ def main(argv: Optional[Sequence[str]] = None) -> List[Path]:
                                  energy_function=energy_function)
         m = d2h.fetch(gen['mel_post'])
         written.append(write_output(m, name, args.vocoder, out_path, dsp, voc,
-                                    getattr(args, 'target', 11000), getattr(args, 'overlap', 550)))
+                                    getattr(args, 'target', 11000), getattr(args, 'overlap', 550),
+                                    mel_dev=gen['mel_post']))
     print('\n\nDone.\n')
     return written
 

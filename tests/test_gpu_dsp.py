@@ -115,6 +115,17 @@ def test_griffinlim_api_and_round_trip(dsp):
     assert isinstance(wav, np.ndarray) and wav.shape == (256 * 39,) and wav.dtype == np.float32
     again = dsp.griffinlim(REF_MEL, random_state=0)
     np.testing.assert_array_equal(wav, again)
+    # the phase draw taken ahead (gen_forward draws it while the device decodes) is the same
+    # draw: from a RandomState, and from the global np.random stream in the same order
+    u = dsp.draw_uniforms(REF_MEL.shape[1], random_state=0)
+    np.testing.assert_array_equal(dsp.griffinlim(REF_MEL, uniforms=u), wav)
+    np.random.seed(7)
+    w1 = dsp.griffinlim(REF_MEL)
+    np.random.seed(7)
+    w2 = dsp.griffinlim(REF_MEL, uniforms=dsp.draw_uniforms(REF_MEL.shape[1]))
+    np.testing.assert_array_equal(w1, w2)
+    with pytest.raises(ValueError):
+        dsp.griffinlim(REF_MEL, uniforms=u[:, :-1])
     m2 = D.wav_to_mel(wav)
     assert np.abs(m2 - REF_MEL).mean() < 0.2
 
