@@ -183,10 +183,19 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # FTMI_BENCH_BACKEND=gloo: a rehearsal of the N > 1 path on fewer GPUs than ranks (ranks
+    # share devices, collectives on host copies); the measured configuration is nccl (RCCL)
+    backend = os.environ.get('FTMI_BENCH_BACKEND', 'nccl')
+    if backend != 'nccl':
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    cdev = dev if backend == 'nccl' else torch.device('cpu')  # timing all-reduces
     if args.model == 'wavernn':
         bench_wavernn(args, world, rank, dev)
         if world > 1:
@@ -332,7 +341,7 @@ def main():
                       else None)
 
     if world > 1:
-        t = torch.tensor([elapsed, host_elapsed or 0.0, host_serial or 0.0], device=dev,
+        t = torch.tensor([elapsed, host_elapsed or 0.0, host_serial or 0.0], device=cdev,
                          dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0].item())
@@ -499,7 +508,8 @@ def bench_wavernn(args, world, rank, dev):
         elapsed = time.perf_counter() - t0
     kern = probe.summary()
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == 'nccl' else 'cpu')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0].item())
     if rank != 0:
