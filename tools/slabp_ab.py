@@ -1,7 +1,7 @@
 """A/B of the slab kernels on the model's slab shapes: the fragment-prefetch kernel
 (FTMI_SLAB_PF=1) against the previous kernel (FTMI_SLAB_PF=0, warp-specialised form for
 k > 1), HIP events over back-to-back launches, interleaved rounds in one process.
-usage: python tools/slabp_ab.py [rounds]"""
+usage: python tools/slabp_ab.py [rounds [ENV v0 v1]]  (default FTMI_SLAB_PF 0 1)"""
 import os
 import sys
 
@@ -23,6 +23,7 @@ SHAPES = {  # name: (kind, B, T, Cin, N, k)
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    env, vals = (sys.argv[2], sys.argv[3:5]) if len(sys.argv) > 4 else ('FTMI_SLAB_PF', ['0', '1'])
     torch.manual_seed(0)
     fns = {}
     for name, s in SHAPES.items():
@@ -47,8 +48,8 @@ def main():
     res = {}
     for _ in range(rounds):
         for name, (fn, flops) in fns.items():
-            for pf in ('0', '1'):
-                os.environ['FTMI_SLAB_PF'] = pf
+            for pf in vals:
+                os.environ[env] = pf
                 for _ in range(2):
                     fn()
                 torch.cuda.synchronize()
@@ -59,8 +60,8 @@ def main():
                 torch.cuda.synchronize()
                 res.setdefault((name, pf), []).append(a.elapsed_time(b) / 10)
     for name, (_, flops) in fns.items():
-        t0, t1 = min(res[(name, '0')]), min(res[(name, '1')])
-        print(f'{name:16s} old {t0 * 1e3:8.1f} us ({flops / t0 / 1e9:6.1f} TF/s) | prefetch '
+        t0, t1 = min(res[(name, vals[0])]), min(res[(name, vals[1])])
+        print(f'{name:16s} {env}={vals[0]} {t0 * 1e3:8.1f} us ({flops / t0 / 1e9:6.1f} TF/s) | ={vals[1]} '
               f'{t1 * 1e3:8.1f} us ({flops / t1 / 1e9:6.1f} TF/s) | {t0 / t1:.3f}x', flush=True)
 
 
