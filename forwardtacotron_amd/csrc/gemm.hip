@@ -2607,15 +2607,42 @@ struct HwStackParams {
 
 // acc[mi][ni] (rows 16 mi + 4 fs + i, GEMM column of bp[ni] + fr) = A x B^T over nks k-steps
 // of 32, f16x3 (small terms first, as the slab kernel).  bp[ni]: the lane's B0 row + 8 fs.
-template <int NI>
-__device__ __forceinline__ void hs_step(f32x4 (&acc)[4][NI], const _Float16 *Ah,
+template <int NI, int MI = 4>
+__device__ __forceinline__ void hs_step(f32x4 (&acc)[MI][NI], const _Float16 *Ah,
                                         const _Float16 *At, const f16x8 (&b0)[NI],
                                         const f16x8 (&b1)[NI], int ks, int fr, int fs) {
   f16x8 bh[NI];
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) bh[ni] = b0[ni] * (_Float16)(1.0f / H3_SCALE);
+  if constexpr (MI > 4) {  // the A fragments of row block mi + 1 read under the MFMAs of mi,
+                           // one block ahead only (register budget: sched barriers)
+    f16x8 ah = *(const f16x8 *)(Ah + fr * HS_P + 32 * ks + 8 * fs);
+    f16x8 at = *(const f16x8 *)(At + fr * HS_P + 32 * ks + 8 * fs);
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {  // A fragments one row block at a time (register budget)
+    for (int mi = 0; mi < MI; ++mi) {
+      f16x8 nh = ah, nt = at;
+      if (mi + 1 < MI) {
+        const int o = (16 * (mi + 1) + fr) * HS_P + 32 * ks + 8 * fs;
+        nh = *(const f16x8 *)(Ah + o);
+        nt = *(const f16x8 *)(At + o);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        f32x4 c = acc[mi][ni];
+        c = mma16(at, bh[ni], c);
+        c = mma16(ah, b1[ni], c);
+        c = mma16(ah, b0[ni], c);
+        acc[mi][ni] = c;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      ah = nh;
+      at = nt;
+    }
+    return;
+  }
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi) {  // A fragments one row block at a time (register budget)
     const int o = (16 * mi + fr) * HS_P + 32 * ks + 8 * fs;
     const f16x8 ah = *(const f16x8 *)(Ah + o);
     const f16x8 at = *(const f16x8 *)(At + o);
@@ -2635,8 +2662,8 @@ __device__ __forceinline__ void hs_step(f32x4 (&acc)[4][NI], const _Float16 *Ah,
 // B fragments rotate through three register sets, loaded three k-steps ahead (the loop is
 // kept rolled and the steps fenced by sched barriers: otherwise the compiler hoists further
 // loads and LDS reads across steps and spills).
-template <int NI>
-__device__ __forceinline__ void hs_gemm_acc(f32x4 (&acc)[4][NI], const _Float16 *Ah,
+template <int NI, int MI = 4>
+__device__ __forceinline__ void hs_gemm_acc(f32x4 (&acc)[MI][NI], const _Float16 *Ah,
                                             const _Float16 *At, const _Float16 *const (&bp)[NI],
                                             int64_t plane, int nks, int fr, int fs) {
   // three register sets in a ring: the loads of k-step ks + 3 are issued right after step
@@ -2656,33 +2683,40 @@ __device__ __forceinline__ void hs_gemm_acc(f32x4 (&acc)[4][NI], const _Float16 
   load(z0, z1, 2);
 #pragma unroll 1
   for (int ks = 0; ks < nks; ks += 3) {
-    hs_step<NI>(acc, Ah, At, x0, x1, ks, fr, fs);
+    hs_step<NI, MI>(acc, Ah, At, x0, x1, ks, fr, fs);
     load(x0, x1, ks + 3);
     __builtin_amdgcn_sched_barrier(0);  // no hoisting across steps (register budget)
     if (ks + 1 >= nks) break;
-    hs_step<NI>(acc, Ah, At, y0, y1, ks + 1, fr, fs);
+    hs_step<NI, MI>(acc, Ah, At, y0, y1, ks + 1, fr, fs);
     load(y0, y1, ks + 4);
     __builtin_amdgcn_sched_barrier(0);
     if (ks + 2 >= nks) break;
-    hs_step<NI>(acc, Ah, At, z0, z1, ks + 2, fr, fs);
+    hs_step<NI, MI>(acc, Ah, At, z0, z1, ks + 2, fr, fs);
     load(z0, z1, ks + 5);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-template <int NI>
-__device__ __forceinline__ void hs_gemm(f32x4 (&acc)[4][NI], const _Float16 *Ah,
+template <int NI, int MI = 4>
+__device__ __forceinline__ void hs_gemm(f32x4 (&acc)[MI][NI], const _Float16 *Ah,
                                         const _Float16 *At, const _Float16 *const (&bp)[NI],
                                         int64_t plane, int nks, int fr, int fs) {
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+  for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  hs_gemm_acc<NI>(acc, Ah, At, bp, plane, nks, fr, fs);
+  hs_gemm_acc<NI, MI>(acc, Ah, At, bp, plane, nks, fr, fs);
 }
 
+// BM = 64: two LDS images, ping-pong (each layer reads one, writes the other); BM = 96: one
+// image of 96 rows, overwritten in place behind a barrier (104 KB) — each weight fragment a
+// wave fetches then feeds 6 row blocks instead of 4, cutting the per-CU L2 fetch per flop,
+// which is what bounds this kernel, by a third.
+template <int BM>
 __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackParams p) {
-  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * 2 * HS_IMG];  // [image][head|tail]
+  constexpr int MI = BM / 16, NIMG = BM == 64 ? 2 : 1, IMG = BM * HS_P;
+  static_assert(BM == 64 || BM == 96, "rows per workgroup");
+  __shared__ __attribute__((aligned(16))) _Float16 lds[NIMG * 2 * IMG];  // [image][head|tail]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fs = lane >> 4;
   // column block of this wave, rotated per workgroup so that the CUs of one XCD (blocks
@@ -2696,12 +2730,12 @@ __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackPara
   auto bptr = [&](const _Float16 *base, int n0, int Kpad) -> const _Float16 * {
     return base + (int64_t)(n0 >> 4) * (Kpad / 32) * 512 + lane * 8;
   };
-  const int m0 = blockIdx.x * HS_BM;
+  const int m0 = blockIdx.x * BM;
   float amax = 0.f;  // range guard: largest |activation| fed to the f16 split
 
   // ---- the input rows (Cp channels, zero-padded to kp_pre; rows past M zero) -> image 0
   const int q4 = p.kp_pre / 4;
-  for (int e = tid; e < HS_BM * q4; e += 512) {
+  for (int e = tid; e < BM * q4; e += 512) {
     const int r = e / q4, c = (e - r * q4) * 4;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (m0 + r < p.M && c < p.Cp) v = *(const f32x4 *)(p.x + (int64_t)(m0 + r) * p.x_stride + c);
@@ -2709,15 +2743,15 @@ __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackPara
     f16x4 hh, tt;
     split2h(v, hh, tt);
     *(f16x4 *)(lds + r * HS_P + c) = hh;
-    *(f16x4 *)(lds + HS_IMG + r * HS_P + c) = tt;
+    *(f16x4 *)(lds + IMG + r * HS_P + c) = tt;
   }
   __syncthreads();
 
-  f32x4 xs[4][2];  // this wave's 64 x 32 block of the current activations, fp32
+  f32x4 xs[MI][2];  // this wave's BM x 32 block of the current activations, fp32
   auto put = [&](int img) {  // xs -> LDS image img (split)
-    _Float16 *Hd = lds + img * 2 * HS_IMG, *Tl = Hd + HS_IMG;
+    _Float16 *Hd = lds + img * 2 * IMG, *Tl = Hd + IMG;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int nj = 0; nj < 2; ++nj)
 #pragma unroll
@@ -2733,40 +2767,41 @@ __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackPara
 
   // ---- pre_highway (Linear, no bias): x W_pre^T, K = kp_pre
   {
-    f32x4 acc[4][2];
+    f32x4 acc[MI][2];
     const _Float16 *bp[2];
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni)
       bp[ni] = bptr(p.w_pre, 32 * cb + 16 * ni, p.kp_pre);
-    hs_gemm<2>(acc, lds, lds + HS_IMG, bp, (int64_t)HS_C * p.kp_pre, p.kp_pre / 32, fr, fs);
+    hs_gemm<2, MI>(acc, lds, lds + IMG, bp, (int64_t)HS_C * p.kp_pre, p.kp_pre / 32, fr, fs);
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
       const float cs = p.cs_pre[32 * cb + 16 * ni + fr];
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) xs[mi][ni] = acc[mi][ni] * cs;
+      for (int mi = 0; mi < MI; ++mi) xs[mi][ni] = acc[mi][ni] * cs;
     }
   }
-  put(1);
+  int cur = NIMG - 1;
+  if (NIMG == 1) __syncthreads();  // every wave is done reading the input image
+  put(cur);
   __syncthreads();
-  int cur = 1;
 
   // ---- highways: g = sigmoid(x W2^T + b2), x <- g relu(x W1^T + b1) + (1 - g) x
   for (int l = 0; l < p.L; ++l) {
-    const _Float16 *A = lds + cur * 2 * HS_IMG;
+    const _Float16 *A = lds + cur * 2 * IMG;
     // two halves: W1 tile nj with its W2 tile (GEMM columns 64 cb + 16 nj, + 32), so one
     // half's accumulators and B ring stay small
 #pragma unroll
     for (int nj = 0; nj < 2; ++nj) {
-      f32x4 acc[4][2];
+      f32x4 acc[MI][2];
       const _Float16 *bp[2] = {bptr(p.w_hw[l], 64 * cb + 16 * nj, HS_C),
                                bptr(p.w_hw[l], 64 * cb + 32 + 16 * nj, HS_C)};
-      hs_gemm<2>(acc, A, A + HS_IMG, bp, (int64_t)2 * HS_C * HS_C, HS_C / 32, fr, fs);
+      hs_gemm<2, MI>(acc, A, A + IMG, bp, (int64_t)2 * HS_C * HS_C, HS_C / 32, fr, fs);
       const int col = 32 * cb + 16 * nj + fr;
       const float c1 = p.cs_hw[l][64 * cb + 16 * nj + fr];
       const float c2 = p.cs_hw[l][64 * cb + 32 + 16 * nj + fr];
       const float bb1 = p.b1[l][col], bb2 = p.b2[l][col];
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float x1, x2;
@@ -2780,13 +2815,17 @@ __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackPara
           xs[mi][nj][i] = highway_mix(g, x1, xs[mi][nj][i]);
         }
     }
-    cur ^= 1;
-    put(cur);  // the image read two layers ago: every wave passed the barrier since
+    if (NIMG == 2) {
+      cur ^= 1;  // the image read two layers ago: every wave passed the barrier since
+    } else {
+      __syncthreads();  // every wave is done reading the image it overwrites
+    }
+    put(cur);
     __syncthreads();
   }
   if (p.h) {
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + 16 * mi + 4 * fs + i;
@@ -2799,18 +2838,18 @@ __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackPara
 
   // ---- output projection (the GRU's x W_ih^T + b_ih), HS_NPASS columns per pass
   if (p.w_out) {
-    const _Float16 *A = lds + cur * 2 * HS_IMG;
+    const _Float16 *A = lds + cur * 2 * IMG;
     for (int q = 0; q < 2 * p.n_out / HS_NPASS; ++q) {  // 256 columns (32 per wave) a pass
-      f32x4 acc[4][2];
+      f32x4 acc[MI][2];
       const int n0 = (HS_NPASS / 2) * q + 32 * cb;
       const _Float16 *bp[2] = {bptr(p.w_out, n0, HS_C), bptr(p.w_out, n0 + 16, HS_C)};
-      hs_gemm<2>(acc, A, A + HS_IMG, bp, (int64_t)p.n_out * HS_C, HS_C / 32, fr, fs);
+      hs_gemm<2, MI>(acc, A, A + IMG, bp, (int64_t)p.n_out * HS_C, HS_C / 32, fr, fs);
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
         const int col = n0 + 16 * ni + fr;
         const float cs = p.cs_out[col], b = p.b_out ? p.b_out[col] : 0.f;
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
 #pragma clang fp contract(off)
@@ -3690,8 +3729,17 @@ extern "C" int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, i
   p.h = h;
   p.h_stride = h_stride;
   p.status = status;
-  const unsigned blocks = (unsigned)((M + HS_BM - 1) / HS_BM);
-  hipLaunchKernelGGL(highway_stack_kernel, dim3(blocks), dim3(512), 0, ftmi_hs(stream), p);
+  // 96 rows per workgroup once the grid still fills the chip (FTMI_HS_BM = 64 / 96, read per
+  // call, forces one; 128 rows would need ~290 VGPRs and spills)
+  const char *e = getenv("FTMI_HS_BM");
+  const int bm = e ? atoi(e) : (M >= 96 * 256 ? 96 : 64);
+  if (bm == 96) {
+    const unsigned blocks = (unsigned)((M + 95) / 96);
+    hipLaunchKernelGGL(highway_stack_kernel<96>, dim3(blocks), dim3(512), 0, ftmi_hs(stream), p);
+  } else {
+    const unsigned blocks = (unsigned)((M + HS_BM - 1) / HS_BM);
+    hipLaunchKernelGGL(highway_stack_kernel<64>, dim3(blocks), dim3(512), 0, ftmi_hs(stream), p);
+  }
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
 }

@@ -394,6 +394,32 @@ def test_highway_stack(B, T, Cp, L, rng, monkeypatch):
         close(host(y), host(yu), rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize('B,T', [(3, 333), (64, 1368)])
+def test_highway_stack_rows96_bit_identical(B, T, rng, monkeypatch):
+    """The 96-row workgroup form (one LDS image overwritten in place, default from 24,576
+    rows) against the 64-row ping-pong form: same MFMA order and epilogue, bit for bit,
+    incl. a ragged last row tile; the second case is the c3 postnet (87,552 rows)."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import CBHG
+    C, Cp, L = 256, 80, 4
+    torch.manual_seed(5)
+    m = CBHG(K=2, in_channels=Cp, channels=C, proj_channels=[C, Cp], num_highways=L)
+    with torch.no_grad():
+        for hw in m.highways:
+            hw.W1.bias.normal_(0, 0.1)
+    m = m.cuda()
+    xd = dev(rng.normal(0, 1, (B, T, Cp)).astype(np.float32))
+    _, _, b_in, _, _ = m.rnn.packed_weights()
+    pre_f, hw_f, b1s, b2s, ih_f, _, n_out = m._stack_pack()
+    outs = []
+    for bm in ('96', '64'):
+        monkeypatch.setenv('FTMI_HS_BM', bm)
+        y, h = ops.highway_stack(xd, pre_f, C, hw_f, b1s, b2s, ih_f, b_in, n_out, want_h=True)
+        outs.append((host(y), host(h)))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
 def test_highway_stack_range_guard(rng):
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import CBHG

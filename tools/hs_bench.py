@@ -1,6 +1,7 @@
 """Fused highway stack (ftmi_highway_stack) vs the unfused chain it replaces, at the
 BASELINE shapes: c3 postnet (M = 64 x 1368, Cp = 80), c3 prenet (M = 64 x 200, Cp = 256),
-c2 postnet / prenet (M = 816 / 120).  Prints us per call (HIP events, 50 calls)."""
+c2 postnet / prenet (M = 816 / 120).  Prints us per call (HIP events, 50 calls).
+usage: python tools/hs_bench.py [ncases [rows-per-workgroup ...]]  (FTMI_HS_BM A/B, fused only)"""
 import os
 import sys
 
@@ -44,6 +45,16 @@ for name, M, Cp in CASES:
             h = ops.highway(h, w12, b1, b2, w_split=s3)
         ops.conv1d(h, w_ih, 1, 0, bias=b_in, w_split=w3)
 
+    if len(sys.argv) > 2:  # fused, per FTMI_HS_BM setting, interleaved rounds, min
+        res = {}
+        for _ in range(3):
+            for bm in sys.argv[2:]:
+                os.environ['FTMI_HS_BM'] = bm
+                res.setdefault(bm, []).append(timeit(fused))
+        os.environ.pop('FTMI_HS_BM')
+        print(f'{name:11s} M={M:6d}: ' + '  '.join(f'bm={bm} {min(v):8.1f} us' for bm, v in res.items()),
+              flush=True)
+        continue
     tf = timeit(fused)
     tu = timeit(unfused) if len(sys.argv) == 1 else float('nan')
     fl = 2.0 * M * 256 * (Cp + 4 * 512 + 1536)
