@@ -561,6 +561,210 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
   }
 }
 
+// ---- transposed form: S^T = K (q c)^T and O^T = V^T P^T ----------------------------------
+// The same f16x3 flash attention with both MFMAs' operands swapped, so the C layout puts ONE
+// query in each lane (column c16) and keys / head dims in its rows: a lane's 16 scores of a
+// 64-key tile all belong to its query, so the softmax runs in-lane plus two cross-group
+// shuffles (no 16-lane row reductions per row), the running max / sum are one value per
+// lane, the O rescale multiplies whole accumulators by the lane's own alpha, and P needs no
+// LDS round trip: the 8 scores a lane holds of a 32-key step (keys 4g .. 4g+3 of two 16-key
+// blocks) ARE its B fragment for O^T = V^T P^T once V^T's keys are stored in the same order
+// (position 8g + j of a 32-key group holds key 4g + j, j < 4, else 16 + 4g + j - 4).  K and V^T
+// fragments are read at the same LDS addresses as attention_h3_kernel's; LDS drops the P
+// buffers.  PRE only (K / V from the split-plane workspace).  Numerically the same algorithm;
+// the P V products sum in a permuted key order inside each MFMA.
+template <int HD>
+__global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
+    const float *__restrict__ qkv, int64_t rs, int B, int T, int H, int q_off,
+    const uint8_t *__restrict__ kpm, float qscale, float *__restrict__ out, int64_t os,
+    unsigned *status, const _Float16 *__restrict__ kv, int Tp) {
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  typedef float f32x8 __attribute__((ext_vector_type(8)));
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  constexpr int NTH = 64 * AH_W;
+  constexpr float TS = 2048.f, TU = 1.f / 2048.f;
+  constexpr float LOG2E = 1.4426950408889634f;
+  constexpr int KP = HD + 16, VP = AH_KT + 16;
+  constexpr int NT = HD / 16, KQ = HD / 32, NB = AH_KT / 16, KK = AH_KT / 32;
+  __shared__ __attribute__((aligned(16))) _Float16 Kh[AH_KT * KP], Kt[AH_KT * KP];
+  __shared__ __attribute__((aligned(16))) _Float16 Vh[HD * VP], Vt[HD * VP];
+
+  const int nq = (T + 16 * AH_W - 1) / (16 * AH_W), nbh = B * H;
+  int bh, qtile;
+  if (nbh % 8 == 0) {
+    const int L = blockIdx.x, q8 = L >> 3;
+    bh = (L & 7) + 8 * (q8 / nq);
+    qtile = q8 % nq;
+  } else {
+    bh = blockIdx.x / nq;
+    qtile = blockIdx.x % nq;
+  }
+  const int b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int q0 = qtile * 16 * AH_W + wave * 16;
+  const float *base = qkv + (int64_t)b * T * rs;
+  float amax = 0.f;
+
+  // B fragments of this wave's 16 queries (lane: query c16, d = 32 ks + 8 g + j), q c in fp32
+  f16x8 qh[KQ], qt[KQ];
+  {
+    const int qr = q0 + c16;
+    const float *src = base + (int64_t)(qr < T ? qr : 0) * rs + q_off + h * HD;
+#pragma unroll
+    for (int ks = 0; ks < KQ; ++ks) {
+      f32x4 a = *(const f32x4 *)(src + 32 * ks + 8 * g) * qscale;
+      f32x4 c = *(const f32x4 *)(src + 32 * ks + 8 * g + 4) * qscale;
+      if (qr >= T) a = c = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const f32x8 v = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+      qh[ks] = __builtin_convertvector(v, f16x8);
+      qt[ks] = __builtin_convertvector((v - __builtin_convertvector(qh[ks], f32x8)) * TS, f16x8);
+    }
+  }
+  f32x4 ob[NT], osm[NT];  // O^T: lane (query c16, d = 16 n + 4 g + i); big / small terms
+#pragma unroll
+  for (int n = 0; n < NT; ++n) ob[n] = osm[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  constexpr int NKC = 2 * AH_KT * HD / 8 / NTH, NVC = 2 * HD * AH_KT / 8 / NTH;
+  static_assert(NKC * NTH == 2 * AH_KT * HD / 8 && NVC * NTH == 2 * HD * AH_KT / 8, "slots");
+  u32x4 kr[NKC], vr[NVC];
+  const size_t plane = (size_t)B * H * Tp * HD;
+  const int last0 = (T - 1) / AH_KT * AH_KT;
+  auto load_tile = [&](int k0) {
+    k0 = k0 < last0 ? k0 : last0;  // past the end: a clamped (unused) reload
+    const _Float16 *kb = kv + ((size_t)bh * Tp + k0) * HD;
+    const _Float16 *vb = kv + 2 * plane + (size_t)bh * HD * Tp + k0;
+#pragma unroll
+    for (int i = 0; i < NKC; ++i) {
+      const int e = tid + NTH * i, pl = e / (AH_KT * HD / 8), q = e - pl * (AH_KT * HD / 8);
+      const int r = q / (HD / 8), c8 = (q - r * (HD / 8)) * 8;
+      kr[i] = *(const u32x4 *)(kb + pl * plane + (size_t)r * HD + c8);
+    }
+#pragma unroll
+    for (int i = 0; i < NVC; ++i) {
+      const int e = tid + NTH * i, pl = e / (HD * AH_KT / 8), q = e - pl * (HD * AH_KT / 8);
+      const int d = q / (AH_KT / 8), c8 = (q - d * (AH_KT / 8)) * 8;
+      vr[i] = *(const u32x4 *)(vb + pl * plane + (size_t)d * Tp + c8);
+    }
+  };
+  // position of key w (0..31) of a 32-key group: the k order of the lanes' P fragments
+  auto kpos = [](int w) { return w < 16 ? 2 * w : 2 * (w - 16) + 4; };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < NKC; ++i) {
+      const int e = tid + NTH * i, pl = e / (AH_KT * HD / 8), q = e - pl * (AH_KT * HD / 8);
+      const int r = q / (HD / 8), c8 = (q - r * (HD / 8)) * 8;
+      *(u32x4 *)&(pl ? Kt : Kh)[r * KP + c8] = kr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NVC; ++i) {
+      const int e = tid + NTH * i, pl = e / (HD * AH_KT / 8), q = e - pl * (HD * AH_KT / 8);
+      const int d = q / (AH_KT / 8), c8 = (q - d * (AH_KT / 8)) * 8;
+      _Float16 *row = &(pl ? Vt : Vh)[d * VP + (c8 & ~31)];
+      const int w = c8 & 31;
+      *(u32x2 *)(row + kpos(w)) = (u32x2){vr[i].x, vr[i].y};
+      *(u32x2 *)(row + kpos(w + 4)) = (u32x2){vr[i].z, vr[i].w};
+    }
+  };
+  load_tile(0);
+
+  for (int k0 = 0; k0 < T; k0 += AH_KT) {
+    __syncthreads();  // every wave is done with the previous tile's LDS planes
+    store_tile();
+    __syncthreads();
+    load_tile(k0 + AH_KT);
+    // dead keys of the tile (past T or flagged in key_padding_mask), one bit per key: lane l
+    // reads key k0 + l's flag (issued here, under the S MFMAs)
+    const bool masked = k0 + AH_KT > T || kpm;
+    unsigned long long dm = 0;
+    if (masked) {
+      const int key = k0 + lane;
+      dm = __ballot(key >= T || (kpm && kpm[(int64_t)b * T + key]));
+    }
+    // ---- S^T = K (q c)^T: lane (query c16, keys 16 n + 4 g + i)
+    f32x4 s[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      f32x4 big = {0.f, 0.f, 0.f, 0.f}, sm = {0.f, 0.f, 0.f, 0.f};
+      const int o = (n * 16 + c16) * KP + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < KQ; ++ks) {
+        const f16x8 kh = *(const f16x8 *)&Kh[o + 32 * ks];
+        const f16x8 kt = *(const f16x8 *)&Kt[o + 32 * ks];
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[ks], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_f16(kt, qh[ks], sm, 0, 0, 0);
+        big = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qh[ks], big, 0, 0, 0);
+      }
+      s[n] = big + sm * TU;
+      if (masked) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if ((dm >> (n * 16 + 4 * g + i)) & 1ull) s[n][i] = -INFINITY;
+      }
+    }
+    // ---- online softmax of the lane's query (lazy running max, as attention_h3_kernel)
+    float mx = s[0][0];
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[n][i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const bool up = mx > m + AH_LAZY;  // false while the query has only masked keys
+    const float mn = up ? mx : m;
+    const float alpha = up ? __builtin_amdgcn_exp2f((m - mn) * LOG2E) : 1.f;
+    const float off = mn == -INFINITY ? 0.f : -mn * LOG2E;
+    float ps = 0.f;
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pv = __builtin_amdgcn_exp2f(fmaf(s[n][i], LOG2E, off));
+        s[n][i] = pv;
+        ps += pv;
+      }
+    ps += __shfl_xor(ps, 16);
+    ps += __shfl_xor(ps, 32);
+    l = l * alpha + ps;
+    m = mn;
+    if (__any(up)) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        ob[n] *= alpha;
+        osm[n] *= alpha;
+      }
+    }
+    // ---- O^T += V^T P^T: the lane's 8 probabilities of key step kk are its B fragment
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const f32x4 a = s[2 * kk], c = s[2 * kk + 1];
+      const f32x8 v = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      const f16x8 ph = __builtin_convertvector(v, f16x8);
+      const f16x8 pt = __builtin_convertvector((v - __builtin_convertvector(ph, f32x8)) * TS, f16x8);
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int o = (n * 16 + c16) * VP + 32 * kk + 8 * g;
+        const f16x8 vh = *(const f16x8 *)&Vh[o];
+        const f16x8 vt = *(const f16x8 *)&Vt[o];
+        osm[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pt, osm[n], 0, 0, 0);
+        osm[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vt, ph, osm[n], 0, 0, 0);
+        ob[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, ob[n], 0, 0, 0);
+      }
+    }
+  }
+  if (!(amax <= 65504.f) && status) atomicOr(status, 1u);
+  const int qr = q0 + c16;
+  if (qr < T) {  // the lane's query row: 4 consecutive head dims per block, 16-B stores
+    float *dst = out + ((int64_t)b * T + qr) * os + h * HD + 4 * g;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) *(f32x4 *)(dst + 16 * n) = (ob[n] + osm[n] * TU) / l;
+  }
+}
+
 // K and V of every (batch, head) split once into f16 head / scaled tail planes for the
 // PRE attention kernel: K [B*H][Tp][HD], V transposed [B*H][HD][Tp] (keys >= T zero).  One
 // workgroup per (64 keys, b*h): K rows straight through, V through an LDS tile.  A value
@@ -670,6 +874,13 @@ extern "C" int64_t ftmi_attention_workspace_bytes(int32_t B, int32_t T, int32_t 
   return 4 * (int64_t)B * H * Tp * head_dim * 2;
 }
 
+// the transposed kernel for the pre-split (K / V workspace) paths with 16-B aligned output
+// rows; FTMI_ATTN_T=0 (read per call) keeps attention_h3_kernel
+static bool attn_transposed() {
+  const char *e = getenv("FTMI_ATTN_T");
+  return !e || atoi(e) != 0;
+}
+
 extern "C" int ftmi_attention_kv(const float *q, int64_t row_stride, int32_t B, int32_t T,
                                  int32_t H, int32_t head_dim, const uint8_t *key_padding_mask,
                                  float qscale, float *out, int64_t out_stride, uint32_t *status,
@@ -683,7 +894,14 @@ extern "C" int ftmi_attention_kv(const float *q, int64_t row_stride, int32_t B, 
   const dim3 g1((unsigned)(nq * B * H)), b1(64 * AH_W);
   const _Float16 *kv = (const _Float16 *)kv_workspace;
   const hipStream_t s = ftmi_hs(stream);
-  if (head_dim == 64)
+  if (attn_transposed() && (out_stride & 3) == 0 && ftmi_aligned16(out)) {
+    if (head_dim == 64)
+      hipLaunchKernelGGL(attention_t3_kernel<64>, g1, b1, 0, s, q, row_stride, B, T, H, 0,
+                         key_padding_mask, qscale, out, out_stride, status, kv, Tp);
+    else
+      hipLaunchKernelGGL(attention_t3_kernel<128>, g1, b1, 0, s, q, row_stride, B, T, H, 0,
+                         key_padding_mask, qscale, out, out_stride, status, kv, Tp);
+  } else if (head_dim == 64)
     hipLaunchKernelGGL((attention_h3_kernel<64, true>), g1, b1, 0, s, q, row_stride, B, T, H, 0,
                        0, 0, key_padding_mask, qscale, out, out_stride, status, kv, Tp);
   else
@@ -716,9 +934,14 @@ extern "C" int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, i
   if (pre) {                                                                                     \
     hipLaunchKernelGGL(attn_split_kv_kernel<HD_>, dim3((unsigned)(Tp / 64), (unsigned)(B * H)),  \
                        dim3(256), 0, s, qkv, row_stride, B, T, H, k_off, v_off, Tp, kv, status); \
-    hipLaunchKernelGGL((attention_h3_kernel<HD_, true>), g1, b1, 0, s, qkv, row_stride, B, T, H, \
-                       q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride, status,  \
-                       (const _Float16 *)kv, Tp);                                               \
+    if (attn_transposed() && (out_stride & 3) == 0 && ftmi_aligned16(out))                      \
+      hipLaunchKernelGGL(attention_t3_kernel<HD_>, g1, b1, 0, s, qkv, row_stride, B, T, H, q_off, \
+                         key_padding_mask, qscale, out, out_stride, status, (const _Float16 *)kv, \
+                         Tp);                                                                     \
+    else                                                                                          \
+      hipLaunchKernelGGL((attention_h3_kernel<HD_, true>), g1, b1, 0, s, qkv, row_stride, B, T,  \
+                         H, q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride,       \
+                         status, (const _Float16 *)kv, Tp);                                       \
   } else {                                                                                       \
     hipLaunchKernelGGL((attention_h3_kernel<HD_, false>), g1, b1, 0, s, qkv, row_stride, B, T,  \
                        H, q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride,       \
