@@ -571,7 +571,8 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
 // blocks) ARE its B fragment for O^T = V^T P^T once V^T's keys are stored in the same order
 // (position 8g + j of a 32-key group holds key 4g + j, j < 4, else 16 + 4g + j - 4).  K and V^T
 // fragments are read at the same LDS addresses as attention_h3_kernel's; LDS drops the P
-// buffers.  PRE only (K / V from the split-plane workspace).  Numerically the same algorithm;
+// buffers, which leaves room for two K / V tile buffers: one barrier per tile, and the tile
+// stores overlap other waves' MFMAs instead of a phase where no wave multiplies.  PRE only (K / V from the split-plane workspace).  Numerically the same algorithm;
 // the P V products sum in a permuted key order inside each MFMA.
 template <int HD>
 __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
@@ -587,8 +588,9 @@ __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
   constexpr float LOG2E = 1.4426950408889634f;
   constexpr int KP = HD + 16, VP = AH_KT + 16;
   constexpr int NT = HD / 16, KQ = HD / 32, NB = AH_KT / 16, KK = AH_KT / 32;
-  __shared__ __attribute__((aligned(16))) _Float16 Kh[AH_KT * KP], Kt[AH_KT * KP];
-  __shared__ __attribute__((aligned(16))) _Float16 Vh[HD * VP], Vt[HD * VP];
+  // two tile buffers (152 KB at HD = 128): tile t + 1 is stored while tile t is multiplied
+  __shared__ __attribute__((aligned(16))) _Float16 Kh[2][AH_KT * KP], Kt[2][AH_KT * KP];
+  __shared__ __attribute__((aligned(16))) _Float16 Vh[2][HD * VP], Vt[2][HD * VP];
 
   const int nq = (T + 16 * AH_W - 1) / (16 * AH_W), nbh = B * H;
   int bh, qtile;
@@ -653,30 +655,29 @@ __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
   };
   // position of key w (0..31) of a 32-key group: the k order of the lanes' P fragments
   auto kpos = [](int w) { return w < 16 ? 2 * w : 2 * (w - 16) + 4; };
-  auto store_tile = [&]() {
+  auto store_tile = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < NKC; ++i) {
       const int e = tid + NTH * i, pl = e / (AH_KT * HD / 8), q = e - pl * (AH_KT * HD / 8);
       const int r = q / (HD / 8), c8 = (q - r * (HD / 8)) * 8;
-      *(u32x4 *)&(pl ? Kt : Kh)[r * KP + c8] = kr[i];
+      *(u32x4 *)&(pl ? Kt : Kh)[buf][r * KP + c8] = kr[i];
     }
 #pragma unroll
     for (int i = 0; i < NVC; ++i) {
       const int e = tid + NTH * i, pl = e / (HD * AH_KT / 8), q = e - pl * (HD * AH_KT / 8);
       const int d = q / (AH_KT / 8), c8 = (q - d * (AH_KT / 8)) * 8;
-      _Float16 *row = &(pl ? Vt : Vh)[d * VP + (c8 & ~31)];
+      _Float16 *row = &(pl ? Vt : Vh)[buf][d * VP + (c8 & ~31)];
       const int w = c8 & 31;
       *(u32x2 *)(row + kpos(w)) = (u32x2){vr[i].x, vr[i].y};
       *(u32x2 *)(row + kpos(w + 4)) = (u32x2){vr[i].z, vr[i].w};
     }
   };
   load_tile(0);
+  store_tile(0);
+  load_tile(AH_KT);
+  __syncthreads();
 
-  for (int k0 = 0; k0 < T; k0 += AH_KT) {
-    __syncthreads();  // every wave is done with the previous tile's LDS planes
-    store_tile();
-    __syncthreads();
-    load_tile(k0 + AH_KT);
+  for (int k0 = 0, cb = 0; k0 < T; k0 += AH_KT, cb ^= 1) {
     // dead keys of the tile (past T or flagged in key_padding_mask), one bit per key: lane l
     // reads key k0 + l's flag (issued here, under the S MFMAs)
     const bool masked = k0 + AH_KT > T || kpm;
@@ -693,8 +694,8 @@ __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
       const int o = (n * 16 + c16) * KP + 8 * g;
 #pragma unroll
       for (int ks = 0; ks < KQ; ++ks) {
-        const f16x8 kh = *(const f16x8 *)&Kh[o + 32 * ks];
-        const f16x8 kt = *(const f16x8 *)&Kt[o + 32 * ks];
+        const f16x8 kh = *(const f16x8 *)&Kh[cb][o + 32 * ks];
+        const f16x8 kt = *(const f16x8 *)&Kt[cb][o + 32 * ks];
         sm = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qt[ks], sm, 0, 0, 0);
         sm = __builtin_amdgcn_mfma_f32_16x16x32_f16(kt, qh[ks], sm, 0, 0, 0);
         big = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qh[ks], big, 0, 0, 0);
@@ -748,13 +749,20 @@ __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
         const int o = (n * 16 + c16) * VP + 32 * kk + 8 * g;
-        const f16x8 vh = *(const f16x8 *)&Vh[o];
-        const f16x8 vt = *(const f16x8 *)&Vt[o];
+        const f16x8 vh = *(const f16x8 *)&Vh[cb][o];
+        const f16x8 vt = *(const f16x8 *)&Vt[cb][o];
         osm[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pt, osm[n], 0, 0, 0);
         osm[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vt, ph, osm[n], 0, 0, 0);
         ob[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, ob[n], 0, 0, 0);
       }
     }
+    // the next tile into the other buffer (every wave passed the barrier after its last read
+    // of that buffer), then the loads of the one after
+    if (k0 + AH_KT < T) {
+      store_tile(cb ^ 1);
+      load_tile(k0 + 2 * AH_KT);
+    }
+    __syncthreads();
   }
   if (!(amax <= 65504.f) && status) atomicOr(status, 1u);
   const int qr = q0 + c16;
