@@ -561,9 +561,9 @@ _KV_OLD = []
 def kv_fused_ok(T: int, d: int, heads: int, w_frag) -> bool:
     """Whether FastPitch's in_proj + attention take ftmi_panel_proj_qkv + ftmi_attention_kv
     (the split pass folded into the projection): f16x3 in force, the attention would
-    presplit (T > 384), d = 256, head_dim 64 / 128.  FTMI_KV_FUSED=0 turns it off."""
+    presplit (T > 256), d = 256, head_dim 64 / 128.  FTMI_KV_FUSED=0 turns it off."""
     return (os.environ.get('FTMI_KV_FUSED', '1') != '0' and panel_ok(d, 3 * d, False, w_frag)
-            and ATTN_PRESPLIT and T > 384 and d == PANEL_N and d % heads == 0
+            and ATTN_PRESPLIT and T > 256 and d == PANEL_N and d % heads == 0
             and d // heads in (64, 128))
 
 
@@ -826,7 +826,7 @@ def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Te
               mma: Optional[int] = None, presplit: Optional[bool] = None) -> torch.Tensor:
     """Self-attention core of nn.MultiheadAttention on packed in_proj rows (B, T, 3d).
     mma: 2 = f16x3 contractions (default, MMA), 0 = fp32 MFMA (exact_paths(), MMA 0/1).
-    presplit (f16x3; default: ATTN_PRESPLIT and T > 384): K and V split once into f16
+    presplit (f16x3; default: ATTN_PRESPLIT and T > 256): K and V split once into f16
     planes in a workspace instead of per query tile (identical results; measured at c5's
     postnet T = 1400: 825 -> 618 us incl. the split pass, slower at T = 200)."""
     _dev(qkv, key_padding_mask)
@@ -841,8 +841,9 @@ def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Te
         kpm = key_padding_mask.to(torch.uint8).contiguous()
     qscale = float(np.float32(np.sqrt(1.0 / hd)))
     ws, nws = None, 0
-    if presplit is None:  # pays off once K / V are re-read by >= 4 query tiles (T > 384)
-        presplit = ATTN_PRESPLIT and T > 384
+    if presplit is None:  # with the transposed kernel from T > 256 (tools/attn_short_ab.py,
+        # B = 64: T 200 0.81-0.86x, T 300 1.05-1.08x, T 400 1.05-1.13x against the in-kernel split)
+        presplit = ATTN_PRESPLIT and T > 256
     if m == 2 and presplit:
         nws = int(_lib.load().ftmi_attention_workspace_bytes(B, T, heads, hd))
         ws = torch.empty(nws, device=qkv.device, dtype=torch.uint8)
