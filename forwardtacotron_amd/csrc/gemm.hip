@@ -3145,9 +3145,9 @@ static bool slab_enabled() {
 }
 
 // slab kernel eligibility: same-length output, Cin % 16 == 0, k taps within the slab halo,
-// groups of equal width (conv bank), 32-bit activation offsets; a k = 1 GEMM only when it
-// has more than
-// one column tile (narrow Linear layers run faster on the 128 x 128 x6b tiles).
+// groups of equal width (conv bank), 32-bit activation offsets; a k = 1 GEMM only from one
+// whole column tile (N >= 128: the FastPitch predictors' N = 128 projections 23.3 -> 17.2
+// us at 12,800 rows; narrower Linear layers, N = 80, run faster on the 128 x 128 x6b tiles).
 // FTMI_GEMM_SLAB_MIN (MACs, read per call; default 0) keeps smaller contractions on the
 // x6b kernel: tests use it to cover both kernels, A/B runs to size the choice (taking
 // the slab for every eligible shape measured fastest on c3: 10.01 vs 10.19 ms/step with
@@ -3162,7 +3162,11 @@ static bool slab_ok(const GemmParams &p, int epi) {
   const GemmGroup &g = p.g[0];
   int64_t macs = 0;
   for (int i = 0; i < p.ngroups; ++i) macs += (int64_t)p.M * p.g[i].N * p.g[i].Ktot;
-  if (!(slab_enabled() && p.To == p.T && p.Cin % 16 == 0 && (g.k > 1 || g.N > SL_BN) &&
+  static const int nmin = [] {  // FTMI_SLAB_K1_NMIN: narrowest k = 1 GEMM on the slab kernels
+    const char *e = getenv("FTMI_SLAB_K1_NMIN");
+    return e ? atoi(e) : SL_BN;
+  }();
+  if (!(slab_enabled() && p.To == p.T && p.Cin % 16 == 0 && (g.k > 1 || g.N >= nmin) &&
         macs >= slab_min_macs() && (int64_t)p.M * p.x_stride < ((int64_t)1 << 31)))
     return false;
   if (p.ngroups > 1 && p.split_req > 1) return false;  // the split-K finish is single-group

@@ -130,9 +130,12 @@ def _num_cus() -> int:
 SLAB = os.environ.get('FTMI_GEMM_SLAB', '1') != '0'
 
 
+SLAB_K1_NMIN = int(os.environ.get('FTMI_SLAB_K1_NMIN', 128))  # gemm.hip slab_ok
+
+
 def _slab(mma: int, T: int, To: int, Cin: int, k: int, N: int, M: int) -> bool:
     """Whether ftmi_conv1d takes the slab kernel (gemm.hip slab_ok)."""
-    return (SLAB and mma == 2 and To == T and Cin % 16 == 0 and k <= 16 and (k > 1 or N > 128)
+    return (SLAB and mma == 2 and To == T and Cin % 16 == 0 and k <= 16 and (k > 1 or N >= SLAB_K1_NMIN)
             and M * N * k * Cin >= int(os.environ.get('FTMI_GEMM_SLAB_MIN', 0)))
 
 

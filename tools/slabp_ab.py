@@ -11,6 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from forwardtacotron_amd import ops  # noqa: E402
 
 SHAPES = {  # name: (kind, B, T, Cin, N, k)
+    'c5.pred_k1_n128': ('conv', 64, 200, 128, 128, 1),
+    'c5.pred_k1_n384': ('conv', 64, 200, 128, 384, 1),
     'c5.ffn_conv1': ('conv', 64, 1400, 256, 1024, 9),
     'c3.post_proj1': ('conv', 64, 1368, 2048, 256, 3),
     'c3.pred_conv': ('conv', 64, 200, 256, 256, 5),
@@ -26,7 +28,10 @@ def main():
     env, vals = (sys.argv[2], sys.argv[3:5]) if len(sys.argv) > 4 else ('FTMI_SLAB_PF', ['0', '1'])
     torch.manual_seed(0)
     fns = {}
+    only = os.environ.get('SLABP_ONLY')  # comma-separated name prefixes
     for name, s in SHAPES.items():
+        if only and not any(name.startswith(o) for o in only.split(',')):
+            continue
         if s[0] == 'conv':
             _, B, T, Cin, N, k = s
             x = torch.randn(B, T, Cin, device='cuda')
