@@ -574,11 +574,11 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
 // buffers, which leaves room for two K / V tile buffers: one barrier per tile, and the tile
 // stores overlap other waves' MFMAs instead of a phase where no wave multiplies.  PRE only (K / V from the split-plane workspace).  Numerically the same algorithm;
 // the P V products sum in a permuted key order inside each MFMA.
-template <int HD>
+template <int HD, bool PRE>
 __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
-    const float *__restrict__ qkv, int64_t rs, int B, int T, int H, int q_off,
-    const uint8_t *__restrict__ kpm, float qscale, float *__restrict__ out, int64_t os,
-    unsigned *status, const _Float16 *__restrict__ kv, int Tp) {
+    const float *__restrict__ qkv, int64_t rs, int B, int T, int H, int q_off, int k_off,
+    int v_off, const uint8_t *__restrict__ kpm, float qscale, float *__restrict__ out,
+    int64_t os, unsigned *status, const _Float16 *__restrict__ kv, int Tp) {
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   typedef float f32x8 __attribute__((ext_vector_type(8)));
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -631,13 +631,36 @@ __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
   for (int n = 0; n < NT; ++n) ob[n] = osm[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
 
-  constexpr int NKC = 2 * AH_KT * HD / 8 / NTH, NVC = 2 * HD * AH_KT / 8 / NTH;
-  static_assert(NKC * NTH == 2 * AH_KT * HD / 8 && NVC * NTH == 2 * HD * AH_KT / 8, "slots");
-  u32x4 kr[NKC], vr[NVC];
-  const size_t plane = (size_t)B * H * Tp * HD;
+  // PRE: K / V f16 planes from the workspace (16-B copies); else fp32 rows of qkv, split here
+  // (attention_h3_kernel's loads: K a float4 of a key row, V 8 keys of one column)
+  constexpr int NKC = PRE ? 2 * AH_KT * HD / 8 / NTH : AH_KT * HD / 4 / NTH;
+  constexpr int NVC = PRE ? 2 * HD * AH_KT / 8 / NTH : HD * (AH_KT / 8) / NTH;
+  static_assert(NKC * NTH == (PRE ? 2 * AH_KT * HD / 8 : AH_KT * HD / 4) &&
+                NVC * NTH == (PRE ? 2 * HD * AH_KT / 8 : HD * (AH_KT / 8)), "slots");
+  u32x4 kr[NKC], vr[PRE ? NVC : 1];
+  float vs[PRE ? 1 : NVC][8];
+  const size_t plane = PRE ? (size_t)B * H * Tp * HD : 0;
   const int last0 = (T - 1) / AH_KT * AH_KT;
   auto load_tile = [&](int k0) {
     k0 = k0 < last0 ? k0 : last0;  // past the end: a clamped (unused) reload
+    if constexpr (!PRE) {
+#pragma unroll
+      for (int i = 0; i < NKC; ++i) {
+        const int e = tid + NTH * i, r = e / (HD / 4), c4 = (e - r * (HD / 4)) * 4;
+        const int key = min(k0 + r, T - 1);
+        kr[i] = *(const u32x4 *)(base + (int64_t)key * rs + k_off + h * HD + c4);
+      }
+#pragma unroll
+      for (int i = 0; i < NVC; ++i) {
+        const int e = tid + NTH * i, d = e % HD, kg = e / HD;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int key = min(k0 + kg * 8 + j, T - 1);
+          vs[i][j] = base[(int64_t)key * rs + v_off + h * HD + d];
+        }
+      }
+      return;
+    }
     const _Float16 *kb = kv + ((size_t)bh * Tp + k0) * HD;
     const _Float16 *vb = kv + 2 * plane + (size_t)bh * HD * Tp + k0;
 #pragma unroll
@@ -655,7 +678,45 @@ __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
   };
   // position of key w (0..31) of a 32-key group: the k order of the lanes' P fragments
   auto kpos = [](int w) { return w < 16 ? 2 * w : 2 * (w - 16) + 4; };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, int k0) {
+    if constexpr (!PRE) {
+#pragma unroll
+      for (int i = 0; i < NKC; ++i) {
+        const int e = tid + NTH * i, r = e / (HD / 4), c4 = (e - r * (HD / 4)) * 4;
+        f32x4 kvv = __builtin_bit_cast(f32x4, kr[i]);
+        if (k0 + r >= T) kvv = (f32x4){0.f, 0.f, 0.f, 0.f};
+        typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+        f16x4 hh, tt;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          amax = fmaxf(amax, fabsf(kvv[j]));
+          hh[j] = (_Float16)kvv[j];
+          tt[j] = (_Float16)((kvv[j] - (float)hh[j]) * TS);
+        }
+        *(f16x4 *)&Kh[buf][r * KP + c4] = hh;
+        *(f16x4 *)&Kt[buf][r * KP + c4] = tt;
+      }
+#pragma unroll
+      for (int i = 0; i < NVC; ++i) {
+        const int e = tid + NTH * i, d = e % HD, kg = e / HD;
+        f32x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[j] = k0 + kg * 8 + j < T ? vs[i][j] : 0.f;
+          amax = fmaxf(amax, fabsf(v[j]));
+        }
+        const f16x8 hh = __builtin_convertvector(v, f16x8);
+        const f16x8 tt = __builtin_convertvector((v - __builtin_convertvector(hh, f32x8)) * TS, f16x8);
+        const u32x4 hb = __builtin_bit_cast(u32x4, hh), tb = __builtin_bit_cast(u32x4, tt);
+        const int c8 = kg * 8, w = c8 & 31;
+        _Float16 *rh = &Vh[buf][d * VP + (c8 & ~31)], *rt = &Vt[buf][d * VP + (c8 & ~31)];
+        *(u32x2 *)(rh + kpos(w)) = (u32x2){hb.x, hb.y};
+        *(u32x2 *)(rh + kpos(w + 4)) = (u32x2){hb.z, hb.w};
+        *(u32x2 *)(rt + kpos(w)) = (u32x2){tb.x, tb.y};
+        *(u32x2 *)(rt + kpos(w + 4)) = (u32x2){tb.z, tb.w};
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NKC; ++i) {
       const int e = tid + NTH * i, pl = e / (AH_KT * HD / 8), q = e - pl * (AH_KT * HD / 8);
@@ -673,7 +734,7 @@ __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
     }
   };
   load_tile(0);
-  store_tile(0);
+  store_tile(0, 0);
   load_tile(AH_KT);
   __syncthreads();
 
@@ -759,7 +820,7 @@ __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
     // the next tile into the other buffer (every wave passed the barrier after its last read
     // of that buffer), then the loads of the one after
     if (k0 + AH_KT < T) {
-      store_tile(cb ^ 1);
+      store_tile(cb ^ 1, k0 + AH_KT);
       load_tile(k0 + 2 * AH_KT);
     }
     __syncthreads();
@@ -904,11 +965,11 @@ extern "C" int ftmi_attention_kv(const float *q, int64_t row_stride, int32_t B, 
   const hipStream_t s = ftmi_hs(stream);
   if (attn_transposed() && (out_stride & 3) == 0 && ftmi_aligned16(out)) {
     if (head_dim == 64)
-      hipLaunchKernelGGL(attention_t3_kernel<64>, g1, b1, 0, s, q, row_stride, B, T, H, 0,
-                         key_padding_mask, qscale, out, out_stride, status, kv, Tp);
+      hipLaunchKernelGGL((attention_t3_kernel<64, true>), g1, b1, 0, s, q, row_stride, B, T, H,
+                         0, 0, 0, key_padding_mask, qscale, out, out_stride, status, kv, Tp);
     else
-      hipLaunchKernelGGL(attention_t3_kernel<128>, g1, b1, 0, s, q, row_stride, B, T, H, 0,
-                         key_padding_mask, qscale, out, out_stride, status, kv, Tp);
+      hipLaunchKernelGGL((attention_t3_kernel<128, true>), g1, b1, 0, s, q, row_stride, B, T, H,
+                         0, 0, 0, key_padding_mask, qscale, out, out_stride, status, kv, Tp);
   } else if (head_dim == 64)
     hipLaunchKernelGGL((attention_h3_kernel<64, true>), g1, b1, 0, s, q, row_stride, B, T, H, 0,
                        0, 0, key_padding_mask, qscale, out, out_stride, status, kv, Tp);
@@ -943,13 +1004,17 @@ extern "C" int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, i
     hipLaunchKernelGGL(attn_split_kv_kernel<HD_>, dim3((unsigned)(Tp / 64), (unsigned)(B * H)),  \
                        dim3(256), 0, s, qkv, row_stride, B, T, H, k_off, v_off, Tp, kv, status); \
     if (attn_transposed() && (out_stride & 3) == 0 && ftmi_aligned16(out))                      \
-      hipLaunchKernelGGL(attention_t3_kernel<HD_>, g1, b1, 0, s, qkv, row_stride, B, T, H, q_off, \
-                         key_padding_mask, qscale, out, out_stride, status, (const _Float16 *)kv, \
-                         Tp);                                                                     \
+      hipLaunchKernelGGL((attention_t3_kernel<HD_, true>), g1, b1, 0, s, qkv, row_stride, B, T,  \
+                         H, q_off, 0, 0, key_padding_mask, qscale, out, out_stride, status,       \
+                         (const _Float16 *)kv, Tp);                                               \
     else                                                                                          \
       hipLaunchKernelGGL((attention_h3_kernel<HD_, true>), g1, b1, 0, s, qkv, row_stride, B, T,  \
                          H, q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride,       \
                          status, (const _Float16 *)kv, Tp);                                       \
+  } else if (attn_transposed() && (out_stride & 3) == 0 && ftmi_aligned16(out)) {                 \
+    hipLaunchKernelGGL((attention_t3_kernel<HD_, false>), g1, b1, 0, s, qkv, row_stride, B, T,  \
+                       H, q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride, status,\
+                       (const _Float16 *)nullptr, 0);                                            \
   } else {                                                                                       \
     hipLaunchKernelGGL((attention_h3_kernel<HD_, false>), g1, b1, 0, s, qkv, row_stride, B, T,  \
                        H, q_off, k_off, v_off, key_padding_mask, qscale, out, out_stride,       \

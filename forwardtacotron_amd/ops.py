@@ -829,7 +829,7 @@ def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Te
               mma: Optional[int] = None, presplit: Optional[bool] = None) -> torch.Tensor:
     """Self-attention core of nn.MultiheadAttention on packed in_proj rows (B, T, 3d).
     mma: 2 = f16x3 contractions (default, MMA), 0 = fp32 MFMA (exact_paths(), MMA 0/1).
-    presplit (f16x3; default: ATTN_PRESPLIT and T > 256): K and V split once into f16
+    presplit (f16x3; default: ATTN_PRESPLIT and T > 512): K and V split once into f16
     planes in a workspace instead of per query tile (identical results; measured at c5's
     postnet T = 1400: 825 -> 618 us incl. the split pass, slower at T = 200)."""
     _dev(qkv, key_padding_mask)
@@ -844,9 +844,10 @@ def attention(qkv: torch.Tensor, heads: int, key_padding_mask: Optional[torch.Te
         kpm = key_padding_mask.to(torch.uint8).contiguous()
     qscale = float(np.float32(np.sqrt(1.0 / hd)))
     ws, nws = None, 0
-    if presplit is None:  # with the transposed kernel from T > 256 (tools/attn_short_ab.py,
-        # B = 64: T 200 0.81-0.86x, T 300 1.05-1.08x, T 400 1.05-1.13x against the in-kernel split)
-        presplit = ATTN_PRESPLIT and T > 256
+    if presplit is None:  # the transposed kernel with the split pass against its in-kernel
+        # split (tools/attn_short_ab.py, B = 64, masked): T 300-400 0.91-0.95x, T 600 1.01x,
+        # T 1000 1.01-1.06x, T 1400 1.02-1.08x
+        presplit = ATTN_PRESPLIT and T > 512
     if m == 2 and presplit:
         nws = int(_lib.load().ftmi_attention_workspace_bytes(B, T, heads, hd))
         ws = torch.empty(nws, device=qkv.device, dtype=torch.uint8)

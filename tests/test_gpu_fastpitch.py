@@ -51,9 +51,9 @@ def test_layernorm(C):
 @pytest.mark.parametrize('hd,T,masked', [(64, 37, False), (128, 200, True), (128, 33, False),
                                          (64, 129, True), (128, 1, False), (128, 1400, False)])
 def test_attention(hd, T, masked, mma, presplit, monkeypatch):
-    """presplit: the transposed kernel (attention_t3_kernel, default) against the oracle, and
-    attention_h3_kernel on the pre-split planes (FTMI_ATTN_T=0) bit-identical to its in-kernel
-    split form; the two kernels agree within 2e-6 (P V sums in a permuted key order)."""
+    """f16x3: the transposed kernel (attention_t3_kernel, default) against the oracle, its
+    pre-split and in-kernel-split forms bit-identical, likewise attention_h3_kernel's
+    (FTMI_ATTN_T=0); the two kernels agree within 2e-6 (P V sums in a permuted key order)."""
     from forwardtacotron_amd import ops
     rng = np.random.RandomState(T + hd)
     B, H = 3, 2
@@ -76,13 +76,14 @@ def test_attention(hd, T, masked, mma, presplit, monkeypatch):
                              presplit=presplit))
     np.testing.assert_allclose(got, ref, atol=2e-5, rtol=2e-5)
     assert int(st.item()) == 0
-    if presplit:  # the same arithmetic as the in-kernel split: identical results
-        other = host(ops.attention(dev(qkv), H, dev(kpm) if kpm is not None else None, mma=mma,
-                                   presplit=False))
+    if presplit:  # the split pass has the in-kernel split's arithmetic: identical results
+        mk = dev(kpm) if kpm is not None else None
+        other = host(ops.attention(dev(qkv), H, mk, mma=mma, presplit=False))
+        np.testing.assert_array_equal(got, other)
         monkeypatch.setenv('FTMI_ATTN_T', '0')
-        h3 = host(ops.attention(dev(qkv), H, dev(kpm) if kpm is not None else None, mma=mma,
-                                presplit=True))
-        np.testing.assert_array_equal(h3, other)
+        h3 = host(ops.attention(dev(qkv), H, mk, mma=mma, presplit=True))
+        h3u = host(ops.attention(dev(qkv), H, mk, mma=mma, presplit=False))
+        np.testing.assert_array_equal(h3, h3u)
         np.testing.assert_allclose(got, h3, atol=2e-6, rtol=2e-6)
 
 

@@ -1,7 +1,7 @@
-"""Short-sequence attention (the phoneme side, T = 200, B = 64): the in-kernel split
-(attention_h3_kernel, PRE off) against the split pass + the transposed kernel (presplit),
+"""Short-sequence attention (the phoneme side, T = 200, B = 64): attention_h3_kernel and the
+transposed kernel (FTMI_ATTN_T), each with the in-kernel split and with the split pass,
 for hd 64 (2 heads of 64 at d = 128) and hd 128 (2 heads at d = 256); HIP events, 20 calls,
-interleaved rounds, min.  usage: python tools/attn_short_ab.py"""
+interleaved rounds, min.  usage: python tools/attn_short_ab.py [T ...]"""
 import os
 import sys
 
@@ -25,15 +25,18 @@ def timed(fn, reps=20):
 
 
 torch.manual_seed(0)
-for T in (200, 300, 400):
+for T in ([int(a) for a in sys.argv[1:]] or (200, 300, 400)):
     for d in (128, 256):
         qkv = torch.randn(64, T, 3 * d, device='cuda')
         lens = torch.randint(T // 2, T + 1, (64,), device='cuda')
         mask = torch.arange(T, device='cuda')[None, :] >= lens[:, None]
         res = {}
         for _ in range(3):
-            for pre in (False, True):
-                res.setdefault(pre, []).append(timed(lambda: ops.attention(qkv, 2, mask, mma=2, presplit=pre)))
-        t0, t1 = min(res[False]), min(res[True])
-        print(f'T={T} hd={d // 2}: in-kernel split {t0:6.1f} us  split pass + t3 {t1:6.1f} us  {t0 / t1:.3f}x',
-              flush=True)
+            for at in ('0', '1'):
+                os.environ['FTMI_ATTN_T'] = at
+                for pre in (False, True):
+                    res.setdefault((at, pre), []).append(
+                        timed(lambda: ops.attention(qkv, 2, mask, mma=2, presplit=pre)))
+        print(f'T={T} hd={d // 2}: ' + '  '.join(
+            f'{"t3" if at == "1" else "h3"}{"+split" if pre else ""} {min(v):6.1f}'
+            for (at, pre), v in res.items()) + ' us', flush=True)
