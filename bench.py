@@ -83,6 +83,7 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r3_pmc_traffic.json')        # c3
 PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r3c2_pmc_traffic.json')   # c2 (--config c2)
+PMC_PROFILE_C5 = os.path.join(ROOT, 'profiles', 'r3c5_pmc_traffic.json')   # c5 (--model fast_pitch)
 
 
 def rocprof_name(label: str):
@@ -119,6 +120,27 @@ def pmc_traffic(label: str, path: str = PMC_PROFILE):
             'read_bytes_corrected': hit[0]['read_bytes_corrected'],
             'write_bytes': hit[0]['write_bytes'],
             'source': os.path.relpath(path, ROOT)}
+
+
+def pmc_traffic_slab(label: str, path: str):
+    """The same for a conv1d label run by the slab kernels (one kernel name for many shapes:
+    the dispatch is told apart by its grid, gemm.hip launch_slab: whole XCD rounds of
+    256-row tiles x 128-column tiles, 768 threads warp-specialised or 512), or None."""
+    if not label.startswith('conv1d[') or not os.path.exists(path):
+        return None
+    f = dict(kv.split('=') for kv in label[7:-1].split(',') if '=' in kv)
+    M, N = int(f['M']), int(f['N'])
+    mt = -(-M // 256)
+    nblk = (mt if mt < 8 else -(-mt // 8) * 8) * -(-N // 128)
+    ks = json.load(open(path)).get('kernels_by_grid', {})
+    hit = [(k, v) for k, v in ks.items() if k.startswith('conv_gemm_slab')
+           and int(k.rsplit('|', 1)[1]) in (nblk * 768, nblk * 512)]
+    if len(hit) != 1:
+        return None
+    k, v = hit[0]
+    return {'bytes_per_launch': v['hbm_bytes_per_launch'],
+            'read_bytes_corrected': v['read_bytes_corrected'], 'write_bytes': v['write_bytes'],
+            'kernel_grid': k, 'source': os.path.relpath(path, ROOT)}
 
 
 def time_prenet_bank(model, x, reps: int = 20) -> float:
@@ -385,6 +407,8 @@ def main():
                     'traffic': None}
             tr = (pmc_traffic(dom_label, pmc_path)
                   if pmc_path and args.model == 'forward_tacotron' and world == 1 else None)
+            if tr is None and args.model == 'fast_pitch' and world == 1 and shape == (64, 50, 200):
+                tr = pmc_traffic_slab(dom_label, PMC_PROFILE_C5)
             if tr is not None:
                 roof['traffic'] = tr['bytes_per_launch']
                 roof['traffic_detail'] = tr

@@ -23,16 +23,20 @@ def short(n):
     return n.split('(')[0]
 
 
-def pmc(src, counter):
-    acc, cnt = defaultdict(float), defaultdict(int)
+def pmc(src, counter, by_grid=False):
+    """average counter value per dispatch, keyed by kernel name (by_grid: 'name|grid size',
+    which tells apart the shapes one kernel runs)"""
+    acc, disp = defaultdict(float), defaultdict(set)
     for f in glob.glob(f'{src}/**/*counter_collection.csv', recursive=True):
         for r in csv.DictReader(open(f)):
             if r['Counter_Name'] != counter:
                 continue
             k = short(r['Kernel_Name'])
+            if by_grid:
+                k = f'{k}|{r["Grid_Size"]}'
             acc[k] += float(r['Counter_Value'])
-            cnt[k] += 1
-    return {k: acc[k] / cnt[k] for k in acc}
+            disp[k].add((f, r['Dispatch_Id']))
+    return {k: acc[k] / len(disp[k]) for k in acc}
 
 
 def main():
@@ -53,18 +57,22 @@ def main():
             print('stats ->', f'profiles/{a.tag}_kernel_stats.csv')
     if not (fetch_dir and write_dir and os.path.isdir(fetch_dir) and os.path.isdir(write_dir)):
         return
-    fetch, write = pmc(fetch_dir, 'FETCH_SIZE'), pmc(write_dir, 'WRITE_SIZE')
-    out = {}
-    for k in sorted(set(fetch) | set(write)):
-        f = fetch.get(k)
-        w = write.get(k)
-        out[k] = {'fetch_size_kb_raw': f, 'read_bytes_corrected': None if f is None else f * 1024 * 2,
-                  'write_bytes': None if w is None else w * 1024,
-                  'hbm_bytes_per_launch': (f * 1024 * 2 if f else 0) + (w * 1024 if w else 0)}
+    def table(fetch, write):
+        out = {}
+        for k in sorted(set(fetch) | set(write)):
+            f = fetch.get(k)
+            w = write.get(k)
+            out[k] = {'fetch_size_kb_raw': f, 'read_bytes_corrected': None if f is None else f * 1024 * 2,
+                      'write_bytes': None if w is None else w * 1024,
+                      'hbm_bytes_per_launch': (f * 1024 * 2 if f else 0) + (w * 1024 if w else 0)}
+        return out
+    out = table(pmc(fetch_dir, 'FETCH_SIZE'), pmc(write_dir, 'WRITE_SIZE'))
+    out_grid = table(pmc(fetch_dir, 'FETCH_SIZE', True), pmc(write_dir, 'WRITE_SIZE', True))
     json.dump({'source': [fetch_dir, write_dir],
                'units': 'FETCH_SIZE / WRITE_SIZE are KB (rocprofv3 derived); read bytes = '
                         'FETCH_SIZE x 1024 x 2 (gfx950: 128-B requests tallied at 64 B)',
-               'kernels': out}, open(os.path.join(DST, f'{a.tag}_pmc_traffic.json'), 'w'), indent=1)
+               'kernels': out, 'kernels_by_grid': out_grid},
+              open(os.path.join(DST, f'{a.tag}_pmc_traffic.json'), 'w'), indent=1)
     print(f'{len(out)} kernels -> profiles/{a.tag}_pmc_traffic.json')
     for k, v in sorted(out.items(), key=lambda kv: -kv[1]['hbm_bytes_per_launch'])[:15]:
         print(f'{v["hbm_bytes_per_launch"] / 1e6:10.1f} MB  {k[:110]}')
