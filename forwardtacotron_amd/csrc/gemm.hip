@@ -2377,6 +2377,285 @@ __global__ __launch_bounds__(512, 1) void conv_bank_qb_kernel(const GemmParams p
   if (bad && p.status) atomicOr(p.status, 1u);
 }
 
+// ---- the c2 conv bank in one launch: channel halves + pairwise last-arriver finish ------
+// (FTMI_BANK_HALVES; common_layers.py:67-71,92-97 at B = 1, T = 120, K = 16, Cin = 256)
+// What bounds this bank is how fast each CU pulls its share of the 35.65 MB of weight
+// planes, and the fixed costs around that stream (tools/probe_stream.hip, warm: the bank's
+// access pattern with every load of a wave issued up front 6.3 us per launch, with a 4-step
+// ring 10.0 us, an empty launch 3.1 us).  So:
+//  * a block = (group pair (k, K + 1 - k), one 16-column set of each group, one HALF of the
+//    input channels): 8 x 16 x 2 = 256 blocks, one per CU, each streaming (K + 1) taps x
+//    Cin / 2 channels x 16 columns x 2 planes = 139 KB; the two halves of a unit are blocks
+//    b and b + 8 (one XCD under round-robin dispatch: placement only ever affects speed);
+//  * every wave issues ALL its weight loads at once, right after its slab loads: the whole
+//    139 KB of a CU is in flight from the start and the MFMAs consume the steps as they land
+//    (in-order vmcnt), instead of a ring refilled one step at a time;
+//  * the slab holds only the block's channel half (Cin / 2 x (RM + K - 1) rows, f16 head /
+//    scaled tail, the skinny kernel's layout and tap masks);
+//  * the 8 waves split the unit's 4 (K + 1) (group, tap, chunk) steps round-robin and meet
+//    in LDS in wave order; the two halves meet through memory: both write their sums
+//    write-through (16-B sc1 stores, fragment order), wait for them, and bump the unit's
+//    counter (agent-scope atomic, after a barrier behind every storing wave's vmcnt(0));
+//    the block whose add returns 1 resets the counter, reads its partner's sums (16-B sc1
+//    loads), adds them to its own (a + b == b + a: deterministic whichever half arrives
+//    last) and applies colscale, ReLU and the BN affine (MI355X_MICROARCH.md "Valid forms",
+//    the first row of the sc1 table).  No split partials for a finish launch, no second
+//    launch.
+constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
+
+#ifdef FTMI_SKINNY_STAMPS
+// diagnostic build only: per-block s_memtime at phase boundaries (tid 0 = wave 0, tid 448 =
+// wave 7): [0] start, [1] slab staged, [2] wave 0's loop done, [3] wave 7's loop done,
+// [4] the waves' sums reduced, [5] published + counted, [6] end (wave 0), [7] end (wave 7)
+#define BHSTAMP(i, t)                                                                       \
+  do {                                                                                      \
+    if (threadIdx.x == (t)) {                                                               \
+      __builtin_amdgcn_sched_barrier(0);                                                    \
+      ftmi_skinny_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime();              \
+      __builtin_amdgcn_sched_barrier(0);                                                    \
+    }                                                                                       \
+  } while (0)
+#else
+#define BHSTAMP(i, t) \
+  do {                \
+  } while (0)
+#endif
+
+// DIAG (timing experiments only, FTMI_BANK_HALVES_DIAG; results invalid): bit 0 = no MFMAs
+// (the loaded weights feed one VALU add), bit 1 = no A-fragment LDS reads (fixed fragments),
+// bit 2 = no partner exchange (each block stores its own half's sums as the output)
+template <int MI, int DIAG = 0>  // row fragments: RM = 16 MI rows (one row tile, M <= RM)
+__global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmParams p) {
+  BHSTAMP(0, 0);
+  constexpr int RM = MI * 16;
+  constexpr int SRM = RM + SL_MAXK - 1;
+  constexpr int AIMG = (SRM + 1) * SL_P;  // halves per (chunk, plane) image; row SRM is zero
+  constexpr int SLAB_BYTES = BH_MAXCH * 2 * AIMG * 2;
+  constexpr int NIT = 2 * MI * 64;  // f32x4 items of a block's sums: [group of pair][mi][lane]
+  constexpr int RED_BYTES = 8 * NIT * 16;
+  constexpr int LDS_BYTES = SLAB_BYTES > RED_BYTES ? SLAB_BYTES : RED_BYTES;
+  constexpr int NS = (4 * (SL_MAXK + 1) + 7) / 8;  // steps per wave (at most)
+  static_assert(NIT % 512 == 0, "items per thread");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  _Float16 *const lds = (_Float16 *)smem;
+  f32x4 *const red = (f32x4 *)smem;  // aliases the slab after the loop
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const int NC = p.g[0].N / 16;
+  const int b = blockIdx.x, h = (b >> 3) & 1, u = (b & 7) | ((b >> 4) << 3);
+  const int gi = u / NC, cset = u - gi * NC, gl = p.ngroups - 1 - gi;
+  const GemmGroup &GH = p.g[gi];  // the pair's heavy group (k = K - gi): its slab
+  const GemmGroup &GL = p.g[gl];
+  const int kh = GH.k, padh = GH.pad, kl = GL.k, dpl = padh - GL.pad;
+  const int Cin = p.Cin, nch = Cin >> 6, c_half = h * (Cin >> 1);  // chunks of this half
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fs = lane >> 4;
+  const int col = cset * 16 + fr;  // < N (N % 16 == 0: host check)
+
+  // ---- the slab loads first (their wait then leaves the weight loads in flight) ----------
+  constexpr int ASLOTS = (BH_MAXCH * SRM * 8 + 511) / 512;
+  const int SR = RM + kh - 1, nitems = nch * SR * 8;
+  f32x4 av[ASLOTS];
+#pragma unroll
+  for (int i = 0; i < ASLOTS; ++i) {
+    const int idx = tid + 512 * i;
+    av[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
+    if (idx < nitems) {
+      int m = 0 - padh + sr;  // one row tile: m0 = 0
+      m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
+      av[i] = *(const f32x4 *)(p.x + (int64_t)m * p.x_stride + c_half + c * 32 + seg * 4);
+    }
+  }
+  // ---- then every weight fragment of this wave's steps q = wave + 8 i (clamped: a step past
+  // the end reloads the last one and multiplies zeros) ----
+  const int QH = nch * kh, Q = QH + nch * kl;
+  const _Float16 *wh = (const _Float16 *)GH.w3 + (int64_t)col * GH.Kpad + c_half + fs * 8;
+  const _Float16 *wl = (const _Float16 *)GL.w3 + (int64_t)col * GL.Kpad + c_half + fs * 8;
+  const int64_t planeh = (int64_t)GH.N * GH.Kpad, planel = (int64_t)GL.N * GL.Kpad;
+  f16x8 rb0[NS], rb1[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const int q = min(wave + 8 * i, Q - 1);
+    const bool hv = q < QH;
+    const int qq = hv ? q : q - QH, j = qq / nch, c = qq - j * nch;
+    const _Float16 *src = (hv ? wh : wl) + j * Cin + c * 32;
+    rb0[i] = *(const f16x8 *)src;
+    rb1[i] = *(const f16x8 *)(src + (hv ? planeh : planel));
+  }
+  // the epilogue's per-column parameters (their latency hides in the loop)
+  const float cs_h = GH.colscale[col], cs_l = GL.colscale[col];
+  const float sc_h = GH.scale ? GH.scale[col] : 1.f, sh_h = GH.scale ? GH.shift[col] : 0.f;
+  const float sc_l = GL.scale ? GL.scale[col] : 1.f, sh_l = GL.scale ? GL.shift[col] : 0.f;
+  const float bi_h = GH.bias ? GH.bias[col] : 0.f, bi_l = GL.bias ? GL.bias[col] : 0.f;
+
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < ASLOTS; ++i) {
+    const int idx = tid + 512 * i;
+    if (idx >= nitems) break;
+    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
+    const f32x4 x = av[i];
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+    f16x4 hh, tt;
+    split2h(x, hh, tt);
+    _Float16 *dst = lds + c * 2 * AIMG + sr * SL_P + seg * 4;
+    *(f16x4 *)dst = hh;
+    *(f16x4 *)(dst + AIMG) = tt;
+  }
+  if (tid < nch * 2 * (SL_P / 8)) {  // the zero row of every (chunk, plane) image
+    const int img = tid / (SL_P / 8), part = tid % (SL_P / 8);
+    *(u32x4 *)(lds + img * AIMG + SRM * SL_P + part * 8) = (u32x4){0u, 0u, 0u, 0u};
+  }
+  bool bad = !(amax <= 65504.f);
+  // per-row tap masks of both groups (heavy in bits 0-15, light in 16-31): bit j set iff
+  // frame t + j - pad lies in the sequence
+  unsigned msk[MI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi) {
+    const int m = mi * 16 + fr;
+    unsigned a = 0, c = 0;
+    if (m < p.M) {
+      const int t = m % p.T;
+      int lo = max(padh - t, 0), hi = min(p.T - 1 + padh - t, kh - 1);
+      if (lo <= hi) a = (2u << hi) - (1u << lo);
+      lo = max(GL.pad - t, 0), hi = min(p.T - 1 + GL.pad - t, kl - 1);
+      if (lo <= hi) c = (2u << hi) - (1u << lo);
+    }
+    msk[mi] = a | (c << 16);
+  }
+  // LDS stores done, then the barrier: the weight loads stay in flight across it (no vmcnt
+  // wait here — __syncthreads could drain them)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  BHSTAMP(1, 0);
+
+  f32x4 acch[MI], accl[MI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi) acch[mi] = accl[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // a step's row fragments in blocks of 4: each accumulator still adds at . bh, ah . b1,
+  // ah . b0 in that order (the skinny kernel's per-accumulator order), with half the A
+  // fragments live at once
+  constexpr int MB = MI < 4 ? MI : 4;
+  auto step = [&](f32x4 (&acc)[MI], const _Float16 *Ab, int sh_j, int dr, f16x8 b0, f16x8 b1) {
+    const f16x8 bh = b0 * (_Float16)(1.0f / H3_SCALE);
+#pragma unroll
+    for (int m0 = 0; m0 < MI; m0 += MB) {
+      f16x8 ah[MB], at[MB];
+#pragma unroll
+      for (int mm = 0; mm < MB; ++mm) {
+        const int mi = m0 + mm;
+        const bool ok = ((msk[mi] >> sh_j) & 1u) != 0;
+        const int o = (ok ? mi * 16 + fr + dr : SRM) * SL_P + fs * 8;
+        if constexpr (DIAG & 2) {
+          ah[mm] = b1;
+          at[mm] = bh;
+        } else {
+          ah[mm] = *(const f16x8 *)(Ab + o);
+          at[mm] = *(const f16x8 *)(Ab + AIMG + o);
+        }
+      }
+      if constexpr (DIAG & 1) {
+        acc[m0][0] += (float)bh[0] + (float)b1[0] + (float)ah[0][0] + (float)at[MB - 1][0];
+        continue;
+      }
+#pragma unroll
+      for (int mm = 0; mm < MB; ++mm) acc[m0 + mm] = mma16(at[mm], bh, acc[m0 + mm]);  // small terms first
+#pragma unroll
+      for (int mm = 0; mm < MB; ++mm) acc[m0 + mm] = mma16(ah[mm], b1, acc[m0 + mm]);
+#pragma unroll
+      for (int mm = 0; mm < MB; ++mm) acc[m0 + mm] = mma16(ah[mm], b0, acc[m0 + mm]);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const int q = wave + 8 * i;
+    if (q >= Q) break;  // wave-uniform
+    const bool hv = q < QH;
+    const int qq = hv ? q : q - QH, j = qq / nch, c = qq - j * nch;
+    const _Float16 *Ab = lds + c * 2 * AIMG;
+    if (hv)
+      step(acch, Ab, j, j, rb0[i], rb1[i]);
+    else
+      step(accl, Ab, j + 16, j + dpl, rb0[i], rb1[i]);
+  }
+  BHSTAMP(2, 0);
+  BHSTAMP(3, 448);
+
+  // ---- the 8 waves' sums meet in LDS, in wave order (the slab is dead after the barrier) --
+  __syncthreads();
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi) {
+    red[(wave * 2 + 0) * MI * 64 + mi * 64 + lane] = acch[mi];
+    red[(wave * 2 + 1) * MI * 64 + mi * 64 + lane] = accl[mi];
+  }
+  __syncthreads();
+  // thread t owns items e = t + 512 r: (group of the pair ug, fragment mi, lane ln)
+  constexpr int IPT = NIT >= 512 ? NIT / 512 : 1;
+  f32x4 v[IPT];
+  int eo[IPT];
+#pragma unroll
+  for (int r = 0; r < IPT; ++r) {
+    const int e = min(tid + 512 * r, NIT - 1);
+    eo[r] = e;
+    f32x4 s = red[e];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) s += red[w * NIT + e];
+    v[r] = s;
+  }
+  BHSTAMP(4, 0);
+  // ---- write-through publish of this half's sums, then the unit's arrival counter -------
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.part, (short)0, 0x7FFFFFF0, 0x00020000);
+  const int ubase = (u * 2) * NIT * 16;  // bytes: [unit][half][item]; < 2^31 (host check)
+#pragma unroll
+  for (int r = 0; r < IPT; ++r)
+    if (tid + 512 * r < NIT)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[r]), rs,
+                                             ubase + (h * NIT + eo[r]) * 16, 0, 16 /* sc1 */);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores done
+  __syncthreads();
+  __shared__ int s_last;
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(p.tile_cnt + u, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == 1u;
+    if (old == 1u)  // both halves have added: zero for the next launch
+      __hip_atomic_store(p.tile_cnt + u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  BHSTAMP(5, 0);
+  if (DIAG & 4) s_last = h == 0;  // (barrier-free: every thread reads the same value below)
+  if (s_last) {
+    u32x4 pr[IPT];
+#pragma unroll
+    for (int r = 0; r < IPT; ++r)
+      pr[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, ubase + ((1 - h) * NIT + eo[r]) * 16, 0,
+                                                    16 /* sc1 */);
+#pragma unroll
+    for (int r = 0; r < IPT; ++r) {
+      if (tid + 512 * r >= NIT) continue;
+      const int e = eo[r], ug = e / (MI * 64), mi = (e >> 6) % MI;
+      const f32x4 s = (DIAG & 4) ? v[r] : v[r] + __builtin_bit_cast(f32x4, pr[r]);  // commutative
+      const GemmGroup &GW = ug ? GL : GH;
+      const float cs = ug ? cs_l : cs_h, sc = ug ? sc_l : sc_h, sh = ug ? sh_l : sh_h;
+      const float bi = ug ? bi_l : bi_h;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = mi * 16 + 4 * fs + i;
+        if (row >= p.M) continue;
+        bad |= !__builtin_isfinite(s[i]);
+        float y = s[i] * cs + bi;
+        if (p.relu) y = fmaxf(y, 0.f);
+        if (GW.scale) y = y * sc + sh;
+        p.y[(int64_t)row * p.y_stride + GW.ycol0 + col] = y;
+      }
+    }
+  }
+  if (bad && p.status) atomicOr(p.status, 1u);
+  BHSTAMP(6, 0);
+  BHSTAMP(7, 448);
+}
+
 // sum of the skinny kernel's split partials + the conv epilogue; blockIdx.y is the group
 // (uniform: its parameters stay scalar loads).  L = 4 lanes share an element when there
 // are many splits (L = 1 below 8): lane q adds splits q, q + L, ... in order and xor-
@@ -3355,6 +3634,48 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
   return FTMI_OK;
 }
 
+// conv_bank_halves_kernel (FTMI_BANK_HALVES): one row tile (M <= 128), groups k = K .. 1 of
+// equal 16-column-multiple widths, Cin a multiple of 64 up to 256, plain conv epilogue into
+// y, the counters + sums workspace; units a multiple of 8 (the block -> (unit, half) map)
+static bool bank_halves_ok(const GemmParams &p) {
+  if (p.M <= 0 || p.M > 128 || p.ngroups < 2 || p.ngroups % 2 || p.To != p.T) return false;
+  if (p.Cin % 64 || p.Cin > 2 * BH_MAXCH * 32) return false;
+  if (!p.y || p.yt || p.residual || p.x_split || p.pool_out || p.y_split_c) return false;
+  if (!p.tile_cnt || !p.part || p.g[0].N % 16) return false;
+  const int units = (p.ngroups / 2) * (p.g[0].N / 16);
+  if (units % 8 || units > FTMI_BANK_COUNTERS) return false;
+  for (int i = 0; i < p.ngroups; ++i)
+    if (p.g[i].k != p.ngroups - i || p.g[i].N != p.g[0].N || !p.g[i].w3 || !p.g[i].colscale)
+      return false;
+  return true;
+}
+
+// floats of the FTMI_BANK_HALVES workspace after the counters: [unit][half][2 MI 64 lanes][4]
+static int64_t bank_halves_floats(int M, int K, int N) {
+  const int MI = M <= 64 ? 4 : 8;
+  return (int64_t)(K / 2) * (N / 16) * 2 * (2 * MI * 64) * 4;
+}
+
+static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
+  const int units = (p.ngroups / 2) * (p.g[0].N / 16);
+  const char *dg = getenv("FTMI_BANK_HALVES_DIAG");  // timing experiments (results invalid)
+  const int diag = dg ? atoi(dg) : 0;
+  if (p.M <= 64) {
+    hipLaunchKernelGGL(conv_bank_halves_kernel<4>, dim3(2 * units), dim3(512), 0, s, p);
+  } else switch (diag) {
+#define FTMI_BH_DIAG(D_)                                                                      \
+  case D_:                                                                                    \
+    hipLaunchKernelGGL((conv_bank_halves_kernel<8, D_>), dim3(2 * units), dim3(512), 0, s, p); \
+    break;
+      FTMI_BH_DIAG(1) FTMI_BH_DIAG(2) FTMI_BH_DIAG(3) FTMI_BH_DIAG(4) FTMI_BH_DIAG(7)
+#undef FTMI_BH_DIAG
+      default:
+        hipLaunchKernelGGL(conv_bank_halves_kernel<8>, dim3(2 * units), dim3(512), 0, s, p);
+  }
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
 int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hipStream_t s) {
   if (nblocks <= 0) return FTMI_OK;
   dim3 grid(nblocks), block(256);
@@ -3533,6 +3854,11 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   return launch(p, EPI_CONV, a->maxpool != 0, mtiles * g.ntiles, a->mma, ftmi_hs(stream));
 }
 
+extern "C" int64_t ftmi_conv_bank_halves_ws_floats(int32_t B, int32_t T, int32_t K, int32_t Cout) {
+  if (B <= 0 || T <= 0 || K <= 0 || Cout <= 0 || (int64_t)B * T > 128) return 0;
+  return FTMI_BANK_COUNTERS + bank_halves_floats(B * T, K, Cout);
+}
+
 extern "C" int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T,
                               int32_t Cin, const float *w, const void *w_split, int32_t K,
                               int32_t Cout, const float *bn_scale, const float *bn_shift,
@@ -3577,8 +3903,11 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
   p.y = y;
   p.y_stride = y_stride;
   p.status = status;
-  if (pool_out & ~(FTMI_BANK_POOL | FTMI_BANK_Y_SPLIT | FTMI_BANK_X_SPLIT | FTMI_BANK_LAST))
+  if (pool_out & ~(FTMI_BANK_POOL | FTMI_BANK_Y_SPLIT | FTMI_BANK_X_SPLIT | FTMI_BANK_LAST |
+                   FTMI_BANK_HALVES))
     return FTMI_E_ARG;
+  const bool halves = (pool_out & FTMI_BANK_HALVES) != 0;
+  if (halves && (!split_ws || mma != 2 || (pool_out & ~FTMI_BANK_HALVES))) return FTMI_E_ARG;
   if ((pool_out & FTMI_BANK_LAST) && (split_k <= 1 || !split_ws)) return FTMI_E_ARG;
   p.pool_out = pool_out & FTMI_BANK_POOL;
   if (pool_out & FTMI_BANK_Y_SPLIT) {  // split output rows need the pooled epilogue
@@ -3616,6 +3945,12 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
     g.ntiles = ntiles;
     g.tile0 = tile0;
     tile0 += mtiles * ntiles;
+  }
+  if (halves) {  // one launch: channel halves, the unit's last half finishes it
+    p.tile_cnt = (unsigned *)split_ws;
+    p.part = split_ws + FTMI_BANK_COUNTERS;
+    if (!bank_halves_ok(p)) return FTMI_E_UNSUPPORTED;
+    return launch_bank_halves(p, ftmi_hs(stream));
   }
   if (split_k > 1) {
     p.split_req = split_k;

@@ -1522,7 +1522,7 @@ static bool cst_enabled() {
 // bytes per workgroup and step); FTMI_RNN_NB=16 keeps 16 (read per call)
 static int legacy_nbl(int cell, int B, int H, int mma, bool spread, int maxb) {
   const char *v = getenv("FTMI_RNN_NB");
-  if (!spread || mma != 2 || cell != 0 || (H != 256 && H != 128) || !cst_enabled() ||
+  if (!spread || mma != 2 || cell != 0 || H != 256 || !cst_enabled() ||
       (v && atoi(v) == 16))
     return NB;
   return 2 * ((B + 7) / 8) * (H / 16) <= maxb ? 8 : NB;
@@ -1691,15 +1691,14 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
     return v ? atoi(v) : 4;
   }();
   // f16x3, 16 units per workgroup: the compute waves store their own h (CST) and a spread
-  // GRU runs 8 live sequences per group (legacy_nbl)
-  if (mma == 2 && cst_enabled() && ((cell == 1 && H == 512) || (cell == 0 && (H == 256 || H == 128)))) {
+  // GRU runs 8 live sequences per group (legacy_nbl).  H = 128 keeps the form above (it
+  // returned before this block since round 3; legacy_nbl agrees, so ftmi_rnn_blocks reports
+  // the launch's real workgroup count)
+  if (mma == 2 && cst_enabled() && ((cell == 1 && H == 512) || (cell == 0 && H == 256))) {
     const bool nb8 = legacy_nbl(cell, B, H, mma, spread, maxb) == 8;
     if (cell == 1) return launch_rnn<1, 512, 16, 4, 2, false, true>(p, nchunks, maxb, s);
-    if (H == 256)
-      return nb8 ? launch_rnn<0, 256, 16, 4, 2, false, true, 8>(p, nchunks, maxb, s)
-                 : launch_rnn<0, 256, 16, 4, 2, false, true>(p, nchunks, maxb, s);
-    return nb8 ? launch_rnn<0, 128, 16, 4, 2, false, true, 8>(p, nchunks, maxb, s)
-               : launch_rnn<0, 128, 16, 4, 2, false, true>(p, nchunks, maxb, s);
+    return nb8 ? launch_rnn<0, 256, 16, 4, 2, false, true, 8>(p, nchunks, maxb, s)
+               : launch_rnn<0, 256, 16, 4, 2, false, true>(p, nchunks, maxb, s);
   }
   if (wk_env == 2 && mma == 2 && cell == 1 && H == 512)
     return launch_rnn<1, 512, 16, 2, 2>(p, nchunks, maxb, s);

@@ -124,6 +124,20 @@ __device__ __forceinline__ float dpp_ror(float v) {
   } while (0)
 __device__ __forceinline__ float add2(float a, float b) { return a + b; }
 
+// PRE staging of the last key tile: 8 f16 keys key0 .. key0 + 7 of one plane row with the
+// keys >= T zeroed.  The workspace's pad keys T..Tp-1 are never written by the producers and
+// may hold a non-finite value left by an earlier, overflowing call (it reran on the exact
+// path); a masked key has P = 0, and 0 * inf in the P V MFMA would be NaN.
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4_t zero_keys_past(u32x4_t v, int key0, int T) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = key0 + 2 * i;  // word i = keys k (low half) and k + 1 (high half)
+    v[i] &= k >= T ? 0u : (k + 1 >= T ? 0xFFFFu : 0xFFFFFFFFu);
+  }
+  return v;
+}
+
 template <int HD>
 __global__ __launch_bounds__(256) void attention_kernel(const float *__restrict__ qkv, int64_t rs,
                                                         int B, int T, int H, int q_off, int k_off,
@@ -408,17 +422,20 @@ __global__ __launch_bounds__(64 * AH_W) void attention_h3_kernel(
   };
   auto store_tile = [&](int k0) {
     if constexpr (PRE) {
+      const bool tail = k0 + AH_KT > T;  // the last tile: pad keys are zeroed (uniform)
 #pragma unroll
       for (int i = 0; i < NKC; ++i) {
         const int e = tid + NTH * i, pl = e / (AH_KT * HD / 8), q = e - pl * (AH_KT * HD / 8);
         const int r = q / (HD / 8), c8 = (q - r * (HD / 8)) * 8;
-        *(u32x4 *)&(pl ? Kt : Kh)[r * KP + c8] = kr[i];
+        u32x4 kk = kr[i];
+        if (tail && k0 + r >= T) kk = (u32x4){0u, 0u, 0u, 0u};
+        *(u32x4 *)&(pl ? Kt : Kh)[r * KP + c8] = kk;
       }
 #pragma unroll
       for (int i = 0; i < NVC; ++i) {
         const int e = tid + NTH * i, pl = e / (HD * AH_KT / 8), q = e - pl * (HD * AH_KT / 8);
         const int d = q / (AH_KT / 8), c8 = (q - d * (AH_KT / 8)) * 8;
-        *(u32x4 *)&(pl ? Vt : Vh)[d * VP + c8] = vr[i];
+        *(u32x4 *)&(pl ? Vt : Vh)[d * VP + c8] = tail ? zero_keys_past(vr[i], k0 + c8, T) : vr[i];
       }
     } else {
 #pragma unroll
@@ -717,11 +734,14 @@ __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
       }
       return;
     }
+    const bool tail = k0 + AH_KT > T;  // the last tile: pad keys are zeroed (uniform)
 #pragma unroll
     for (int i = 0; i < NKC; ++i) {
       const int e = tid + NTH * i, pl = e / (AH_KT * HD / 8), q = e - pl * (AH_KT * HD / 8);
       const int r = q / (HD / 8), c8 = (q - r * (HD / 8)) * 8;
-      *(u32x4 *)&(pl ? Kt : Kh)[buf][r * KP + c8] = kr[i];
+      u32x4 kk = kr[i];
+      if (tail && k0 + r >= T) kk = (u32x4){0u, 0u, 0u, 0u};
+      *(u32x4 *)&(pl ? Kt : Kh)[buf][r * KP + c8] = kk;
     }
 #pragma unroll
     for (int i = 0; i < NVC; ++i) {
@@ -729,8 +749,9 @@ __global__ __launch_bounds__(64 * AH_W) void attention_t3_kernel(
       const int d = q / (AH_KT / 8), c8 = (q - d * (AH_KT / 8)) * 8;
       _Float16 *row = &(pl ? Vt : Vh)[buf][d * VP + (c8 & ~31)];
       const int w = c8 & 31;
-      *(u32x2 *)(row + kpos(w)) = (u32x2){vr[i].x, vr[i].y};
-      *(u32x2 *)(row + kpos(w + 4)) = (u32x2){vr[i].z, vr[i].w};
+      const u32x4 vv = tail ? zero_keys_past(vr[i], k0 + c8, T) : vr[i];
+      *(u32x2 *)(row + kpos(w)) = (u32x2){vv.x, vv.y};
+      *(u32x2 *)(row + kpos(w + 4)) = (u32x2){vv.z, vv.w};
     }
   };
   load_tile(0);

@@ -119,10 +119,19 @@ def _looks_raw(line: str) -> bool:
     return any(('A' <= c <= 'Z') or c.isdigit() for c in line)
 
 
+def _maybe_raw(line: str) -> bool:
+    """A line of lowercase ASCII only (no IPA symbol, no stress mark) passes _looks_raw but
+    may be raw English ('hello world' is made of phoneme-set symbols too); espeak's output
+    nearly always carries a stress mark or a non-ASCII vowel, so such a line gets a warning."""
+    return all(ord(c) < 128 for c in line)
+
+
 def read_inputs(args) -> List[List[int]]:
     """Token id lists, one per sentence.  Phonemised input only: the reference cleans raw
-    text first (`gen_forward.py:86,109`), which needs espeak — raw text is refused with that
-    reason, never tokenised as if it were phonemes."""
+    text first (`gen_forward.py:86,109`), which needs espeak.  Lines that are certainly raw
+    text (uppercase letters or digits) are refused with that reason; lowercase ASCII-only
+    lines cannot be told apart from phonemes by their symbols and are tokenised with a
+    warning."""
     from .text.symbols import phonemes
     from .text.tokenizer import Tokenizer
     tok = Tokenizer()
@@ -141,6 +150,9 @@ def read_inputs(args) -> List[List[int]]:
     for i, line in enumerate(lines, 1):
         if _looks_raw(line):
             raise SystemExit(f'{path}:{i} looks like raw text ({line[:40]!r}); it ' + RAW_TEXT_HINT)
+        if _maybe_raw(line):
+            print(f'warning: {path}:{i}: no IPA symbol or stress mark ({line[:40]!r}); if this '
+                  'is raw text it ' + RAW_TEXT_HINT)
         skipped = sorted(set(line) - known)
         if skipped:  # the reference Tokenizer drops them too (utils/text/tokenizer.py)
             print(f'warning: {path}:{i}: symbols outside the phoneme set skipped: {skipped}')

@@ -92,7 +92,8 @@ class RnnTimeout(RuntimeError):
 
 def run_checked(fn, device, reduce=None):
     """fn() with the status-word checks: zero the word, run, read it (one host sync).
-    A recurrence timeout raises RnnTimeout.  A range bit (f16x3 overflow) runs fn() again
+    A recurrence timeout reruns fn() once with the recurrences compact
+    (compact_recurrences()); a second one raises RnnTimeout.  A range bit (f16x3 overflow) runs fn() again
     under exact_paths() — which calls the model's pitch / energy callbacks a second time
     (the first pass's callback outputs derive from the out-of-range predictions and are not
     reused).  reduce(word) -> word combines the status over ranks (sharded generation)
@@ -109,7 +110,15 @@ def run_checked(fn, device, reduce=None):
                              'workgroups co-resident): the result is invalid')
         return res, w
 
-    out, w = attempt()
+    try:
+        out, w = attempt()
+    except RnnTimeout:
+        # a persistent recurrence could not seat every workgroup at once: another kernel
+        # (an RCCL collective, a copy, another process) held CUs past the spin limit.  The
+        # launch is rerun once in the compact form (a spread recurrence otherwise takes all
+        # 256 CUs); a second timeout raises.
+        with compact_recurrences():
+            out, w = attempt()
     if w and not _FORCED:
         # the rerun is checked like the first pass (a timeout there raises too; its range
         # bits cannot recur on the range-unlimited paths); afterwards the word shows the
@@ -118,6 +127,20 @@ def run_checked(fn, device, reduce=None):
             out, _ = attempt()
         st.fill_(w)
     return out
+
+
+_COMPACT = []  # non-empty: recurrences ignore `spread` (run_checked's timeout rerun)
+
+
+@contextlib.contextmanager
+def compact_recurrences():
+    """Run the enclosed recurrences in their compact form (`spread` ignored: 16 live sequences
+    per group, fewer workgroups than CUs where the shape allows)."""
+    _COMPACT.append(True)
+    try:
+        yield
+    finally:
+        _COMPACT.pop()
 
 
 def _num_cus() -> int:
@@ -379,7 +402,11 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
     flops = 2.0 * M * Cout * Cin * K * (K + 1) / 2
     mma, wsp = _gemm_mma(mma, w_split)
     sk, part, last = 0, None, 0
-    if not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
+    if not pool and not x_split and _bank_halves(mma, B, T, Cin, K, Cout):
+        # the few-row bank in one launch (gemm.hip conv_bank_halves_kernel)
+        n = int(_lib.load().ftmi_conv_bank_halves_ws_floats(B, T, K, Cout)) - BANK_COUNTERS
+        sk, part, last = 2, _bank_workspace(n, x.device), BANK_HALVES
+    elif not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
         sk = _skinny_split(Cin)  # weight-streaming kernel: partial sums, finished in order
         if os.environ.get('FTMI_BANK_LAST', '0') != '0':
             # tile counters + partials, finished in-kernel by each tile's last split block
@@ -397,6 +424,17 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
 
 
 BANK_LAST, BANK_COUNTERS = 8, 4096  # include/ftmi.h FTMI_BANK_LAST, FTMI_BANK_COUNTERS
+BANK_HALVES = 16  # include/ftmi.h FTMI_BANK_HALVES
+
+
+def _bank_halves(mma: int, B: int, T: int, Cin: int, K: int, Cout: int) -> bool:
+    """Whether conv_bank takes the one-launch channel-halves kernel (gemm.hip
+    bank_halves_ok): f16x3, one row tile of at most 128 rows (batch-1 generation, BASELINE
+    config c2), Cin a multiple of 64 up to 256, even K, (K / 2)(Cout / 16) a multiple of 8.
+    FTMI_BANK_HALVES=0 (read per call) keeps the channel-split kernel + finish."""
+    return (os.environ.get('FTMI_BANK_HALVES', '1') != '0' and mma == 2 and 0 < B * T <= 128
+            and Cin % 64 == 0 and Cin <= 256 and K % 2 == 0 and Cout % 16 == 0
+            and (K // 2) * (Cout // 16) % 8 == 0 and K <= 16)
 _BANK_WS = {}
 
 
@@ -545,9 +583,10 @@ _KV_WS = {}
 
 def _kv_workspace(nbytes: int, device) -> torch.Tensor:
     """The attention K / V plane workspace of the current stream (ftmi_panel_proj_qkv /
-    ftmi_attention_kv): zeroed once at allocation — the planes' pad keys T..Tp-1 are never
-    written and must stay finite — then reused by every call on the stream (stream order
-    separates the layers' uses); grown when too small."""
+    ftmi_attention_kv), reused by every call on the stream (stream order separates the
+    layers' uses); grown when too small.  The planes' pad keys T..Tp-1 are never written;
+    the attention kernels zero them while staging (a stale value there, even an inf left by
+    an overflowing call that reran on the exact path, never reaches the output)."""
     stream = torch.cuda.current_stream(device)
     key = (torch.device(device), stream.cuda_stream)
     t = _KV_WS.get(key)
@@ -649,7 +688,7 @@ def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Opt
            4.0 * (B * T * 2 * G * H + 2 * G * H * H + B * T * 2 * H),
            cell, B, T, H, xp.data_ptr(), xs, T_src, _ptr(index), _ptr(xp_zero),
            w_hh.data_ptr(), _ptr(b_hh), _ptr(lengths), float(pad_value), y.data_ptr(), y.stride(1),
-           int(mma) | (RNN_SPREAD if spread else 0), status_word(xp.device).data_ptr(),
+           int(mma) | (RNN_SPREAD if spread and not _COMPACT else 0), status_word(xp.device).data_ptr(),
            ws.data_ptr(), _stream())
     if check:
         torch.cuda.current_stream().synchronize()

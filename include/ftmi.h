@@ -63,16 +63,26 @@ enum { FTMI_STATUS_F16_RANGE = 1, FTMI_STATUS_WHH_RANGE = 2, FTMI_STATUS_RNN_TIM
 enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
        FTMI_BANK_Y_SPLIT = 2, /* with FTMI_BANK_POOL: y as f16x3 split rows of K*Cout */
        FTMI_BANK_X_SPLIT = 4, /* x given as f16x3 split rows of Cin (FTMI_MMA_F16X3) */
-       FTMI_BANK_LAST = 8     /* ABI 12, with split_k > 1: split_ws starts with
+       FTMI_BANK_LAST = 8,    /* ABI 12, with split_k > 1: split_ws starts with
                                  FTMI_BANK_COUNTERS 32-bit tile counters, zeroed once by the
                                  caller and left zero by every launch; the partial sums follow.
                                  The weight-streaming bank then finishes in-kernel (each tile's
                                  last split block sums the splits in order) instead of a second
                                  launch.  One workspace per stream: concurrent launches must not
-                                 share the counters. */ };
+                                 share the counters. */
+       FTMI_BANK_HALVES = 16  /* ABI 15 (alone, FTMI_MMA_F16X3): the few-row bank in ONE
+                                 launch — a block per (group pair, 16-column set, half of the
+                                 input channels), each wave's weight stream issued at once, the
+                                 unit's two halves combined in-kernel by the last to arrive
+                                 (deterministic).  B*T <= 128, Cin % 64 == 0, Cin <= 256, K even,
+                                 (K / 2)(Cout / 16) % 8 == 0; else FTMI_E_UNSUPPORTED.  split_ws:
+                                 ftmi_conv_bank_halves_ws_floats(B, T, K, Cout) floats, the first
+                                 FTMI_BANK_COUNTERS zeroed once by the caller (every launch leaves
+                                 them zero); split_k is ignored.  One workspace per stream. */ };
 enum { FTMI_BANK_COUNTERS = 4096 };
 
-/* ABI version; bumped on any signature change (14: ftmi_panel_proj_qkv, ftmi_attention_kv). */
+/* ABI version; bumped on any signature change (14: ftmi_panel_proj_qkv, ftmi_attention_kv;
+ * 15: FTMI_BANK_HALVES, ftmi_conv_bank_halves_ws_floats). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
@@ -187,6 +197,9 @@ int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32
  * only on the f16x3 slab kernel (mma = FTMI_MMA_F16X3, B*T > 256 rows, no split), elsewhere
  * FTMI_E_UNSUPPORTED.  | FTMI_BANK_Y_SPLIT: y as split rows (proj1 then reads them with
  * ftmi_conv_args.x_split = 1).  FTMI_BANK_X_SPLIT: x is given as split rows. */
+/* Floats of the FTMI_BANK_HALVES workspace (counters included) for a bank of B*T <= 128
+ * rows, K groups of Cout columns; 0 for other sizes. */
+int64_t ftmi_conv_bank_halves_ws_floats(int32_t B, int32_t T, int32_t K, int32_t Cout);
 int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t Cin,
                          const float *w, const void *w_split, int32_t K, int32_t Cout,
                          const float *bn_scale, const float *bn_shift, float *y,
@@ -499,8 +512,9 @@ int ftmi_attention(const float *qkv, int64_t row_stride, int32_t B, int32_t T, i
  * rows (q_out, q_stride >= d) and K / V into kv_workspace (>= ftmi_attention_workspace_bytes
  * (B, T, heads, d / heads) bytes) as the f16 head / scaled-tail planes ftmi_attention's split
  * pass would write for the same values (K [B*heads][Tp][hd], V [B*heads][hd][Tp], Tp = T
- * rounded up to 64; keys T..Tp-1 are never written and must hold finite values: zero the
- * workspace once at allocation — later calls only ever store finite values into it).
+ * rounded up to 64; keys T..Tp-1 are never written: the attention kernels zero them while
+ * staging the last key tile, so the workspace may hold anything there — including the
+ * non-finite values an earlier, overflowing call stored).
  * ftmi_attention_kv = ftmi_attention (f16x3) with Q rows q (row_stride) and K / V taken from
  * such a workspace: no split pass.  The pair computes exactly what ftmi_panel_proj +
  * ftmi_attention with a workspace compute (bit-identical); |value| > 65504 sets status bit 0. */

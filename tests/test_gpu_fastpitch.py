@@ -225,8 +225,8 @@ def test_panel_path_matches_unfused(fp_model, monkeypatch):
 def test_kv_fused_in_proj_bit_identical(B, T, H, kpm):
     """ftmi_panel_proj_qkv + ftmi_attention_kv (the attention's K / V split folded into
     in_proj, FTMI_KV_FUSED) against ftmi_panel_proj + ftmi_attention with its split pass:
-    bit-identical Q rows and attention outputs; the pad keys of the stream's reused
-    workspace (zeroed at allocation, then holding earlier calls' planes) stay finite."""
+    bit-identical Q rows and attention outputs, with the stream's workspace reused across
+    the cases (its pad keys hold earlier calls' planes)."""
     from forwardtacotron_amd import ops
     g = torch.Generator().manual_seed(B * T)
     d = 256
@@ -245,8 +245,37 @@ def test_kv_fused_in_proj_bit_identical(B, T, H, kpm):
     torch.cuda.synchronize()
     assert torch.equal(q, qkv[:, :, :d])
     assert torch.equal(got, ref)
-    hd, Tp = d // H, -(-T // 64) * 64
-    planes = kv[:4 * B * H * Tp * hd * 2].view(torch.float16).view(4, B * H, -1)
-    if Tp > T:  # pad keys of K [bh][Tp][hd] and of V^T [bh][hd][Tp] are finite
-        assert torch.isfinite(planes[:2].view(2, B * H, Tp, hd)[:, :, T:]).all()
-        assert torch.isfinite(planes[2:].view(2, B * H, hd, Tp)[:, :, :, T:]).all()
+
+
+def test_kv_workspace_after_overflow_stays_finite():
+    """an overflowing call leaves inf in the reused K / V workspace (its K / V
+    planes are split from out-of-range values; the call reports status bit 0 and reruns on
+    the exact path).  A later call with a shorter T on the same stream must not read those
+    as pad keys: the attention kernels zero keys >= T while staging the last tile."""
+    from forwardtacotron_amd import ops
+    g = torch.Generator().manual_seed(7)
+    d, H = 256, 2
+    w = (torch.randn(3 * d, d, generator=g) / 16).cuda()
+    wf = ops.split_weights_f16(w, frag=True)
+    st = ops.status_word('cuda')
+    for B in (2, 3):  # a different B also shifts the planes' layout
+        x = torch.randn(3, 300, d, generator=g).cuda() * 1e5  # K / V beyond 65504
+        st.zero_()
+        q, kv = ops.panel_proj_qkv(x, wf, d, H)
+        ops.attention_kv(q, kv, H)
+        torch.cuda.synchronize()
+        assert int(st.item()) & 1
+        hd, Tp = d // H, 320
+        planes = kv[:4 * 3 * H * Tp * hd * 2].view(torch.float16)
+        assert not torch.isfinite(planes).all()  # the workspace does hold non-finite values
+        planes.view(4, -1)[:, :].fill_(float('inf'))  # and, worst case, in every pad slot
+        x2 = torch.randn(B, 290, d, generator=g).cuda()
+        st.zero_()
+        q2, kv2 = ops.panel_proj_qkv(x2, wf, d, H)
+        assert kv2.data_ptr() == kv.data_ptr()
+        got = ops.attention_kv(q2, kv2, H)
+        ref = ops.attention(ops.panel_proj(x2, wf, 3 * d), H, mma=2, presplit=True)
+        torch.cuda.synchronize()
+        assert int(st.item()) == 0
+        assert torch.isfinite(got).all()
+        assert torch.equal(got, ref)

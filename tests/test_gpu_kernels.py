@@ -247,6 +247,61 @@ def test_conv_bank_last_arriver_counters(rng, monkeypatch):
     assert not ops._BANK_WS[key][:ops.BANK_COUNTERS].any()  # counters back to zero
 
 
+@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (16, 256, 1, 50), (8, 128, 2, 64)])
+def test_conv_bank_halves(K, Cin, B, T, rng, monkeypatch):
+    """The one-launch channel-halves bank (FTMI_BANK_HALVES, c2's prenet bank): bit-identical
+    across repeated calls whichever half of a unit arrives last (the two halves' sums are
+    added by one fp32 add: commutative), every launch leaves the unit counters zero (a bank
+    of another shape on the same stream's workspace, then this one again: the same bits),
+    within the fp32 bound of the channel-split kernel + finish, and status 0."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    C = 256
+    x = dev(rng.normal(0, 1, (B, T, Cin)).astype(np.float32))
+    ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
+    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
+    w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
+    sc = dev(rng.uniform(0.5, 1.5, K * C).astype(np.float32))
+    sh = dev(rng.normal(0, 0.1, K * C).astype(np.float32))
+    assert ops._bank_halves(2, B, T, Cin, K, C)
+    st = ops.status_word(x.device)
+    st.zero_()
+    a0 = host(ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3))
+    other = dev(rng.normal(0, 1, (1, 100, 64)).astype(np.float32))
+    ws2 = [rng.normal(0, 0.1, (C, 64, k)).astype(np.float32) for k in range(1, 5)]
+    wp2 = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws2]).cuda()
+    w32 = ops.split_bank_weights(wp2, 4, 64, C, 2)
+    for _ in range(4):
+        assert np.array_equal(host(ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3)), a0)
+        ops.conv_bank(other, wp2, 4, C, sc[:4 * C], sh[:4 * C], mma=2, w_split=w32)
+    assert int(st.item()) == 0
+    key = (torch.device('cuda', torch.cuda.current_device()), torch.cuda.current_stream().cuda_stream)
+    assert not ops._BANK_WS[key][:ops.BANK_COUNTERS].any()  # counters back to zero
+    monkeypatch.setenv('FTMI_BANK_HALVES', '0')
+    b0 = host(ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3))
+    close(a0, b0, rtol=1e-5, atol=1e-5)
+
+
+def test_conv_bank_halves_range_guard(rng):
+    """An input beyond the f16 range sets status bit 0 on the halves bank (the model then
+    reruns on the exact path)."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    K, Cin, C = 16, 256, 256
+    xn = rng.normal(0, 1, (1, 120, Cin)).astype(np.float32)
+    xn[0, 7, 200] = 1e5  # in the second channel half
+    ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
+    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
+    w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
+    st = ops.status_word('cuda')
+    st.zero_()
+    ops.conv_bank(dev(xn), wp, K, C, dev(np.ones(K * C, np.float32)),
+                  dev(np.zeros(K * C, np.float32)), mma=2, w_split=w3)
+    torch.cuda.synchronize()
+    assert int(st.item()) & 1
+    st.zero_()
+
+
 def split_rows_host(v):
     """The f16x3 split rows of include/ftmi.h (per row C heads, then C scaled tails)."""
     h = v.astype(np.float16)
@@ -300,19 +355,23 @@ def test_split_rows_bank_to_proj1(K, Cin, B, T, split_k, rng, monkeypatch):
         ops.conv1d(ys, w1, 3, 1, mma=0, x_split=True)
 
 
-@pytest.mark.parametrize('schedule', ['pairs', 'pairs-finish', 'quarters', 'quarters-finish', 'groups'])
+@pytest.mark.parametrize('schedule', ['halves', 'pairs', 'pairs-finish', 'quarters',
+                                      'quarters-finish', 'groups'])
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (8, 80, 1, 100), (4, 64, 2, 50),
                                      (16, 256, 2, 64), (16, 256, 1, 37), (2, 32, 1, 128),
-                                     (16, 256, 1, 129)])
+                                     (16, 256, 1, 129), (8, 128, 1, 128), (16, 192, 3, 40)])
 def test_conv_bank_skinny_schedules(K, Cin, B, T, schedule, rng, monkeypatch):
-    """The weight-streaming bank at batch-1 sizes on every block schedule: group pairs
-    (k, K + 1 - k) per block with one (unit, half) per wave (the default), the same with each
-    wave on a quarter of a heavy and of a light unit (conv_bank_qb_kernel, FTMI_BANK_QB=1),
-    one group per block (FTMI_BANK_BALANCED=0); each with the in-kernel last-arriver finish
+    """The weight-streaming bank at batch-1 sizes on every block schedule: the one-launch
+    channel-halves kernel (conv_bank_halves_kernel, the default where it applies: M <= 128,
+    Cin % 64 == 0; other shapes fall through to the next), group pairs (k, K + 1 - k) per
+    block with one (unit, half) per wave, the same with each wave on a quarter of a heavy
+    and of a light unit (conv_bank_qb_kernel, FTMI_BANK_QB=1), one group per block
+    (FTMI_BANK_BALANCED=0); the split schedules with the in-kernel last-arriver finish
     (FTMI_BANK_LAST=1) or the finish launch; f16x3, against the numpy oracle.  M = 129: two
     row tiles, the second with one row."""
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
+    monkeypatch.setenv('FTMI_BANK_HALVES', '1' if schedule == 'halves' else '0')
     monkeypatch.setenv('FTMI_BANK_BALANCED', '0' if schedule == 'groups' else '1')
     monkeypatch.setenv('FTMI_BANK_QB', '1' if schedule.startswith('quarters') else '0')
     # the tile's last split block finishes in-kernel (FTMI_BANK_LAST, default), or *-finish:

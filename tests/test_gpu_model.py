@@ -351,3 +351,37 @@ def test_recurrence_timeout_raises(gpu_model, monkeypatch):
         lib.ftmi_set_rnn_spin_limit(0)
     torch.cuda.synchronize()
     check(gpu_model.generate(x), g)
+
+
+def test_recurrence_timeout_reruns_compact(gpu_model, monkeypatch):
+    """a spread recurrence takes every CU, so a kernel that holds CUs past the spin
+    limit (an RCCL collective, a copy, another process) times it out.  run_checked reruns the
+    call once with the recurrences compact (ops.compact_recurrences) instead of raising at
+    once; here the first pass times out (spin bound 1) and the rerun, with the default bound,
+    returns the correct result."""
+    from forwardtacotron_amd import _lib, ops
+    from forwardtacotron_amd import forward_tacotron as FT
+    g = load_golden('gen_b3')
+    x = torch.from_numpy(g['x']).cuda()
+    monkeypatch.setattr(FT, 'GRAPH', False)
+    lib = _lib.load()
+    orig = ops.compact_recurrences
+    entered = []
+
+    @contextlib.contextmanager
+    def compact_with_default_bound():
+        torch.cuda.synchronize()
+        lib.ftmi_set_rnn_spin_limit(0)
+        entered.append(True)
+        with orig():
+            yield
+
+    monkeypatch.setattr(ops, 'compact_recurrences', compact_with_default_bound)
+    lib.ftmi_set_rnn_spin_limit(1)
+    try:
+        out = gpu_model.generate(x)
+    finally:
+        torch.cuda.synchronize()
+        lib.ftmi_set_rnn_spin_limit(0)
+    assert entered
+    check(out, g)

@@ -1,7 +1,7 @@
 """c2 prenet bank (B = 1, T = 120, K = 16, Cin = Cout = 256) on the channel-split bank
-schedules: group pairs per block (default) or quarter-balanced waves (FTMI_BANK_QB=1), each
-finished by the finish launch or in-kernel by each tile's last split block
-(FTMI_BANK_LAST=1).  HIP events over back-to-back calls ('warm': the weight planes stay
+schedules: the one-launch channel-halves kernel (default), group pairs per block or
+quarter-balanced waves (FTMI_BANK_QB=1), each finished by the finish launch or in-kernel by
+each tile's last split block (FTMI_BANK_LAST=1).  HIP events over back-to-back calls ('warm': the weight planes stay
 Infinity-Cache resident, as in a generate() loop) and per call behind a 512 MiB overwrite
 ('cold'); max |d| against the first variant.  Run under rocprofv3 --kernel-trace --stats
 for the kernel durations.  usage: python tools/bank_bench.py [T] [reps] [variant ...]"""
@@ -15,10 +15,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from forwardtacotron_amd import ops  # noqa: E402
 from forwardtacotron_amd.common_layers import pack_conv  # noqa: E402
 
-VARIANTS = {'pairs+finish': {'FTMI_BANK_QB': '0', 'FTMI_BANK_LAST': '0'},
-            'pairs+last': {'FTMI_BANK_QB': '0', 'FTMI_BANK_LAST': '1'},
-            'qb+finish': {'FTMI_BANK_QB': '1', 'FTMI_BANK_LAST': '0'},
-            'qb+last': {'FTMI_BANK_QB': '1', 'FTMI_BANK_LAST': '1'}}
+VARIANTS = {'halves': {'FTMI_BANK_HALVES': '1'},
+            'pairs+finish': {'FTMI_BANK_HALVES': '0', 'FTMI_BANK_QB': '0', 'FTMI_BANK_LAST': '0'},
+            'pairs+last': {'FTMI_BANK_HALVES': '0', 'FTMI_BANK_QB': '0', 'FTMI_BANK_LAST': '1'},
+            'qb+finish': {'FTMI_BANK_HALVES': '0', 'FTMI_BANK_QB': '1', 'FTMI_BANK_LAST': '0'},
+            'qb+last': {'FTMI_BANK_HALVES': '0', 'FTMI_BANK_QB': '1', 'FTMI_BANK_LAST': '1'}}
 
 
 def main():
@@ -52,6 +53,19 @@ def main():
         b.record()
         torch.cuda.synchronize()
         warm = a.elapsed_time(b) / reps
+        # the same calls replayed from a HIP graph: device time without the host's
+        # per-call issue cost (ctypes + argument packing)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        graph = a.elapsed_time(b) / reps
         cold = 0.0
         for _ in range(10):
             flush.fill_(1)
@@ -61,7 +75,8 @@ def main():
             torch.cuda.synchronize()
             cold += a.elapsed_time(b) / 10
         print(f'{name:13s} T={T}: warm {warm * 1e3:6.1f} us ({nbytes / warm / 1e6:6.0f} GB/s, '
-              f'{nbytes / warm / 1e6 / 8000:.1%} of HBM) | cold {cold * 1e3:6.1f} us '
+              f'{nbytes / warm / 1e6 / 8000:.1%} of HBM) | graph {graph * 1e3:6.1f} us '
+              f'({nbytes / graph / 1e6 / 8000:.1%}) | cold {cold * 1e3:6.1f} us '
               f'({nbytes / cold / 1e6:6.0f} GB/s) | max|d| vs {names[0]} {d:.2e}', flush=True)
 
 
