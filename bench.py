@@ -239,9 +239,9 @@ def main():
 
     if args.callbacks == 'gen_forward':  # gen_forward.py:103-104 (same objects every call)
         amp = args.amp
-        # pure for the run's fixed amp: graph_safe, as the CLI marks them
-        cb = dict(pitch_function=ft_module.graph_safe(lambda v: v * amp),
-                  energy_function=ft_module.graph_safe(lambda v: v))
+        # plain lambdas, exactly as the reference CLI passes them (not marked graph_safe):
+        # generate() replays its split phoneme graph and runs them eagerly between
+        cb = dict(pitch_function=lambda v: v * amp, energy_function=lambda v: v)
     else:
         cb = {}
     if world > 1:  # c4: one global batch sharded over the ranks (reference-identical result),
@@ -655,10 +655,8 @@ def cpu_baseline(sd, x_np, out, kind='forward_tacotron', cb_kind='identity', amp
     else:
         from oracle import ft_torch_cpu
     cb = {}
-    if cb_kind == 'gen_forward':
-        # pure for the run's fixed amp: graph_safe, as the CLI marks them
-        cb = dict(pitch_function=ft_module.graph_safe(lambda v: v * amp),
-                  energy_function=ft_module.graph_safe(lambda v: v))
+    if cb_kind == 'gen_forward':  # gen_forward.py:103-104, plain lambdas
+        cb = dict(pitch_function=lambda v: v * amp, energy_function=lambda v: v)
     sdt = ft_torch_cpu.to_torch(sd)
     xt = torch.from_numpy(x_np)
     threads_before = torch.get_num_threads()

@@ -317,11 +317,16 @@ class ForwardTacotron(nn.Module):
         host issue rate, not the device, set the phase's length).
         Keyed on (device, x shape, alpha, the callbacks' identity, matrix paths); a key is
         captured the SECOND time it is seen (a one-off shape — gen_forward.py's sentences
-        of different lengths — stays eager: capture costs ~3 eager phases).  The callbacks
-        are captured with the phase, so only the default identity and callbacks marked
-        `graph_safe` (pure device-side torch ops whose effect does not change between calls,
-        as gen_forward.py's `lambda x: x * amp`) get here; generate() runs any other
-        callback eagerly.  FTMI_GRAPH=0 (or forward_tacotron.GRAPH = False) turns capture
+        of different lengths — stays eager: capture costs ~3 eager phases).  The default
+        identity and callbacks marked `graph_safe` (pure device-side torch ops whose effect
+        does not change between calls) are captured with the phase.  Any other callback —
+        gen_forward.py's plain `lambda x: x * amp` — splits it: the graph holds everything
+        but the callbacks and the one launch that reads their outputs (the pitch / energy
+        projections added to the LSTM input projection, series_proj_add); after each replay
+        the callbacks run eagerly on the predictors' outputs (fresh tensors, on the caller's
+        stream), as the reference calls them, and that launch follows.  The split graph is
+        keyed without the callbacks' identity (they are not in it).  FTMI_GRAPH=0 (or
+        forward_tacotron.GRAPH = False) turns capture
         off.  A capture that fails (a callback that syncs or leaves the device) marks the
         key eager for good.
         Static buffers: x is copied in, dur / pitch / energy are cloned out (they go back to
@@ -336,7 +341,12 @@ class ForwardTacotron(nn.Module):
         Returns (phase outputs, entry) or None (run the eager phase)."""
         cache = self.__dict__.setdefault('_ftmi_graphs', {})
         seen = self.__dict__.setdefault('_ftmi_graph_seen', {})
-        key = (x.device, tuple(x.shape), float(alpha), pitch_fn, energy_fn, ops.MMA, ops.RNN_MMA)
+        # split: a callback that is not graph_safe runs eagerly between the captured
+        # predictors and the one launch that consumes its output (series_proj_add)
+        split = not (_graphable(pitch_fn) and _graphable(energy_fn))
+        key = ((x.device, tuple(x.shape), float(alpha), 'split', ops.MMA, ops.RNN_MMA) if split else
+               (x.device, tuple(x.shape), float(alpha), pitch_fn, energy_fn, ops.MMA, ops.RNN_MMA))
+        cap_p, cap_e = (None, None) if split else (pitch_fn, energy_fn)
         ent = cache.pop(key, None)
         fresh = False
         if ent is None:
@@ -351,11 +361,11 @@ class ForwardTacotron(nn.Module):
             wkey = self._weights_key()
             sx = x.clone()
             try:
-                self._phoneme_phase(sx, alpha, pitch_fn, energy_fn, capture=True)  # warm-up
+                self._phoneme_phase(sx, alpha, cap_p, cap_e, capture=True)  # warm-up
                 torch.cuda.synchronize(x.device)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    outs = self._phoneme_phase(sx, alpha, pitch_fn, energy_fn, capture=True)
+                    outs = self._phoneme_phase(sx, alpha, cap_p, cap_e, capture=True)
             except Exception:  # pylint: disable=broad-except
                 torch.cuda.synchronize(x.device)
                 seen[key] = -1
@@ -382,6 +392,11 @@ class ForwardTacotron(nn.Module):
         t_ready = torch.cuda.Event()
         t_ready.record(main)
         dur_hat, pitch_hat, energy_hat = dur_hat.clone(), pitch_hat.clone(), energy_hat.clone()
+        if split:  # the callbacks on the predictors' outputs, then their projections
+            pitch_hat, energy_hat = pitch_fn(pitch_hat), energy_fn(energy_hat)
+            wp, bp, we, be = self._folded_series_weights()
+            ops.series_proj_add(xp, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we,
+                                be, self.energy_strength)
         t_ready.synchronize()
         return (dur_hat, pitch_hat, energy_hat, enc, offsets, int(t_host), xp), ent
 
@@ -400,7 +415,9 @@ class ForwardTacotron(nn.Module):
         plus the pitch / energy projections, folded through W_ih; enc itself does not carry
         them; index: the LR index map, queued on the caller's stream before it joins the side
         streams).  capture=True (graph capture, see _phoneme_graph): no host sync, the T_mel
-        slot holds max(totals) on the device and the offsets slot plain offsets."""
+        slot holds max(totals) on the device and the offsets slot plain offsets.
+        pitch_fn = energy_fn = None (capture only): the predictors' raw outputs are returned
+        and xp does not carry their projections yet (the split graph of _phoneme_graph)."""
         main = torch.cuda.current_stream(x.device)
         s_pitch, s_energy, s_prenet = self._side_streams(x.device, x.size(0))
         for s in (s_pitch, s_energy, s_prenet):
@@ -425,17 +442,22 @@ class ForwardTacotron(nn.Module):
             t_ready = torch.cuda.Event()
             t_ready.record(main)
         with torch.cuda.stream(s_pitch):
-            pitch_hat = pitch_fn(self.pitch_pred.forward_bt(x).unsqueeze(1))
+            pitch_hat = self.pitch_pred.forward_bt(x).unsqueeze(1)
+            if pitch_fn is not None:
+                pitch_hat = pitch_fn(pitch_hat)
         with torch.cuda.stream(s_energy):
-            energy_hat = energy_fn(self.energy_pred.forward_bt(x).unsqueeze(1))
-        with torch.cuda.stream(s_prenet):
-            for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat)):
-                s_prenet.wait_stream(s)
-                if not capture:
-                    t.record_stream(s_prenet)
-            wp, bp, we, be = self._folded_series_weights()
-            ops.series_proj_add(xp, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we,
-                                be, self.energy_strength)
+            energy_hat = self.energy_pred.forward_bt(x).unsqueeze(1)
+            if energy_fn is not None:
+                energy_hat = energy_fn(energy_hat)
+        if pitch_fn is not None and energy_fn is not None:
+            with torch.cuda.stream(s_prenet):
+                for s, t in ((s_pitch, pitch_hat), (s_energy, energy_hat)):
+                    s_prenet.wait_stream(s)
+                    if not capture:
+                        t.record_stream(s_prenet)
+                wp, bp, we, be = self._folded_series_weights()
+                ops.series_proj_add(xp, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we,
+                                    be, self.energy_strength)
         if batch is not None:  # a shard of a larger batch (sharded.GlobalBatch): batch-global
             offsets, totals = batch.duration_counts(dur_hat)  # fill rule / T_mel
             T_mel = batch.t_mel(totals)
@@ -472,9 +494,9 @@ class ForwardTacotron(nn.Module):
         self._check_device(x)
 
         # only callbacks known to be pure are captured (graph_safe): a replay would freeze any
-        # Python-side state an arbitrary callback reads
-        graph = (GRAPH and batch is None and x.numel() <= GRAPH_MAX_TOKENS
-                 and _graphable(pitch_function) and _graphable(energy_function))
+        # Python-side state an arbitrary callback reads; any other callback runs eagerly
+        # between the captured predictors and the launch that consumes its output
+        graph = GRAPH and batch is None and x.numel() <= GRAPH_MAX_TOKENS
 
         def run():
             with torch.no_grad():
@@ -494,13 +516,14 @@ class ForwardTacotron(nn.Module):
         return ops.run_checked(run, x.device, reduce=None if batch is None else batch.status)
 
     def __prepare_scriptable__(self):
-        """`torch.jit.script(model)` (README.md:149-161 exports the reference this way) is not
-        possible here: the compute runs in libftmi.so through ctypes, which TorchScript
-        cannot call.  Fail with the reason instead of a TorchScript frontend error; the
-        scripted entry point's behaviour is available eagerly (`generate_jit`)."""
-        raise RuntimeError(f'{type(self).__name__} runs on libftmi.so (HIP kernels called through '
-                           'ctypes) and cannot be compiled by torch.jit.script; call generate_jit / '
-                           'generate eagerly')
+        """`torch.jit.script(model)` (the reference's export, README.md:149-161): the compute
+        runs in libftmi.so through ctypes, which TorchScript cannot compile, so what gets
+        scripted is `jit.ScriptedForwardTacotron` — the reference's scriptable surface
+        (`forward(batch)`, `generate_jit(x, alpha, beta)`) over dispatcher operators
+        (`torch.ops.ftmi.*`) that run this model's HIP path.  The scripted module (and a
+        torch.jit.save / load of it) runs in this process."""
+        from .jit import ScriptedForwardTacotron
+        return ScriptedForwardTacotron(self)
 
     def generate_jit(self, x: torch.Tensor, alpha: float = 1.0, beta: float = 1.0) -> Dict[str, torch.Tensor]:
         """`models/forward_tacotron.py:270-284` (pitch scaled by beta, no callbacks)."""

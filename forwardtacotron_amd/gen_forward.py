@@ -237,11 +237,10 @@ def main(argv: Optional[Sequence[str]] = None) -> List[Path]:
         voc[0].to(device)
     tts_k = tts_model.get_step() // 1000
     texts = read_inputs(args)
-    # gen_forward.py:103-104; amp is fixed for the run, so the lambdas are pure (graph_safe:
-    # the phoneme phase may replay them from a HIP graph)
-    from .forward_tacotron import graph_safe
-    pitch_function = graph_safe(lambda x: x * args.amp)
-    energy_function = graph_safe(lambda x: x)
+    # gen_forward.py:103-104, the same plain lambdas: generate() replays the phoneme phase
+    # from its split graph and runs them eagerly in between (forward_tacotron._phoneme_graph)
+    pitch_function = lambda x: x * args.amp  # noqa: E731
+    energy_function = lambda x: x  # noqa: E731
     from .host_io import PinnedD2H
     d2h = PinnedD2H(device, depth=1)  # pinned D2H: the drop-in for .cpu() (gen_forward.py:120)
     written = []

@@ -112,10 +112,11 @@ def test_dsp_api_surface():
         d.wav_to_mel(__import__('torch').zeros(4000))
 
 
-@pytest.mark.parametrize('kind', ['forward_tacotron', 'fast_pitch', 'wavernn'])
+@pytest.mark.parametrize('kind', ['fast_pitch', 'wavernn'])
 def test_torchscript_export_fails_with_reason(kind):
-    """README.md:149-161 scripts the reference model; the HIP path cannot be scripted
-    (ctypes calls), and says so instead of a TorchScript frontend error."""
+    """The reference scripts only ForwardTacotron (README.md:149-161, the one
+    @torch.jit.export); FastPitch / WaveRNN on the HIP path cannot be scripted (ctypes
+    calls), and say so instead of a TorchScript frontend error."""
     from forwardtacotron_amd.checkpoints import init_tts_model
     from forwardtacotron_amd.synthetic import default_config
     from forwardtacotron_amd.wavernn import WaveRNN
@@ -124,6 +125,52 @@ def test_torchscript_export_fails_with_reason(kind):
     m = WaveRNN.from_config(cfg) if kind == 'wavernn' else init_tts_model(cfg)
     with pytest.raises(RuntimeError, match='cannot be compiled by torch.jit.script'):
         torch.jit.script(m)
+
+
+def test_torchscript_forward_tacotron(tmp_path):
+    """README.md:149-161 verbatim (from_checkpoint, eval, torch.jit.script, generate_jit on a
+    CPU tensor) scripts ForwardTacotron: the ScriptModule's forward / generate_jit call the
+    ftmi dispatcher operators with the eager model's handle, and a torch.jit.save / load
+    round trip keeps that (in-process).  Without a GPU (this suite) the call reaches the
+    operator's kernel, which refuses with the reason; tests/test_gpu_model.py runs it."""
+    from forwardtacotron_amd.forward_tacotron import ForwardTacotron
+    from forwardtacotron_amd.synthetic import default_config
+    cfg = default_config()
+    path = tmp_path / 'latest_model.pt'
+    torch.save({'model': ForwardTacotron.from_config(cfg).state_dict(), 'config': cfg}, path)
+    # README.md:149-161
+    tts_model = ForwardTacotron.from_checkpoint(path)
+    tts_model.eval()
+    model_script = torch.jit.script(tts_model)
+    x = torch.ones((1, 5)).long()
+    assert isinstance(model_script, torch.jit.ScriptModule)
+    assert model_script.handle == tts_model.__dict__['_ftmi_jit_handle']
+    assert 'ftmi.ft_generate_jit' in model_script.generate_jit.code
+    assert 'ftmi.ft_forward' in model_script.code
+    buf = tmp_path / 'scripted.pt'
+    torch.jit.save(model_script, str(buf))
+    loaded = torch.jit.load(str(buf))
+    assert loaded.handle == model_script.handle
+    assert 'ftmi.ft_generate_jit' in loaded.generate_jit.code
+    if not torch.cuda.is_available():
+        for mod in (model_script, loaded):
+            with pytest.raises(RuntimeError, match='computes on a HIP device'):
+                mod.generate_jit(x)
+
+
+def test_torchscript_handle_registry():
+    """The registry maps a scripted module's handle to its eager model (weakly); an unknown
+    handle fails with the reason."""
+    from forwardtacotron_amd import jit as J
+    from forwardtacotron_amd.forward_tacotron import ForwardTacotron
+    from forwardtacotron_amd.synthetic import default_config
+    m = ForwardTacotron.from_config(default_config())
+    h = J.register(m)
+    assert J.register(m) == h and J._model(h) is m
+    with pytest.raises(RuntimeError, match='no ForwardTacotron with that handle'):
+        J._model(10 ** 9)
+    with pytest.raises(RuntimeError, match='no ForwardTacotron with that handle'):
+        torch.ops.ftmi.ft_generate_jit(10 ** 9, torch.ones(1, 5, dtype=torch.long), 1.0, 1.0)
 
 
 def test_run_checked_checks_the_rerun(monkeypatch):
