@@ -2567,17 +2567,24 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
       for (int mm = 0; mm < MB; ++mm) acc[m0 + mm] = mma16(ah[mm], b0, acc[m0 + mm]);
     }
   };
+  // the heavy group's steps, then the light group's: two code regions, each updating its
+  // own accumulators in place (one loop choosing the set per step made the compiler copy
+  // both sets at every join); the steps' weights were issued in this order
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     const int q = wave + 8 * i;
-    if (q >= Q) break;  // wave-uniform
-    const bool hv = q < QH;
-    const int qq = hv ? q : q - QH, j = qq / nch, c = qq - j * nch;
-    const _Float16 *Ab = lds + c * 2 * AIMG;
-    if (hv)
-      step(acch, Ab, j, j, rb0[i], rb1[i]);
-    else
-      step(accl, Ab, j + 16, j + dpl, rb0[i], rb1[i]);
+    if (q < QH) {  // wave-uniform
+      const int j = q / nch, c = q - j * nch;
+      step(acch, lds + c * 2 * AIMG, j, j, rb0[i], rb1[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const int q = wave + 8 * i;
+    if (q >= QH && q < Q) {  // wave-uniform
+      const int qq = q - QH, j = qq / nch, c = qq - j * nch;
+      step(accl, lds + c * 2 * AIMG, j + 16, j + dpl, rb0[i], rb1[i]);
+    }
   }
   BHSTAMP(2, 0);
   BHSTAMP(3, 448);

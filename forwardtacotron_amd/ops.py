@@ -368,11 +368,11 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
 
 POOL_BANK = os.environ.get('FTMI_POOL_BANK', '1') != '0'
 # the pooled bank hands proj1 its operand as f16x3 split rows (split once, not per column
-# tile of proj1: c3 proj1 -2..3 %, tools/ab_split.sh); FTMI_SPLIT_ROWS=0: fp32 rows
+# tile of proj1: c3 proj1 -2..3 %; a round-3 shell A/B loop, since replaced by tools/ab_bench.py); FTMI_SPLIT_ROWS=0: fp32 rows
 SPLIT_ROWS = os.environ.get('FTMI_SPLIT_ROWS', '1') != '0'
 # FTMI_SPLIT_BANK_IN=1: the bank also takes its own input split once (split_rows) instead of
 # per group / column tile — measured neutral at c3 (the bank kernel saved what the extra
-# split launch cost: tools/ab_split.sh), so off by default
+# split launch cost; a round-3 shell A/B loop, since replaced by tools/ab_bench.py), so off by default
 SPLIT_BANK_IN = os.environ.get('FTMI_SPLIT_BANK_IN', '0') == '1'
 
 

@@ -223,6 +223,26 @@ def test_baseline_size_vs_torch_cpu(gpu_model, synth_sd):
         assert d.mean() < MEAN_TOL and d.max() < MAX_TOL, (k, d.mean(), d.max())
 
 
+@pytest.mark.slow
+def test_c4_global_batch_vs_torch_cpu(gpu_model, synth_sd):
+    """BASELINE c4's global batch (512 utterances, lengths U{50..200}) through ONE HIP
+    generate on one GPU — the result the 8-GPU sharded run must reproduce —
+    against the torch-CPU restatement of the reference on the same inputs: mel / mel_post
+    mean |d| < 1e-4, max < 5e-4, LengthRegulator counts bit-exact."""
+    from forwardtacotron_amd.synthetic import synthetic_tokens
+    from oracle import ft_torch_cpu as TC
+    x = synthetic_tokens(512, 200, seed=3, min_len=50)
+    out = gpu_model.generate(torch.from_numpy(x).cuda())
+    ref = TC.generate(TC.to_torch(synth_sd), torch.from_numpy(x))
+    dur_g, dur_r = out['dur'].cpu().numpy(), ref['dur'].numpy()
+    assert np.array_equal(O.duration_counts(dur_g), O.duration_counts(dur_r))
+    for k in ('mel', 'mel_post'):
+        a, b = out[k].cpu().numpy(), ref[k].numpy()
+        assert a.shape == b.shape and a.shape[0] == 512
+        d = np.abs(a - b)
+        assert d.mean() < 1e-4 and d.max() < 5e-4, (k, d.mean(), d.max())
+
+
 def _fresh_graphs(model):
     for k in ('_ftmi_graphs', '_ftmi_graph_seen'):
         model.__dict__.pop(k, None)

@@ -113,8 +113,10 @@ def test_broadcast_state_gloo():
     mp.spawn(_broadcast, args=(2, _port()), nprocs=2, join=True)
 
 
-def _oracle_protocol(rank, world, port, alpha, out_path):
-    """Each rank runs the numpy oracle on its shard with the globally decided quantities."""
+def _oracle_protocol(rank, world, port, alpha, out_path, lengths=(9, 5, 6), bounds=(0, 1, 3)):
+    """Each rank runs the numpy oracle on its shard (items bounds[rank] .. bounds[rank + 1]
+    of a batch with the given phoneme lengths, trimmed to its own longest item) with the
+    globally decided quantities."""
     import json
     from pathlib import Path
 
@@ -125,8 +127,9 @@ def _oracle_protocol(rank, world, port, alpha, out_path):
     try:
         keys = json.loads((Path(__file__).parent / 'golden' / 'state_dict_keys.json').read_text())
         sd = {k: synthetic_array(k, s, d, 0) for k, s, d in keys}
-        full = synthetic_tokens(3, 9, seed=4, lengths=[9, 5, 6])
-        shard = [full[:1], full[1:, :6]][rank]  # rank 1's shard is locally shorter
+        full = synthetic_tokens(len(lengths), max(lengths), seed=4, lengths=list(lengths))
+        lo, hi = bounds[rank], bounds[rank + 1]
+        shard = full[lo:hi, :max(lengths[lo:hi])]  # locally shorter than the global batch
         T = S.global_max(shard.shape[1])
         x = S.pad_tokens(torch.from_numpy(shard), T).numpy()
         dur = O.series_predictor(sd, 'dur_pred', x, np.float32, alpha)[..., 0]
@@ -159,6 +162,26 @@ def test_protocol_reproduces_one_reference_call(alpha, tmp_path):
     if alpha == 1000.0:
         assert s <= 0  # the global rule fired
     assert got.shape == ref.shape
+    np.testing.assert_allclose(got, ref, atol=2e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize('alpha', [1.0, 1000.0], ids=['normal', 'global-fill2'])
+def test_protocol_world8_uneven_shards(alpha, tmp_path):
+    """VERDICT r3 item 6 (c4's protocol at world size 8, CPU): 8 gloo ranks, uneven shards
+    (1 or 2 items, each rank's local phoneme length different from the global one) of one
+    11-item batch reproduce the oracle's single call on the whole batch, incl. the
+    batch-global fill-2 rule."""
+    lengths = (9, 5, 6, 3, 8, 7, 4, 9, 2, 6, 5)
+    bounds = (0, 2, 3, 5, 6, 7, 9, 10, 11)
+    out = str(tmp_path / 'r8.npz')
+    mp.spawn(_oracle_protocol, args=(8, _port(), alpha, out, lengths, bounds), nprocs=8, join=True)
+    z = np.load(out)
+    got, ref, s = z['got'], z['ref'], int(z['s'])
+    if alpha == 1000.0:
+        assert s <= 0
+    else:
+        assert s > 0
+    assert got.shape == ref.shape == (11, 80, ref.shape[2])
     np.testing.assert_allclose(got, ref, atol=2e-4, rtol=1e-5)
 
 
