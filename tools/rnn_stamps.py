@@ -1,4 +1,7 @@
 """Per-phase cycle breakdown of the persistent recurrence (diagnostic build).
+Each phase ends in a stamp that first waits for the wave's outstanding memory operations
+(s_waitcnt vmcnt(0) lgkmcnt(0)), so the build runs slower than the real kernel: the phase
+split is the evidence, the real step time comes from tools/rnn_diag.py.
 usage: FTMI_LIB=forwardtacotron_amd/libftmi_stamps.so python tools/rnn_stamps.py"""
 import ctypes, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -15,13 +18,15 @@ for cell, H, B, T in [(1, 512, 64, 1368), (0, 256, 64, 1368), (0, 128, 64, 200),
     xp = torch.randn(B, T, 2 * G * H, device='cuda') * 0.5
     w = torch.randn(2, G * H, H, device='cuda') / H ** 0.5
     bh = torch.randn(2 * G * H, device='cuda') * 0.1
+    # the decoder LSTM and the postnet GRU run spread in the model (forward_tacotron.py)
+    sp = T > 800 and B > 4 and ((cell == 1 and H == 512) or (cell == 0 and H == 256))
     for _ in range(2):
-        ops.rnn_bidir(cell, xp, H, w, bh if cell == 0 else None, check=True)
+        ops.rnn_bidir(cell, xp, H, w, bh if cell == 0 else None, check=True, spread=sp)
     torch.cuda.synchronize()
-    t0 = time.perf_counter(); ops.rnn_bidir(cell, xp, H, w, bh if cell == 0 else None, check=True)
+    t0 = time.perf_counter()
+    ops.rnn_bidir(cell, xp, H, w, bh if cell == 0 else None, check=True, spread=sp)
     dt = time.perf_counter() - t0
-    U = {512: 16, 256: 16, 128: 16, 64: 32}[H]
-    nb = max(2 * ((B + 15) // 16) * (H // U), 8 * (H // U))
+    nb = ops.rnn_blocks(cell, B, H) if not sp else ops.rnn_blocks(cell, B, H, 2 | ops.RNN_SPREAD)
     buf = (ctypes.c_ulonglong * (nb * 8))()
     assert fn(buf, nb * 8) == 0
     a = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8)[:, :6].astype(np.float64)
