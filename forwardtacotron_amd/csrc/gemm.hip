@@ -2423,7 +2423,10 @@ constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 
 // DIAG (timing experiments only, FTMI_BANK_HALVES_DIAG; results invalid): bit 0 = no MFMAs
 // (the loaded weights feed one VALU add), bit 1 = no A-fragment LDS reads (fixed fragments),
-// bit 2 = no partner exchange (each block stores its own half's sums as the output)
+// bit 2 = no partner exchange (each block stores its own half's sums as the output), bit 3 =
+// the same weight bytes per block read as 1 KB contiguous runs (block b's 139 KB slice from
+// the start of the split-weight buffer: sized for the c2 prenet bank only), bit 4 = no weight
+// loads
 template <int MI, int DIAG = 0>  // row fragments: RM = 16 MI rows (one row tile, M <= RM)
 __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmParams p) {
   BHSTAMP(0, 0);
@@ -2479,8 +2482,19 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
     const bool hv = q < QH;
     const int qq = hv ? q : q - QH, j = qq / nch, c = qq - j * nch;
     const _Float16 *src = (hv ? wh : wl) + j * Cin + c * 32;
-    rb0[i] = *(const f16x8 *)src;
-    rb1[i] = *(const f16x8 *)(src + (hv ? planeh : planel));
+    if constexpr (DIAG & 16) {  // no weight loads at all
+      rb0[i] = rb1[i] = (f16x8){};
+    } else if constexpr (DIAG & 8) {  // the same bytes per block, 1 KB contiguous per load
+      // from the start of the whole split-weight buffer (the k = 1 group's block comes first;
+      // the bank's buffer holds 1.5x the 35.65 MB read here)
+      const _Float16 *cb = (const _Float16 *)p.g[p.ngroups - 1].w3 + (size_t)b * 69632 +
+                           (wave * 2 * NS + 2 * i) * 512 + lane * 8;
+      rb0[i] = *(const f16x8 *)cb;
+      rb1[i] = *(const f16x8 *)(cb + 512);
+    } else {
+      rb0[i] = *(const f16x8 *)src;
+      rb1[i] = *(const f16x8 *)(src + (hv ? planeh : planel));
+    }
   }
   // the epilogue's per-column parameters (their latency hides in the loop)
   const float cs_h = GH.colscale[col], cs_l = GL.colscale[col];
@@ -3675,6 +3689,7 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
     hipLaunchKernelGGL((conv_bank_halves_kernel<8, D_>), dim3(2 * units), dim3(512), 0, s, p); \
     break;
       FTMI_BH_DIAG(1) FTMI_BH_DIAG(2) FTMI_BH_DIAG(3) FTMI_BH_DIAG(4) FTMI_BH_DIAG(7)
+      FTMI_BH_DIAG(8) FTMI_BH_DIAG(16) FTMI_BH_DIAG(11) FTMI_BH_DIAG(19)
 #undef FTMI_BH_DIAG
       default:
         hipLaunchKernelGGL(conv_bank_halves_kernel<8>, dim3(2 * units), dim3(512), 0, s, p);
