@@ -29,8 +29,9 @@ from .forward_tacotron import Embedding, _graphable, _identity
 
 # generate() replays the phoneme phase (three predictors, the prenet, the duration counts:
 # ~160 launches over four streams) as a HIP graph, captured on the second sighting of a
-# (device, x shape, alpha, callbacks) key; callbacks must be the identity or graph_safe
-# (forward_tacotron.graph_safe).  FTMI_FP_GRAPH=0 keeps it eager.
+# (device, x shape, alpha, callbacks) key; callbacks that are not the identity or graph_safe
+# (forward_tacotron.graph_safe) run eagerly between the replay and the launch that reads their
+# outputs (a split graph keyed without them).  FTMI_FP_GRAPH=0 keeps it eager.
 FP_GRAPH = os.environ.get('FTMI_FP_GRAPH', '1') != '0'
 FP_GRAPH_CACHE = 8
 from .text.symbols import phonemes
@@ -333,7 +334,9 @@ class FastPitch(nn.Module):
         predictors, the duration predictor and counts on the caller's stream, then the
         pitch / energy projections added to the prenet output.  Returns (dur_hat, pitch_hat,
         energy_hat, h, offsets, T_mel); capture=True (graph capture): no host sync, the T_mel
-        slot holds max(totals) on the device."""
+        slot holds max(totals) on the device.  pitch_function = energy_function = None
+        (capture only): the predictors' raw outputs, h without their projections (the split
+        graph of _phase_graph)."""
         main = torch.cuda.current_stream(x.device)
         s_pitch, s_energy, s_prenet = self._side_streams(x.device)
         for s in (s_pitch, s_energy, s_prenet):
@@ -343,9 +346,13 @@ class FastPitch(nn.Module):
             h = self.prenet.embed(x, self.embedding.weight.detach())
             h = self.prenet.layers_cl(h, len_mask)
         with torch.cuda.stream(s_pitch):
-            pitch_hat = pitch_function(self.pitch_pred.forward_bt(x).unsqueeze(1))
+            pitch_hat = self.pitch_pred.forward_bt(x).unsqueeze(1)
+            if pitch_function is not None:
+                pitch_hat = pitch_function(pitch_hat)
         with torch.cuda.stream(s_energy):
-            energy_hat = energy_function(self.energy_pred.forward_bt(x).unsqueeze(1))
+            energy_hat = self.energy_pred.forward_bt(x).unsqueeze(1)
+            if energy_function is not None:
+                energy_hat = energy_function(energy_hat)
         dur_hat = self.dur_pred.forward_bt(x, alpha=alpha)
         if batch is None:
             offsets, totals, _ = ops.duration_counts(dur_hat, apply_fill=True)
@@ -358,9 +365,10 @@ class FastPitch(nn.Module):
             main.wait_stream(s)
             if not capture:
                 t.record_stream(main)
-        wp, bp, we, be = self._series_proj_weights()
-        ops.series_proj_add(h, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
-                            self.energy_strength)
+        if pitch_function is not None and energy_function is not None:
+            wp, bp, we, be = self._series_proj_weights()
+            ops.series_proj_add(h, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
+                                self.energy_strength)
         return dur_hat, pitch_hat, energy_hat, h, offsets, T_mel
 
     def _weights_key(self):
@@ -377,7 +385,12 @@ class FastPitch(nn.Module):
         None (run the eager phase)."""
         cache = self.__dict__.setdefault('_ftmi_graphs', {})
         seen = self.__dict__.setdefault('_ftmi_graph_seen', {})
-        key = (x.device, tuple(x.shape), float(alpha), pitch_fn, energy_fn, ops.MMA)
+        # callbacks not marked graph_safe run eagerly between the replay and the one launch
+        # that reads their outputs (ForwardTacotron._phoneme_graph's split graph)
+        split = not (_graphable(pitch_fn) and _graphable(energy_fn))
+        key = ((x.device, tuple(x.shape), float(alpha), 'split', ops.MMA) if split else
+               (x.device, tuple(x.shape), float(alpha), pitch_fn, energy_fn, ops.MMA))
+        cap_p, cap_e = (None, None) if split else (pitch_fn, energy_fn)
         ent = cache.pop(key, None)
         fresh = False
         if ent is None:
@@ -392,11 +405,11 @@ class FastPitch(nn.Module):
             wkey = self._weights_key()
             sx = x.clone()
             try:
-                self._phase(sx, alpha, pitch_fn, energy_fn, capture=True)  # warm-up
+                self._phase(sx, alpha, cap_p, cap_e, capture=True)  # warm-up
                 torch.cuda.synchronize(x.device)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    outs = self._phase(sx, alpha, pitch_fn, energy_fn, capture=True)
+                    outs = self._phase(sx, alpha, cap_p, cap_e, capture=True)
             except Exception:  # pylint: disable=broad-except
                 torch.cuda.synchronize(x.device)
                 seen[key] = -1
@@ -421,14 +434,18 @@ class FastPitch(nn.Module):
         t_ready = torch.cuda.Event()
         t_ready.record(main)
         dur_hat, pitch_hat, energy_hat = dur_hat.clone(), pitch_hat.clone(), energy_hat.clone()
+        if split:  # the callbacks on the predictors' outputs, then their projections
+            pitch_hat, energy_hat = pitch_fn(pitch_hat), energy_fn(energy_hat)
+            wp, bp, we, be = self._series_proj_weights()
+            ops.series_proj_add(h, pitch_hat, wp, bp, self.pitch_strength, energy_hat, we, be,
+                                self.energy_strength)
         t_ready.synchronize()
         return (dur_hat, pitch_hat, energy_hat, h, offsets, int(t_host)), ent
 
     def _generate(self, x, alpha, pitch_function, energy_function, batch):
         with torch.no_grad():
             phase = ent = None
-            if (FP_GRAPH and batch is None and not ops.forced_exact()
-                    and _graphable(pitch_function) and _graphable(energy_function)):
+            if FP_GRAPH and batch is None and not ops.forced_exact():
                 r = self._phase_graph(x, alpha, pitch_function, energy_function)
                 if r is not None:
                     phase, ent = r

@@ -176,7 +176,7 @@ def test_graph_phase_matches_eager(fp_model, monkeypatch):
     """generate() replays FastPitch's phoneme phase as a HIP graph (captured on the second
     call of a shape): identical (bit for bit) to the eager phase across replays with new
     tokens of the same shape; the returned dur / pitch / energy are not graph buffers; an
-    unmarked callback is never captured."""
+    unmarked callback is never captured (it runs eagerly beside the split graph)."""
     from forwardtacotron_amd import fast_pitch as FPM
     m, _ = fp_model
     g = load_golden('fp_gen_b3')
@@ -195,10 +195,22 @@ def test_graph_phase_matches_eager(fp_model, monkeypatch):
                   (eager[1], graph[3])):
         for k in ('mel', 'dur', 'pitch', 'energy'):
             assert torch.equal(e[k], gr[k]), k
-    fn = lambda p: p * 1.1  # noqa: E731  (not graph_safe)
-    for _ in range(3):
-        m.generate(x1, pitch_function=fn)
-    assert len(m.__dict__['_ftmi_graphs']) == 1
+    # a callback not marked graph_safe: the split graph (captured without it), the callback
+    # run eagerly on every call (Python-side state it reads is seen), bit-identical to eager
+    amp = [1.1]
+    fn = lambda p: p * amp[0]  # noqa: E731  (not graph_safe)
+    outs = []
+    for a in (1.1, 1.1, 0.7, 1.3):
+        amp[0] = a
+        outs.append(m.generate(x1, pitch_function=fn))
+    assert len(m.__dict__['_ftmi_graphs']) == 2
+    assert any('split' in k for k in m.__dict__['_ftmi_graphs'])
+    monkeypatch.setattr(FPM, 'FP_GRAPH', False)
+    for a, o in zip((1.1, 1.1, 0.7, 1.3), outs):
+        amp[0] = a
+        ref = m.generate(x1, pitch_function=fn)
+        for k in ('mel', 'dur', 'pitch', 'energy'):
+            assert torch.equal(o[k], ref[k]), (a, k)
 
 
 def test_panel_path_matches_unfused(fp_model, monkeypatch):
