@@ -2423,91 +2423,105 @@ constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 
 // DIAG (timing experiments only, FTMI_BANK_HALVES_DIAG; results invalid): bit 0 = no MFMAs
 // (the loaded weights feed one VALU add), bit 1 = no A-fragment LDS reads (fixed fragments),
-// bit 2 = no partner exchange (each block stores its own half's sums as the output), bit 3 =
-// the same weight bytes per block read as 1 KB contiguous runs (block b's 139 KB slice from
-// the start of the split-weight buffer: sized for the c2 prenet bank only), bit 4 = no weight
-// loads
-template <int MI, int DIAG = 0>  // row fragments: RM = 16 MI rows (one row tile, M <= RM)
+// bit 2 = no partner exchange (each block stores its own half's sums as the output), bit 4 =
+// no weight loads
+//
+// Address arithmetic is compile-time wherever it can be (measured with the phase stamps of a
+// first version: the slab staging took ~12 k cycles with NO weight loads at all — ~1,300
+// instructions per wave, most of them integer divisions by the runtime slab height and chunk
+// count — against ~3 k for the same loads in tools/probe_slab.hip): NCH (32-channel chunks
+// per half) is a template parameter, the slab always holds RM + 15 rows (a lighter pair's
+// extra rows are staged and never read), a thread's slab items share one channel segment
+// (tid & 7), and the tap masks step through the rows without a division per row.
+//
+// Kernel arguments live in memory the first load of a launch misses in every cache, so a
+// chain of DEPENDENT argument loads (N -> the block's group -> that group's pointers) costs
+// a round trip each before the first data load can issue: KT (groups) and NCT (16-column sets
+// per group) are template parameters for the c2 prenet bank (16, 16), so a block's group
+// index comes from blockIdx alone and every argument load issues in the first batch; 0 = read
+// them at run time (other banks).  The weight loads of the first NPRE steps go out with the
+// slab, the rest right after the barrier: the slab wait no longer queues behind the whole
+// 139 KB stream (vector memory returns in issue order), and the loop's first steps overlap
+// the stream's remainder.
+template <int MI, int NCH, int DIAG = 0, int KT = 0, int NCT = 0>
 __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmParams p) {
   BHSTAMP(0, 0);
   constexpr int RM = MI * 16;
-  constexpr int SRM = RM + SL_MAXK - 1;
+  constexpr int SRM = RM + SL_MAXK - 1;   // staged slab rows (every pair)
   constexpr int AIMG = (SRM + 1) * SL_P;  // halves per (chunk, plane) image; row SRM is zero
-  constexpr int SLAB_BYTES = BH_MAXCH * 2 * AIMG * 2;
+  constexpr int SLAB_BYTES = NCH * 2 * AIMG * 2;
   constexpr int NIT = 2 * MI * 64;  // f32x4 items of a block's sums: [group of pair][mi][lane]
   constexpr int RED_BYTES = 8 * NIT * 16;
   constexpr int LDS_BYTES = SLAB_BYTES > RED_BYTES ? SLAB_BYTES : RED_BYTES;
-  constexpr int NS = (4 * (SL_MAXK + 1) + 7) / 8;  // steps per wave (at most)
+  constexpr int NS = (NCH * (SL_MAXK + 1) + 7) / 8;  // steps per wave (at most)
   static_assert(NIT % 512 == 0, "items per thread");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   _Float16 *const lds = (_Float16 *)smem;
   f32x4 *const red = (f32x4 *)smem;  // aliases the slab after the loop
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const int NC = p.g[0].N / 16;
+  const int NC = NCT ? NCT : p.g[0].N >> 4, K = KT ? KT : p.ngroups;
   const int b = blockIdx.x, h = (b >> 3) & 1, u = (b & 7) | ((b >> 4) << 3);
-  const int gi = u / NC, cset = u - gi * NC, gl = p.ngroups - 1 - gi;
+  const int gi = __builtin_amdgcn_readfirstlane(u / NC);
+  const int cset = u - gi * NC, gl = K - 1 - gi;
   const GemmGroup &GH = p.g[gi];  // the pair's heavy group (k = K - gi): its slab
   const GemmGroup &GL = p.g[gl];
-  const int kh = GH.k, padh = GH.pad, kl = GL.k, dpl = padh - GL.pad;
-  const int Cin = p.Cin, nch = Cin >> 6, c_half = h * (Cin >> 1);  // chunks of this half
+  const int kh = GH.k, padh = GH.pad, kl = GL.k, padl = GL.pad, dpl = padh - padl;
+  const int Cin = p.Cin, c_half = h * (NCH * 32);  // channels of this half
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fs = lane >> 4;
   const int col = cset * 16 + fr;  // < N (N % 16 == 0: host check)
 
-  // ---- the slab loads first (their wait then leaves the weight loads in flight) ----------
-  constexpr int ASLOTS = (BH_MAXCH * SRM * 8 + 511) / 512;
-  const int SR = RM + kh - 1, nitems = nch * SR * 8;
-  f32x4 av[ASLOTS];
-#pragma unroll
-  for (int i = 0; i < ASLOTS; ++i) {
-    const int idx = tid + 512 * i;
-    av[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
-    if (idx < nitems) {
-      int m = 0 - padh + sr;  // one row tile: m0 = 0
-      m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
-      av[i] = *(const f32x4 *)(p.x + (int64_t)m * p.x_stride + c_half + c * 32 + seg * 4);
-    }
-  }
-  // ---- then every weight fragment of this wave's steps q = wave + 8 i (clamped: a step past
-  // the end reloads the last one and multiplies zeros) ----
-  const int QH = nch * kh, Q = QH + nch * kl;
-  const _Float16 *wh = (const _Float16 *)GH.w3 + (int64_t)col * GH.Kpad + c_half + fs * 8;
-  const _Float16 *wl = (const _Float16 *)GL.w3 + (int64_t)col * GL.Kpad + c_half + fs * 8;
-  const int64_t planeh = (int64_t)GH.N * GH.Kpad, planel = (int64_t)GL.N * GL.Kpad;
-  f16x8 rb0[NS], rb1[NS];
-#pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    const int q = min(wave + 8 * i, Q - 1);
-    const bool hv = q < QH;
-    const int qq = hv ? q : q - QH, j = qq / nch, c = qq - j * nch;
-    const _Float16 *src = (hv ? wh : wl) + j * Cin + c * 32;
-    if constexpr (DIAG & 16) {  // no weight loads at all
-      rb0[i] = rb1[i] = (f16x8){};
-    } else if constexpr (DIAG & 8) {  // the same bytes per block, 1 KB contiguous per load
-      // from the start of the whole split-weight buffer (the k = 1 group's block comes first;
-      // the bank's buffer holds 1.5x the 35.65 MB read here)
-      const _Float16 *cb = (const _Float16 *)p.g[p.ngroups - 1].w3 + (size_t)b * 69632 +
-                           (wave * 2 * NS + 2 * i) * 512 + lane * 8;
-      rb0[i] = *(const f16x8 *)cb;
-      rb1[i] = *(const f16x8 *)(cb + 512);
-    } else {
-      rb0[i] = *(const f16x8 *)src;
-      rb1[i] = *(const f16x8 *)(src + (hv ? planeh : planel));
-    }
-  }
-  // the epilogue's per-column parameters (their latency hides in the loop)
+  // the epilogue's per-column parameters first (small; their latency hides in the loop)
   const float cs_h = GH.colscale[col], cs_l = GL.colscale[col];
   const float sc_h = GH.scale ? GH.scale[col] : 1.f, sh_h = GH.scale ? GH.shift[col] : 0.f;
   const float sc_l = GL.scale ? GL.scale[col] : 1.f, sh_l = GL.scale ? GL.shift[col] : 0.f;
   const float bi_h = GH.bias ? GH.bias[col] : 0.f, bi_l = GL.bias ? GL.bias[col] : 0.f;
+  // ---- the slab loads: item (row-chunk r = (tid >> 3) + 64 i, channel segment tid & 7);
+  // r = c SRM + sr ----
+  constexpr int ASLOTS = (NCH * SRM + 63) / 64;
+  const int seg = tid & 7;
+  f32x4 av[ASLOTS];
+#pragma unroll
+  for (int i = 0; i < ASLOTS; ++i) {
+    const int r = (tid >> 3) + 64 * i, c = r / SRM, sr = r - c * SRM;
+    int m = sr - padh;  // one row tile: m0 = 0
+    m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
+    av[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (r < NCH * SRM)
+      av[i] = *(const f32x4 *)(p.x + (int64_t)m * p.x_stride + c_half + c * 32 + seg * 4);
+  }
+  // ---- the weight fragments of this wave's CONTIGUOUS step range [q0, q1) of the unit's
+  // (group, tap, chunk) list, heavy group first, chunks fastest (consecutive steps of a wave
+  // read the two halves of each 128-B weight line back to back); clamped, so a step past the
+  // range reloads its last one and is never used.  The first NPRE steps now, the rest after
+  // the barrier. ----
+  const int QH = NCH * kh, Q = QH + NCH * kl;
+  const int q0 = (wave * Q) >> 3, q1 = ((wave + 1) * Q) >> 3;
+  const _Float16 *wh = (const _Float16 *)GH.w3 + (int64_t)col * GH.Kpad + c_half + fs * 8;
+  const _Float16 *wl = (const _Float16 *)GL.w3 + (int64_t)col * GL.Kpad + c_half + fs * 8;
+  const int64_t planeh = (int64_t)GH.N * GH.Kpad, planel = (int64_t)GL.N * GL.Kpad;
+  f16x8 rb0[NS], rb1[NS];
+  auto wload = [&](int i) {
+    const int q = min(q0 + i, q1 - 1);
+    const bool hv = q < QH;
+    const int qq = hv ? q : q - QH, j = qq / NCH, c = qq - j * NCH;
+    const _Float16 *src = (hv ? wh : wl) + j * Cin + c * 32;
+    if constexpr (DIAG & 16) {  // no weight loads at all
+      rb0[i] = rb1[i] = (f16x8){};
+    } else {
+      rb0[i] = *(const f16x8 *)src;
+      rb1[i] = *(const f16x8 *)(src + (hv ? planeh : planel));
+    }
+  };
+  constexpr int NPRE = NS < 2 ? NS : 2;
+#pragma unroll
+  for (int i = 0; i < NPRE; ++i) wload(i);
 
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < ASLOTS; ++i) {
-    const int idx = tid + 512 * i;
-    if (idx >= nitems) break;
-    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
+    const int r = (tid >> 3) + 64 * i, c = r / SRM, sr = r - c * SRM;
+    if (r >= NCH * SRM) break;
     const f32x4 x = av[i];
     amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
     f16x4 hh, tt;
@@ -2516,26 +2530,30 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
     *(f16x4 *)dst = hh;
     *(f16x4 *)(dst + AIMG) = tt;
   }
-  if (tid < nch * 2 * (SL_P / 8)) {  // the zero row of every (chunk, plane) image
+  if (tid < NCH * 2 * (SL_P / 8)) {  // the zero row of every (chunk, plane) image
     const int img = tid / (SL_P / 8), part = tid % (SL_P / 8);
     *(u32x4 *)(lds + img * AIMG + SRM * SL_P + part * 8) = (u32x4){0u, 0u, 0u, 0u};
   }
   bool bad = !(amax <= 65504.f);
   // per-row tap masks of both groups (heavy in bits 0-15, light in 16-31): bit j set iff
-  // frame t + j - pad lies in the sequence
+  // frame t + j - pad lies in the sequence; t = row mod T stepped 16 rows at a time
   unsigned msk[MI];
+  {
+    int t = fr % p.T;
 #pragma unroll
-  for (int mi = 0; mi < MI; ++mi) {
-    const int m = mi * 16 + fr;
-    unsigned a = 0, c = 0;
-    if (m < p.M) {
-      const int t = m % p.T;
-      int lo = max(padh - t, 0), hi = min(p.T - 1 + padh - t, kh - 1);
-      if (lo <= hi) a = (2u << hi) - (1u << lo);
-      lo = max(GL.pad - t, 0), hi = min(p.T - 1 + GL.pad - t, kl - 1);
-      if (lo <= hi) c = (2u << hi) - (1u << lo);
+    for (int mi = 0; mi < MI; ++mi) {
+      const int m = mi * 16 + fr;
+      unsigned a = 0, c = 0;
+      if (m < p.M) {
+        int lo = max(padh - t, 0), hi = min(p.T - 1 + padh - t, kh - 1);
+        if (lo <= hi) a = (2u << hi) - (1u << lo);
+        lo = max(padl - t, 0), hi = min(p.T - 1 + padl - t, kl - 1);
+        if (lo <= hi) c = (2u << hi) - (1u << lo);
+      }
+      msk[mi] = a | (c << 16);
+      t += 16;
+      while (t >= p.T) t -= p.T;
     }
-    msk[mi] = a | (c << 16);
   }
   // LDS stores done, then the barrier: the weight loads stay in flight across it (no vmcnt
   // wait here — __syncthreads could drain them)
@@ -2543,6 +2561,8 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   BHSTAMP(1, 0);
+#pragma unroll
+  for (int i = NPRE; i < NS; ++i) wload(i);
 
   f32x4 acch[MI], accl[MI];
 #pragma unroll
@@ -2586,42 +2606,58 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   // both sets at every join); the steps' weights were issued in this order
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
-    const int q = wave + 8 * i;
-    if (q < QH) {  // wave-uniform
-      const int j = q / nch, c = q - j * nch;
+    const int q = q0 + i;
+    if (q < q1 && q < QH) {  // wave-uniform
+      const int j = q / NCH, c = q - j * NCH;
       step(acch, lds + c * 2 * AIMG, j, j, rb0[i], rb1[i]);
     }
   }
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
-    const int q = wave + 8 * i;
-    if (q >= QH && q < Q) {  // wave-uniform
-      const int qq = q - QH, j = qq / nch, c = qq - j * nch;
+    const int q = q0 + i;
+    if (q < q1 && q >= QH) {  // wave-uniform
+      const int qq = q - QH, j = qq / NCH, c = qq - j * NCH;
       step(accl, lds + c * 2 * AIMG, j + 16, j + dpl, rb0[i], rb1[i]);
     }
   }
   BHSTAMP(2, 0);
   BHSTAMP(3, 448);
 
-  // ---- the 8 waves' sums meet in LDS, in wave order (the slab is dead after the barrier) --
+  // ---- the waves' sums meet in LDS, in wave order (the slab is dead after the barrier):
+  // only the waves whose range holds steps of a group write and are summed for it ----
+  const bool has_h = q0 < QH, has_l = q1 > QH;
   __syncthreads();
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi) {
-    red[(wave * 2 + 0) * MI * 64 + mi * 64 + lane] = acch[mi];
-    red[(wave * 2 + 1) * MI * 64 + mi * 64 + lane] = accl[mi];
+    if (has_h) red[(wave * 2 + 0) * MI * 64 + mi * 64 + lane] = acch[mi];
+    if (has_l) red[(wave * 2 + 1) * MI * 64 + mi * 64 + lane] = accl[mi];
   }
   __syncthreads();
-  // thread t owns items e = t + 512 r: (group of the pair ug, fragment mi, lane ln)
-  constexpr int IPT = NIT >= 512 ? NIT / 512 : 1;
+  // thread t owns items e = t + 512 r: (group of the pair ug, fragment mi, lane ln); the
+  // waves holding heavy steps are 0 .. wlast_h, light ones wfirst_l .. 7
+  int wlast_h = 0, wfirst_l = 7;  // exactly the waves whose has_h / has_l held above
+#pragma unroll
+  for (int w = 7; w >= 0; --w)
+    if (((w * Q) >> 3) < QH) {
+      wlast_h = w;
+      break;
+    }
+#pragma unroll
+  for (int w = 0; w < 8; ++w)
+    if ((((w + 1) * Q) >> 3) > QH) {
+      wfirst_l = w;
+      break;
+    }
+  constexpr int IPT = NIT / 512;
   f32x4 v[IPT];
   int eo[IPT];
 #pragma unroll
   for (int r = 0; r < IPT; ++r) {
-    const int e = min(tid + 512 * r, NIT - 1);
+    const int e = tid + 512 * r, ug = e / (MI * 64);
     eo[r] = e;
-    f32x4 s = red[e];
-#pragma unroll
-    for (int w = 1; w < 8; ++w) s += red[w * NIT + e];
+    const int w0 = ug ? wfirst_l : 0, w1 = ug ? 7 : wlast_h;
+    f32x4 s = red[w0 * NIT + e];
+    for (int w = w0 + 1; w <= w1; ++w) s += red[w * NIT + e];
     v[r] = s;
   }
   BHSTAMP(4, 0);
@@ -2630,9 +2666,8 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   const int ubase = (u * 2) * NIT * 16;  // bytes: [unit][half][item]; < 2^31 (host check)
 #pragma unroll
   for (int r = 0; r < IPT; ++r)
-    if (tid + 512 * r < NIT)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[r]), rs,
-                                             ubase + (h * NIT + eo[r]) * 16, 0, 16 /* sc1 */);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[r]), rs,
+                                           ubase + (h * NIT + eo[r]) * 16, 0, 16 /* sc1 */);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores done
   __syncthreads();
   __shared__ int s_last;
@@ -2645,7 +2680,7 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   }
   __syncthreads();
   BHSTAMP(5, 0);
-  if (DIAG & 4) s_last = h == 0;  // (barrier-free: every thread reads the same value below)
+  if (DIAG & 4) s_last = h == 0;  // (every thread reads the value it wrote)
   if (s_last) {
     u32x4 pr[IPT];
 #pragma unroll
@@ -2654,12 +2689,12 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
                                                     16 /* sc1 */);
 #pragma unroll
     for (int r = 0; r < IPT; ++r) {
-      if (tid + 512 * r >= NIT) continue;
       const int e = eo[r], ug = e / (MI * 64), mi = (e >> 6) % MI;
       const f32x4 s = (DIAG & 4) ? v[r] : v[r] + __builtin_bit_cast(f32x4, pr[r]);  // commutative
       const GemmGroup &GW = ug ? GL : GH;
       const float cs = ug ? cs_l : cs_h, sc = ug ? sc_l : sc_h, sh = ug ? sh_l : sh_h;
       const float bi = ug ? bi_l : bi_h;
+      float *yc = p.y + GW.ycol0 + col;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = mi * 16 + 4 * fs + i;
@@ -2668,7 +2703,7 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
         float y = s[i] * cs + bi;
         if (p.relu) y = fmaxf(y, 0.f);
         if (GW.scale) y = y * sc + sh;
-        p.y[(int64_t)row * p.y_stride + GW.ycol0 + col] = y;
+        yc[(int64_t)row * p.y_stride] = y;
       }
     }
   }
@@ -3681,19 +3716,34 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
   const int units = (p.ngroups / 2) * (p.g[0].N / 16);
   const char *dg = getenv("FTMI_BANK_HALVES_DIAG");  // timing experiments (results invalid)
   const int diag = dg ? atoi(dg) : 0;
+  const dim3 grid(2 * units), block(512);
+  const int nch = p.Cin / 64;
+#define FTMI_BH_NCH(MI_, D_)                                                                       \
+  switch (nch) {                                                                                   \
+    case 1: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 1, D_>), grid, block, 0, s, p); break; \
+    case 2: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 2, D_>), grid, block, 0, s, p); break; \
+    case 3: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 3, D_>), grid, block, 0, s, p); break; \
+    default: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 4, D_>), grid, block, 0, s, p);       \
+  }
+  const bool prenet = p.ngroups == 16 && p.g[0].N == 256 && nch == 4;  // c2: (KT, NCT) = (16, 16)
   if (p.M <= 64) {
-    hipLaunchKernelGGL(conv_bank_halves_kernel<4>, dim3(2 * units), dim3(512), 0, s, p);
+    FTMI_BH_NCH(4, 0)
+  } else if (prenet && diag == 0) {
+    hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16>), grid, block, 0, s, p);
+  } else if (diag == 0 || !prenet) {  // the timing switches exist for the c2 prenet only
+    FTMI_BH_NCH(8, 0)
   } else switch (diag) {
-#define FTMI_BH_DIAG(D_)                                                                      \
-  case D_:                                                                                    \
-    hipLaunchKernelGGL((conv_bank_halves_kernel<8, D_>), dim3(2 * units), dim3(512), 0, s, p); \
+#define FTMI_BH_DIAG(D_)                                                                       \
+  case D_:                                                                                     \
+    hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, D_, 16, 16>), grid, block, 0, s, p);       \
     break;
       FTMI_BH_DIAG(1) FTMI_BH_DIAG(2) FTMI_BH_DIAG(3) FTMI_BH_DIAG(4) FTMI_BH_DIAG(7)
-      FTMI_BH_DIAG(8) FTMI_BH_DIAG(16) FTMI_BH_DIAG(11) FTMI_BH_DIAG(19)
+      FTMI_BH_DIAG(16) FTMI_BH_DIAG(19)
 #undef FTMI_BH_DIAG
       default:
-        hipLaunchKernelGGL(conv_bank_halves_kernel<8>, dim3(2 * units), dim3(512), 0, s, p);
+        hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4>), grid, block, 0, s, p);
   }
+#undef FTMI_BH_NCH
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
 }
