@@ -2424,7 +2424,9 @@ constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 // DIAG (timing experiments only, FTMI_BANK_HALVES_DIAG; results invalid): bit 0 = no MFMAs
 // (the loaded weights feed one VALU add), bit 1 = no A-fragment LDS reads (fixed fragments),
 // bit 2 = no partner exchange (each block stores its own half's sums as the output), bit 4 =
-// no weight loads
+// no weight loads, bit 5 = every weight load before the slab wait, bit 6 = a step's 8 row
+// fragments read at once instead of in two blocks of 4, bit 7 = every weight load up front
+// behind a workgroup barrier after the slab loads' issue (bits 5-7: valid results)
 //
 // Address arithmetic is compile-time wherever it can be (measured with the phase stamps of a
 // first version: the slab staging took ~12 k cycles with NO weight loads at all — ~1,300
@@ -2471,24 +2473,28 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   const int fr = lane & 15, fs = lane >> 4;
   const int col = cset * 16 + fr;  // < N (N % 16 == 0: host check)
 
-  // the epilogue's per-column parameters first (small; their latency hides in the loop)
+  // the epilogue's per-column parameters first (small; their latency hides in the loop).
+  // Every load of the prologue is unconditional (absent parameters read the column scales
+  // and are replaced at use): a load inside a branch makes the compiler wait for it — and,
+  // in issue order, for every load before it — right there.
   const float cs_h = GH.colscale[col], cs_l = GL.colscale[col];
-  const float sc_h = GH.scale ? GH.scale[col] : 1.f, sh_h = GH.scale ? GH.shift[col] : 0.f;
-  const float sc_l = GL.scale ? GL.scale[col] : 1.f, sh_l = GL.scale ? GL.shift[col] : 0.f;
-  const float bi_h = GH.bias ? GH.bias[col] : 0.f, bi_l = GL.bias ? GL.bias[col] : 0.f;
+  const float sc_h0 = (GH.scale ? GH.scale : GH.colscale)[col];
+  const float sh_h0 = (GH.scale ? GH.shift : GH.colscale)[col];
+  const float sc_l0 = (GL.scale ? GL.scale : GL.colscale)[col];
+  const float sh_l0 = (GL.scale ? GL.shift : GL.colscale)[col];
+  const float bi_h0 = (GH.bias ? GH.bias : GH.colscale)[col];
+  const float bi_l0 = (GL.bias ? GL.bias : GL.colscale)[col];
   // ---- the slab loads: item (row-chunk r = (tid >> 3) + 64 i, channel segment tid & 7);
   // r = c SRM + sr ----
   constexpr int ASLOTS = (NCH * SRM + 63) / 64;
   const int seg = tid & 7;
   f32x4 av[ASLOTS];
 #pragma unroll
-  for (int i = 0; i < ASLOTS; ++i) {
-    const int r = (tid >> 3) + 64 * i, c = r / SRM, sr = r - c * SRM;
+  for (int i = 0; i < ASLOTS; ++i) {  // past the slab: a clamped (unused) reload
+    const int r = min((tid >> 3) + 64 * i, NCH * SRM - 1), c = r / SRM, sr = r - c * SRM;
     int m = sr - padh;  // one row tile: m0 = 0
     m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
-    av[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (r < NCH * SRM)
-      av[i] = *(const f32x4 *)(p.x + (int64_t)m * p.x_stride + c_half + c * 32 + seg * 4);
+    av[i] = *(const f32x4 *)(p.x + (int64_t)m * p.x_stride + c_half + c * 32 + seg * 4);
   }
   // ---- the weight fragments of this wave's CONTIGUOUS step range [q0, q1) of the unit's
   // (group, tap, chunk) list, heavy group first, chunks fastest (consecutive steps of a wave
@@ -2513,9 +2519,19 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
       rb1[i] = *(const f16x8 *)(src + (hv ? planeh : planel));
     }
   };
-  constexpr int NPRE = NS < 2 ? NS : 2;
+  constexpr int NPRE = (DIAG & (32 | 128)) ? NS : (NS < 2 ? NS : 2);  // bit 5: every step up front
+  if constexpr (DIAG & 128) {
+    // every wave's slab loads are issued before any wave's weight loads (a barrier with no
+    // wait: vector memory is served in issue order per CU, so the slab no longer queues
+    // behind other waves' weight streams)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #pragma unroll
   for (int i = 0; i < NPRE; ++i) wload(i);
+  // keep the issue order: the scheduler would otherwise sink loads below the slab's use
+  __builtin_amdgcn_sched_barrier(0);
 
   float amax = 0.f;
 #pragma unroll
@@ -2563,6 +2579,7 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   BHSTAMP(1, 0);
 #pragma unroll
   for (int i = NPRE; i < NS; ++i) wload(i);
+  __builtin_amdgcn_sched_barrier(0);
 
   f32x4 acch[MI], accl[MI];
 #pragma unroll
@@ -2570,7 +2587,7 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   // a step's row fragments in blocks of 4: each accumulator still adds at . bh, ah . b1,
   // ah . b0 in that order (the skinny kernel's per-accumulator order), with half the A
   // fragments live at once
-  constexpr int MB = MI < 4 ? MI : 4;
+  constexpr int MB = (DIAG & 64) ? MI : (MI < 4 ? MI : 4);  // bit 6: all row fragments at once
   auto step = [&](f32x4 (&acc)[MI], const _Float16 *Ab, int sh_j, int dr, f16x8 b0, f16x8 b1) {
     const f16x8 bh = b0 * (_Float16)(1.0f / H3_SCALE);
 #pragma unroll
@@ -2692,8 +2709,10 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
       const int e = eo[r], ug = e / (MI * 64), mi = (e >> 6) % MI;
       const f32x4 s = (DIAG & 4) ? v[r] : v[r] + __builtin_bit_cast(f32x4, pr[r]);  // commutative
       const GemmGroup &GW = ug ? GL : GH;
-      const float cs = ug ? cs_l : cs_h, sc = ug ? sc_l : sc_h, sh = ug ? sh_l : sh_h;
-      const float bi = ug ? bi_l : bi_h;
+      const float cs = ug ? cs_l : cs_h;
+      const float sc = (ug ? GL.scale : GH.scale) ? (ug ? sc_l0 : sc_h0) : 1.f;
+      const float sh = (ug ? GL.scale : GH.scale) ? (ug ? sh_l0 : sh_h0) : 0.f;
+      const float bi = (ug ? GL.bias : GH.bias) ? (ug ? bi_l0 : bi_h0) : 0.f;
       float *yc = p.y + GW.ycol0 + col;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -3738,7 +3757,8 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
     hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, D_, 16, 16>), grid, block, 0, s, p);       \
     break;
       FTMI_BH_DIAG(1) FTMI_BH_DIAG(2) FTMI_BH_DIAG(3) FTMI_BH_DIAG(4) FTMI_BH_DIAG(7)
-      FTMI_BH_DIAG(16) FTMI_BH_DIAG(19)
+      FTMI_BH_DIAG(16) FTMI_BH_DIAG(19) FTMI_BH_DIAG(32) FTMI_BH_DIAG(64) FTMI_BH_DIAG(96)
+      FTMI_BH_DIAG(128) FTMI_BH_DIAG(192)
 #undef FTMI_BH_DIAG
       default:
         hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4>), grid, block, 0, s, p);
