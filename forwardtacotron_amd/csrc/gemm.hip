@@ -1936,36 +1936,35 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
   const int nch_all = (Cin + 31) / 32;
   const int c_begin = blockIdx.y * p.kc_per;
   const int nch = min(nch_all - c_begin, p.kc_per);  // >= 1 (no empty splits)
-  const int SR = SK_BM + k - 1;
 
   // ---- prologue: the slab of this block's chunks (one float4 of 4 channels per item); every
-  // load is issued before the first split / store, so their latencies overlap ----
-  constexpr int SK_ASLOTS = (SK_CPB * SK_SR * 8 + 511) / 512;
-  const int nitems = nch * SR * 8;
+  // load is issued before the first split / store, so their latencies overlap.  Item = (row
+  // chunk r = (tid >> 3) + 64 i = c SK_SR + sr, channel segment tid & 7): the slab always has
+  // SK_SR rows (rows past this group's BM + k - 1 are staged and never read), so the indexing
+  // divides by constants only, and every load is unconditional (clamped; a load inside a
+  // branch makes the compiler wait for it there — conv_bank_halves_kernel's finding).
+  // Channels past Cin read a valid clamped address: their weights are zeroed at use. ----
+  constexpr int SK_ASLOTS = (SK_CPB * SK_SR + 63) / 64;
+  const int seg = tid & 7;
   f32x4 av[SK_ASLOTS], au[MAXPOOL ? SK_ASLOTS : 1];
 #pragma unroll
   for (int i = 0; i < SK_ASLOTS; ++i) {
-    const int idx = tid + 512 * i;
-    av[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if constexpr (MAXPOOL) au[i] = av[i];
-    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
-    const int ch = (c_begin + c) * 32 + seg * 4;
-    if (idx < nitems && ch < Cin) {
-      int m = m0 - pad + sr;
-      m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
-      const float *src = p.x + (int64_t)m * p.x_stride + ch;
-      av[i] = *(const f32x4 *)src;
-      // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
-      if constexpr (MAXPOOL) au[i] = *(const f32x4 *)(src - (m % p.T > 0 ? p.x_stride : 0));
-    }
+    const int r = min((tid >> 3) + 64 * i, nch * SK_SR - 1), c = r / SK_SR, sr = r - c * SK_SR;
+    const int ch0 = (c_begin + c) * 32 + seg * 4, ch = ch0 < Cin ? ch0 : 0;
+    int m = m0 - pad + sr;
+    m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
+    const float *src = p.x + (int64_t)m * p.x_stride + ch;
+    av[i] = *(const f32x4 *)src;
+    // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
+    if constexpr (MAXPOOL) au[i] = *(const f32x4 *)(src - (m % p.T > 0 ? p.x_stride : 0));
   }
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < SK_ASLOTS; ++i) {
-    const int idx = tid + 512 * i;
-    if (idx >= nitems) break;
-    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
+    const int r = (tid >> 3) + 64 * i, c = r / SK_SR, sr = r - c * SK_SR;
+    if (r >= nch * SK_SR) break;
     f32x4 x = av[i];
+    if ((c_begin + c) * 32 + seg * 4 >= Cin) x = (f32x4){0.f, 0.f, 0.f, 0.f};
     if constexpr (MAXPOOL) x = fmax4(x, au[i]);
     amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
     f16x4 h, t;
@@ -2037,7 +2036,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     // Loads are unconditional (a missing channel segment of a partial chunk reads channel 0
     // and is zeroed at use): a select on a loaded value would force a wait at the load.
     auto loadB = [&](int s, f16x8 &b0, f16x8 &b1) {
-      const int j = s / nch, c = s - j * nch;
+      const int j = nch == 2 ? s >> 1 : s, c = s - j * nch;  // nch is 1 or 2 (SK_CPB)
       const int ch = (c_begin + c) * 32 + fs * 8;
       const int off = (DIAG & 4) ? fs * 8 : j * Cin + (ch < Cin ? ch : 0);  // Cin % 16 == 0
       b0 = *(const f16x8 *)(w0 + off);
@@ -2064,7 +2063,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
       for (int u = 0; u < SK_PF; ++u) {
         const int s = s0 + u;
         {  // steps past the end (nsteps rounded up to SK_PF) multiply zeros: no branch
-          const int sl = min(s, s_end - 1), j = sl / nch, c = sl - j * nch;
+          const int sl = min(s, s_end - 1), j = nch == 2 ? sl >> 1 : sl, c = sl - j * nch;
           const _Float16 *Ab = lds + c * 2 * SK_AIMG;
           f16x8 ah[8], at[8];
 #pragma unroll

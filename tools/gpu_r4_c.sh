@@ -13,7 +13,7 @@ run() {  # name timeout cmd...
   tail -${TAILN:-12} gpurun_out/$name.txt
   [ $rc -eq 0 ] || { echo "=== $name FAILED rc=$rc"; exit $rc; }
 }
-run r4c_bank_tests 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "conv_bank"
+run r4c_bank_tests 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "conv_bank or conv1d or highway or f16x3_range or split_rows"
 run r4c_stamps 200 env FTMI_LIB=$PWD/forwardtacotron_amd/libftmi_stamps.so python -u tools/bank_halves_stamps.py 0 128 192
 run r4c_bank_bench 200 python -u tools/bank_bench.py 120 50 halves pairs+finish
 for d in 128 192 64 0; do run r4c_bank_bench_d$d 200 env FTMI_BANK_HALVES_DIAG=$d python -u tools/bank_bench.py 120 50 halves; done

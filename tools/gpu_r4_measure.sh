@@ -1,11 +1,11 @@
-# Round-3 measurement (run on the GPU box through gpurun): the bench lines of every config
+# Round-4 measurement (run on the GPU box through gpurun): the bench lines of every config
 # with their CPU baselines (c3, c2 as gen_forward calls it, c2 with the Griffin-Lim vocoder,
 # c5 FastPitch, the WaveRNN vocoder), rocprofv3 kernel-trace summaries of the c3 / c2 / c5 /
 # WaveRNN benches, and the PMC traffic passes (FETCH_SIZE, WRITE_SIZE: separate runs) of
-# c3 and c2.  usage: OUT=r3 bash tools/gpu_r3_measure.sh [part]   part: bench | prof | pmc | all
+# c3 and c2.  usage: OUT=r4 bash tools/gpu_r4_measure.sh [part]   part: bench | prof | pmc | all
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/${OUT:-r3}
+O=gpurun_out/${OUT:-r4}
 PART=${1:-all}
 mkdir -p $O
 step() {  # name timeout cmd...
@@ -32,6 +32,8 @@ fi
 if [ "$PART" = pmc ] || [ "$PART" = all ]; then
   step fetch_c3 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_c3 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-loop
   step write_c3 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_c3 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-loop
+  step fetch_c5 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_c5 -o run -- python3 bench.py --model fast_pitch --steps 2 --warmup 1 --no-cpu-baseline --no-host-loop
+  step write_c5 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_c5 -o run -- python3 bench.py --model fast_pitch --steps 2 --warmup 1 --no-cpu-baseline --no-host-loop
   step fetch_c2 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_c2 -o run -- python3 bench.py --config c2 --callbacks gen_forward --steps 3 --warmup 2 --no-cpu-baseline --no-host-loop
   step write_c2 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_c2 -o run -- python3 bench.py --config c2 --callbacks gen_forward --steps 3 --warmup 2 --no-cpu-baseline --no-host-loop
 fi
