@@ -86,6 +86,7 @@ struct GemmParams {
   int kc_per;
   int split_req;  // the caller's split_k (the slab kernel re-derives split / kc_per from it)
   int diag;       // slab kernel timing experiments (FTMI_SLAB_DIAG; results invalid when set)
+  int band;       // slab kernels: column-band tile order (FTMI_SLAB_BAND, see slab_tile)
   float *part;
   int ldp;  // skinny kernel: columns of a partial-sum row (all groups, output order)
   int force_part;  // skinny kernel: partial sums even with one split (highway finish)
@@ -1066,6 +1067,37 @@ constexpr int SL_AIMG = (SL_SR + 1) * SL_P;         // halves per (buffer, plane
 constexpr int SL_BIMG = SL_BN * SL_P;               // halves per (buffer, plane) B image
 constexpr int SL_TP = SL_BN + 4;                    // floats per row of the epilogue tile
 
+// Tile of slab-kernel block bid (conv_gemm_slab_kernel, conv_gemm_slabp_kernel): blocks b
+// and b + 8 run on the same XCD under round-robin dispatch (placement only ever affects
+// speed), so XCD x = bid & 7 takes the row tiles mt = 8 lr + x.  band = 0: within an XCD, all
+// VT (group, column) tiles of a row tile are consecutive — its slab rows shared through L2.
+// band = CB > 0: the XCD walks its row tiles once per band of CB consecutive (group, column)
+// tiles, so one band's weight planes stay L2-resident while every row tile of the XCD
+// passes (a 1024-column layer's 9.4 MB of planes do not fit a 4 MB L2; two 128-column tiles'
+// 2.4 MB do), at the price of re-reading each row tile once per band.
+__device__ __forceinline__ void slab_tile(int bid, int MT, int VT, int band, int &mt, int &v8) {
+  if (MT < 8) {  // few row tiles: a compact grid, row tile fastest (spread over the XCDs)
+    mt = bid % MT;
+    v8 = bid / MT;
+    return;
+  }
+  const int x = bid & 7, s8 = bid >> 3;
+  if (band <= 0 || band >= VT) {
+    const int q8 = s8 / VT;
+    mt = q8 * 8 + x;
+    v8 = s8 - q8 * VT;
+    return;
+  }
+  const int MTx = (MT + 7) >> 3;           // row tiles per XCD (padded grid)
+  const int per = MTx * band, b = s8 / per, rem = s8 - b * per;
+  const int cbn = min(band, VT - b * band);  // the last band may be narrower
+  const int lr = rem / cbn;
+  mt = lr * 8 + x;
+  v8 = b * band + (rem - lr * cbn);
+  if (lr >= MTx) mt = MT;  // (never: rem < MTx * cbn) — out of range, the block returns
+}
+
+
 // The slab kernels' epilogue: the finished fp32 tile [SL_BM][SL_TP] (colscale applied) in
 // LDS -> split-K partials, or bias / ReLU / BN / residual (conv: plain, transposed or pooled
 // rows, optionally as f16x3 split rows), or the highway gating.  Every store moves 16 B.
@@ -1185,12 +1217,8 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
   const int MT = (p.M + TS - 1) / TS, NT = p.g[0].ntiles, VT = p.ngroups * NT;
   // With fewer than 8 row tiles (small batches) that order would put every working block on
   // one XCD: the grid is then compact, row tile fastest, and consecutive blocks spread.
-  const int bid = blockIdx.x, s8 = bid >> 3, q8 = s8 / VT;
-  int mt = q8 * 8 + (bid & 7), v8 = s8 - q8 * VT;
-  if (MT < 8) {
-    mt = bid % MT;
-    v8 = bid / MT;
-  }
+  int mt, v8;
+  slab_tile(blockIdx.x, MT, VT, p.band, mt, v8);
   const int gi = v8 / NT, nt = v8 - gi * NT;
   if (mt >= MT) return;  // the grid is padded to whole XCD rounds
   const GemmGroup &G = p.g[gi];
@@ -1553,12 +1581,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slabp_kernel(const GemmParam
   // tile order: conv_gemm_slab_kernel's (XCD-aware)
   const int TS = p.pool_out ? SL_BM - 1 : SL_BM;
   const int MT = (p.M + TS - 1) / TS, NT = p.g[0].ntiles, VT = p.ngroups * NT;
-  const int bid = blockIdx.x, s8 = bid >> 3, q8 = s8 / VT;
-  int mt = q8 * 8 + (bid & 7), v8 = s8 - q8 * VT;
-  if (MT < 8) {
-    mt = bid % MT;
-    v8 = bid / MT;
-  }
+  int mt, v8;
+  slab_tile(blockIdx.x, MT, VT, p.band, mt, v8);
   const int gi = v8 / NT, nt = v8 - gi * NT;
   if (mt >= MT) return;
   const GemmGroup &G = p.g[gi];
@@ -3566,6 +3590,8 @@ static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s
     return e ? atoi(e) : 0;
   }();
   q.diag = diag;
+  const char *be = getenv("FTMI_SLAB_BAND");  // read per call (A/B runs)
+  q.band = be ? atoi(be) : 0;
   q.kc_per = nch;
   if (p.split_req > 1 && p.part) {  // split over channel chunks, no empty splits
     q.kc_per = (nch + p.split_req - 1) / p.split_req;
