@@ -3590,8 +3590,12 @@ static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s
     return e ? atoi(e) : 0;
   }();
   q.diag = diag;
-  const char *be = getenv("FTMI_SLAB_BAND");  // read per call (A/B runs)
-  q.band = be ? atoi(be) : 0;
+  // column bands of 2 (slab_tile): tools/gemm_one.py under rocprofv3, band 0 -> 2: c5 FFN conv
+  // 1179 -> 1147 us (L2->fabric reads 913 -> 662 MB per launch), c3 prenet bank 803 -> 713,
+  // postnet bank 710 -> 683, LSTM input projection 305 -> 297; proj1 (2 column tiles)
+  // unchanged.  FTMI_SLAB_BAND (read per call) overrides, 0 = the row-tile order.
+  const char *be = getenv("FTMI_SLAB_BAND");
+  q.band = be ? atoi(be) : 2;
   q.kc_per = nch;
   if (p.split_req > 1 && p.part) {  // split over channel chunks, no empty splits
     q.kc_per = (nch + p.split_req - 1) / p.split_req;
