@@ -2447,7 +2447,9 @@ constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 // DIAG (timing experiments only, FTMI_BANK_HALVES_DIAG; results invalid): bit 0 = no MFMAs
 // (the loaded weights feed one VALU add), bit 1 = no A-fragment LDS reads (fixed fragments),
 // bit 2 = no partner exchange (each block stores its own half's sums as the output), bit 4 =
-// no weight loads, bit 5 = every weight load before the slab wait, bit 6 = a step's 8 row
+// no weight loads, bit 3 = the same weight bytes per block read as 1 KB contiguous runs from
+// the start of the split-weight buffer (c2 prenet: 256 x 139 KB of its 53 MB; results
+// invalid), bit 5 = every weight load before the slab wait, bit 6 = a step's 8 row
 // fragments read at once instead of in two blocks of 4, bit 7 = every weight load up front
 // behind a workgroup barrier after the slab loads' issue (bits 5-7: valid results)
 //
@@ -2496,17 +2498,8 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   const int fr = lane & 15, fs = lane >> 4;
   const int col = cset * 16 + fr;  // < N (N % 16 == 0: host check)
 
-  // the epilogue's per-column parameters first (small; their latency hides in the loop).
-  // Every load of the prologue is unconditional (absent parameters read the column scales
-  // and are replaced at use): a load inside a branch makes the compiler wait for it — and,
-  // in issue order, for every load before it — right there.
-  const float cs_h = GH.colscale[col], cs_l = GL.colscale[col];
-  const float sc_h0 = (GH.scale ? GH.scale : GH.colscale)[col];
-  const float sh_h0 = (GH.scale ? GH.shift : GH.colscale)[col];
-  const float sc_l0 = (GL.scale ? GL.scale : GL.colscale)[col];
-  const float sh_l0 = (GL.scale ? GL.shift : GL.colscale)[col];
-  const float bi_h0 = (GH.bias ? GH.bias : GH.colscale)[col];
-  const float bi_l0 = (GL.bias ? GL.bias : GL.colscale)[col];
+  // Every load of the prologue is unconditional: a load inside a branch makes the compiler
+  // wait for it — and, in issue order, for every load before it — right there.
   // ---- the slab loads: item (row-chunk r = (tid >> 3) + 64 i, channel segment tid & 7);
   // r = c SRM + sr ----
   constexpr int ASLOTS = (NCH * SRM + 63) / 64;
@@ -2537,6 +2530,11 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
     const _Float16 *src = (hv ? wh : wl) + j * Cin + c * 32;
     if constexpr (DIAG & 16) {  // no weight loads at all
       rb0[i] = rb1[i] = (f16x8){};
+    } else if constexpr (DIAG & 8) {  // the same bytes per block as 1 KB contiguous runs
+      const _Float16 *cb = (const _Float16 *)p.g[K - 1].w3 + (size_t)b * 69632 +
+                           (wave * 2 * NS + 2 * i) * 512 + lane * 8;
+      rb0[i] = *(const f16x8 *)cb;
+      rb1[i] = *(const f16x8 *)(cb + 512);
     } else {
       rb0[i] = *(const f16x8 *)src;
       rb1[i] = *(const f16x8 *)(src + (hv ? planeh : planel));
@@ -2602,6 +2600,16 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   BHSTAMP(1, 0);
 #pragma unroll
   for (int i = NPRE; i < NS; ++i) wload(i);
+  // the epilogue's per-column parameters, behind every weight load (vector memory completes
+  // in issue order: ahead of the slab they held its wait back by a miss's latency); absent
+  // parameters read the column scales and are replaced at use (unconditional loads)
+  const float cs_h = GH.colscale[col], cs_l = GL.colscale[col];
+  const float sc_h0 = (GH.scale ? GH.scale : GH.colscale)[col];
+  const float sh_h0 = (GH.scale ? GH.shift : GH.colscale)[col];
+  const float sc_l0 = (GL.scale ? GL.scale : GL.colscale)[col];
+  const float sh_l0 = (GL.scale ? GL.shift : GL.colscale)[col];
+  const float bi_h0 = (GH.bias ? GH.bias : GH.colscale)[col];
+  const float bi_l0 = (GL.bias ? GL.bias : GL.colscale)[col];
   __builtin_amdgcn_sched_barrier(0);
 
   f32x4 acch[MI], accl[MI];
@@ -3787,7 +3795,7 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
     break;
       FTMI_BH_DIAG(1) FTMI_BH_DIAG(2) FTMI_BH_DIAG(3) FTMI_BH_DIAG(4) FTMI_BH_DIAG(7)
       FTMI_BH_DIAG(16) FTMI_BH_DIAG(19) FTMI_BH_DIAG(32) FTMI_BH_DIAG(64) FTMI_BH_DIAG(96)
-      FTMI_BH_DIAG(128) FTMI_BH_DIAG(192)
+      FTMI_BH_DIAG(128) FTMI_BH_DIAG(192) FTMI_BH_DIAG(8) FTMI_BH_DIAG(136)
 #undef FTMI_BH_DIAG
       default:
         hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4>), grid, block, 0, s, p);

@@ -14,9 +14,9 @@ run() {  # name timeout cmd...
   [ $rc -eq 0 ] || { echo "=== $name FAILED rc=$rc"; exit $rc; }
 }
 run r4c_bank_tests 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "conv_bank or conv1d or highway or f16x3_range or split_rows"
-run r4c_stamps 200 env FTMI_LIB=$PWD/forwardtacotron_amd/libftmi_stamps.so python -u tools/bank_halves_stamps.py 0 128 192
+run r4c_stamps 200 env FTMI_LIB=$PWD/forwardtacotron_amd/libftmi_stamps.so python -u tools/bank_halves_stamps.py 0 8 128 136
 run r4c_bank_bench 200 python -u tools/bank_bench.py 120 50 halves pairs+finish
-for d in 128 192 64 0; do run r4c_bank_bench_d$d 200 env FTMI_BANK_HALVES_DIAG=$d python -u tools/bank_bench.py 120 50 halves; done
+
 run r4c_bank_prof 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4c_prof -o run -- python3 tools/bank_bench.py 120 50 halves pairs+finish
 find gpurun_out/r4c_prof -name "*kernel_stats.csv" -exec head -6 {} \;
 echo ALLOK
