@@ -156,12 +156,12 @@ def time_prenet_bank(model, x, reps: int = 20):
     from forwardtacotron_amd import ops
     cb = model.prenet
     h = ops.embedding(x, model.embedding.weight.detach())
-    bank_w, scale, shift, _, bank3, _ = cb.packed_weights()
+    bank_w, scale, shift, _, bank3, _, img = cb.packed_weights()
     pooled = ops.bank_pools(h, cb.K, cb.channels, w_split=bank3)
 
     def call():
         return ops.conv_bank(h, bank_w, cb.K, cb.channels, scale, shift, w_split=bank3,
-                             pool=pooled, split_out=pooled and ops.SPLIT_ROWS)
+                             pool=pooled, split_out=pooled and ops.SPLIT_ROWS, w_image=img)
 
     def timed(fn):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 15
+ABI_VERSION = 16
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -59,6 +59,8 @@ SIGNATURES = {
     'ftmi_conv_bank_split': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P,
                                      c_int64, c_int, P, c_int, P, c_int, P]),
     'ftmi_conv_bank_halves_ws_floats': (c_int64, [c_int, c_int, c_int, c_int]),
+    'ftmi_conv_bank_halves_image_bytes': (c_int64, [c_int, c_int, c_int]),
+    'ftmi_conv_bank_halves_image': (c_int, [P, c_int, c_int, c_int, P, P]),
     'ftmi_highway': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P, P]),
     'ftmi_highway_split': (c_int, [P, c_int64, c_int64, c_int, P, P, P, P, P, c_int64, c_int, P,
                                    c_int, P, P]),

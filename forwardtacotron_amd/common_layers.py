@@ -297,11 +297,12 @@ class CBHG(Packed):
         shift = torch.cat([f[1] for f in folds]).contiguous()
         w_pre = self.pre_highway.weight.detach().contiguous()
         bank3 = ops.split_bank_weights(bank_w, self.K, ws[0].size(1), self.channels)
-        return bank_w, scale, shift, w_pre, bank3, presplit(w_pre)
+        img = ops.bank_halves_image(bank3, self.K, ws[0].size(1), self.channels)
+        return bank_w, scale, shift, w_pre, bank3, presplit(w_pre), img
 
     def forward_cl(self, x: torch.Tensor) -> torch.Tensor:
         """(B, T, Cin) channels-last -> (B, T, 2*channels)."""
-        bank_w, scale, shift, w_pre, bank3, pre3 = self.packed_weights()
+        bank_w, scale, shift, w_pre, bank3, pre3, img = self.packed_weights()
         pooled = ops.bank_pools(x, self.K, self.channels, w_split=bank3)
         # pooled: the bank kernel applied the maxpool, and (split) stored its output as the
         # f16x3 split rows proj1 multiplies
@@ -309,7 +310,7 @@ class CBHG(Packed):
         xin = pooled and ops.SPLIT_BANK_IN  # x stays fp32 too: it is the proj2 residual
         bank = ops.conv_bank(ops.split_rows(x) if xin else x, bank_w, self.K, self.channels,
                              scale, shift, w_split=bank3, pool=pooled, split_out=split,
-                             x_split=xin)
+                             x_split=xin, w_image=img)
         y = self.conv_project1.forward_cl(bank, maxpool=not pooled, x_split=split)
         del bank
         y = self.conv_project2.forward_cl(y, residual=x)

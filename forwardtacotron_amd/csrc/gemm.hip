@@ -104,6 +104,9 @@ struct GemmParams {
   // skinny conv bank (FTMI_BANK_LAST): per-tile arrival counters (zero between launches);
   // the last split block of a tile sums the splits and finishes it (no finish launch)
   unsigned *tile_cnt;
+  // conv_bank_halves_kernel (FTMI_BANK_IMAGE): the stream-order weight image — every wave's
+  // weight fragments in the order it loads them, 1 KB per wave load (bank_halves_pack_kernel)
+  const _Float16 *wimg;
   GemmGroup g[MAX_GROUPS];
 };
 
@@ -2470,7 +2473,13 @@ constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 // slab, the rest right after the barrier: the slab wait no longer queues behind the whole
 // 139 KB stream (vector memory returns in issue order), and the loop's first steps overlap
 // the stream's remainder.
-template <int MI, int NCH, int DIAG = 0, int KT = 0, int NCT = 0>
+//
+// PK (FTMI_BANK_IMAGE): the weights come from the stream-order image instead of the split
+// planes: the 16 B a lane loads for a step sit next to its neighbours', so each wave load
+// is one contiguous 1 KB run (from the planes it touches 16 half-used 128-B lines, their
+// other halves loaded by the next step).  Measured with the bit-3 timing variant's layout
+// (r4c stamps): 17.8 vs 20.4 us per call.
+template <int MI, int NCH, int DIAG = 0, int KT = 0, int NCT = 0, bool PK = false>
 __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmParams p) {
   BHSTAMP(0, 0);
   constexpr int RM = MI * 16;
@@ -2533,6 +2542,11 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
     } else if constexpr (DIAG & 8) {  // the same bytes per block as 1 KB contiguous runs
       const _Float16 *cb = (const _Float16 *)p.g[K - 1].w3 + (size_t)b * 69632 +
                            (wave * 2 * NS + 2 * i) * 512 + lane * 8;
+      rb0[i] = *(const f16x8 *)cb;
+      rb1[i] = *(const f16x8 *)(cb + 512);
+    } else if constexpr (PK) {  // slot [block][wave][step][plane][lane]; past the range: its last
+      const int ii = max(min(i, q1 - q0 - 1), 0);
+      const _Float16 *cb = p.wimg + ((int64_t)(b * 8 + wave) * NS + ii) * 1024 + lane * 8;
       rb0[i] = *(const f16x8 *)cb;
       rb1[i] = *(const f16x8 *)(cb + 512);
     } else {
@@ -2760,6 +2774,44 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   if (bad && p.status) atomicOr(p.status, 1u);
   BHSTAMP(6, 0);
   BHSTAMP(7, 448);
+}
+
+// steps per wave of conv_bank_halves_kernel (its NS) and the halves of its weight image
+constexpr int bh_steps(int nch) { return (nch * (SL_MAXK + 1) + 7) / 8; }
+static int64_t bank_halves_image_halves(int K, int N, int Cin) {
+  return (int64_t)(K / 2) * (N / 16) * 2 * 8 * bh_steps(Cin / 64) * 1024;
+}
+
+// The weight image of conv_bank_halves_kernel<..., PK = true>: block b, wave w, step slot i,
+// plane pl, lane l hold the 8 halves that lane loads for that step in the plane-reading
+// kernel — the same (unit, half, step range, clamp) arithmetic, with the one difference that
+// a wave whose range is empty copies step 0 (the kernel loads that slot and never uses it).
+// Built once per weights version (ops.bank_halves_image); p.wimg is the output here.
+template <int NCH>
+__global__ __launch_bounds__(512) void bank_halves_pack_kernel(const GemmParams p) {
+  constexpr int NS = bh_steps(NCH);
+  const int NC = p.g[0].N >> 4, K = p.ngroups;
+  const int b = blockIdx.x, h = (b >> 3) & 1, u = (b & 7) | ((b >> 4) << 3);
+  const int gi = u / NC, cset = u - gi * NC, gl = K - 1 - gi;
+  const GemmGroup &GH = p.g[gi];
+  const GemmGroup &GL = p.g[gl];
+  const int Cin = p.Cin, c_half = h * (NCH * 32);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fs = lane >> 4, col = cset * 16 + fr;
+  const int QH = NCH * GH.k, Q = QH + NCH * GL.k;
+  const int q0 = (wave * Q) >> 3, q1 = ((wave + 1) * Q) >> 3;
+  const _Float16 *wh = (const _Float16 *)GH.w3 + (int64_t)col * GH.Kpad + c_half + fs * 8;
+  const _Float16 *wl = (const _Float16 *)GL.w3 + (int64_t)col * GL.Kpad + c_half + fs * 8;
+  const int64_t planeh = (int64_t)GH.N * GH.Kpad, planel = (int64_t)GL.N * GL.Kpad;
+  _Float16 *dst = (_Float16 *)p.wimg + (int64_t)(b * 8 + wave) * NS * 1024 + lane * 8;
+  for (int i = 0; i < NS; ++i) {
+    const int q = max(min(q0 + i, q1 - 1), 0);
+    const bool hv = q < QH;
+    const int qq = hv ? q : q - QH, j = qq / NCH, c = qq - j * NCH;
+    const _Float16 *src = (hv ? wh : wl) + j * Cin + c * 32;
+    *(f16x8 *)(dst + i * 1024) = *(const f16x8 *)src;
+    *(f16x8 *)(dst + i * 1024 + 512) = *(const f16x8 *)(src + (hv ? planeh : planel));
+  }
 }
 
 // sum of the skinny kernel's split partials + the conv epilogue; blockIdx.y is the group
@@ -3782,7 +3834,23 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
     default: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 4, D_>), grid, block, 0, s, p);       \
   }
   const bool prenet = p.ngroups == 16 && p.g[0].N == 256 && nch == 4;  // c2: (KT, NCT) = (16, 16)
-  if (p.M <= 64) {
+  if (p.wimg) {  // the stream-order weight image (no timing variants)
+#define FTMI_BH_PK(MI_)                                                                                  \
+  switch (nch) {                                                                                         \
+    case 1: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 1, 0, 0, 0, true>), grid, block, 0, s, p); break; \
+    case 2: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 2, 0, 0, 0, true>), grid, block, 0, s, p); break; \
+    case 3: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 3, 0, 0, 0, true>), grid, block, 0, s, p); break; \
+    default: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 4, 0, 0, 0, true>), grid, block, 0, s, p);       \
+  }
+    if (p.M <= 64) {
+      FTMI_BH_PK(4)
+    } else if (prenet) {
+      hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16, true>), grid, block, 0, s, p);
+    } else {
+      FTMI_BH_PK(8)
+    }
+#undef FTMI_BH_PK
+  } else if (p.M <= 64) {
     FTMI_BH_NCH(4, 0)
   } else if (prenet && diag == 0) {
     hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16>), grid, block, 0, s, p);
@@ -3983,6 +4051,88 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   return launch(p, EPI_CONV, a->maxpool != 0, mtiles * g.ntiles, a->mma, ftmi_hs(stream));
 }
 
+namespace {
+// the bank's groups, heaviest first (group gi has k = K - gi taps, pad k / 2, output columns
+// (k - 1) Cout ..): weights, split blocks (w_split: ftmi_split_weights[_f16] blocks of
+// k = 1 .. K back to back), BN affine; returns the tile count of the generic kernels
+int set_bank_groups(GemmParams &p, const float *w, const void *w_split, int K, int Cout, int mma,
+                    const float *bn_scale, const float *bn_shift) {
+  const int Cin = p.Cin;
+  const int mtiles = (p.M + BM - 1) / BM;
+  const int ntiles = (Cout + BN - 1) / BN;
+  int tile0 = 0;
+  for (int gi = 0; gi < K; ++gi) {
+    const int ks = K - gi;  // heaviest group first
+    const int gidx = ks - 1;
+    GemmGroup &g = p.g[gi];
+    g.w = w ? w + (int64_t)Cout * Cin * gidx * (gidx + 1) / 2 : nullptr;
+    g.Kpad = (ks * Cin + X6_BK - 1) / X6_BK * X6_BK;
+    g.N = Cout;
+    const void *blk = nullptr;
+    if (w_split) {  // per-group split blocks back to back (ftmi_split_weights[_f16] layout)
+      int64_t off = 0;
+      for (int j = 0; j < gidx; ++j) off += split_block_bytes(Cout, (int64_t)(j + 1) * Cin, mma);
+      blk = (const char *)w_split + off;
+    }
+    set_split(g, blk, mma);
+    g.bias = nullptr;
+    g.scale = bn_scale ? bn_scale + (int64_t)gidx * Cout : nullptr;
+    g.shift = bn_shift ? bn_shift + (int64_t)gidx * Cout : nullptr;
+    g.k = ks;
+    g.pad = ks / 2;
+    g.Ktot = ks * Cin;
+    g.ycol0 = gidx * Cout;
+    g.ntiles = ntiles;
+    g.tile0 = tile0;
+    tile0 += mtiles * ntiles;
+  }
+  return tile0;
+}
+
+// the shapes FTMI_BANK_HALVES accepts, independent of the row count
+bool bank_halves_shape(int Cin, int K, int Cout) {
+  return Cin > 0 && Cin % 64 == 0 && Cin <= 2 * BH_MAXCH * 32 && K >= 2 && K % 2 == 0 &&
+         K <= MAX_GROUPS && Cout > 0 && Cout % 16 == 0 && ((K / 2) * (Cout / 16)) % 8 == 0 &&
+         (K / 2) * (Cout / 16) <= FTMI_BANK_COUNTERS;
+}
+}  // namespace
+
+extern "C" int64_t ftmi_conv_bank_halves_image_bytes(int32_t Cin, int32_t K, int32_t Cout) {
+  if (!bank_halves_shape(Cin, K, Cout)) return 0;
+  return bank_halves_image_halves(K, Cout, Cin) * 2 + (int64_t)K * Cout * 4;
+}
+
+extern "C" int ftmi_conv_bank_halves_image(const void *w_split, int32_t Cin, int32_t K,
+                                           int32_t Cout, void *image, ftmi_stream_t stream) {
+  if (!w_split || !image) return FTMI_E_ARG;
+  if (!bank_halves_shape(Cin, K, Cout)) return FTMI_E_UNSUPPORTED;
+  if (!ftmi_aligned16(w_split) || !ftmi_aligned16(image)) return FTMI_E_ALIGN;
+  GemmParams p = {};
+  p.Cin = Cin;
+  p.M = 1;
+  p.ngroups = K;
+  set_bank_groups(p, nullptr, w_split, K, Cout, 2, nullptr, nullptr);
+  p.wimg = (const _Float16 *)image;
+  const hipStream_t s = ftmi_hs(stream);
+  const dim3 grid(2 * (K / 2) * (Cout / 16)), block(512);
+  switch (Cin / 64) {
+    case 1: hipLaunchKernelGGL(bank_halves_pack_kernel<1>, grid, block, 0, s, p); break;
+    case 2: hipLaunchKernelGGL(bank_halves_pack_kernel<2>, grid, block, 0, s, p); break;
+    case 3: hipLaunchKernelGGL(bank_halves_pack_kernel<3>, grid, block, 0, s, p); break;
+    default: hipLaunchKernelGGL(bank_halves_pack_kernel<4>, grid, block, 0, s, p);
+  }
+  FTMI_CHECK_LAUNCH();
+  // the column scales of the groups k = 1 .. K after the weights
+  char *cs = (char *)image + bank_halves_image_halves(K, Cout, Cin) * 2;
+  for (int gi = 0; gi < K; ++gi) {
+    const int gidx = K - 1 - gi;
+    const hipError_t e = hipMemcpyAsync(cs + (int64_t)gidx * Cout * 4, p.g[gi].colscale,
+                                        (size_t)Cout * 4, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return (int)e;
+  }
+  return FTMI_OK;
+}
+
 extern "C" int64_t ftmi_conv_bank_halves_ws_floats(int32_t B, int32_t T, int32_t K, int32_t Cout) {
   if (B <= 0 || T <= 0 || K <= 0 || Cout <= 0 || (int64_t)B * T > 128) return 0;
   return FTMI_BANK_COUNTERS + bank_halves_floats(B * T, K, Cout);
@@ -4033,10 +4183,13 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
   p.y_stride = y_stride;
   p.status = status;
   if (pool_out & ~(FTMI_BANK_POOL | FTMI_BANK_Y_SPLIT | FTMI_BANK_X_SPLIT | FTMI_BANK_LAST |
-                   FTMI_BANK_HALVES))
+                   FTMI_BANK_HALVES | FTMI_BANK_IMAGE))
     return FTMI_E_ARG;
   const bool halves = (pool_out & FTMI_BANK_HALVES) != 0;
-  if (halves && (!split_ws || mma != 2 || (pool_out & ~FTMI_BANK_HALVES))) return FTMI_E_ARG;
+  const bool image = (pool_out & FTMI_BANK_IMAGE) != 0;
+  if (image && !halves) return FTMI_E_ARG;
+  if (halves && (!split_ws || mma != 2 || (pool_out & ~(FTMI_BANK_HALVES | FTMI_BANK_IMAGE))))
+    return FTMI_E_ARG;
   if ((pool_out & FTMI_BANK_LAST) && (split_k <= 1 || !split_ws)) return FTMI_E_ARG;
   p.pool_out = pool_out & FTMI_BANK_POOL;
   if (pool_out & FTMI_BANK_Y_SPLIT) {  // split output rows need the pooled epilogue
@@ -4046,38 +4199,21 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
   }
   p.x_split = (pool_out & FTMI_BANK_X_SPLIT) != 0;
   if (p.x_split && mma != 2) return FTMI_E_UNSUPPORTED;
-  const int mtiles = (p.M + BM - 1) / BM;
-  const int ntiles = (Cout + BN - 1) / BN;
-  int tile0 = 0;
-  for (int gi = 0; gi < K; ++gi) {
-    const int ks = K - gi;  // heaviest group first
-    const int gidx = ks - 1;
-    GemmGroup &g = p.g[gi];
-    g.w = w + (int64_t)Cout * Cin * gidx * (gidx + 1) / 2;
-    g.Kpad = (ks * Cin + X6_BK - 1) / X6_BK * X6_BK;
-    g.N = Cout;
-    const void *blk = nullptr;
-    if (w_split) {  // per-group split blocks back to back (ftmi_split_weights[_f16] layout)
-      int64_t off = 0;
-      for (int j = 0; j < gidx; ++j) off += split_block_bytes(Cout, (int64_t)(j + 1) * Cin, mma);
-      blk = (const char *)w_split + off;
-    }
-    set_split(g, blk, mma);
-    g.bias = nullptr;
-    g.scale = bn_scale + (int64_t)gidx * Cout;
-    g.shift = bn_shift + (int64_t)gidx * Cout;
-    g.N = Cout;
-    g.k = ks;
-    g.pad = ks / 2;
-    g.Ktot = ks * Cin;
-    g.ycol0 = gidx * Cout;
-    g.ntiles = ntiles;
-    g.tile0 = tile0;
-    tile0 += mtiles * ntiles;
-  }
+  const int tile0 = set_bank_groups(p, w, image ? nullptr : w_split, K, Cout, mma, bn_scale,
+                                    bn_shift);
   if (halves) {  // one launch: channel halves, the unit's last half finishes it
     p.tile_cnt = (unsigned *)split_ws;
     p.part = split_ws + FTMI_BANK_COUNTERS;
+    if (image) {  // the stream-order image: weights, then the groups' column scales
+      if (!ftmi_aligned16(w_split)) return FTMI_E_ALIGN;
+      p.wimg = (const _Float16 *)w_split;
+      const float *cs =
+          (const float *)(p.wimg + bank_halves_image_halves(K, Cout, Cin));
+      for (int gi = 0; gi < K; ++gi) {
+        p.g[gi].w3 = (const __bf16 *)w_split;  // (not read by the image kernel)
+        p.g[gi].colscale = cs + (int64_t)(K - 1 - gi) * Cout;
+      }
+    }
     if (!bank_halves_ok(p)) return FTMI_E_UNSUPPORTED;
     return launch_bank_halves(p, ftmi_hs(stream));
   }

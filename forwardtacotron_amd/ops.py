@@ -385,14 +385,36 @@ def bank_pools(x: torch.Tensor, K: int, Cout: int, mma: Optional[int] = None, w_
             and _slab(m, T, T, Cin, K, Cout, B * T))
 
 
+def bank_halves_image(w_split: Optional[torch.Tensor], K: int, Cin: int,
+                      Cout: int) -> Optional[torch.Tensor]:
+    """The stream-order weight image of the one-launch few-row bank
+    (`ftmi_conv_bank_halves_image`: every wave's weight fragments in its load order, one
+    contiguous 1 KB run per wave load), built once per weights version from the f16x3 split
+    blocks `split_bank_weights` made; None when those are not f16 planes or the shape has no
+    halves kernel.  FTMI_BANK_IMAGE=0 (read when the weights are packed) keeps the planes."""
+    if (w_split is None or w_split.dtype != torch.uint8 or not w_split.is_cuda
+            or os.environ.get('FTMI_BANK_IMAGE', '1') == '0'):
+        return None
+    lib = _lib.load()
+    n = int(lib.ftmi_conv_bank_halves_image_bytes(Cin, K, Cout))
+    if n <= 0:
+        return None
+    img = torch.empty(n, device=w_split.device, dtype=torch.uint8)
+    launch('ftmi_conv_bank_halves_image', f'bank_halves_image[K={K},Cin={Cin},Cout={Cout}]', 0,
+           2.0 * n, w_split.data_ptr(), Cin, K, Cout, img.data_ptr(), _stream())
+    return img
+
+
 def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.Tensor,
               shift: torch.Tensor, mma: Optional[int] = None,
               w_split: Optional[torch.Tensor] = None, pool: bool = False,
-              split_out: bool = False, x_split: bool = False) -> torch.Tensor:
+              split_out: bool = False, x_split: bool = False,
+              w_image: Optional[torch.Tensor] = None) -> torch.Tensor:
     """CBHG conv bank, (B, T, Cin) -> (B, T, K*Cout); pool: the maxpool(2, 1) of it
     (common_layers.py:73,100), stored by the bank kernel (see bank_pools); split_out (with
     pool): stored as f16x3 split rows for proj1 (conv1d(x_split=True)); x_split: x holds
-    split rows (split_rows)."""
+    split rows (split_rows); w_image: `bank_halves_image(w_split, ...)`, read instead of
+    w_split where the one-launch few-row kernel runs (same results bit for bit)."""
     if split_out and not pool:
         raise ValueError('split_out needs pool')
     _dev(x, w, scale, shift, w_split)
@@ -406,6 +428,9 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
         # the few-row bank in one launch (gemm.hip conv_bank_halves_kernel)
         n = int(_lib.load().ftmi_conv_bank_halves_ws_floats(B, T, K, Cout)) - BANK_COUNTERS
         sk, part, last = 2, _bank_workspace(n, x.device), BANK_HALVES
+        if w_image is not None:
+            _dev(w_image)
+            wsp, last = w_image.data_ptr(), BANK_HALVES | BANK_IMAGE
     elif not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
         sk = _skinny_split(Cin)  # weight-streaming kernel: partial sums, finished in order
         if os.environ.get('FTMI_BANK_LAST', '0') != '0':
@@ -424,7 +449,7 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
 
 
 BANK_LAST, BANK_COUNTERS = 8, 4096  # include/ftmi.h FTMI_BANK_LAST, FTMI_BANK_COUNTERS
-BANK_HALVES = 16  # include/ftmi.h FTMI_BANK_HALVES
+BANK_HALVES, BANK_IMAGE = 16, 32  # include/ftmi.h FTMI_BANK_HALVES, FTMI_BANK_IMAGE
 
 
 def _bank_halves(mma: int, B: int, T: int, Cin: int, K: int, Cout: int) -> bool:

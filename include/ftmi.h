@@ -70,7 +70,7 @@ enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
                                  last split block sums the splits in order) instead of a second
                                  launch.  One workspace per stream: concurrent launches must not
                                  share the counters. */
-       FTMI_BANK_HALVES = 16  /* ABI 15 (alone, FTMI_MMA_F16X3): the few-row bank in ONE
+       FTMI_BANK_HALVES = 16, /* ABI 15 (alone, FTMI_MMA_F16X3): the few-row bank in ONE
                                  launch — a block per (group pair, 16-column set, half of the
                                  input channels), each wave's weight stream issued at once, the
                                  unit's two halves combined in-kernel by the last to arrive
@@ -78,11 +78,16 @@ enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
                                  (K / 2)(Cout / 16) % 8 == 0; else FTMI_E_UNSUPPORTED.  split_ws:
                                  ftmi_conv_bank_halves_ws_floats(B, T, K, Cout) floats, the first
                                  FTMI_BANK_COUNTERS zeroed once by the caller (every launch leaves
-                                 them zero); split_k is ignored.  One workspace per stream. */ };
+                                 them zero); split_k is ignored.  One workspace per stream. */
+       FTMI_BANK_IMAGE = 32   /* ABI 16, with FTMI_BANK_HALVES: w_split is the bank's
+                                 stream-order weight image (ftmi_conv_bank_halves_image), which
+                                 the kernel reads as one contiguous 1 KB run per wave load;
+                                 same results bit for bit. */ };
 enum { FTMI_BANK_COUNTERS = 4096 };
 
 /* ABI version; bumped on any signature change (14: ftmi_panel_proj_qkv, ftmi_attention_kv;
- * 15: FTMI_BANK_HALVES, ftmi_conv_bank_halves_ws_floats). */
+ * 15: FTMI_BANK_HALVES, ftmi_conv_bank_halves_ws_floats; 16: FTMI_BANK_IMAGE,
+ * ftmi_conv_bank_halves_image[_bytes]). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
@@ -200,6 +205,15 @@ int ftmi_conv_bank(const float *x, int64_t x_stride, int32_t B, int32_t T, int32
 /* Floats of the FTMI_BANK_HALVES workspace (counters included) for a bank of B*T <= 128
  * rows, K groups of Cout columns; 0 for other sizes. */
 int64_t ftmi_conv_bank_halves_ws_floats(int32_t B, int32_t T, int32_t K, int32_t Cout);
+/* Bytes of the FTMI_BANK_IMAGE weight image of a bank (Cin input channels, K groups of Cout
+ * columns; any B*T); 0 for shapes FTMI_BANK_HALVES refuses. */
+int64_t ftmi_conv_bank_halves_image_bytes(int32_t Cin, int32_t K, int32_t Cout);
+/* Builds that image (16-B aligned, ftmi_conv_bank_halves_image_bytes bytes) from the bank's
+ * f16x3 split blocks (the FTMI_MMA_F16X3 w_split of ftmi_conv_bank_split); stream-ordered.
+ * Once per weights version: it replaces `w_split` (a prepared layout like the split blocks
+ * themselves, models/common_layers.py:68-71's bank weights reordered, not recomputed). */
+int ftmi_conv_bank_halves_image(const void *w_split, int32_t Cin, int32_t K, int32_t Cout,
+                                void *image, ftmi_stream_t stream);
 int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B, int32_t T, int32_t Cin,
                          const float *w, const void *w_split, int32_t K, int32_t Cout,
                          const float *bn_scale, const float *bn_shift, float *y,

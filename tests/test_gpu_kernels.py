@@ -247,7 +247,8 @@ def test_conv_bank_last_arriver_counters(rng, monkeypatch):
     assert not ops._BANK_WS[key][:ops.BANK_COUNTERS].any()  # counters back to zero
 
 
-@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (16, 256, 1, 50), (8, 128, 2, 64)])
+@pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (16, 256, 1, 50), (8, 128, 2, 64),
+                                     (4, 64, 1, 50)])
 def test_conv_bank_halves(K, Cin, B, T, rng, monkeypatch):
     """The one-launch channel-halves bank (FTMI_BANK_HALVES, c2's prenet bank): bit-identical
     across repeated calls whichever half of a unit arrives last (the two halves' sums are
@@ -274,6 +275,12 @@ def test_conv_bank_halves(K, Cin, B, T, rng, monkeypatch):
     for _ in range(4):
         assert np.array_equal(host(ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3)), a0)
         ops.conv_bank(other, wp2, 4, C, sc[:4 * C], sh[:4 * C], mma=2, w_split=w32)
+    # the stream-order weight image: the same bits, repeatedly
+    img = ops.bank_halves_image(w3, K, Cin, C)
+    assert img.numel() == ops._lib.load().ftmi_conv_bank_halves_image_bytes(Cin, K, C)
+    for _ in range(2):
+        yi = ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, w_image=img)
+        np.testing.assert_array_equal(host(yi), a0)
     assert int(st.item()) == 0
     key = (torch.device('cuda', torch.cuda.current_device()), torch.cuda.current_stream().cuda_stream)
     assert not ops._BANK_WS[key][:ops.BANK_COUNTERS].any()  # counters back to zero
@@ -355,8 +362,8 @@ def test_split_rows_bank_to_proj1(K, Cin, B, T, split_k, rng, monkeypatch):
         ops.conv1d(ys, w1, 3, 1, mma=0, x_split=True)
 
 
-@pytest.mark.parametrize('schedule', ['halves', 'pairs', 'pairs-finish', 'quarters',
-                                      'quarters-finish', 'groups'])
+@pytest.mark.parametrize('schedule', ['halves', 'halves-image', 'pairs', 'pairs-finish',
+                                      'quarters', 'quarters-finish', 'groups'])
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (8, 80, 1, 100), (4, 64, 2, 50),
                                      (16, 256, 2, 64), (16, 256, 1, 37), (2, 32, 1, 128),
                                      (16, 256, 1, 129), (8, 128, 1, 128), (16, 192, 3, 40)])
@@ -368,10 +375,11 @@ def test_conv_bank_skinny_schedules(K, Cin, B, T, schedule, rng, monkeypatch):
     and of a light unit (conv_bank_qb_kernel, FTMI_BANK_QB=1), one group per block
     (FTMI_BANK_BALANCED=0); the split schedules with the in-kernel last-arriver finish
     (FTMI_BANK_LAST=1) or the finish launch; f16x3, against the numpy oracle.  M = 129: two
-    row tiles, the second with one row."""
+    row tiles, the second with one row.  halves-image: the halves kernel reading the
+    stream-order weight image (FTMI_BANK_IMAGE), bit-identical to it reading the planes."""
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
-    monkeypatch.setenv('FTMI_BANK_HALVES', '1' if schedule == 'halves' else '0')
+    monkeypatch.setenv('FTMI_BANK_HALVES', '1' if schedule.startswith('halves') else '0')
     monkeypatch.setenv('FTMI_BANK_BALANCED', '0' if schedule == 'groups' else '1')
     monkeypatch.setenv('FTMI_BANK_QB', '1' if schedule.startswith('quarters') else '0')
     # the tile's last split block finishes in-kernel (FTMI_BANK_LAST, default), or *-finish:
@@ -388,6 +396,13 @@ def test_conv_bank_skinny_schedules(K, Cin, B, T, schedule, rng, monkeypatch):
     w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
     y = ops.conv_bank(dev(x), wp, K, C, dev(sc), dev(sh), mma=2, w_split=w3)
     close(host(y), ref.transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
+    if schedule == 'halves-image':
+        img = ops.bank_halves_image(w3, K, Cin, C)
+        if Cin % 64 == 0 and K % 2 == 0 and (K // 2) * (C // 16) % 8 == 0:
+            assert img is not None
+        if img is not None:
+            yi = ops.conv_bank(dev(x), wp, K, C, dev(sc), dev(sh), mma=2, w_split=w3, w_image=img)
+            np.testing.assert_array_equal(host(yi), host(y))
 
 
 @pytest.mark.parametrize('C,B,T,mma,pre,kernel',
@@ -426,7 +441,7 @@ def test_highway_stack(B, T, Cp, L, rng, monkeypatch):
             hw.W1.bias.normal_(0, 0.1)
     m = m.cuda()
     x = rng.normal(0, 1, (B, T, Cp)).astype(np.float32)
-    *_, w_pre, _, pre3 = m.packed_weights()
+    w_pre, pre3 = m.packed_weights()[3], m.packed_weights()[5]
     hws = [hw.packed_weights() for hw in m.highways]
     w_ih, b_in, _, _, w3 = m.rnn.packed_weights()
     xd = dev(x)

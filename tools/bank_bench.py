@@ -1,5 +1,6 @@
 """c2 prenet bank (B = 1, T = 120, K = 16, Cin = Cout = 256) on the channel-split bank
-schedules: the one-launch channel-halves kernel (default), group pairs per block or
+schedules: the one-launch channel-halves kernel (default; halves-image: reading the
+stream-order weight image), group pairs per block or
 quarter-balanced waves (FTMI_BANK_QB=1), each finished by the finish launch or in-kernel by
 each tile's last split block (FTMI_BANK_LAST=1).  HIP events over back-to-back calls ('warm': the weight planes stay
 Infinity-Cache resident, as in a generate() loop) and per call behind a 512 MiB overwrite
@@ -16,6 +17,7 @@ from forwardtacotron_amd import ops  # noqa: E402
 from forwardtacotron_amd.common_layers import pack_conv  # noqa: E402
 
 VARIANTS = {'halves': {'FTMI_BANK_HALVES': '1'},
+            'halves-image': {'FTMI_BANK_HALVES': '1'},  # + the stream-order weight image
             'pairs+finish': {'FTMI_BANK_HALVES': '0', 'FTMI_BANK_QB': '0', 'FTMI_BANK_LAST': '0'},
             'pairs+last': {'FTMI_BANK_HALVES': '0', 'FTMI_BANK_QB': '0', 'FTMI_BANK_LAST': '1'},
             'qb+finish': {'FTMI_BANK_HALVES': '0', 'FTMI_BANK_QB': '1', 'FTMI_BANK_LAST': '0'},
@@ -32,6 +34,7 @@ def main():
     ws = [rng.normal(0, 1 / np.sqrt(C * k), (C, C, k)).astype(np.float32) for k in range(1, K + 1)]
     wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
     w3 = ops.split_bank_weights(wp, K, C, C, 2)
+    img = ops.bank_halves_image(w3, K, C, C)
     sc = torch.from_numpy(rng.uniform(0.5, 1.5, K * C).astype(np.float32)).cuda()
     sh = torch.from_numpy(rng.normal(0, 0.1, K * C).astype(np.float32)).cuda()
     nbytes = 4.0 * (B * T * C + C * C * K * (K + 1) / 2 + B * T * K * C)
@@ -39,7 +42,8 @@ def main():
     ref = None
     for name in names:
         os.environ.update(VARIANTS[name])
-        fn = lambda: ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3)  # noqa: E731
+        wi = img if name.endswith('-image') else None
+        fn = lambda: ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, w_image=wi)  # noqa: E731
         for _ in range(5):
             y = fn()
         torch.cuda.synchronize()

@@ -1,7 +1,8 @@
 """Phase timeline of the one-launch channel-halves bank (conv_bank_halves_kernel) on the c2
 prenet bank, in the diagnostic build (s_memtime stamps), for each FTMI_BANK_HALVES_DIAG
 variant (0 = the real kernel; 1 no MFMAs, 2 no A-fragment LDS reads, 4 no partner exchange:
-timing only, results invalid).
+timing only, results invalid; 'img' = the real kernel on the stream-order weight image).
+s_memtime counts per XCD, so every stamp is taken relative to its own block's start.
 usage: FTMI_LIB=forwardtacotron_amd/libftmi_stamps.so python tools/bank_halves_stamps.py [diag ...]"""
 import ctypes
 import os
@@ -23,30 +24,31 @@ x = torch.from_numpy(rng.normal(0, 1, (B, T, C)).astype(np.float32)).cuda()
 ws = [rng.normal(0, 1 / np.sqrt(C * k), (C, C, k)).astype(np.float32) for k in range(1, K + 1)]
 wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
 w3 = ops.split_bank_weights(wp, K, C, C, 2)
+img = ops.bank_halves_image(w3, K, C, C)
 sc = torch.ones(K * C, device='cuda')
 sh = torch.zeros(K * C, device='cuda')
 names = ['start', 'slab', 'loop w0', 'loop w7', 'reduced', 'counted', 'end w0', 'end w7']
 for diag in (sys.argv[1:] or ['0', '1', '2', '4']):
-    os.environ['FTMI_BANK_HALVES_DIAG'] = diag
+    os.environ['FTMI_BANK_HALVES_DIAG'] = '0' if diag == 'img' else diag
+    wi = img if diag == 'img' else None
     for _ in range(5):
-        ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3)
+        ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, w_image=wi)
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(20):
-        ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3)
+        ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, w_image=wi)
     b.record()
     torch.cuda.synchronize()
     n = 4096 * 8
     buf = (ctypes.c_ulonglong * n)()
     assert fn(buf, n) == 0
     st = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8)[:256].astype(np.float64)
-    t0 = st[:, 0].min()
-    rel = st - t0
+    rel = st - st[:, :1]
     print(f'diag {diag}: {a.elapsed_time(b) / 20 * 1e3:.1f} us per call (events, host-issued); '
-          f'cycles from the first block start, median (max) over 256 blocks:')
+          f'cycles from each block start, median (max) over 256 blocks:')
     print('   ' + '  '.join(f'{nm} {np.median(rel[:, i]):7.0f} ({rel[:, i].max():6.0f})'
                             for i, nm in enumerate(names)))
     d = rel[:, 2] - rel[:, 1]
     print(f'   wave-0 loop {np.median(d):.0f} cycles (min {d.min():.0f}, max {d.max():.0f}); '
-          f'kernel span {rel[:, 6:8].max():.0f} cycles', flush=True)
+          f'longest block {rel[:, 6:8].max():.0f} cycles', flush=True)

@@ -31,7 +31,7 @@ if len(sys.argv) > 1:  # fused only, the first argv[1] cases
     CASES = CASES[:int(sys.argv[1])]
 for name, M, Cp in CASES:
     m = CBHG(K=2, in_channels=Cp, channels=256, proj_channels=[256, Cp], num_highways=4).cuda()
-    *_, w_pre, _, pre3 = m.packed_weights()
+    w_pre, pre3 = m.packed_weights()[3], m.packed_weights()[5]
     hws = [hw.packed_weights() for hw in m.highways]
     w_ih, b_in, _, _, w3 = m.rnn.packed_weights()
     x = torch.randn(1, M, Cp, device='cuda')
