@@ -159,9 +159,9 @@ def time_prenet_bank(model, x, reps: int = 20):
     bank_w, scale, shift, _, bank3, _, img = cb.packed_weights()
     pooled = ops.bank_pools(h, cb.K, cb.channels, w_split=bank3)
 
-    def call():
+    def call(image=img):
         return ops.conv_bank(h, bank_w, cb.K, cb.channels, scale, shift, w_split=bank3,
-                             pool=pooled, split_out=pooled and ops.SPLIT_ROWS, w_image=img)
+                             pool=pooled, split_out=pooled and ops.SPLIT_ROWS, w_image=image)
 
     def timed(fn):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -177,8 +177,11 @@ def time_prenet_bank(model, x, reps: int = 20):
     eager = timed(lambda: [call() for _ in range(reps)]) / reps
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=x.device)
     graphs = {}
-    for name, body in (('warm', lambda: call()), ('flush', lambda: flush.fill_(1)),
-                       ('cold', lambda: (flush.fill_(1), call()))):
+    bodies = [('warm', lambda: call()), ('flush', lambda: flush.fill_(1)),
+              ('cold', lambda: (flush.fill_(1), call()))]
+    if img is not None:  # A/B: the same bank reading the split planes instead of the image
+        bodies.append(('planes', lambda: call(None)))
+    for name, body in bodies:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             for _ in range(reps):
@@ -187,8 +190,10 @@ def time_prenet_bank(model, x, reps: int = 20):
         graphs[name] = g
     warm = timed(graphs['warm'].replay) / reps
     cold = (timed(graphs['cold'].replay) - timed(graphs['flush'].replay)) / reps
+    planes = timed(graphs['planes'].replay) / reps if img is not None else None
     del graphs, flush
-    return {'warm': warm, 'eager': eager, 'cold': cold}
+    return {'warm': warm, 'eager': eager, 'cold': cold, 'planes': planes,
+            'weights': 'stream-order image' if img is not None else 'split planes'}
 
 
 def log(*a):
@@ -474,6 +479,9 @@ def main():
                 prenet['cold_basis'] = ('each call behind a 512 MiB overwrite of another buffer '
                                         '(weights from HBM): graph [overwrite, call] minus graph '
                                         '[overwrite], per call')
+                prenet['weights_read'] = pb['weights']
+                if pb['planes'] is not None:
+                    prenet['warm_ms_reading_split_planes'] = round(pb['planes'], 4)
         value = frames / elapsed
         # valid frames: frames of the non-pad phonemes (the rest of B * T_mel is padding)
         tok = (x_np != 0) if world == 1 else None

@@ -2420,13 +2420,12 @@ __global__ __launch_bounds__(512, 1) void conv_bank_qb_kernel(const GemmParams p
 //    scaled tail, the skinny kernel's layout and tap masks);
 //  * the 8 waves split the unit's 4 (K + 1) (group, tap, chunk) steps round-robin and meet
 //    in LDS in wave order; the two halves meet through memory: both write their sums
-//    write-through (16-B sc1 stores, fragment order), wait for them, and bump the unit's
-//    counter (agent-scope atomic, after a barrier behind every storing wave's vmcnt(0));
-//    the block whose add returns 1 resets the counter, reads its partner's sums (16-B sc1
-//    loads), adds them to its own (a + b == b + a: deterministic whichever half arrives
-//    last) and applies colscale, ReLU and the BN affine (MI355X_MICROARCH.md "Valid forms",
-//    the first row of the sc1 table).  No split partials for a finish launch, no second
-//    launch.
+//    write-through (16-B sc1 stores, fragment order); each wave waits for its own stores and
+//    bumps its slice's counter (agent-scope atomic, 8 per unit); the wave whose add returns
+//    1 resets the counter, reads its partner wave's sums (16-B sc1 loads), adds them to its
+//    own (a + b == b + a: deterministic whichever half arrives last) and applies colscale,
+//    ReLU and the BN affine (MI355X_MICROARCH.md "Valid forms", the first row of the sc1
+//    table, at wave granularity).  No split partials for a finish launch, no second launch.
 constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 
 #ifdef FTMI_SKINNY_STAMPS
@@ -2454,7 +2453,8 @@ constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 // the start of the split-weight buffer (c2 prenet: 256 x 139 KB of its 53 MB; results
 // invalid), bit 5 = every weight load before the slab wait, bit 6 = a step's 8 row
 // fragments read at once instead of in two blocks of 4, bit 7 = every weight load up front
-// behind a workgroup barrier after the slab loads' issue (bits 5-7: valid results)
+// behind a workgroup barrier after the slab loads' issue, bits 8 / 9 = the first 2 / 4 steps'
+// weight loads before the slab wait instead of 6 (bits 5-9: valid results)
 //
 // Address arithmetic is compile-time wherever it can be (measured with the phase stamps of a
 // first version: the slab staging took ~12 k cycles with NO weight loads at all — ~1,300
@@ -2469,7 +2469,7 @@ constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 // a round trip each before the first data load can issue: KT (groups) and NCT (16-column sets
 // per group) are template parameters for the c2 prenet bank (16, 16), so a block's group
 // index comes from blockIdx alone and every argument load issues in the first batch; 0 = read
-// them at run time (other banks).  The weight loads of the first NPRE steps go out with the
+// them at run time (other banks).  The weight loads of the first NPRE (6) steps go out with the
 // slab, the rest right after the barrier: the slab wait no longer queues behind the whole
 // 139 KB stream (vector memory returns in issue order), and the loop's first steps overlap
 // the stream's remainder.
@@ -2554,7 +2554,12 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
       rb1[i] = *(const f16x8 *)(src + (hv ? planeh : planel));
     }
   };
-  constexpr int NPRE = (DIAG & (32 | 128)) ? NS : (NS < 2 ? NS : 2);  // bit 5: every step up front
+  // bit 5: every step up front; bits 8 / 9: the first 2 / 4 steps (timing variants); else
+  // 6 (r4g stamps, image kernel: 2 / 4 / 6 steps 18.3 / 17.6 / 17.5 us per call, the
+  // longest block 33.7 / 33.3 / 32.6 k cycles; every step up front behind a barrier, bit 7:
+  // 18.7, the slab wait then queues behind the whole stream)
+  constexpr int NPRE0 = (DIAG & 256) ? 2 : (DIAG & 512) ? 4 : 6;
+  constexpr int NPRE = (DIAG & (32 | 128)) ? NS : (NS < NPRE0 ? NS : NPRE0);
   if constexpr (DIAG & 128) {
     // every wave's slab loads are issued before any wave's weight loads (a barrier with no
     // wait: vector memory is served in issue order per CU, so the slab no longer queues
@@ -2723,27 +2728,30 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
     v[r] = s;
   }
   BHSTAMP(4, 0);
-  // ---- write-through publish of this half's sums, then the unit's arrival counter -------
+  // ---- write-through publish of this half's sums, then an arrival counter PER WAVE: wave w
+  // owns row fragment w of both groups (items e = tid + 512 r), publishes them, waits for its
+  // own stores and adds to the unit's counter w; the wave whose add returns 1 (its partner
+  // wave in the other half has published) finishes that slice.  No block barrier: each
+  // slice is finished by whichever half's wave arrives last (MI355X_MICROARCH.md "Valid
+  // forms": each storing wave signalling for itself, the last adder told by the value its
+  // add returned, loads after that add has returned) ----
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.part, (short)0, 0x7FFFFFF0, 0x00020000);
   const int ubase = (u * 2) * NIT * 16;  // bytes: [unit][half][item]; < 2^31 (host check)
 #pragma unroll
   for (int r = 0; r < IPT; ++r)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[r]), rs,
                                            ubase + (h * NIT + eo[r]) * 16, 0, 16 /* sc1 */);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores done
-  __syncthreads();
-  __shared__ int s_last;
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(p.tile_cnt + u, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == 1u;
-    if (old == 1u)  // both halves have added: zero for the next launch
-      __hip_atomic_store(p.tile_cnt + u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores done
+  unsigned old = 0;
+  if (lane == 0) {
+    unsigned *const cnt = p.tile_cnt + u * 8 + wave;
+    old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == 1u)  // both halves' waves have added: zero for the next launch
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __syncthreads();
+  const bool last = (DIAG & 4) ? h == 0 : __builtin_amdgcn_readfirstlane(old) == 1u;
   BHSTAMP(5, 0);
-  if (DIAG & 4) s_last = h == 0;  // (every thread reads the value it wrote)
-  if (s_last) {
+  if (last) {
     u32x4 pr[IPT];
 #pragma unroll
     for (int r = 0; r < IPT; ++r)
@@ -3807,7 +3815,7 @@ static bool bank_halves_ok(const GemmParams &p) {
   if (!p.y || p.yt || p.residual || p.x_split || p.pool_out || p.y_split_c) return false;
   if (!p.tile_cnt || !p.part || p.g[0].N % 16) return false;
   const int units = (p.ngroups / 2) * (p.g[0].N / 16);
-  if (units % 8 || units > FTMI_BANK_COUNTERS) return false;
+  if (units % 8 || units * 8 > FTMI_BANK_COUNTERS) return false;  // 8 counters per unit
   for (int i = 0; i < p.ngroups; ++i)
     if (p.g[i].k != p.ngroups - i || p.g[i].N != p.g[0].N || !p.g[i].w3 || !p.g[i].colscale)
       return false;
@@ -3834,7 +3842,19 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
     default: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 4, D_>), grid, block, 0, s, p);       \
   }
   const bool prenet = p.ngroups == 16 && p.g[0].N == 256 && nch == 4;  // c2: (KT, NCT) = (16, 16)
-  if (p.wimg) {  // the stream-order weight image (no timing variants)
+  if (p.wimg && prenet && diag) {  // timing variants of the image kernel (c2 prenet only)
+    switch (diag) {
+#define FTMI_BH_DIAG(D_)                                                                          \
+  case D_:                                                                                        \
+    hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, D_, 16, 16, true>), grid, block, 0, s, p);    \
+    break;
+      FTMI_BH_DIAG(1) FTMI_BH_DIAG(2) FTMI_BH_DIAG(4) FTMI_BH_DIAG(32) FTMI_BH_DIAG(128)
+      FTMI_BH_DIAG(256) FTMI_BH_DIAG(512)
+#undef FTMI_BH_DIAG
+      default:
+        hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16, true>), grid, block, 0, s, p);
+    }
+  } else if (p.wimg) {  // the stream-order weight image
 #define FTMI_BH_PK(MI_)                                                                                  \
   switch (nch) {                                                                                         \
     case 1: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 1, 0, 0, 0, true>), grid, block, 0, s, p); break; \
@@ -4093,7 +4113,7 @@ int set_bank_groups(GemmParams &p, const float *w, const void *w_split, int K, i
 bool bank_halves_shape(int Cin, int K, int Cout) {
   return Cin > 0 && Cin % 64 == 0 && Cin <= 2 * BH_MAXCH * 32 && K >= 2 && K % 2 == 0 &&
          K <= MAX_GROUPS && Cout > 0 && Cout % 16 == 0 && ((K / 2) * (Cout / 16)) % 8 == 0 &&
-         (K / 2) * (Cout / 16) <= FTMI_BANK_COUNTERS;
+         (K / 2) * (Cout / 16) * 8 <= FTMI_BANK_COUNTERS;
 }
 }  // namespace
 

@@ -455,11 +455,12 @@ BANK_HALVES, BANK_IMAGE = 16, 32  # include/ftmi.h FTMI_BANK_HALVES, FTMI_BANK_I
 def _bank_halves(mma: int, B: int, T: int, Cin: int, K: int, Cout: int) -> bool:
     """Whether conv_bank takes the one-launch channel-halves kernel (gemm.hip
     bank_halves_ok): f16x3, one row tile of at most 128 rows (batch-1 generation, BASELINE
-    config c2), Cin a multiple of 64 up to 256, even K, (K / 2)(Cout / 16) a multiple of 8.
+    config c2), Cin a multiple of 64 up to 256, even K, (K / 2)(Cout / 16) a multiple of 8 up
+    to 512 (8 arrival counters per unit).
     FTMI_BANK_HALVES=0 (read per call) keeps the channel-split kernel + finish."""
     return (os.environ.get('FTMI_BANK_HALVES', '1') != '0' and mma == 2 and 0 < B * T <= 128
             and Cin % 64 == 0 and Cin <= 256 and K % 2 == 0 and Cout % 16 == 0
-            and (K // 2) * (Cout // 16) % 8 == 0 and K <= 16)
+            and (K // 2) * (Cout // 16) % 8 == 0 and (K // 2) * (Cout // 16) <= 512 and K <= 16)
 _BANK_WS = {}
 
 

@@ -75,7 +75,7 @@ enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
                                  input channels), each wave's weight stream issued at once, the
                                  unit's two halves combined in-kernel by the last to arrive
                                  (deterministic).  B*T <= 128, Cin % 64 == 0, Cin <= 256, K even,
-                                 (K / 2)(Cout / 16) % 8 == 0; else FTMI_E_UNSUPPORTED.  split_ws:
+                                 (K / 2)(Cout / 16) % 8 == 0 and <= 512; else FTMI_E_UNSUPPORTED.  split_ws:
                                  ftmi_conv_bank_halves_ws_floats(B, T, K, Cout) floats, the first
                                  FTMI_BANK_COUNTERS zeroed once by the caller (every launch leaves
                                  them zero); split_k is ignored.  One workspace per stream. */

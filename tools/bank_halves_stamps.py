@@ -29,8 +29,10 @@ sc = torch.ones(K * C, device='cuda')
 sh = torch.zeros(K * C, device='cuda')
 names = ['start', 'slab', 'loop w0', 'loop w7', 'reduced', 'counted', 'end w0', 'end w7']
 for diag in (sys.argv[1:] or ['0', '1', '2', '4']):
-    os.environ['FTMI_BANK_HALVES_DIAG'] = '0' if diag == 'img' else diag
-    wi = img if diag == 'img' else None
+    # 'img' = the image kernel; 'img:<bits>' = its timing variant <bits>
+    os.environ['FTMI_BANK_HALVES_DIAG'] = diag.split(':')[1] if ':' in diag else (
+        '0' if diag == 'img' else diag)
+    wi = img if diag.startswith('img') else None
     for _ in range(5):
         ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, w_image=wi)
     torch.cuda.synchronize()
