@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 16
+ABI_VERSION = 17
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -34,6 +34,7 @@ class ConvArgs(ctypes.Structure):
         ('residual', P), ('res_stride', c_int64),
         ('y', P), ('y_stride', c_int64), ('yt', P), ('T_out', c_int), ('mma', c_int),
         ('split_k', c_int), ('split_ws', P), ('w_split', P), ('status', P), ('x_split', c_int),
+        ('x_plane', c_int64), ('x_fin', P),
     ]
 
 

@@ -107,6 +107,13 @@ struct GemmParams {
   // conv_bank_halves_kernel (FTMI_BANK_IMAGE): the stream-order weight image — every wave's
   // weight fragments in the order it loads them, 1 KB per wave load (bank_halves_pack_kernel)
   const _Float16 *wimg;
+  // conv_bank_halves_kernel PAIR (FTMI_BANK_PAIR): each half's raw sums go to its own plane,
+  // y + h * y_plane; conv_gemm_skinny_kernel PAIR (ftmi_conv_args.x_fin): the operand row is
+  // the bank epilogue of the two planes' sum, x_fin = [4][Cin] (colscale, bias, BN scale,
+  // BN shift), the second plane at x + x_plane
+  int64_t y_plane;
+  int64_t x_plane;
+  const float *x_fin;
   GemmGroup g[MAX_GROUPS];
 };
 
@@ -1938,7 +1945,11 @@ __device__ __forceinline__ bool bank_last_reduce(const GemmParams &p, int gi, in
 // bit 0 = the A fragments read once before the loop (no LDS reads in it), bit 1 = no MFMAs
 // (the loaded weights feed one VALU add), bit 2 = every weight load from one L2-hot line
 // LAST (BANK, split > 1): the tile's last split block finishes it (see conv_bank_qb_kernel)
-template <bool MAXPOOL, bool BANK = false, int DIAG = 0, bool LAST = false>
+// PAIR: the operand is a FTMI_BANK_PAIR bank output — x and x + x_plane hold the two
+// channel halves' raw sums; each staged value is the bank's own finish of their sum
+// (s * colscale + bias, ReLU, BN affine: the same expressions, so bit-identical), taken
+// before the maxpool
+template <bool MAXPOOL, bool BANK = false, int DIAG = 0, bool LAST = false, bool PAIR = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmParams p) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[SK_CPB * 2 * SK_AIMG];
   SKSTAMP(0);
@@ -1974,6 +1985,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
   constexpr int SK_ASLOTS = (SK_CPB * SK_SR + 63) / 64;
   const int seg = tid & 7;
   f32x4 av[SK_ASLOTS], au[MAXPOOL ? SK_ASLOTS : 1];
+  f32x4 bv[PAIR ? SK_ASLOTS : 1], bu[PAIR && MAXPOOL ? SK_ASLOTS : 1];
+  static_assert(!PAIR || SK_CPB == 2, "bank_finish selects between two chunks");
 #pragma unroll
   for (int i = 0; i < SK_ASLOTS; ++i) {
     const int r = min((tid >> 3) + 64 * i, nch * SK_SR - 1), c = r / SK_SR, sr = r - c * SK_SR;
@@ -1982,17 +1995,50 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
     const float *src = p.x + (int64_t)m * p.x_stride + ch;
     av[i] = *(const f32x4 *)src;
+    if constexpr (PAIR) bv[i] = *(const f32x4 *)(src + p.x_plane);
     // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
-    if constexpr (MAXPOOL) au[i] = *(const f32x4 *)(src - (m % p.T > 0 ? p.x_stride : 0));
+    if constexpr (MAXPOOL) {
+      const float *prv = src - (m % p.T > 0 ? p.x_stride : 0);
+      au[i] = *(const f32x4 *)prv;
+      if constexpr (PAIR) bu[i] = *(const f32x4 *)(prv + p.x_plane);
+    }
   }
+  // PAIR: the bank epilogue parameters of this thread's channels in each of its chunks
+  f32x4 fcs[SK_CPB], fbi[SK_CPB], fsc[SK_CPB], fsh[SK_CPB];  // (dead without PAIR)
+  if constexpr (PAIR) {
+#pragma unroll
+    for (int c = 0; c < SK_CPB; ++c) {
+      const int ch0 = (c_begin + min(c, nch - 1)) * 32 + seg * 4, ch = ch0 < Cin ? ch0 : 0;
+      fcs[c] = *(const f32x4 *)(p.x_fin + ch);
+      fbi[c] = *(const f32x4 *)(p.x_fin + Cin + ch);
+      fsc[c] = *(const f32x4 *)(p.x_fin + 2 * Cin + ch);
+      fsh[c] = *(const f32x4 *)(p.x_fin + 3 * Cin + ch);
+    }
+  }
+  bool pbad = false;  // PAIR: a non-finite bank sum (the bank's own status bit 0)
+  auto bank_finish = [&](f32x4 a, f32x4 b, int c) {
+    const f32x4 cs = c ? fcs[SK_CPB - 1] : fcs[0], bi = c ? fbi[SK_CPB - 1] : fbi[0];
+    const f32x4 sc = c ? fsc[SK_CPB - 1] : fsc[0], sh = c ? fsh[SK_CPB - 1] : fsh[0];
+    f32x4 y;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float sum = a[q] + b[q];  // the two halves (commutative: as the bank adds them)
+      pbad |= !__builtin_isfinite(sum);
+      float t = sum * cs[q] + bi[q];
+      t = fmaxf(t, 0.f);
+      y[q] = t * sc[q] + sh[q];
+    }
+    return y;
+  };
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < SK_ASLOTS; ++i) {
     const int r = (tid >> 3) + 64 * i, c = r / SK_SR, sr = r - c * SK_SR;
     if (r >= nch * SK_SR) break;
     f32x4 x = av[i];
+    if constexpr (PAIR) x = bank_finish(av[i], bv[i], c);
     if ((c_begin + c) * 32 + seg * 4 >= Cin) x = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if constexpr (MAXPOOL) x = fmax4(x, au[i]);
+    if constexpr (MAXPOOL) x = fmax4(x, PAIR ? bank_finish(au[i], bu[i], c) : au[i]);
     amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
     f16x4 h, t;
     split2h(x, h, t);
@@ -2006,7 +2052,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
   }
   __syncthreads();
   SKSTAMP(1);
-  bool bad = !(amax <= 65504.f);
+  bool bad = !(amax <= 65504.f) || pbad;
 
   // 8 waves: wave w multiplies columns col0 + [0, 16) (column set w & 3) over one half of
   // the steps (w >> 2); the two halves meet in LDS after the loop.  BANK: unit slot cw =
@@ -2479,7 +2525,13 @@ constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 // is one contiguous 1 KB run (from the planes it touches 16 half-used 128-B lines, their
 // other halves loaded by the next step).  Measured with the bit-3 timing variant's layout
 // (r4c stamps): 17.8 vs 20.4 us per call.
-template <int MI, int NCH, int DIAG = 0, int KT = 0, int NCT = 0, bool PK = false>
+//
+// PAIR (FTMI_BANK_PAIR): no exchange at all — each half stores its raw sums into its own
+// plane of y and the consumer (proj1's operand staging, conv_gemm_skinny_kernel PAIR) adds
+// the two planes and applies colscale, ReLU and the BN affine with the same expressions,
+// before its maxpool: bit-identical to this kernel's own finish.
+template <int MI, int NCH, int DIAG = 0, int KT = 0, int NCT = 0, bool PK = false,
+          bool PAIR = false>
 __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmParams p) {
   BHSTAMP(0, 0);
   constexpr int RM = MI * 16;
@@ -2728,6 +2780,24 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
     v[r] = s;
   }
   BHSTAMP(4, 0);
+  if constexpr (PAIR) {  // this half's raw sums into plane h: no exchange, no counter
+    float *const yp = p.y + h * p.y_plane;
+#pragma unroll
+    for (int r = 0; r < IPT; ++r) {
+      const int e = eo[r], ug = e / (MI * 64), mi = (e >> 6) % MI;
+      float *const yc = yp + (ug ? GL.ycol0 : GH.ycol0) + col;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = mi * 16 + 4 * fs + i;
+        if (row < p.M) yc[(int64_t)row * p.y_stride] = v[r][i];
+      }
+    }
+    if (bad && p.status) atomicOr(p.status, 1u);
+    BHSTAMP(5, 0);
+    BHSTAMP(6, 0);
+    BHSTAMP(7, 448);
+    return;
+  }
   // ---- write-through publish of this half's sums, then an arrival counter PER WAVE: wave w
   // owns row fragment w of both groups (items e = tid + 512 r), publishes them, waits for its
   // own stores and adds to the unit's counter w; the wave whose add returns 1 (its partner
@@ -3747,7 +3817,7 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
   }
   // a CBHG bank (groups k = K .. 1, even K, 16-column multiples): the balanced schedule
   bool bank = q.ngroups >= 2 && q.ngroups % 2 == 0 && !maxpool && epi == EPI_CONV &&
-              q.g[0].N % 32 == 0 && bank_balanced_enabled();
+              q.g[0].N % 32 == 0 && bank_balanced_enabled() && !q.x_fin;
   for (int i = 0; bank && i < q.ngroups; ++i) bank = q.g[i].k == q.ngroups - i;
   if (bank) {
     dim3 grid(MT * (q.ngroups / 2) * (q.g[0].N / 32), q.split), block(512);
@@ -3781,7 +3851,11 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
     }
   } else {
     dim3 grid(MT * q.ngroups * NT, q.split), block(512);
-    if (maxpool)
+    if (q.x_fin && maxpool)
+      hipLaunchKernelGGL((conv_gemm_skinny_kernel<true, false, 0, false, true>), grid, block, 0, s, q);
+    else if (q.x_fin)
+      hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, false, 0, false, true>), grid, block, 0, s, q);
+    else if (maxpool)
       hipLaunchKernelGGL(conv_gemm_skinny_kernel<true>, grid, block, 0, s, q);
     else
       hipLaunchKernelGGL(conv_gemm_skinny_kernel<false>, grid, block, 0, s, q);
@@ -3842,7 +3916,29 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
     default: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 4, D_>), grid, block, 0, s, p);       \
   }
   const bool prenet = p.ngroups == 16 && p.g[0].N == 256 && nch == 4;  // c2: (KT, NCT) = (16, 16)
-  if (p.wimg && prenet && diag) {  // timing variants of the image kernel (c2 prenet only)
+  if (p.y_plane) {  // FTMI_BANK_PAIR: raw half sums, finished by the consumer
+#define FTMI_BH_PR(MI_, PK_)                                                                                 \
+  switch (nch) {                                                                                             \
+    case 1: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 1, 0, 0, 0, PK_, true>), grid, block, 0, s, p); break; \
+    case 2: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 2, 0, 0, 0, PK_, true>), grid, block, 0, s, p); break; \
+    case 3: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 3, 0, 0, 0, PK_, true>), grid, block, 0, s, p); break; \
+    default: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 4, 0, 0, 0, PK_, true>), grid, block, 0, s, p);       \
+  }
+    if (p.wimg && prenet && p.M > 64) {
+      hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16, true, true>), grid, block, 0, s, p);
+    } else if (p.wimg) {
+      if (p.M <= 64) {
+        FTMI_BH_PR(4, true)
+      } else {
+        FTMI_BH_PR(8, true)
+      }
+    } else if (p.M <= 64) {
+      FTMI_BH_PR(4, false)
+    } else {
+      FTMI_BH_PR(8, false)
+    }
+#undef FTMI_BH_PR
+  } else if (p.wimg && prenet && diag) {  // timing variants of the image kernel (c2 prenet only)
     switch (diag) {
 #define FTMI_BH_DIAG(D_)                                                                          \
   case D_:                                                                                        \
@@ -3907,6 +4003,12 @@ int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hip
           p.y && slab_ok(q, epi)))
       return FTMI_E_UNSUPPORTED;
     return launch_slab(q, epi, false, s);
+  }
+  if (p.x_fin) {  // a FTMI_BANK_PAIR operand: only the skinny kernel finishes it in staging
+    if (!(mma == 2 && presplit && epi == EPI_CONV && p.ngroups == 1 && !p.x_split &&
+          !p.y_split_c && skinny_ok(p, epi)))
+      return FTMI_E_UNSUPPORTED;
+    return launch_skinny(p, epi, maxpool, s);
   }
   if (p.y_split_c) return FTMI_E_UNSUPPORTED;  // split output rows: pool_out only
   if (p.x_split) {  // split operand rows: only the slab kernel stages them
@@ -4043,6 +4145,10 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   p.x_split = a->x_split != 0;
   if (p.x_split && (a->mma != 2 || a->maxpool || a->x_stride < a->Cin))
     return FTMI_E_UNSUPPORTED;
+  p.x_fin = a->x_fin;
+  p.x_plane = a->x_plane;
+  if (p.x_fin && (!ftmi_aligned16(a->x_fin) || (a->x_plane & 3) || a->Cin % 4))
+    return FTMI_E_ALIGN;
   GemmGroup &g = p.g[0];
   g.w = a->w;
   g.Kpad = (a->k * a->Cin + X6_BK - 1) / X6_BK * X6_BK;
@@ -4203,12 +4309,14 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
   p.y_stride = y_stride;
   p.status = status;
   if (pool_out & ~(FTMI_BANK_POOL | FTMI_BANK_Y_SPLIT | FTMI_BANK_X_SPLIT | FTMI_BANK_LAST |
-                   FTMI_BANK_HALVES | FTMI_BANK_IMAGE))
+                   FTMI_BANK_HALVES | FTMI_BANK_IMAGE | FTMI_BANK_PAIR))
     return FTMI_E_ARG;
   const bool halves = (pool_out & FTMI_BANK_HALVES) != 0;
   const bool image = (pool_out & FTMI_BANK_IMAGE) != 0;
-  if (image && !halves) return FTMI_E_ARG;
-  if (halves && (!split_ws || mma != 2 || (pool_out & ~(FTMI_BANK_HALVES | FTMI_BANK_IMAGE))))
+  const bool pair = (pool_out & FTMI_BANK_PAIR) != 0;
+  if ((image || pair) && !halves) return FTMI_E_ARG;
+  if (halves && (!split_ws || mma != 2 ||
+                 (pool_out & ~(FTMI_BANK_HALVES | FTMI_BANK_IMAGE | FTMI_BANK_PAIR))))
     return FTMI_E_ARG;
   if ((pool_out & FTMI_BANK_LAST) && (split_k <= 1 || !split_ws)) return FTMI_E_ARG;
   p.pool_out = pool_out & FTMI_BANK_POOL;
@@ -4234,6 +4342,7 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
         p.g[gi].colscale = cs + (int64_t)(K - 1 - gi) * Cout;
       }
     }
+    if (pair) p.y_plane = (int64_t)p.M * y_stride;  // the second half's plane
     if (!bank_halves_ok(p)) return FTMI_E_UNSUPPORTED;
     return launch_bank_halves(p, ftmi_hs(stream));
   }

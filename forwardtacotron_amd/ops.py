@@ -312,15 +312,25 @@ def split_bank_weights(w: torch.Tensor, K: int, Cin: int, Cout: int,
 def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, relu=False,
            bn=None, maxpool=False, residual=None, out=None, out_t=None, want_y=True,
            T_out: int = 0, mma: Optional[int] = None, w_split: Optional[torch.Tensor] = None,
-           x_split: bool = False):
+           x_split: bool = False, x_fin: Optional[torch.Tensor] = None):
     """Fused Conv1d (+bias, ReLU, BN, residual) on a channels-last (B, T, Cin) view.
 
     w: packed [N][k*Cin].  Returns (y, yt) where y is (B, T_out, N) (or `out`) and yt is
     the optional (B, N, T_out) transposed copy (`out_t`).  w_split: optional
     `split_weights(w)` (bf16x6 path without the per-call weight split).  x_split: x holds
     f16x3 split rows (include/ftmi.h, e.g. conv_bank(split_out=True)); f16x3 slab kernel
-    only (the C side refuses other shapes with FTMI_E_UNSUPPORTED).
+    only (the C side refuses other shapes with FTMI_E_UNSUPPORTED).  x_fin: x is a
+    conv_bank(pair=True) output (2, B, T, Cin) and the operand is the bank's finish of its
+    two planes' sum, x_fin = (4, Cin) colscale / bias / BN scale / BN shift (few-row kernel
+    only: FTMI_E_UNSUPPORTED elsewhere).
     """
+    x_plane = 0
+    if x_fin is not None:
+        if x.dim() != 4 or x.size(0) != 2:
+            raise ValueError('x_fin: a (2, B, T, C) bank pair expected')
+        _dev(x_fin)
+        x_plane = (x[1].data_ptr() - x[0].data_ptr()) // 4
+        x = x[0]
     _dev(x, w, bias, residual, out, out_t, w_split)
     B, T, Cin, xs = _rows(x)
     N = w.size(0)
@@ -350,6 +360,8 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
     a.mma, a.w_split = _gemm_mma(mma, w_split)
     a.status = status_word(x.device).data_ptr()
     a.x_split = int(x_split)
+    if x_fin is not None:
+        a.x_plane, a.x_fin = x_plane, x_fin.data_ptr()
     M = B * To
     if _skinny(a.mma, T, To, Cin, k, M, N):
         sk = _skinny_split(Cin)
@@ -359,9 +371,10 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
         part = torch.empty(sk * M * N, device=x.device, dtype=_f32)
         a.split_k, a.split_ws = sk, part.data_ptr()
     label = (f'conv1d[M={M},N={N},K={k * Cin}{",maxpool" if maxpool else ""}'
-             f'{",xsplit" if x_split else ""},mma={a.mma}]')
+             f'{",xsplit" if x_split else ""}{",xpair" if x_fin is not None else ""},mma={a.mma}]')
     launch('ftmi_conv1d', label, 2.0 * M * N * k * Cin,
-           4.0 * (B * T * Cin + N * k * Cin + M * N * (1 + (residual is not None))),
+           4.0 * (B * T * Cin * (1 + (x_fin is not None)) + N * k * Cin
+                  + M * N * (1 + (residual is not None))),
            ctypes.byref(a), _stream())
     return y, out_t
 
@@ -409,17 +422,21 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
               shift: torch.Tensor, mma: Optional[int] = None,
               w_split: Optional[torch.Tensor] = None, pool: bool = False,
               split_out: bool = False, x_split: bool = False,
-              w_image: Optional[torch.Tensor] = None) -> torch.Tensor:
+              w_image: Optional[torch.Tensor] = None, pair: bool = False) -> torch.Tensor:
     """CBHG conv bank, (B, T, Cin) -> (B, T, K*Cout); pool: the maxpool(2, 1) of it
     (common_layers.py:73,100), stored by the bank kernel (see bank_pools); split_out (with
     pool): stored as f16x3 split rows for proj1 (conv1d(x_split=True)); x_split: x holds
     split rows (split_rows); w_image: `bank_halves_image(w_split, ...)`, read instead of
-    w_split where the one-launch few-row kernel runs (same results bit for bit)."""
+    w_split where the one-launch few-row kernel runs (same results bit for bit); pair
+    (`bank_pair_ok`): the few-row kernel without its finish — returns (2, B, T, K*Cout), the
+    two channel halves' raw sums, which conv1d(x_fin=...) finishes in its operand staging."""
     if split_out and not pool:
         raise ValueError('split_out needs pool')
     _dev(x, w, scale, shift, w_split)
     B, T, Cin, xs = _rows(x)
-    y = torch.empty(B, T, K * Cout, device=x.device, dtype=_f32)
+    if pair and not bank_pair_ok(x, K, Cout, mma, w_split):
+        raise ValueError('conv_bank(pair=True) needs the one-launch few-row kernel (bank_pair_ok)')
+    y = torch.empty((2,) * pair + (B, T, K * Cout), device=x.device, dtype=_f32)
     M = B * T
     flops = 2.0 * M * Cout * Cin * K * (K + 1) / 2
     mma, wsp = _gemm_mma(mma, w_split)
@@ -431,6 +448,8 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
         if w_image is not None:
             _dev(w_image)
             wsp, last = w_image.data_ptr(), BANK_HALVES | BANK_IMAGE
+        if pair:
+            last |= BANK_PAIR
     elif not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
         sk = _skinny_split(Cin)  # weight-streaming kernel: partial sums, finished in order
         if os.environ.get('FTMI_BANK_LAST', '0') != '0':
@@ -439,17 +458,31 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
         else:
             part = torch.empty(sk * M * K * Cout, device=x.device, dtype=_f32)
     launch('ftmi_conv_bank_split', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}'
-           f'{",pool" if pool else ""}{",split" if split_out else ""}{",xsplit" if x_split else ""}]',
+           f'{",pool" if pool else ""}{",split" if split_out else ""}{",xsplit" if x_split else ""}'
+           f'{",pair" if pair else ""}]',
            flops, 4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
            x.data_ptr(), xs, B, T, Cin, w.data_ptr(), wsp, K, Cout,
-           scale.data_ptr(), shift.data_ptr(), y.data_ptr(), y.stride(1), mma,
+           scale.data_ptr(), shift.data_ptr(), y.data_ptr(), y.stride(-2), mma,
            status_word(x.device).data_ptr(), sk, _ptr(part),
            int(pool) | (2 * int(split_out)) | (4 * int(x_split)) | last, _stream())
     return y
 
 
 BANK_LAST, BANK_COUNTERS = 8, 4096  # include/ftmi.h FTMI_BANK_LAST, FTMI_BANK_COUNTERS
-BANK_HALVES, BANK_IMAGE = 16, 32  # include/ftmi.h FTMI_BANK_HALVES, FTMI_BANK_IMAGE
+BANK_HALVES, BANK_IMAGE, BANK_PAIR = 16, 32, 64  # include/ftmi.h FTMI_BANK_HALVES / _IMAGE / _PAIR
+# FTMI_BANK_PAIR=1 (read per call; default 0): the few-row bank leaves its two raw channel
+# halves and proj1's operand staging finishes them.  Measured at c2 (r4m, HIP graphs): bank
+# 14.7 us instead of 17.2, but proj1 20.2 instead of 17.7 us — the second plane's loads in
+# proj1's prologue cost what the exchange did (bank + proj1 34.9 us either way): off.
+
+
+def bank_pair_ok(x: torch.Tensor, K: int, Cout: int, mma: Optional[int] = None,
+                 w_split=None) -> bool:
+    """Whether conv_bank(pair=True) applies: the one-launch few-row kernel (_bank_halves) on
+    a plain (not split, not pooled) operand, FTMI_BANK_PAIR=1 (opt-in)."""
+    m, _ = _gemm_mma(mma, w_split)
+    return (os.environ.get('FTMI_BANK_PAIR', '0') != '0' and x.dim() == 3
+            and _bank_halves(m, x.size(0), x.size(1), x.size(2), K, Cout))
 
 
 def _bank_halves(mma: int, B: int, T: int, Cin: int, K: int, Cout: int) -> bool:

@@ -79,15 +79,20 @@ enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
                                  ftmi_conv_bank_halves_ws_floats(B, T, K, Cout) floats, the first
                                  FTMI_BANK_COUNTERS zeroed once by the caller (every launch leaves
                                  them zero); split_k is ignored.  One workspace per stream. */
-       FTMI_BANK_IMAGE = 32   /* ABI 16, with FTMI_BANK_HALVES: w_split is the bank's
+       FTMI_BANK_IMAGE = 32,  /* ABI 16, with FTMI_BANK_HALVES: w_split is the bank's
                                  stream-order weight image (ftmi_conv_bank_halves_image), which
                                  the kernel reads as one contiguous 1 KB run per wave load;
-                                 same results bit for bit. */ };
+                                 same results bit for bit. */
+       FTMI_BANK_PAIR = 64    /* ABI 17, with FTMI_BANK_HALVES: no in-kernel finish — y holds
+                                 TWO planes, y and y + B*T*y_stride, the two channel halves'
+                                 raw sums (no colscale, ReLU or BN); the consumer finishes them
+                                 (ftmi_conv_args.x_fin: proj1's operand staging).  No exchange
+                                 workspace is read (split_ws still required). */ };
 enum { FTMI_BANK_COUNTERS = 4096 };
 
 /* ABI version; bumped on any signature change (14: ftmi_panel_proj_qkv, ftmi_attention_kv;
  * 15: FTMI_BANK_HALVES, ftmi_conv_bank_halves_ws_floats; 16: FTMI_BANK_IMAGE,
- * ftmi_conv_bank_halves_image[_bytes]). */
+ * ftmi_conv_bank_halves_image[_bytes]; 17: FTMI_BANK_PAIR, ftmi_conv_args.x_plane / x_fin). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
@@ -148,6 +153,15 @@ typedef struct ftmi_conv_args {
   int32_t x_split;     /* ABI 10: x holds f16x3 SPLIT ROWS (below) instead of floats; only
                           FTMI_MMA_F16X3 without maxpool on the slab kernel (B*T_out > 256
                           rows), else FTMI_E_UNSUPPORTED.  x_stride (floats) >= Cin. */
+  int64_t x_plane;     /* ABI 17, with x_fin: floats from x to the second plane */
+  const float *x_fin;  /* ABI 17: NULL, or x is a FTMI_BANK_PAIR bank output (two planes of
+                          raw half sums, x and x + x_plane) and the operand row is the bank's
+                          finish of their sum — relu(s * x_fin[c] + x_fin[Cin + c]) *
+                          x_fin[2 Cin + c] + x_fin[3 Cin + c] per channel c — before the
+                          maxpool: [4][Cin] floats (colscale, bias, BN scale, BN shift).
+                          Only the few-row kernel (B*T_out <= 256, FTMI_MMA_F16X3, one
+                          group), else FTMI_E_UNSUPPORTED; a non-finite sum sets status bit 0
+                          as the bank would. */
 } ftmi_conv_args;
 
 /* f16x3 split rows (ABI 10): the activation layout one f16x3 GEMM hands the next.  Row r

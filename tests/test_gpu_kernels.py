@@ -289,6 +289,74 @@ def test_conv_bank_halves(K, Cin, B, T, rng, monkeypatch):
     close(a0, b0, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize('K,Cin,B,T,N', [(16, 256, 1, 120, 256), (16, 256, 1, 50, 256),
+                                       (8, 128, 2, 64, 128), (4, 64, 1, 33, 80)])
+def test_conv_bank_pair_proj1(K, Cin, B, T, N, rng, monkeypatch):
+    """FTMI_BANK_PAIR (opt-in): the halves bank leaves its two channel halves' raw sums and
+    proj1's operand staging (conv1d x_fin, the few-row kernel, maxpool fused) finishes them —
+    the proj1 output is bit-identical to proj1 (maxpool) on the bank's own in-kernel finish,
+    on repeated calls, with status 0; and the planes add up to the finished bank."""
+    monkeypatch.setenv('FTMI_BANK_PAIR', '1')
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    C = 256
+    x = dev(rng.normal(0, 1, (B, T, Cin)).astype(np.float32))
+    ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
+    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
+    w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
+    img = ops.bank_halves_image(w3, K, Cin, C)
+    sc = dev(rng.uniform(0.5, 1.5, K * C).astype(np.float32))
+    sh = dev(rng.normal(0, 0.1, K * C).astype(np.float32))
+    cs = img[img.numel() - 4 * K * C:].view(torch.float32)
+    fin = torch.stack([cs, torch.zeros_like(cs), sc, sh]).contiguous()
+    w1 = rng.normal(0, 1 / np.sqrt(K * C * 3), (N, K * C, 3)).astype(np.float32)
+    w1p = pack_conv(torch.from_numpy(w1)).cuda()
+    w13 = ops.split_weights_f16(w1p)
+    s1 = dev(rng.uniform(0.5, 1.5, N).astype(np.float32))
+    h1 = dev(rng.normal(0, 0.1, N).astype(np.float32))
+    assert ops.bank_pair_ok(x, K, C, 2, w3)
+    st = ops.status_word(x.device)
+    st.zero_()
+    yb = ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, w_image=img)
+    ref, _ = ops.conv1d(yb, w1p, 3, 1, relu=True, bn=(s1, h1), maxpool=True, mma=2, w_split=w13)
+    ref = host(ref)
+    for _ in range(3):
+        pr = ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, w_image=img, pair=True)
+        assert pr.shape == (2, B, T, K * C)
+        y, _ = ops.conv1d(pr, w1p, 3, 1, relu=True, bn=(s1, h1), maxpool=True, mma=2,
+                          w_split=w13, x_fin=fin)
+        np.testing.assert_array_equal(host(y), ref)
+    # the planes' sum, finished by torch (separate multiply and add: within rounding)
+    s = (pr[0] + pr[1]) * cs
+    np.testing.assert_allclose(host(torch.relu(s) * sc + sh), host(yb), rtol=1e-6, atol=1e-6)
+    assert int(st.item()) == 0
+    # the plane path (no image) as well
+    pr2 = ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, pair=True)
+    np.testing.assert_array_equal(host(pr2), host(pr))
+
+
+def test_conv_bank_pair_status(rng):
+    """A non-finite bank sum reaching proj1's pair staging sets status bit 0, as the bank's
+    own finish would."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    K, Cin, C, T = 4, 64, 256, 40
+    ws = [rng.normal(0, 0.1, (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
+    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
+    w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
+    img = ops.bank_halves_image(w3, K, Cin, C)
+    cs = img[img.numel() - 4 * K * C:].view(torch.float32)
+    fin = torch.stack([cs, torch.zeros_like(cs), torch.ones_like(cs), torch.zeros_like(cs)]).contiguous()
+    pr = torch.zeros(2, 1, T, K * C, device='cuda')
+    pr[1, 0, 5, 300] = float('inf')
+    pr[0, 0, 5, 300] = float('-inf')  # inf + -inf = NaN: ReLU would hide it
+    w1p = pack_conv(torch.from_numpy(rng.normal(0, 0.01, (80, K * C, 3)).astype(np.float32))).cuda()
+    st = ops.status_word('cuda')
+    st.zero_()
+    ops.conv1d(pr, w1p, 3, 1, maxpool=True, mma=2, w_split=ops.split_weights_f16(w1p), x_fin=fin)
+    assert int(st.item()) & 1
+
+
 def test_conv_bank_halves_range_guard(rng):
     """An input beyond the f16 range sets status bit 0 on the halves bank (the model then
     reruns on the exact path)."""

@@ -51,6 +51,23 @@ for diag in (sys.argv[1:] or ['0', '1', '2', '4']):
           f'cycles from each block start, median (max) over 256 blocks:')
     print('   ' + '  '.join(f'{nm} {np.median(rel[:, i]):7.0f} ({rel[:, i].max():6.0f})'
                             for i, nm in enumerate(names)))
+    if os.environ.get('SLOWEST'):
+        # the slowest blocks: block id, XCD (b & 7), half, unit, the pair's heavy group, phases
+        order = np.argsort(-rel[:, 6:8].max(1))[:int(os.environ['SLOWEST'])]
+        for blk in order:
+            h, u = (blk >> 3) & 1, (blk & 7) | ((blk >> 4) << 3)
+            print(f'   block {blk:3d} xcd {blk & 7} half {h} unit {u:3d} gi {u // 16:2d}: ' +
+                  ' '.join(f'{rel[blk, i]:6.0f}' for i in range(1, 8)))
+        fast = np.argsort(rel[:, 6:8].max(1))[:3]
+        for blk in fast:
+            print(f'   fast  {blk:3d} xcd {blk & 7}: ' + ' '.join(f'{rel[blk, i]:6.0f}' for i in range(1, 8)))
+        ends = rel[:, 6:8].max(1)
+        for xc in range(8):
+            # s_memtime is one counter per XCD: absolute stamps compare within an XCD
+            s0, e0 = st[xc::8, 0], st[xc::8, 6:8].max(1)
+            print(f'   xcd {xc}: median block {np.median(ends[xc::8]):6.0f} max {ends[xc::8].max():6.0f}'
+                  f' | starts spread {s0.max() - s0.min():6.0f}, first start -> last end '
+                  f'{e0.max() - s0.min():6.0f} cycles')
     d = rel[:, 2] - rel[:, 1]
     print(f'   wave-0 loop {np.median(d):.0f} cycles (min {d.min():.0f}, max {d.max():.0f}); '
           f'longest block {rel[:, 6:8].max():.0f} cycles', flush=True)
