@@ -84,6 +84,9 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r4_pmc_traffic.json')        # c3
 PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r4c2_pmc_traffic.json')   # c2 (--config c2)
 PMC_PROFILE_C5 = os.path.join(ROOT, 'profiles', 'r4c5_pmc_traffic.json')   # c5 (--model fast_pitch)
+# the PMC files are a prior run of the same workload (separate FETCH_SIZE / WRITE_SIZE passes
+# cannot share the timed run), taken on this tree
+PMC_TREE = 'cf0df58 (round 4, tools/gpu_r4_measure.sh pmc)'
 
 
 def rocprof_name(label: str):
@@ -119,7 +122,8 @@ def pmc_traffic(label: str, path: str = PMC_PROFILE):
     return {'bytes_per_launch': hit[0]['hbm_bytes_per_launch'],
             'read_bytes_corrected': hit[0]['read_bytes_corrected'],
             'write_bytes': hit[0]['write_bytes'],
-            'source': os.path.relpath(path, ROOT)}
+            'source': os.path.relpath(path, ROOT), 'measured_on_tree': PMC_TREE,
+            'note': 'a prior PMC run of this workload, not this run'}
 
 
 def pmc_traffic_slab(label: str, path: str):
@@ -140,7 +144,8 @@ def pmc_traffic_slab(label: str, path: str):
     k, v = hit[0]
     return {'bytes_per_launch': v['hbm_bytes_per_launch'],
             'read_bytes_corrected': v['read_bytes_corrected'], 'write_bytes': v['write_bytes'],
-            'kernel_grid': k, 'source': os.path.relpath(path, ROOT)}
+            'kernel_grid': k, 'source': os.path.relpath(path, ROOT), 'measured_on_tree': PMC_TREE,
+            'note': 'a prior PMC run of this workload, not this run'}
 
 
 def time_prenet_bank(model, x, reps: int = 20):
