@@ -513,6 +513,21 @@ def main():
                                         '(weights from HBM): graph [overwrite, call] minus graph '
                                         '[overwrite], per call')
                 prenet['weights_read'] = pb['weights']
+                # PMC traffic of the bank kernel from the committed passes of this workload
+                if pmc_path and os.path.exists(pmc_path) and pb['weights'] == 'stream-order image':
+                    ks = json.load(open(pmc_path))['kernels']
+                    hit = [v_ for k_, v_ in ks.items()
+                           if k_.startswith('conv_bank_halves_kernel<8, 4, 0, 16, 16, true>')]
+                    if len(hit) == 1:
+                        prenet['traffic'] = hit[0]['hbm_bytes_per_launch']
+                        prenet['traffic_detail'] = {
+                            'read_bytes_corrected': hit[0]['read_bytes_corrected'],
+                            'write_bytes': hit[0]['write_bytes'],
+                            'vs_algorithmic': round(hit[0]['hbm_bytes_per_launch'] / v['bytes'], 3),
+                            'what': 'FETCH_SIZE x 2 + WRITE_SIZE per launch (writes include the '
+                                    'halves\' 4 MB exchange and the counters)',
+                            'source': os.path.relpath(pmc_path, ROOT), 'measured_on_tree': PMC_TREE,
+                            'note': 'a prior PMC run of this workload, not this run'}
                 if 'planes' in pb:
                     prenet['warm_ms_in_kernel_finish'] = round(pb['inkernel'], 4)
                     prenet['warm_ms_in_kernel_finish_split_planes'] = round(pb['planes'], 4)
