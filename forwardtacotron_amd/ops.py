@@ -549,9 +549,11 @@ def highway(x: torch.Tensor, w12: torch.Tensor, b1: torch.Tensor, b2: torch.Tens
 
 
 HS_C, HS_NPASS, HS_MAXL = 256, 512, 8  # gemm.hip highway_stack_kernel shape limits
-# The fused stack below FTMI_HS_MIN rows falls back to the per-layer launches (the skinny
-# weight-streaming kernels win there: a handful of row tiles cannot spread the weight reads)
-HS_MIN_ROWS = int(os.environ.get('FTMI_HS_MIN', 256))
+# The fused stack below FTMI_HS_MIN rows falls back to the per-layer launches.  Round 4
+# moved the default 256 -> 64: at c2 (the prenet's 120 rows) the one launch replaces four
+# skinny GEMMs + four finish launches, c2 2.81 / 2.96 / 2.83 -> 2.80 / 2.81 / 2.80 ms per
+# step (tools/ab_bench.py, 3 interleaved rounds, profiles/r4_ab_c2_env.jsonl)
+HS_MIN_ROWS = int(os.environ.get('FTMI_HS_MIN', 64))
 
 
 def highway_stack_ok(M: int, Cp: int, C: int, L: int, n_out: int, splits) -> bool:
