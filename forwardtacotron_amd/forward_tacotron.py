@@ -137,7 +137,10 @@ class ForwardTacotron(nn.Module):
                  postnet_dropout: float,
                  n_mels: int,
                  padding_value=-11.5129):
+        # the constructor keywords, for the TorchScript archive (jit.model_config)
+        ctor = {k: v for k, v in locals().items() if k not in ('self', '__class__')}
         super().__init__()
+        self._ctor_kwargs = ctor
         self.rnn_dims = rnn_dims
         self.padding_value = padding_value
         self.register_buffer('step', torch.zeros(1, dtype=torch.long))
@@ -520,8 +523,9 @@ class ForwardTacotron(nn.Module):
         runs in libftmi.so through ctypes, which TorchScript cannot compile, so what gets
         scripted is `jit.ScriptedForwardTacotron` — the reference's scriptable surface
         (`forward(batch)`, `generate_jit(x, alpha, beta)`) over dispatcher operators
-        (`torch.ops.ftmi.*`) that run this model's HIP path.  The scripted module (and a
-        torch.jit.save / load of it) runs in this process."""
+        (`torch.ops.ftmi.*`) that run this model's HIP path.  The scripted module carries the
+        constructor keywords and the weights, so a torch.jit.save'd archive loads and runs
+        in any process that has imported forwardtacotron_amd."""
         from .jit import ScriptedForwardTacotron
         return ScriptedForwardTacotron(self)
 

@@ -62,7 +62,8 @@ def test_torchscript_readme_on_hip(gpu_model, synth_sd, tmp_path):
     on the HIP device (a device replica of the CPU model) and returns CPU tensors equal bit
     for bit to the eager generate_jit of the same weights on the GPU model; the reference
     golden holds; a torch.jit.save / load round trip gives the same bits; the scripted
-    forward(batch) equals the eager forward; a scripted GPU model returns GPU tensors."""
+    forward(batch) equals the eager forward; a scripted GPU model returns GPU tensors; the
+    saved archive computes the same bits in a fresh process."""
     from forwardtacotron_amd.forward_tacotron import ForwardTacotron
     from forwardtacotron_amd.synthetic import default_config
     cfg = default_config()
@@ -96,6 +97,34 @@ def test_torchscript_readme_on_hip(gpu_model, synth_sd, tmp_path):
     scripted = model_script({k: v.clone() for k, v in batch.items()})
     for k in ('mel', 'mel_post', 'dur', 'pitch', 'energy'):
         assert torch.equal(scripted[k], eager[k].cpu()), k
+    # the archive is self-contained — a FRESH process that imports
+    # forwardtacotron_amd loads it and computes the same bits
+    import subprocess
+    import sys
+    out = tmp_path / 'fresh.pt'
+    code = ('import torch, forwardtacotron_amd\n'
+            f'm = torch.jit.load({str(tmp_path / "s.pt")!r})\n'
+            f'x = torch.load({str(tmp_path / "x.pt")!r})\n'
+            f'torch.save(m.generate_jit(x, 1.1, 0.7), {str(out)!r})\n')
+    torch.save(xg, str(tmp_path / 'x.pt'))
+    r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    yf = torch.load(str(out), weights_only=True)
+    for k in yg:
+        assert torch.equal(yf[k], yg[k]), k
+    # an in-place weight update reaches the scripted module (it shares the eager storage)
+    saved = gpu_model.lin.bias.detach().clone()
+    with torch.no_grad():
+        tts_model.lin.bias.add_(0.25)
+        gpu_model.lin.bias.add_(0.25)
+    try:
+        y2 = model_script.generate_jit(xg, 1.1, 0.7)
+        r2 = gpu_model.generate_jit(xg.cuda(), 1.1, 0.7)
+        assert torch.equal(y2['mel'], r2['mel'].cpu())
+        assert not torch.equal(y2['mel'], yg['mel'])
+    finally:
+        with torch.no_grad():
+            gpu_model.lin.bias.copy_(saved)
 
 
 def test_intermediates_b1(gpu_model):

@@ -129,10 +129,11 @@ def test_torchscript_export_fails_with_reason(kind):
 
 def test_torchscript_forward_tacotron(tmp_path):
     """README.md:149-161 verbatim (from_checkpoint, eval, torch.jit.script, generate_jit on a
-    CPU tensor) scripts ForwardTacotron: the ScriptModule's forward / generate_jit call the
-    ftmi dispatcher operators with the eager model's handle, and a torch.jit.save / load
-    round trip keeps that (in-process).  Without a GPU (this suite) the call reaches the
-    operator's kernel, which refuses with the reason; tests/test_gpu_model.py runs it."""
+    CPU tensor) scripts ForwardTacotron: the ScriptModule carries the constructor keywords and
+    every weight (sharing the eager model's storage), its forward / generate_jit call the
+    ftmi dispatcher operators with them, and a torch.jit.save / load round trip keeps all of
+    it.  Without a GPU (this suite) the call reaches the operator's kernel, which refuses with
+    the reason; tests/test_gpu_model.py runs it (also from a fresh process)."""
     from forwardtacotron_amd.forward_tacotron import ForwardTacotron
     from forwardtacotron_amd.synthetic import default_config
     cfg = default_config()
@@ -144,33 +145,67 @@ def test_torchscript_forward_tacotron(tmp_path):
     model_script = torch.jit.script(tts_model)
     x = torch.ones((1, 5)).long()
     assert isinstance(model_script, torch.jit.ScriptModule)
-    assert model_script.handle == tts_model.__dict__['_ftmi_jit_handle']
     assert 'ftmi.ft_generate_jit' in model_script.generate_jit.code
     assert 'ftmi.ft_forward' in model_script.code
+    sd = tts_model.state_dict()
+    keys = json.loads(model_script.config)['keys']
+    assert keys == [k for k in sd if k != 'step']
+    for k, w in zip(keys, model_script.weights):
+        assert w.data_ptr() == sd[k].data_ptr(), k  # shares the eager model's storage
     buf = tmp_path / 'scripted.pt'
     torch.jit.save(model_script, str(buf))
     loaded = torch.jit.load(str(buf))
-    assert loaded.handle == model_script.handle
+    assert loaded.config == model_script.config
+    for k, w in zip(keys, loaded.weights):
+        assert torch.equal(w, sd[k]), k
     assert 'ftmi.ft_generate_jit' in loaded.generate_jit.code
     if not torch.cuda.is_available():
         for mod in (model_script, loaded):
             with pytest.raises(RuntimeError, match='computes on a HIP device'):
                 mod.generate_jit(x)
+    # the archive rebuilds the same eager model (CPU: construct + load_state_dict only)
+    kw = json.loads(loaded.config)['kwargs']
+    m2 = ForwardTacotron(**kw)
+    m2.load_state_dict(dict(zip(keys, loaded.weights), step=loaded.step))
+    for k, v in m2.state_dict().items():
+        assert torch.equal(v, sd[k]), k
 
 
-def test_torchscript_handle_registry():
-    """The registry maps a scripted module's handle to its eager model (weakly); an unknown
-    handle fails with the reason."""
-    from forwardtacotron_amd import jit as J
+def test_torchscript_archive_loads_in_a_fresh_process(tmp_path):
+    """a torch.jit.save'd archive is self-contained — a fresh Python
+    process that imports forwardtacotron_amd (which registers the ftmi operators) loads it and
+    finds the weights and the configuration (the computation itself: test_gpu_model.py)."""
+    import subprocess
+    import sys
+    from forwardtacotron_amd.forward_tacotron import ForwardTacotron
+    from forwardtacotron_amd.synthetic import default_config
+    m = ForwardTacotron.from_config(default_config()).eval()
+    with torch.no_grad():
+        m.lin.weight.normal_()
+    arc = tmp_path / 'tts.pt'
+    torch.jit.save(torch.jit.script(m), str(arc))
+    expect = float(m.lin.weight.double().sum())
+    code = ('import json, sys, torch, forwardtacotron_amd\n'
+            f'l = torch.jit.load({str(arc)!r})\n'
+            'keys = json.loads(l.config)["keys"]\n'
+            'w = dict(zip(keys, l.weights))\n'
+            'print(len(keys), float(w["lin.weight"].double().sum()), l.step.item())\n')
+    r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=300,
+                       cwd=str(GOLDEN.parent.parent))
+    assert r.returncode == 0, r.stderr[-2000:]
+    n, s, step = r.stdout.split()
+    assert int(n) == len(m.state_dict()) - 1 and float(s) == expect and int(step) == 0
+
+
+def test_torchscript_train_mode_steps():
+    """The reference's forward increments step in training mode (forward_tacotron.py:200-201);
+    the scripted module shares step with the eager model."""
     from forwardtacotron_amd.forward_tacotron import ForwardTacotron
     from forwardtacotron_amd.synthetic import default_config
     m = ForwardTacotron.from_config(default_config())
-    h = J.register(m)
-    assert J.register(m) == h and J._model(h) is m
-    with pytest.raises(RuntimeError, match='no ForwardTacotron with that handle'):
-        J._model(10 ** 9)
-    with pytest.raises(RuntimeError, match='no ForwardTacotron with that handle'):
-        torch.ops.ftmi.ft_generate_jit(10 ** 9, torch.ones(1, 5, dtype=torch.long), 1.0, 1.0)
+    s = torch.jit.script(m)
+    assert s.training and 'step' in s.code
+    assert s.step.data_ptr() == m.step.data_ptr()
 
 
 def test_run_checked_checks_the_rerun(monkeypatch):
