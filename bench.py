@@ -100,11 +100,7 @@ def rocprof_name(label: str):
                 and ((cell == 1 and H == 512) or (cell == 0 and H in (64, 128, 256))))
         if gemv:
             return f'rnn_gemv_kernel<{cell}, {H},'
-        # rnn.hip row_path: FTMI_RNN_ROW=1 runs the f16x3 recurrences of H 128 / 256 / 512
-        # on rnn_row_kernel
-        row = (os.environ.get('FTMI_RNN_ROW', '0') != '0' and 'mma=2' in label
-               and ((cell == 1 and H == 512) or (cell == 0 and H in (128, 256))))
-        return f'rnn_row_kernel<{cell}, {H},' if row else f'rnn_bidir_kernel<{cell}, {H},'
+        return f'rnn_bidir_kernel<{cell}, {H},'
     return None
 
 

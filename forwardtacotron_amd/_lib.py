@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 17
+ABI_VERSION = 18
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -34,7 +34,6 @@ class ConvArgs(ctypes.Structure):
         ('residual', P), ('res_stride', c_int64),
         ('y', P), ('y_stride', c_int64), ('yt', P), ('T_out', c_int), ('mma', c_int),
         ('split_k', c_int), ('split_ws', P), ('w_split', P), ('status', P), ('x_split', c_int),
-        ('x_plane', c_int64), ('x_fin', P),
     ]
 
 
@@ -81,8 +80,6 @@ SIGNATURES = {
     'ftmi_set_rnn_spin_limit': (ctypes.c_uint32, [ctypes.c_uint32]),
     'ftmi_rnn_bidir': (c_int, [c_int, c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,
                                c_float, P, c_int64, c_int, P, P, P]),
-    'ftmi_gru_bidir_fused': (c_int, [c_int, c_int, c_int, P, c_int64, c_int, P, P, P, P, P,
-                                     c_float, P, c_int64, P, P, P]),
     'ftmi_duration_counts': (c_int, [P, c_int, c_int, c_int, c_float, P, P, P, P]),
     'ftmi_duration_trunc_sum': (c_int, [P, c_int, c_int, P, P]),
     'ftmi_duration_counts_global': (c_int, [P, c_int, c_int, P, c_float, P, P, P, P]),

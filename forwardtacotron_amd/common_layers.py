@@ -165,21 +165,13 @@ class BatchNormConv(Packed):
         return w, self.bnorm.folded(), presplit(w)
 
     def forward_cl(self, x: torch.Tensor, T_out: int = 0, residual=None, maxpool=False,
-                   x_split=False, x_fin=None) -> torch.Tensor:
+                   x_split=False) -> torch.Tensor:
         w, bn, w3 = self.packed_weights()
         # bf16x6: the pre-split kernel measured slower on the maxpool (CBHG proj1) shapes
         y, _ = ops.conv1d(x, w, self.kernel, self.kernel // 2, relu=self.relu, bn=bn,
                           residual=residual, maxpool=maxpool, T_out=T_out,
-                          w_split=None if (maxpool and ops.MMA == 1) else w3, x_split=x_split,
-                          x_fin=x_fin)
+                          w_split=None if (maxpool and ops.MMA == 1) else w3, x_split=x_split)
         return y
-
-    def takes_pair(self, B: int, T: int, Cin: int) -> bool:
-        """Whether forward_cl can take a conv_bank(pair=True) operand (x_fin): the few-row
-        f16x3 kernel runs this conv."""
-        w3 = self.packed_weights()[2]
-        m, _ = ops._gemm_mma(None, w3)
-        return ops._skinny(m, T, T, Cin, self.kernel, B * T, self.conv.weight.size(0))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """(B, Cin, T) -> (B, Cout, T + 1 - k % 2), like the reference."""
@@ -251,11 +243,6 @@ class BiRNN(Packed):
     def forward_cl(self, x: torch.Tensor, T: Optional[int] = None, index=None, lengths=None,
                    pad_value: float = 0.0) -> torch.Tensor:
         """x: (B, T_src, In) channels-last; with index, frame t reads row index[b, t]."""
-        if self.cell == 0 and index is None and ops.gru_fused_ok(self.hidden, x.size(2)):
-            # the input projection inside the recurrence (no (B, T, 6H) intermediate)
-            w_ih, b_in, b_hh, w_hh, _ = self.packed_weights()
-            return ops.gru_bidir_fused(x, self.hidden, w_ih, b_in, w_hh, b_hh, lengths=lengths,
-                                       pad_value=pad_value)
         return self.recur(self.project(x), T=T, index=index, lengths=lengths,
                           pad_value=pad_value)
 
@@ -306,30 +293,20 @@ class CBHG(Packed):
         w_pre = self.pre_highway.weight.detach().contiguous()
         bank3 = ops.split_bank_weights(bank_w, self.K, ws[0].size(1), self.channels)
         img = ops.bank_halves_image(bank3, self.K, ws[0].size(1), self.channels)
-        fin = None
-        if img is not None:  # proj1's finish of a pair bank: colscale (the image's tail), bias, BN
-            n = self.K * self.channels
-            cs = img[img.numel() - 4 * n:].view(torch.float32)
-            fin = torch.stack([cs, torch.zeros_like(cs), scale, shift]).contiguous()
-        return bank_w, scale, shift, w_pre, bank3, presplit(w_pre), img, fin
+        return bank_w, scale, shift, w_pre, bank3, presplit(w_pre), img
 
     def forward_cl(self, x: torch.Tensor) -> torch.Tensor:
         """(B, T, Cin) channels-last -> (B, T, 2*channels)."""
-        bank_w, scale, shift, w_pre, bank3, pre3, img, fin = self.packed_weights()
+        bank_w, scale, shift, w_pre, bank3, pre3, img = self.packed_weights()
         pooled = ops.bank_pools(x, self.K, self.channels, w_split=bank3)
         # pooled: the bank kernel applied the maxpool, and (split) stored its output as the
         # f16x3 split rows proj1 multiplies
         split = pooled and ops.SPLIT_ROWS
         xin = pooled and ops.SPLIT_BANK_IN  # x stays fp32 too: it is the proj2 residual
-        # pair (few rows, c2): the bank leaves its two channel halves' raw sums and proj1's
-        # operand staging finishes them (no in-kernel partner exchange; bit-identical)
-        pair = (fin is not None and not pooled and ops.bank_pair_ok(x, self.K, self.channels, w_split=bank3)
-                and self.conv_project1.takes_pair(x.size(0), x.size(1), self.K * self.channels))
         bank = ops.conv_bank(ops.split_rows(x) if xin else x, bank_w, self.K, self.channels,
                              scale, shift, w_split=bank3, pool=pooled, split_out=split,
-                             x_split=xin, w_image=img, pair=pair)
-        y = self.conv_project1.forward_cl(bank, maxpool=not pooled, x_split=split,
-                                          x_fin=fin if pair else None)
+                             x_split=xin, w_image=img)
+        y = self.conv_project1.forward_cl(bank, maxpool=not pooled, x_split=split)
         del bank
         y = self.conv_project2.forward_cl(y, residual=x)
         xp = self._highway_stack(y)

@@ -85,7 +85,7 @@ struct GemmParams {
   int split;
   int kc_per;
   int split_req;  // the caller's split_k (the slab kernel re-derives split / kc_per from it)
-  int diag;       // slab kernel timing experiments (FTMI_SLAB_DIAG; results invalid when set)
+  int diag;       // slab kernel timing experiments (FTMI_SLAB_DIAG, diagnostic build only)
   int band;       // slab kernels: column-band tile order (FTMI_SLAB_BAND, see slab_tile)
   float *part;
   int ldp;  // skinny kernel: columns of a partial-sum row (all groups, output order)
@@ -101,19 +101,11 @@ struct GemmParams {
   // y_split_c > 0 = the pool_out epilogue writes y as split rows of y_split_c channels
   int x_split;
   int y_split_c;
-  // skinny conv bank (FTMI_BANK_LAST): per-tile arrival counters (zero between launches);
-  // the last split block of a tile sums the splits and finishes it (no finish launch)
+  // conv_bank_halves_kernel: per-slice arrival counters (zero between launches)
   unsigned *tile_cnt;
   // conv_bank_halves_kernel (FTMI_BANK_IMAGE): the stream-order weight image — every wave's
   // weight fragments in the order it loads them, 1 KB per wave load (bank_halves_pack_kernel)
   const _Float16 *wimg;
-  // conv_bank_halves_kernel PAIR (FTMI_BANK_PAIR): each half's raw sums go to its own plane,
-  // y + h * y_plane; conv_gemm_skinny_kernel PAIR (ftmi_conv_args.x_fin): the operand row is
-  // the bank epilogue of the two planes' sum, x_fin = [4][Cin] (colscale, bias, BN scale,
-  // BN shift), the second plane at x + x_plane
-  int64_t y_plane;
-  int64_t x_plane;
-  const float *x_fin;
   GemmGroup g[MAX_GROUPS];
 };
 
@@ -1519,18 +1511,23 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
     if (nch > 1) loadA(ra);  // chunk 1
     __syncthreads();
     int c = 0, j = 0;
+#ifdef FTMI_DIAG
+    const int diag = p.diag;  // timing experiments: results invalid when set
+#else
+    constexpr int diag = 0;
+#endif
     auto step = [&](int s, BRaw &rbs) {
       const bool last_tap = j == k - 1 && c + 1 < nch;
       // MFMAs first: the staging below (LDS stores of the next B / slab, the slab's f16
       // split, the next loads) is independent of them and fills the matrix pipe's shadow
-      if (!(p.diag & 2)) mfma_step(acc, c & 1, s & 1, j);
+      if (!(diag & 2)) mfma_step(acc, c & 1, s & 1, j);
       if (s + 1 < nsteps) storeB(rbs, (s + 1) & 1);
       if (last_tap) storeA(ra, (c + 1) & 1);
-      if (!(p.diag & 4)) {
+      if (!(diag & 4)) {
         loadB(rbs);
         if (last_tap) loadA(ra);
       }
-      if (!(p.diag & 1)) __syncthreads();
+      if (!(diag & 1)) __syncthreads();
       if (++j == k) {
         j = 0;
         ++c;
@@ -1885,71 +1882,11 @@ __device__ unsigned long long ftmi_skinny_stamps[4096 * 8];
   } while (0)
 #endif
 
-// The last split block of a bank tile (FTMI_BANK_LAST) finishes it: the tile = rows m0 ..
-// m0 + 127 of the four units (group gi / its pair partner, column sets nt, nt + 1).  Item =
-// (row, unit, 4 columns); every thread issues the write-through-stored partials of ALL its
-// items and splits (16-B sc1 loads, clamped so no load is conditional) before it adds any,
-// so the reducer pays about one round trip instead of one per element and split; the
-// splits are added in split order (the finish kernel's sums, bit for bit).
-__device__ __forceinline__ bool bank_last_reduce(const GemmParams &p, int gi, int nt, int m0) {
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  constexpr int IT = SK_BM * 16 / 512, SPL = 4;  // items per thread, splits per load batch
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.part, (short)0, 0x7FFFFFF0, 0x00020000);
-  const int rows = min(SK_BM, p.M - m0);
-  bool bad = false;
-  f32x4 v[IT];
-  int off[IT];
-#pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    v[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int e = threadIdx.x + 512 * i, r = min(e >> 4, rows - 1), uu = (e >> 2) & 3;
-    const int g = (uu >> 1) ? p.ngroups - 1 - gi : gi;
-    const int c = min((nt + (uu & 1)) * 16 + (e & 3) * 4, p.g[g].N - 4);
-    off[i] = ((m0 + r) * p.ldp + p.g[g].ycol0 + c) * 4;  // bytes; < 2^31 (host check)
-  }
-  const int sb = p.M * p.ldp * 4;  // bytes per split
-  for (int s0 = 0; s0 < p.split; s0 += SPL) {
-    u32x4 r[IT][SPL];
-#pragma unroll
-    for (int i = 0; i < IT; ++i)
-#pragma unroll
-      for (int k = 0; k < SPL; ++k)
-        r[i][k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[i], min(s0 + k, p.split - 1) * sb, 16);
-#pragma unroll
-    for (int i = 0; i < IT; ++i)
-#pragma unroll
-      for (int k = 0; k < SPL; ++k)
-        if (s0 + k < p.split) v[i] += __builtin_bit_cast(f32x4, r[i][k]);
-  }
-#pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int e = threadIdx.x + 512 * i, uu = (e >> 2) & 3;
-    const int g = (uu >> 1) ? p.ngroups - 1 - gi : gi;
-    const GemmGroup &GF = p.g[g];
-    const int c0 = (nt + (uu & 1)) * 16 + (e & 3) * 4, row = m0 + (e >> 4);
-    if ((e >> 4) >= rows || c0 >= GF.N) continue;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float y = v[i][q];
-      bad |= !__builtin_isfinite(y);
-      if (GF.bias) y += GF.bias[c0 + q];
-      if (p.relu) y = fmaxf(y, 0.f);
-      if (GF.scale) y = y * GF.scale[c0 + q] + GF.shift[c0 + q];
-      p.y[(int64_t)row * p.y_stride + GF.ycol0 + c0 + q] = y;
-    }
-  }
-  return bad;
-}
-
 // DIAG (timing experiments only, FTMI_SKINNY_DIAG on the bank schedule; results invalid):
 // bit 0 = the A fragments read once before the loop (no LDS reads in it), bit 1 = no MFMAs
-// (the loaded weights feed one VALU add), bit 2 = every weight load from one L2-hot line
-// LAST (BANK, split > 1): the tile's last split block finishes it (see conv_bank_qb_kernel)
-// PAIR: the operand is a FTMI_BANK_PAIR bank output — x and x + x_plane hold the two
-// channel halves' raw sums; each staged value is the bank's own finish of their sum
-// (s * colscale + bias, ReLU, BN affine: the same expressions, so bit-identical), taken
-// before the maxpool
-template <bool MAXPOOL, bool BANK = false, int DIAG = 0, bool LAST = false, bool PAIR = false>
+// (the loaded weights feed one VALU add), bit 2 = every weight load from one L2-hot line.
+// Instantiated only in the diagnostic build (-DFTMI_DIAG, libftmi_stamps.so).
+template <bool MAXPOOL, bool BANK = false, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmParams p) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[SK_CPB * 2 * SK_AIMG];
   SKSTAMP(0);
@@ -1985,8 +1922,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
   constexpr int SK_ASLOTS = (SK_CPB * SK_SR + 63) / 64;
   const int seg = tid & 7;
   f32x4 av[SK_ASLOTS], au[MAXPOOL ? SK_ASLOTS : 1];
-  f32x4 bv[PAIR ? SK_ASLOTS : 1], bu[PAIR && MAXPOOL ? SK_ASLOTS : 1];
-  static_assert(!PAIR || SK_CPB == 2, "bank_finish selects between two chunks");
 #pragma unroll
   for (int i = 0; i < SK_ASLOTS; ++i) {
     const int r = min((tid >> 3) + 64 * i, nch * SK_SR - 1), c = r / SK_SR, sr = r - c * SK_SR;
@@ -1995,50 +1930,17 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
     const float *src = p.x + (int64_t)m * p.x_stride + ch;
     av[i] = *(const f32x4 *)src;
-    if constexpr (PAIR) bv[i] = *(const f32x4 *)(src + p.x_plane);
     // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
-    if constexpr (MAXPOOL) {
-      const float *prv = src - (m % p.T > 0 ? p.x_stride : 0);
-      au[i] = *(const f32x4 *)prv;
-      if constexpr (PAIR) bu[i] = *(const f32x4 *)(prv + p.x_plane);
-    }
+    if constexpr (MAXPOOL) au[i] = *(const f32x4 *)(src - (m % p.T > 0 ? p.x_stride : 0));
   }
-  // PAIR: the bank epilogue parameters of this thread's channels in each of its chunks
-  f32x4 fcs[SK_CPB], fbi[SK_CPB], fsc[SK_CPB], fsh[SK_CPB];  // (dead without PAIR)
-  if constexpr (PAIR) {
-#pragma unroll
-    for (int c = 0; c < SK_CPB; ++c) {
-      const int ch0 = (c_begin + min(c, nch - 1)) * 32 + seg * 4, ch = ch0 < Cin ? ch0 : 0;
-      fcs[c] = *(const f32x4 *)(p.x_fin + ch);
-      fbi[c] = *(const f32x4 *)(p.x_fin + Cin + ch);
-      fsc[c] = *(const f32x4 *)(p.x_fin + 2 * Cin + ch);
-      fsh[c] = *(const f32x4 *)(p.x_fin + 3 * Cin + ch);
-    }
-  }
-  bool pbad = false;  // PAIR: a non-finite bank sum (the bank's own status bit 0)
-  auto bank_finish = [&](f32x4 a, f32x4 b, int c) {
-    const f32x4 cs = c ? fcs[SK_CPB - 1] : fcs[0], bi = c ? fbi[SK_CPB - 1] : fbi[0];
-    const f32x4 sc = c ? fsc[SK_CPB - 1] : fsc[0], sh = c ? fsh[SK_CPB - 1] : fsh[0];
-    f32x4 y;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float sum = a[q] + b[q];  // the two halves (commutative: as the bank adds them)
-      pbad |= !__builtin_isfinite(sum);
-      float t = sum * cs[q] + bi[q];
-      t = fmaxf(t, 0.f);
-      y[q] = t * sc[q] + sh[q];
-    }
-    return y;
-  };
   float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < SK_ASLOTS; ++i) {
     const int r = (tid >> 3) + 64 * i, c = r / SK_SR, sr = r - c * SK_SR;
     if (r >= nch * SK_SR) break;
     f32x4 x = av[i];
-    if constexpr (PAIR) x = bank_finish(av[i], bv[i], c);
     if ((c_begin + c) * 32 + seg * 4 >= Cin) x = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if constexpr (MAXPOOL) x = fmax4(x, PAIR ? bank_finish(au[i], bu[i], c) : au[i]);
+    if constexpr (MAXPOOL) x = fmax4(x, au[i]);
     amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
     f16x4 h, t;
     split2h(x, h, t);
@@ -2052,7 +1954,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
   }
   __syncthreads();
   SKSTAMP(1);
-  bool bad = !(amax <= 65504.f) || pbad;
+  bool bad = !(amax <= 65504.f);
 
   // 8 waves: wave w multiplies columns col0 + [0, 16) (column set w & 3) over one half of
   // the steps (w >> 2); the two halves meet in LDS after the loop.  BANK: unit slot cw =
@@ -2196,11 +2098,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
           const int row = m0 + mi * 16 + 4 * fs + i;
           if (cok && row < p.M) {
             bad |= !__builtin_isfinite(acc[mi][i]);
-            if constexpr (LAST)  // write-through: the last arriver reads it with sc1 loads
-              __hip_atomic_store(part + (size_t)row * p.ldp + col, acc[mi][i] * cs,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-              part[(size_t)row * p.ldp + col] = acc[mi][i] * cs;
+            part[(size_t)row * p.ldp + col] = acc[mi][i] * cs;
           }
         }
     } else {
@@ -2225,227 +2123,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     }
   }
   SKSTAMP(3);
-  if constexpr (LAST && BANK) {  // the tile = this block's (pair, two column sets)
-    __shared__ int s_last;
-    if (p.split > 1) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores done
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(p.tile_cnt + blockIdx.x, 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == (unsigned)p.split - 1;
-        if (s_last)  // every split block has added: zero for the next launch
-          __hip_atomic_store(p.tile_cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      if (s_last) bad |= bank_last_reduce(p, gi, nt, m0);
-    }
-  }
-  if (bad && p.status) atomicOr(p.status, 1u);
-}
-
-// ---- the c2 conv bank, quarter-balanced (FTMI_BANK_QB, default on) ---------------------
-// The BANK schedule of conv_gemm_skinny_kernel gives a block the group pair (k, K + 1 - k)
-// and two 16-column sets, but a wave only one (unit, half): the heavy group's waves run k
-// steps, the light group's K + 1 - k, so on each SIMD one wave is left alone for most of the
-// loop and the block waits for it at the end.  Here every wave takes one QUARTER of the step
-// range of a heavy unit AND one quarter of the light unit of the same column set: all 8
-// waves run (K + 1) / 4 steps.  The four quarters of a unit meet in LDS (summed in quarter
-// order: deterministic) and all 8 waves share the tail stores (wave w: unit w / 2, row
-// fragments 4 (w % 2) .. + 4).  Slab, per-step loop and epilogue are the skinny kernel's.
-// LAST: the split blocks publish their partial sums write-through (sc1) and bump the tile's
-// arrival counter after every storing wave's vmcnt(0) wait and a barrier; the block whose add
-// returns split - 1 resets the counter, reads the split partials with sc1 loads in split order
-// (deterministic) and applies the epilogue — MI355X_MICROARCH.md "Valid forms", first row of
-// the sc1 table (agent-scope atomic add, the last adder told by its return value).
-constexpr int QB_RED = 4 * 4 * 8 * 64;  // f32x4 [unit][quarter][row fragment][lane]
-
-template <bool LAST>
-__global__ __launch_bounds__(512, 1) void conv_bank_qb_kernel(const GemmParams p) {
-  __shared__ __attribute__((aligned(16))) f32x4 red[QB_RED];  // 128 KB; the slab aliases it
-  _Float16 *const lds = (_Float16 *)red;
-  static_assert(SK_CPB * 2 * SK_AIMG * sizeof(_Float16) <= sizeof(red), "slab alias");
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const int MT = (p.M + SK_BM - 1) / SK_BM, NC = p.g[0].N / 16;
-  const int bid = blockIdx.x, mt = bid % MT, v = bid / MT;
-  const int gi = (2 * v) / NC;  // the pair's heavier group (k = K - gi): its slab
-  const int nt = (2 * v) % NC;  // first of the block's two 16-column sets
-  const GemmGroup &G = p.g[gi];
-  const int m0 = mt * SK_BM, k = G.k, pad = G.pad, Cin = p.Cin;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fs = lane >> 4;
-  const int nch_all = (Cin + 31) / 32;
-  const int c_begin = blockIdx.y * p.kc_per;
-  const int nch = min(nch_all - c_begin, p.kc_per);
-  const int SR = SK_BM + k - 1;
-
-  // ---- prologue: the slab of this block's chunks (as conv_gemm_skinny_kernel) -------------
-  constexpr int SK_ASLOTS = (SK_CPB * SK_SR * 8 + 511) / 512;
-  const int nitems = nch * SR * 8;
-  f32x4 av[SK_ASLOTS];
-#pragma unroll
-  for (int i = 0; i < SK_ASLOTS; ++i) {
-    const int idx = tid + 512 * i;
-    av[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
-    const int ch = (c_begin + c) * 32 + seg * 4;
-    if (idx < nitems && ch < Cin) {
-      int m = m0 - pad + sr;
-      m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);
-      av[i] = *(const f32x4 *)(p.x + (int64_t)m * p.x_stride + ch);
-    }
-  }
-  float amax = 0.f;
-#pragma unroll
-  for (int i = 0; i < SK_ASLOTS; ++i) {
-    const int idx = tid + 512 * i;
-    if (idx >= nitems) break;
-    const int c = idx / (SR * 8), rem = idx - c * (SR * 8), sr = rem >> 3, seg = rem & 7;
-    const f32x4 x = av[i];
-    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
-    f16x4 h, t;
-    split2h(x, h, t);
-    _Float16 *dst = lds + c * 2 * SK_AIMG + sr * SL_P + seg * 4;
-    *(f16x4 *)dst = h;
-    *(f16x4 *)(dst + SK_AIMG) = t;
-  }
-  if (tid < SK_CPB * 2 * (SL_P / 8)) {
-    const int img = tid / (SL_P / 8), part = tid % (SL_P / 8);
-    *(u32x4 *)(lds + img * SK_AIMG + SK_ZROW * SL_P + part * 8) = (u32x4){0u, 0u, 0u, 0u};
-  }
-  __syncthreads();
-  bool bad = !(amax <= 65504.f);
-
-  // ---- wave w: column set w & 1, quarter w >> 1 of the heavy and of the light unit ------
-  const int cset = wave & 1, q = wave >> 1;
-  const int col0 = (nt + cset) * 16;
-  f32x4 acc[2][8];
-  auto run_unit = [&](int gw, f32x4 (&a)[8]) {
-    const GemmGroup &GW = p.g[gw];
-    const int kw = GW.k, padw = GW.pad, dp = pad - padw;
-    const int nsteps = nch * kw;
-    const int s_begin = (nsteps * q) >> 2, s_end = (nsteps * (q + 1)) >> 2;
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) a[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (col0 >= GW.N || s_end <= s_begin) return;  // wave-uniform
-    unsigned vmask[8];
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      const int m = m0 + mi * 16 + fr;
-      unsigned msk = 0;
-      if (m < p.M) {
-        const int t = m % p.T;
-        const int lo = max(padw - t, 0), hi = min(p.T - 1 + padw - t, kw - 1);
-        if (lo <= hi) msk = (2u << hi) - (1u << lo);
-      }
-      vmask[mi] = msk;
-    }
-    const int n = col0 + fr < GW.N ? col0 + fr : GW.N - 1;
-    const _Float16 *w0 = (const _Float16 *)GW.w3 + (int64_t)n * GW.Kpad;
-    const int64_t plane = (int64_t)GW.N * GW.Kpad;
-    auto loadB = [&](int s, f16x8 &b0, f16x8 &b1) {
-      const int j = s / nch, c = s - j * nch;
-      const int ch = (c_begin + c) * 32 + fs * 8;
-      const int off = j * Cin + (ch < Cin ? ch : 0);
-      b0 = *(const f16x8 *)(w0 + off);
-      b1 = *(const f16x8 *)(w0 + plane + off);
-    };
-    f16x8 rb0[SK_PF], rb1[SK_PF];
-#pragma unroll
-    for (int u = 0; u < SK_PF; ++u) loadB(min(s_begin + u, s_end - 1), rb0[u], rb1[u]);
-    for (int s0 = s_begin; s0 < s_end; s0 += SK_PF) {
-#pragma unroll
-      for (int u = 0; u < SK_PF; ++u) {
-        const int s = s0 + u;
-        const int sl = min(s, s_end - 1), j = sl / nch, c = sl - j * nch;
-        const _Float16 *Ab = lds + c * 2 * SK_AIMG;
-        f16x8 ah[8], at[8];
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-          const bool ok = (vmask[mi] >> j) & 1u;
-          const int o = (ok ? mi * 16 + fr + j + dp : SK_ZROW) * SL_P + fs * 8;
-          ah[mi] = *(const f16x8 *)(Ab + o);
-          at[mi] = *(const f16x8 *)(Ab + SK_AIMG + o);
-        }
-        const f16x8 z = {};
-        const bool bok = s < s_end && (c_begin + c) * 32 + fs * 8 < Cin;
-        const f16x8 b0 = bok ? rb0[u] : z, b1 = bok ? rb1[u] : z;
-        const f16x8 bh = b0 * (_Float16)(1.0f / H3_SCALE);
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) a[mi] = mma16(at[mi], bh, a[mi]);
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) a[mi] = mma16(ah[mi], b1, a[mi]);
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) a[mi] = mma16(ah[mi], b0, a[mi]);
-        loadB(min(s + SK_PF, s_end - 1), rb0[u], rb1[u]);
-      }
-    }
-  };
-  run_unit(__builtin_amdgcn_readfirstlane(gi), acc[0]);
-  run_unit(__builtin_amdgcn_readfirstlane(p.ngroups - 1 - gi), acc[1]);
-
-  // ---- the four quarters of each unit meet in LDS (the slab is dead after the barrier) ---
-  __syncthreads();
-#pragma unroll
-  for (int g2 = 0; g2 < 2; ++g2)
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) red[(((2 * cset + g2) * 4 + q) * 8 + mi) * 64 + lane] = acc[g2][mi];
-  __syncthreads();
-  // wave w finishes unit u = w >> 1 (column set u >> 1, heavy / light u & 1), fragments
-  // 4 (w & 1) .. + 4
-  const int u = wave >> 1, mlo = (wave & 1) * 4;
-  const int gw = __builtin_amdgcn_readfirstlane((u & 1) ? p.ngroups - 1 - gi : gi);
-  const GemmGroup &GW = p.g[gw];
-  const int ucol = (nt + (u >> 1)) * 16 + fr;
-  const bool cok = ucol < GW.N;
-  const int ec = cok ? ucol : GW.N - 1;
-  const float cs = GW.colscale[ec];
-  const bool direct = !(p.split > 1 || p.force_part);
-  const float bias = direct && GW.bias ? GW.bias[ec] : 0.f;
-  const float sc = direct && GW.scale ? GW.scale[ec] : 1.f;
-  const float sh = direct && GW.scale ? GW.shift[ec] : 0.f;
-#pragma unroll
-  for (int mj = 0; mj < 4; ++mj) {
-    const int mi = mlo + mj;
-    f32x4 v4 = red[((u * 4 + 0) * 8 + mi) * 64 + lane];
-    v4 += red[((u * 4 + 1) * 8 + mi) * 64 + lane];
-    v4 += red[((u * 4 + 2) * 8 + mi) * 64 + lane];
-    v4 += red[((u * 4 + 3) * 8 + mi) * 64 + lane];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = m0 + mi * 16 + 4 * fs + i;
-      if (!cok || row >= p.M) continue;
-      bad |= !__builtin_isfinite(v4[i]);
-      if (!direct) {
-        float *dst = p.part + (size_t)blockIdx.y * p.M * p.ldp + (size_t)row * p.ldp + GW.ycol0 + ucol;
-        if constexpr (LAST)  // write-through: the last arriver reads it with sc1 loads
-          __hip_atomic_store(dst, v4[i] * cs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          *dst = v4[i] * cs;
-      } else {
-        float y = v4[i] * cs + bias;
-        if (p.relu) y = fmaxf(y, 0.f);
-        if (GW.scale) y = y * sc + sh;
-        if (p.y) p.y[(int64_t)row * p.y_stride + GW.ycol0 + ucol] = y;
-      }
-    }
-  }
-  if constexpr (LAST) {
-    __shared__ int s_last;
-    if (p.split > 1) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores done
-      __syncthreads();
-      if (tid == 0) {
-        const unsigned old = __hip_atomic_fetch_add(p.tile_cnt + blockIdx.x, 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == (unsigned)p.split - 1;
-        if (s_last)  // every split block has added: zero for the next launch
-          __hip_atomic_store(p.tile_cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      if (s_last) bad |= bank_last_reduce(p, gi, nt, m0);
-    }
-  }
   if (bad && p.status) atomicOr(p.status, 1u);
 }
 
@@ -2525,13 +2202,7 @@ constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 // is one contiguous 1 KB run (from the planes it touches 16 half-used 128-B lines, their
 // other halves loaded by the next step).  Measured with the bit-3 timing variant's layout
 // (r4c stamps): 17.8 vs 20.4 us per call.
-//
-// PAIR (FTMI_BANK_PAIR): no exchange at all — each half stores its raw sums into its own
-// plane of y and the consumer (proj1's operand staging, conv_gemm_skinny_kernel PAIR) adds
-// the two planes and applies colscale, ReLU and the BN affine with the same expressions,
-// before its maxpool: bit-identical to this kernel's own finish.
-template <int MI, int NCH, int DIAG = 0, int KT = 0, int NCT = 0, bool PK = false,
-          bool PAIR = false>
+template <int MI, int NCH, int DIAG = 0, int KT = 0, int NCT = 0, bool PK = false>
 __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmParams p) {
   BHSTAMP(0, 0);
   constexpr int RM = MI * 16;
@@ -2780,24 +2451,6 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
     v[r] = s;
   }
   BHSTAMP(4, 0);
-  if constexpr (PAIR) {  // this half's raw sums into plane h: no exchange, no counter
-    float *const yp = p.y + h * p.y_plane;
-#pragma unroll
-    for (int r = 0; r < IPT; ++r) {
-      const int e = eo[r], ug = e / (MI * 64), mi = (e >> 6) % MI;
-      float *const yc = yp + (ug ? GL.ycol0 : GH.ycol0) + col;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = mi * 16 + 4 * fs + i;
-        if (row < p.M) yc[(int64_t)row * p.y_stride] = v[r][i];
-      }
-    }
-    if (bad && p.status) atomicOr(p.status, 1u);
-    BHSTAMP(5, 0);
-    BHSTAMP(6, 0);
-    BHSTAMP(7, 448);
-    return;
-  }
   // ---- write-through publish of this half's sums, then an arrival counter PER WAVE: wave w
   // owns row fragment w of both groups (items e = tid + 512 r), publishes them, waits for its
   // own stores and adds to the unit's counter w; the wave whose add returns 1 (its partner
@@ -3723,11 +3376,13 @@ static int launch_slab(const GemmParams &p, int epi, bool maxpool, hipStream_t s
   GemmParams q = p;
   const int nch = (q.Cin + 31) / 32;
   q.split = 1;
+#ifdef FTMI_DIAG
   static const int diag = [] {
     const char *e = getenv("FTMI_SLAB_DIAG");
     return e ? atoi(e) : 0;
   }();
   q.diag = diag;
+#endif
   // column bands of 2 (slab_tile): tools/gemm_one.py under rocprofv3, band 0 -> 2: c5 FFN conv
   // 1179 -> 1147 us (L2->fabric reads 913 -> 662 MB per launch), c3 prenet bank 803 -> 713,
   // postnet bank 710 -> 683, LSTM input projection 305 -> 297; proj1 (2 column tiles)
@@ -3817,29 +3472,13 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
   }
   // a CBHG bank (groups k = K .. 1, even K, 16-column multiples): the balanced schedule
   bool bank = q.ngroups >= 2 && q.ngroups % 2 == 0 && !maxpool && epi == EPI_CONV &&
-              q.g[0].N % 32 == 0 && bank_balanced_enabled() && !q.x_fin;
+              q.g[0].N % 32 == 0 && bank_balanced_enabled();
   for (int i = 0; bank && i < q.ngroups; ++i) bank = q.g[i].k == q.ngroups - i;
   if (bank) {
     dim3 grid(MT * (q.ngroups / 2) * (q.g[0].N / 32), q.split), block(512);
+#ifdef FTMI_DIAG
     const char *dg = getenv("FTMI_SKINNY_DIAG");  // timing experiments (results invalid)
-    // FTMI_BANK_QB=1: the quarter-balanced kernel (opt-in: measured slower, 27-29 against
-    // 24-25 us for the c2 prenet bank + finish)
-    const char *qb = getenv("FTMI_BANK_QB");
-    const bool qbk = qb && atoi(qb) == 1 && !(dg && atoi(dg) != 0) && !q.yt && !q.residual;
-    const bool last = q.tile_cnt && q.split > 1 && (int)grid.x <= FTMI_BANK_COUNTERS &&
-                      !q.yt && !q.residual && q.y && !(dg && atoi(dg) != 0) &&
-                      (int64_t)q.split * q.M * q.ldp * 4 < INT32_MAX;  // reducer byte offsets
-    if (last) {  // finished in-kernel by each tile's last split block: no finish launch
-      if (qbk)
-        hipLaunchKernelGGL(conv_bank_qb_kernel<true>, grid, block, 0, s, q);
-      else
-        hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true, 0, true>), grid, block, 0, s, q);
-      FTMI_CHECK_LAUNCH();
-      return FTMI_OK;
-    }
-    if (qbk)
-      hipLaunchKernelGGL(conv_bank_qb_kernel<false>, grid, block, 0, s, q);
-    else switch (dg ? atoi(dg) : 0) {
+    switch (dg ? atoi(dg) : 0) {
 #define FTMI_SK_DIAG(D_)                                                                   \
   case D_:                                                                                 \
     hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true, D_>), grid, block, 0, s, q); \
@@ -3849,13 +3488,12 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
       default:
         hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true>), grid, block, 0, s, q);
     }
+#else
+    hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true>), grid, block, 0, s, q);
+#endif
   } else {
     dim3 grid(MT * q.ngroups * NT, q.split), block(512);
-    if (q.x_fin && maxpool)
-      hipLaunchKernelGGL((conv_gemm_skinny_kernel<true, false, 0, false, true>), grid, block, 0, s, q);
-    else if (q.x_fin)
-      hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, false, 0, false, true>), grid, block, 0, s, q);
-    else if (maxpool)
+    if (maxpool)
       hipLaunchKernelGGL(conv_gemm_skinny_kernel<true>, grid, block, 0, s, q);
     else
       hipLaunchKernelGGL(conv_gemm_skinny_kernel<false>, grid, block, 0, s, q);
@@ -3904,41 +3542,14 @@ static int64_t bank_halves_floats(int M, int K, int N) {
 
 static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
   const int units = (p.ngroups / 2) * (p.g[0].N / 16);
-  const char *dg = getenv("FTMI_BANK_HALVES_DIAG");  // timing experiments (results invalid)
-  const int diag = dg ? atoi(dg) : 0;
   const dim3 grid(2 * units), block(512);
   const int nch = p.Cin / 64;
-#define FTMI_BH_NCH(MI_, D_)                                                                       \
-  switch (nch) {                                                                                   \
-    case 1: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 1, D_>), grid, block, 0, s, p); break; \
-    case 2: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 2, D_>), grid, block, 0, s, p); break; \
-    case 3: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 3, D_>), grid, block, 0, s, p); break; \
-    default: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 4, D_>), grid, block, 0, s, p);       \
-  }
   const bool prenet = p.ngroups == 16 && p.g[0].N == 256 && nch == 4;  // c2: (KT, NCT) = (16, 16)
-  if (p.y_plane) {  // FTMI_BANK_PAIR: raw half sums, finished by the consumer
-#define FTMI_BH_PR(MI_, PK_)                                                                                 \
-  switch (nch) {                                                                                             \
-    case 1: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 1, 0, 0, 0, PK_, true>), grid, block, 0, s, p); break; \
-    case 2: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 2, 0, 0, 0, PK_, true>), grid, block, 0, s, p); break; \
-    case 3: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 3, 0, 0, 0, PK_, true>), grid, block, 0, s, p); break; \
-    default: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 4, 0, 0, 0, PK_, true>), grid, block, 0, s, p);       \
-  }
-    if (p.wimg && prenet && p.M > 64) {
-      hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16, true, true>), grid, block, 0, s, p);
-    } else if (p.wimg) {
-      if (p.M <= 64) {
-        FTMI_BH_PR(4, true)
-      } else {
-        FTMI_BH_PR(8, true)
-      }
-    } else if (p.M <= 64) {
-      FTMI_BH_PR(4, false)
-    } else {
-      FTMI_BH_PR(8, false)
-    }
-#undef FTMI_BH_PR
-  } else if (p.wimg && prenet && diag) {  // timing variants of the image kernel (c2 prenet only)
+#ifdef FTMI_DIAG
+  // timing variants of the c2 prenet bank (results invalid for some bits): diagnostic build only
+  const char *dg = getenv("FTMI_BANK_HALVES_DIAG");
+  const int diag = dg && prenet && p.M > 64 ? atoi(dg) : 0;
+  if (diag && p.wimg) {
     switch (diag) {
 #define FTMI_BH_DIAG(D_)                                                                          \
   case D_:                                                                                        \
@@ -3950,39 +3561,31 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
       default:
         hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16, true>), grid, block, 0, s, p);
     }
-  } else if (p.wimg) {  // the stream-order weight image
-#define FTMI_BH_PK(MI_)                                                                                  \
-  switch (nch) {                                                                                         \
-    case 1: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 1, 0, 0, 0, true>), grid, block, 0, s, p); break; \
-    case 2: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 2, 0, 0, 0, true>), grid, block, 0, s, p); break; \
-    case 3: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 3, 0, 0, 0, true>), grid, block, 0, s, p); break; \
-    default: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 4, 0, 0, 0, true>), grid, block, 0, s, p);       \
+    FTMI_CHECK_LAUNCH();
+    return FTMI_OK;
   }
+#endif
+#define FTMI_BH_NCH(MI_, PK_)                                                                            \
+  switch (nch) {                                                                                         \
+    case 1: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 1, 0, 0, 0, PK_>), grid, block, 0, s, p); break; \
+    case 2: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 2, 0, 0, 0, PK_>), grid, block, 0, s, p); break; \
+    case 3: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 3, 0, 0, 0, PK_>), grid, block, 0, s, p); break; \
+    default: hipLaunchKernelGGL((conv_bank_halves_kernel<MI_, 4, 0, 0, 0, PK_>), grid, block, 0, s, p);       \
+  }
+  if (p.wimg) {  // the stream-order weight image
     if (p.M <= 64) {
-      FTMI_BH_PK(4)
+      FTMI_BH_NCH(4, true)
     } else if (prenet) {
       hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16, true>), grid, block, 0, s, p);
     } else {
-      FTMI_BH_PK(8)
+      FTMI_BH_NCH(8, true)
     }
-#undef FTMI_BH_PK
   } else if (p.M <= 64) {
-    FTMI_BH_NCH(4, 0)
-  } else if (prenet && diag == 0) {
+    FTMI_BH_NCH(4, false)
+  } else if (prenet) {
     hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16>), grid, block, 0, s, p);
-  } else if (diag == 0 || !prenet) {  // the timing switches exist for the c2 prenet only
-    FTMI_BH_NCH(8, 0)
-  } else switch (diag) {
-#define FTMI_BH_DIAG(D_)                                                                       \
-  case D_:                                                                                     \
-    hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, D_, 16, 16>), grid, block, 0, s, p);       \
-    break;
-      FTMI_BH_DIAG(1) FTMI_BH_DIAG(2) FTMI_BH_DIAG(3) FTMI_BH_DIAG(4) FTMI_BH_DIAG(7)
-      FTMI_BH_DIAG(16) FTMI_BH_DIAG(19) FTMI_BH_DIAG(32) FTMI_BH_DIAG(64) FTMI_BH_DIAG(96)
-      FTMI_BH_DIAG(128) FTMI_BH_DIAG(192) FTMI_BH_DIAG(8) FTMI_BH_DIAG(136)
-#undef FTMI_BH_DIAG
-      default:
-        hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4>), grid, block, 0, s, p);
+  } else {
+    FTMI_BH_NCH(8, false)
   }
 #undef FTMI_BH_NCH
   FTMI_CHECK_LAUNCH();
@@ -4003,12 +3606,6 @@ int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hip
           p.y && slab_ok(q, epi)))
       return FTMI_E_UNSUPPORTED;
     return launch_slab(q, epi, false, s);
-  }
-  if (p.x_fin) {  // a FTMI_BANK_PAIR operand: only the skinny kernel finishes it in staging
-    if (!(mma == 2 && presplit && epi == EPI_CONV && p.ngroups == 1 && !p.x_split &&
-          !p.y_split_c && skinny_ok(p, epi)))
-      return FTMI_E_UNSUPPORTED;
-    return launch_skinny(p, epi, maxpool, s);
   }
   if (p.y_split_c) return FTMI_E_UNSUPPORTED;  // split output rows: pool_out only
   if (p.x_split) {  // split operand rows: only the slab kernel stages them
@@ -4145,10 +3742,6 @@ extern "C" int ftmi_conv1d(const ftmi_conv_args *a, ftmi_stream_t stream) {
   p.x_split = a->x_split != 0;
   if (p.x_split && (a->mma != 2 || a->maxpool || a->x_stride < a->Cin))
     return FTMI_E_UNSUPPORTED;
-  p.x_fin = a->x_fin;
-  p.x_plane = a->x_plane;
-  if (p.x_fin && (!ftmi_aligned16(a->x_fin) || (a->x_plane & 3) || a->Cin % 4))
-    return FTMI_E_ALIGN;
   GemmGroup &g = p.g[0];
   g.w = a->w;
   g.Kpad = (a->k * a->Cin + X6_BK - 1) / X6_BK * X6_BK;
@@ -4308,17 +3901,14 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
   p.y = y;
   p.y_stride = y_stride;
   p.status = status;
-  if (pool_out & ~(FTMI_BANK_POOL | FTMI_BANK_Y_SPLIT | FTMI_BANK_X_SPLIT | FTMI_BANK_LAST |
-                   FTMI_BANK_HALVES | FTMI_BANK_IMAGE | FTMI_BANK_PAIR))
+  if (pool_out & ~(FTMI_BANK_POOL | FTMI_BANK_Y_SPLIT | FTMI_BANK_X_SPLIT | FTMI_BANK_HALVES |
+                   FTMI_BANK_IMAGE))
     return FTMI_E_ARG;
   const bool halves = (pool_out & FTMI_BANK_HALVES) != 0;
   const bool image = (pool_out & FTMI_BANK_IMAGE) != 0;
-  const bool pair = (pool_out & FTMI_BANK_PAIR) != 0;
-  if ((image || pair) && !halves) return FTMI_E_ARG;
-  if (halves && (!split_ws || mma != 2 ||
-                 (pool_out & ~(FTMI_BANK_HALVES | FTMI_BANK_IMAGE | FTMI_BANK_PAIR))))
+  if (image && !halves) return FTMI_E_ARG;
+  if (halves && (!split_ws || mma != 2 || (pool_out & ~(FTMI_BANK_HALVES | FTMI_BANK_IMAGE))))
     return FTMI_E_ARG;
-  if ((pool_out & FTMI_BANK_LAST) && (split_k <= 1 || !split_ws)) return FTMI_E_ARG;
   p.pool_out = pool_out & FTMI_BANK_POOL;
   if (pool_out & FTMI_BANK_Y_SPLIT) {  // split output rows need the pooled epilogue
     if (!p.pool_out) return FTMI_E_UNSUPPORTED;
@@ -4342,17 +3932,12 @@ extern "C" int ftmi_conv_bank_split(const float *x, int64_t x_stride, int32_t B,
         p.g[gi].colscale = cs + (int64_t)(K - 1 - gi) * Cout;
       }
     }
-    if (pair) p.y_plane = (int64_t)p.M * y_stride;  // the second half's plane
     if (!bank_halves_ok(p)) return FTMI_E_UNSUPPORTED;
     return launch_bank_halves(p, ftmi_hs(stream));
   }
   if (split_k > 1) {
     p.split_req = split_k;
     p.part = split_ws;
-    if (pool_out & FTMI_BANK_LAST) {  // tile counters first, then the partial sums
-      p.tile_cnt = (unsigned *)split_ws;
-      p.part = split_ws + FTMI_BANK_COUNTERS;
-    }
   }
   return launch(p, EPI_CONV, false, tile0, mma, ftmi_hs(stream));
 }

@@ -74,6 +74,12 @@ __device__ unsigned long long ftmi_rnn_stamps[2048 * 8];
   do {           \
   } while (0)
 #endif
+// timing experiments (FTMI_RNN_DIAG, results invalid when set): diagnostic build only
+#ifdef FTMI_DIAG
+#define RNN_DIAG(p) ((p).diag)
+#else
+#define RNN_DIAG(p) ((void)(p), 0u)
+#endif
 
 namespace {
 
@@ -120,15 +126,9 @@ struct RnnParams {
   int xcd_local;  // 1: try the census-based XCD-local mode
   unsigned *ws;   // control words (see WS_*)
   unsigned *status;  // optional: bit 1 = a W_hh entry overflowed f16 (mode 2)
-  // fused input projection (FUSE instances): x (B, T, FUSE_CIN) rows, W_ih [2][G*H][Cin],
-  // b_ih [2*G*H]; the gate inputs x_t W_ih^T + b_ih are computed in the recurrence
-  const float *x;
-  int64_t x_stride;
-  const float *w_ih;
-  const float *b_ih;
   unsigned spin_limit;  // bound of every spin (g_spin_limit at launch)
   int psleep;  // s_sleep(1) count before a step's first h poll (FTMI_RNN_PSLEEP; valid results)
-  int diag;  // timing experiments only (FTMI_RNN_DIAG, results invalid when set): bit 0 =
+  int diag;  // timing experiments only (FTMI_RNN_DIAG, diagnostic build only): bit 0 =
              // input projections from one L2-hot row, bit 1 = no hand-off waits,
              // bit 2 = no drain
 };
@@ -204,13 +204,10 @@ __device__ __forceinline__ void report_timeout(const RnnParams &p) {
   if (p.status) atomicOr(p.status, STATUS_TIMEOUT);
 }
 
-constexpr int FUSE_CIN = 256;  // input width of the fused-projection instances
-
 // NBL: live sequences per group (16, or 8 to spread a recurrence over twice the groups: every
 // workgroup then acquires and stores half the h bytes per step; the MFMA columns past NBL are
 // dead)
-template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false, bool CST = false,
-          int NBL = NB>
+template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB>
 __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(const RnnParams p) {
   constexpr bool X6 = MODE != 0;  // 16x16x32 fragment layout (bf16x6 and f16x3)
   constexpr bool H3 = MODE == 2;
@@ -229,17 +226,12 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   constexpr int CPT = CELLS / 256;
   static_assert(U % 16 == 0 && H % U == 0 && RB % WR == 0 && CELLS % 256 == 0, "shape");
   static_assert(X6 ? (KW % 32 == 0) : (KB % 4 == 0), "K split");
-  // FUSE (f16x3 GRU, several workgroups per group): each wave also multiplies its quarter of
-  // the input channels by W_ih; the partial gate inputs go through the same LDS reduction
-  static_assert(!FUSE || (H3 && CELL == 0 && !LOCAL), "fused input projection: f16x3 GRU");
   // CST: the compute waves store their own tagged h chunks right after the cell update (each
   // wave's 16 chunks are its own cells: CPT == 1), the comm wave only the y rows — barrier C
   // and the comm wave's stage read leave the h hand-off's critical path
   static_assert(!CST || (H3 && !LOCAL && CPT == 1 && U == 16), "compute-wave h stores");
-  static_assert(NBL == NB || (NBL == 8 && !LOCAL && !FUSE), "live sequences per group");
-  constexpr int KWI = FUSE ? FUSE_CIN / WK : 32;  // input channels per wave
-  constexpr int KSI = KWI / 32;                   // their 32-deep k-steps
-  constexpr int RR = FUSE ? 2 * R : R;            // reduction rows: W_hh h [+ W_ih x]
+  static_assert(NBL == NB || (NBL == 8 && !LOCAL), "live sequences per group");
+  constexpr int RR = R;                           // reduction rows
   constexpr float GSC = H3 ? H3_UNSCALE : 1.f;     // scale of the reduced W_hh h sums
 
   __shared__ __attribute__((aligned(16))) float red[WK * RR * RED_STRIDE];
@@ -421,35 +413,12 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
     }
   }
 
-  // ---- FUSE: W_ih slice (this wave's input-channel quarter) -> f16 head / scaled tail ----
-  f16x8 wi[FUSE ? RBW : 1][FUSE ? KSI : 1][2];
-  if constexpr (FUSE) {
-    const float *widir = p.w_ih + (size_t)dir * (G * H) * FUSE_CIN;
-#pragma unroll
-    for (int i = 0; i < RBW; ++i) {
-      const int lrow = (wr * RBW + i) * 16 + lc;
-      const int grow = (lrow / U) * H + u0 + (lrow % U);
-      const float *src = widir + (size_t)grow * FUSE_CIN + wk * KWI;
-#pragma unroll
-      for (int ks = 0; ks < KSI; ++ks) {
-        float v[8];
-        const f32x4 a = *(const f32x4 *)(src + ks * 32 + 8 * ls);
-        const f32x4 b = *(const f32x4 *)(src + ks * 32 + 8 * ls + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        split2h8(v, wi[i][ks][0], wi[i][ks][1]);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) wbad |= !(__builtin_fabsf(v[e]) <= 65504.f);
-      }
-    }
-  }
-
   if (wbad && p.status) atomicOr(p.status, 2u);
 
   // ---- per-thread cells: cell c = tid + 256*j -> (unit u = c % U, seq b = c / U) ------
   int cu[CPT], cb[CPT], cbl[CPT], len[CPT], hxo[CPT];
   bool cvalid[CPT];
-  float hstate[CPT], cstate[CPT], bhh[CPT][G], bih[FUSE ? CPT : 1][G];
+  float hstate[CPT], cstate[CPT], bhh[CPT][G];
 #pragma unroll
   for (int j = 0; j < CPT; ++j) {
     const int c = tid + 256 * j;
@@ -464,7 +433,6 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       bhh[j][g] = (CELL == 0) ? p.b_hh[dir * G * H + g * H + u0 + cu[j]] : 0.f;
-      if constexpr (FUSE) bih[j][g] = p.b_ih[dir * G * H + g * H + u0 + cu[j]];
     }
     // fragment-order position of (seq bl, unit k) in the group's 16*H slab
     const int k = u0 + cu[j];
@@ -525,40 +493,18 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
     for (int j = 0; j < CPT; ++j) {
       const int src = p.index ? ir[j] : tt;
       const float *row = src >= 0 ? xcol + (brow[j] + src) * p.xp_stride : zcol;
-      if (p.diag & 1) row = zcol;  // timing experiment: L2-hot rows
+      if (RNN_DIAG(p) & 1) row = zcol;  // timing experiment: L2-hot rows
 #pragma unroll
       for (int gi = 0; gi < G; ++gi) g[j][gi] = row[gi * H + cu[j]];
     }
   };
   float g0[CPT][G], g1[CPT][G], g2[CPT][G];
   int i0[CPT], i1[CPT], i2[CPT];
-  // FUSE: x rows of the chunk's 16 sequences (lane column lc), this wave's channel quarter,
-  // 8 consecutive channels per k-step (the MFMA B layout), two steps ahead in three sets
-  constexpr int NXR = FUSE ? 2 * KSI : 1;
-  f32x4 x0[NXR], x1[NXR], x2[NXR];
-  const int xb = chunk * NB + lc < p.B ? chunk * NB + lc : p.B - 1;
-  auto load_x = [&](int t, f32x4 (&xr)[NXR]) {
-    if constexpr (FUSE) {
-      const int tt = frame(t < p.T ? t : p.T - 1);
-      const float *row = p.x + ((size_t)xb * p.T + tt) * p.x_stride + wk * KWI + 8 * ls;
-#pragma unroll
-      for (int ks = 0; ks < KSI; ++ks) {
-        xr[2 * ks] = *(const f32x4 *)(row + ks * 32);
-        xr[2 * ks + 1] = *(const f32x4 *)(row + ks * 32 + 4);
-      }
-    }
-  };
-  float xamax = 0.f;  // FUSE range guard: largest |x| fed to the f16 split
-  if constexpr (FUSE) {
-    load_x(0, x0);
-    load_x(1, x1);
-  } else {
-    load_idx(0, i0);
-    load_idx(1, i1);
-    load_gx(0, i0, g0);
-    load_gx(1, i1, g1);
-    load_idx(2, i2);
-  }
+  load_idx(0, i0);
+  load_idx(1, i1);
+  load_gx(0, i0, g0);
+  load_gx(1, i1, g1);
+  load_idx(2, i2);
   if (LOCAL)
     for (int i = tid; i < 16 * H; i += 256) hloc[i] = 0.f;
   __syncthreads();
@@ -570,35 +516,9 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 
   // one time step; returns false when the launch must stop (hand-off timeout)
   auto step = [&](int t, const float (&gx)[CPT][G], float (&gnext)[CPT][G],
-                  const int (&inext)[CPT], int (&iload)[CPT], const f32x4 (&xc)[NXR],
-                  f32x4 (&xl)[NXR]) -> bool {
+                  const int (&inext)[CPT], int (&iload)[CPT]) -> bool {
     const int tt = frame(t);
     STAMP(0);
-    // FUSE: the gate inputs W_ih x_t, computed before the h hand-off wait (x_t was loaded
-    // two steps ago), as a sum of the f16 products w_h x_h + 2^-11 (w_t x_h + w_h x_t)
-    f32x4 axb[FUSE ? RBW : 1], axs[FUSE ? RBW : 1];
-    if constexpr (FUSE) {
-#pragma unroll
-      for (int i = 0; i < RBW; ++i) axb[i] = axs[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KSI; ++ks) {
-        float v[8];
-        v[0] = xc[2 * ks].x; v[1] = xc[2 * ks].y; v[2] = xc[2 * ks].z; v[3] = xc[2 * ks].w;
-        v[4] = xc[2 * ks + 1].x; v[5] = xc[2 * ks + 1].y;
-        v[6] = xc[2 * ks + 1].z; v[7] = xc[2 * ks + 1].w;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xamax = fmaxf(xamax, __builtin_fabsf(v[e]));
-        f16x8 xh, xt;
-        split2h8(v, xh, xt);
-#pragma unroll
-        for (int i = 0; i < RBW; ++i) {
-          axs[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wi[i][ks][1], xh, axs[i], 0, 0, 0);
-          axs[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wi[i][ks][0], xt, axs[i], 0, 0, 0);
-          axb[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wi[i][ks][0], xh, axb[i], 0, 0, 0);
-        }
-      }
-      load_x(t + 2, xl);
-    }
     // h_{t-1} operand: NL float4 per lane (fragment order), zero at t = 0.  f16x3 groups of
     // several workgroups exchange h pre-split: hr[2 ks] = 8 heads, hr[2 ks + 1] = 8 scaled
     // tails (f16), used as MFMA operands directly.
@@ -655,7 +575,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
           for (int i = 1; i < NL; ++i) o |= hr[i];
           fresh = ((o.x | o.y | o.z | o.w) & tmask) == 0u;
         }
-        if (__all(fresh || !hlive) || (p.diag & 2)) break;
+        if (__all(fresh || !hlive) || (RNN_DIAG(p) & 2) != 0) break;
         if (spins > p.spin_limit) {
           if (lane == 0) {
             s_abort = 1;
@@ -665,7 +585,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         }
         // no back-off: a poll is an L2 round trip already, and an s_sleep between polls
         // measured +9 % per step on the postnet GRU (FTMI_RNN_DIAG bit 16 restores it)
-        if (p.diag & 16) __builtin_amdgcn_s_sleep(1);
+        if (RNN_DIAG(p) & 16) __builtin_amdgcn_s_sleep(1);
       }
 #pragma unroll
       for (int i = 0; i < (HSPLIT ? 0 : NL); ++i) {
@@ -679,10 +599,8 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       }
     }
     STAMP(1);
-    if constexpr (!FUSE) {
-      load_gx(t + 2, inext, gnext);
-      load_idx(t + 3, iload);
-    }
+    load_gx(t + 2, inext, gnext);
+    load_idx(t + 3, iload);
     STAMP(2);
 
     // partial gates over this wave's K range
@@ -746,14 +664,6 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         red[(wk * RR + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] = acc[i][e];
-    if constexpr (FUSE) {
-#pragma unroll
-      for (int i = 0; i < RBW; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          red[(wk * RR + R + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] =
-              axb[i][e] + axs[i][e] * H3_UNSCALE;
-    }
     __syncthreads();
     if (!LOCAL && s_abort) return false;  // a wave timed out acquiring h_{t-1}
     STAMP(3);
@@ -770,14 +680,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 #pragma unroll
         for (int w = 1; w < WK; ++w) sum += red[(w * RR + row) * RED_STRIDE + bl];
         gs[g] = sum;  // H3: 2^11 (W_hh h)
-        if constexpr (FUSE) {  // x_t W_ih^T + b_ih (the unfused path adds b_ih in its GEMM)
-          float sx = red[(R + row) * RED_STRIDE + bl];
-#pragma unroll
-          for (int w = 1; w < WK; ++w) sx += red[(w * RR + R + row) * RED_STRIDE + bl];
-          gi[g] = sx + bih[j][g];
-        } else {
-          gi[g] = gx[j][g];
-        }
+        gi[g] = gx[j][g];
       }
       float hn;
       if (CELL == 0) {
@@ -855,11 +758,10 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   };
 
   for (int t = 0; t < p.T; t += 3) {
-    if (!step(t, g0, g2, i2, i0, x0, x2)) break;
-    if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1, x1, x0)) break;
-    if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2, x2, x1)) break;
+    if (!step(t, g0, g2, i2, i0)) break;
+    if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1)) break;
+    if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2)) break;
   }
-  if (FUSE && !(xamax <= 65504.f) && p.status) atomicOr(p.status, 1u);
 #ifdef FTMI_RNN_STAMPS
   if (tid == 0)
     for (int i = 0; i < 6; ++i) ftmi_rnn_stamps[blockIdx.x * 8 + i] = st_acc[i];
@@ -999,7 +901,7 @@ __global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * GV_KSEG) void rnn_gem
           const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, soff, 16);
           const bool fresh = want ? ((r.x & r.y & r.z & r.w) & 1u) != 0u
                                   : ((r.x | r.y | r.z | r.w) & 1u) == 0u;
-          if (fresh || (p.diag & 2)) {
+          if (fresh || (RNN_DIAG(p) & 2)) {
             v = __builtin_bit_cast(f32x4, r);
             break;
           }
@@ -1102,293 +1004,6 @@ __global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * GV_KSEG) void rnn_gem
   }
 }
 
-// ---- row-owning f16x3 recurrence (opt-in, FTMI_RNN_ROW=1; see row_path) ----------------
-// One WAVE owns 4 hidden units: its 16-row W_hh tile is ordered (unit, gate) = (lc / 4,
-// lc % 4), so the 16x16x32 MFMA accumulator of lane (ls, lc) holds the gate sums of unit ls
-// for sequence lc — the cell update runs on the accumulators (no K-split partials, no LDS
-// reduction) and each lane stores its own tagged h (f16 head | scaled f16 tail, one 32-bit
-// word) into the exchange buffer: no comm wave, no staging.  Each wave holds the full K of
-// its rows (H / 4 VGPRs of f16 head + tail).  The group's h_{t-1} is acquired ONCE per
-// workgroup — each wave polls a quarter of it (step tags, as rnn_bidir_kernel) — and written
-// into an LDS B-fragment image the four waves share: ONE barrier per step.
-// NBL live sequences per group (16, 8 or 4; the MFMA's other columns are dead): the h bytes a
-// workgroup acquires per step scale with NBL, the MFMA work per wave does not, so a smaller
-// NBL spreads a small-H recurrence over more CUs at a lower per-step latency.
-// Exchange layout of a group: [H/4 unit quads][NBL sequences][4 units] u32 words; a wave's
-// 64 (or 4 NBL) stores of one step are one contiguous run.
-template <int CELL, int H, int NBL>
-__global__ __launch_bounds__(256, 1) void rnn_row_kernel(const RnnParams p) {
-  constexpr int G = CELL ? 4 : 3;
-  constexpr int U = 16;            // units per workgroup (4 per wave)
-  constexpr int BPG = H / U;
-  constexpr int KS = H / 32;       // 32-deep k-steps of the contraction
-  constexpr int KSW = KS / 4;      // k-steps whose h each wave acquires
-  constexpr int SLAB = H * NBL;    // u32 words of one group's h
-  static_assert(KS % 4 == 0 && BPG >= 2 && BPG <= FLAGS_PER_GROUP && 16 % NBL == 0, "shape");
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  __shared__ u32x4 hl[2][KS][2][64];  // [step parity][k-step][head, tail][lane]
-  __shared__ int s_abort, s_group, s_bi, s_mode;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ls = lane >> 4, lc = lane & 15;
-
-  // ---- group assignment: the census of rnn_bidir_kernel ---------------------------------
-  if (tid == 0) {
-    int mode = 0, group = blockIdx.x % p.ngroups, bi = blockIdx.x / p.ngroups, abort = 0;
-    if (p.xcd_local) {
-      const unsigned x = xcc_id();
-      const unsigned slot = __hip_atomic_fetch_add(p.ws + WS_CENSUS + x * CNT_PAD, 1u,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(p.ws + WS_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (!poll_ge(p.ws + WS_ARRIVE, gridDim.x, p.spin_limit)) {
-        abort = 1;
-        report_timeout(p);
-      } else if (p.ngroups % 8 == 0 || (int)gridDim.x == 8 * BPG) {
-        const int gpx = p.ngroups % 8 == 0 ? p.ngroups / 8 : 1;
-        const unsigned per = (unsigned)gpx * BPG;
-        bool balanced = true;
-        for (int i = 0; i < 8; ++i)
-          balanced &= __hip_atomic_load(p.ws + WS_CENSUS + i * CNT_PAD, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT) == per;
-        if (balanced) {
-          mode = 1;
-          group = (int)(x * gpx + slot / BPG);
-          bi = (int)(slot % BPG);
-        }
-      }
-    }
-    s_mode = mode;
-    s_group = group;
-    s_bi = bi;
-    s_abort = abort;
-  }
-  __syncthreads();
-  if (s_abort) return;
-  if (s_group >= p.ngroups || s_bi >= BPG) return;  // surplus workgroups of a padded grid
-  const int group = s_group, bi = s_bi;
-  const bool xcd_mode = s_mode == 1;
-  const int dir = group & 1;
-  const int chunk = p.chunk0 + (group >> 1);
-  const int gglob = p.chunk0 * 2 + group;
-  const int u0 = bi * U;
-
-  // ---- W_hh tile -> f16 head / scaled tail A-fragments (row lc = unit lc/4, gate lc%4;
-  // the GRU's fourth gate row is zero) ------------------------------------------------------
-  f16x8 wh[KS], wt[KS];
-  bool wbad = false;
-  {
-    const int gate = lc & 3, unit = u0 + 4 * wave + (lc >> 2);
-    const bool gl = gate < G;
-    const float *src = p.w_hh + (size_t)dir * (G * H) * H +
-                       (size_t)((gl ? gate : 0) * H + unit) * H + 8 * ls;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const f32x4 a = *(const f32x4 *)(src + ks * 32);
-      const f32x4 b = *(const f32x4 *)(src + ks * 32 + 4);
-      float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        v[e] = gl ? v[e] : 0.f;
-        wbad |= !(__builtin_fabsf(v[e]) <= 65504.f);
-      }
-      split2h8(v, wh[ks], wt[ks]);
-    }
-  }
-  if (wbad && p.status) atomicOr(p.status, 2u);
-
-  // ---- the cell of this lane: unit cu of the workgroup, sequence lc of the group ---------
-  const int cu = 4 * wave + ls;
-  const int b = chunk * NBL + lc;
-  const bool live = lc < NBL;  // the MFMA column carries a sequence of this group
-  const bool cvalid = live && b < p.B;
-  const int bsafe = cvalid ? b : 0;
-  float hstate = 0.f, cstate = 0.f, bhh[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) bhh[g] = (CELL == 0) ? p.b_hh[dir * G * H + g * H + u0 + cu] : 0.f;
-  const int len = (p.lengths && cvalid) ? p.lengths[b] : p.T;
-  const int32_t *iptr = p.index ? p.index + (size_t)bsafe * p.T : (const int32_t *)p.ws;
-  const size_t brow = (size_t)bsafe * p.T_src;
-  const float *xcol = p.xp + dir * G * H + u0 + cu;
-  const float *zcol = (p.index ? p.xp_zero : p.xp) + dir * G * H + u0 + cu;
-  auto frame = [&](int t) { return dir ? (p.T - 1 - t) : t; };
-  auto load_idx = [&](int t) -> int { return iptr[p.index ? frame(t < p.T ? t : p.T - 1) : 0]; };
-  auto load_gx = [&](int t, int ir, float (&g)[G]) {
-    const int tt = frame(t < p.T ? t : p.T - 1);
-    const int src = p.index ? ir : tt;
-    const float *row = src >= 0 ? xcol + (brow + src) * p.xp_stride : zcol;
-    if (p.diag & 1) row = zcol;  // timing experiment: L2-hot rows
-#pragma unroll
-    for (int gi = 0; gi < G; ++gi) g[gi] = row[gi * H];
-  };
-
-  // ---- exchange addresses ----------------------------------------------------------------
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.hx, (short)0, 0x7FFFFFF0, 0x00020000);
-  const int par_bytes = p.ngroups_total * SLAB * 4;
-  const unsigned gbase = (unsigned)gglob * SLAB * 4u;
-  // producer: word ((quad * NBL + seq) * 4 + unit in quad), quad = (u0 + 4 wave) / 4
-  const unsigned st_off = gbase + (unsigned)((((bi * 4 + wave) * NBL + lc) * 4 + ls) * 4);
-  // consumer: k-step ks = wave * KSW + j needs quads 8 ks + 2 ls and 8 ks + 2 ls + 1 of
-  // sequence lc (dead columns read a live sequence's words: valid addresses, ignored)
-  const int lcl = live ? lc : lc % NBL;
-  unsigned ld_off[KSW];
-#pragma unroll
-  for (int j = 0; j < KSW; ++j)
-    ld_off[j] = gbase + (unsigned)((((wave * KSW + j) * 8 + 2 * ls) * NBL + lcl) * 16);
-
-  float g0[G], g1[G], g2[G];
-  int i0 = load_idx(0), i1 = load_idx(1);
-  load_gx(0, i0, g0);
-  load_gx(1, i1, g1);
-  int i2 = load_idx(2);
-
-  auto step = [&](int t, const float (&gx)[G], float (&gnext)[G], int inext, int &iload) -> bool {
-    const int tt = frame(t);
-    // ---- acquire this wave's quarter of h_{t-1} (tags in bits 0 and 16 of every word) ----
-    u32x4 hr[2 * KSW];
-    if (t == 0) {
-#pragma unroll
-      for (int i = 0; i < 2 * KSW; ++i) hr[i] = (u32x4){0u, 0u, 0u, 0u};
-    } else {
-      const int soff = ((t - 1) & 1) * par_bytes;
-      const bool want1 = h_tag(t - 1) != 0u;
-      for (unsigned spins = 0;; ++spins) {
-        // a compiler memory barrier: without it the loop (no store on its path) lets LICM
-        // hoist the loads out and spin on the first values
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int j = 0; j < KSW; ++j) {
-          hr[2 * j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ld_off[j], soff, 16);
-          hr[2 * j + 1] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ld_off[j] + NBL * 16, soff, 16);
-        }
-        bool fresh;
-        if (want1) {
-          u32x4 a = hr[0];
-#pragma unroll
-          for (int i = 1; i < 2 * KSW; ++i) a &= hr[i];
-          fresh = ((a.x & a.y & a.z & a.w) & 0x00010001u) == 0x00010001u;
-        } else {
-          u32x4 o = hr[0];
-#pragma unroll
-          for (int i = 1; i < 2 * KSW; ++i) o |= hr[i];
-          fresh = ((o.x | o.y | o.z | o.w) & 0x00010001u) == 0u;
-        }
-        if (__all(fresh || !live) || (p.diag & 2)) break;
-        if (spins > p.spin_limit) {
-          if (lane == 0) {
-            s_abort = 1;
-            report_timeout(p);
-          }
-          break;
-        }
-      }
-    }
-    // ---- B-fragment image: heads / tails of units 32 ks + 8 ls + (0..7), sequence lc ----
-#pragma unroll
-    for (int j = 0; j < KSW; ++j) {
-      const u32x4 a = hr[2 * j], c = hr[2 * j + 1];
-      u32x4 hh, ht;
-      hh.x = __builtin_amdgcn_perm(a.y, a.x, 0x05040100u);
-      hh.y = __builtin_amdgcn_perm(a.w, a.z, 0x05040100u);
-      hh.z = __builtin_amdgcn_perm(c.y, c.x, 0x05040100u);
-      hh.w = __builtin_amdgcn_perm(c.w, c.z, 0x05040100u);
-      ht.x = __builtin_amdgcn_perm(a.y, a.x, 0x07060302u);
-      ht.y = __builtin_amdgcn_perm(a.w, a.z, 0x07060302u);
-      ht.z = __builtin_amdgcn_perm(c.y, c.x, 0x07060302u);
-      ht.w = __builtin_amdgcn_perm(c.w, c.z, 0x07060302u);
-      if (!live) hh = ht = (u32x4){0u, 0u, 0u, 0u};
-      hl[t & 1][wave * KSW + j][0][lane] = hh;
-      hl[t & 1][wave * KSW + j][1][lane] = ht;
-    }
-    __syncthreads();
-    if (s_abort) return false;  // a wave timed out acquiring h_{t-1}
-    load_gx(t + 2, inext, gnext);  // the projections two steps ahead (independent of h)
-    iload = load_idx(t + 3);
-
-    // ---- W_hh h over the whole K: big = W_h h_h, sml = W_t h_h + W_h h_t ---------------
-    f32x4 big = {0.f, 0.f, 0.f, 0.f}, sml = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const f16x8 hh = __builtin_bit_cast(f16x8, hl[t & 1][ks][0][lane]);
-      const f16x8 ht = __builtin_bit_cast(f16x8, hl[t & 1][ks][1][lane]);
-      sml = __builtin_amdgcn_mfma_f32_16x16x32_f16(wt[ks], hh, sml, 0, 0, 0);
-      sml = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ks], ht, sml, 0, 0, 0);
-      big = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ks], hh, big, 0, 0, 0);
-    }
-    // ---- cell update on the accumulators: element e = gate e of unit cu, sequence lc ----
-    float gs[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) gs[e] = fmaf(sml[e], H3_UNSCALE, big[e]);
-    float hn;
-    if (CELL == 0) {
-      const float r = fast_sigmoid(gx[0] + (gs[0] + bhh[0]));
-      const float z = fast_sigmoid(gx[1] + (gs[1] + bhh[1]));
-      const float n = fast_tanh(gx[2] + r * (gs[2] + bhh[G - 1]));
-      hn = n + z * (hstate - n);
-    } else {
-      const float ig = fast_sigmoid(gs[0] + gx[0]);
-      const float fg = fast_sigmoid(gs[1] + gx[1]);
-      const float gg = fast_tanh(gs[2] + gx[2]);
-      const float og = fast_sigmoid(gs[3] + gx[G - 1]);
-      cstate = fg * cstate + ig * gg;
-      hn = og * fast_tanh(cstate);
-    }
-    if (tt >= len) {  // packed-sequence padding: reverse direction restarts from zero
-      hn = 0.f;
-      cstate = 0.f;
-    }
-    hstate = hn;
-    // tagged f16 head and scaled tail (tail taken after the head's tag bit is set), as
-    // rnn_bidir_kernel's pre-split exchange; the state and the output stay exact fp32
-    const unsigned short tg = (unsigned short)h_tag(t);
-    const unsigned short h16 =
-        (unsigned short)((__builtin_bit_cast(unsigned short, (_Float16)hn) & 0xFFFEu) | tg);
-    const unsigned short t16 = (unsigned short)(
-        (__builtin_bit_cast(unsigned short,
-                            (_Float16)((hn - (float)__builtin_bit_cast(_Float16, h16)) * H3_SCALE)) &
-         0xFFFEu) | tg);
-    if (live) {
-      const unsigned word = (unsigned)h16 | ((unsigned)t16 << 16);
-      if (xcd_mode)  // stays in this XCD's L2, read back by same-XCD sc1 loads
-        __builtin_amdgcn_raw_buffer_store_b32(word, rsrc, st_off, (t & 1) * par_bytes, 0);
-      else  // write-through (sc1)
-        __builtin_amdgcn_raw_buffer_store_b32(word, rsrc, st_off, (t & 1) * par_bytes, 16);
-    }
-    if (cvalid)
-      p.y[((size_t)b * p.T + tt) * p.y_stride + dir * H + u0 + cu] = tt >= len ? p.pad_value : hn;
-    return true;
-  };
-
-  for (int t = 0; t < p.T; t += 3) {
-    if (!step(t, g0, g2, i2, i0)) break;
-    if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1)) break;
-    if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2)) break;
-  }
-}
-
-template <int CELL, int H, int NBL>
-int launch_row(RnnParams p, int max_blocks, hipStream_t s) {
-  constexpr int BPG = H / 16;
-  const int nchunks = (p.B + NBL - 1) / NBL;
-  p.ngroups_total = 2 * nchunks;
-  if (!hx_fits(p, H, (int64_t)H * NBL)) return FTMI_E_SHAPE;  // never index past the workspace
-  const int max_groups = (max_blocks / BPG) & ~1;
-  if (max_groups < 2) return FTMI_E_UNSUPPORTED;
-  for (int c0 = 0; c0 < nchunks; c0 += max_groups / 2) {
-    const int nc = (nchunks - c0) < max_groups / 2 ? (nchunks - c0) : max_groups / 2;
-    p.chunk0 = c0;
-    p.ngroups = 2 * nc;
-    if (c0 > 0) {  // the census words are per launch
-      hipError_t e = hipMemsetAsync(p.ws + WS_CENSUS, 0, (WS_FLAGS - WS_CENSUS) * 4, s);
-      if (e != hipSuccess) return (int)e;
-    }
-    int nblk = p.ngroups * BPG;
-    if (p.xcd_local && p.ngroups < 8 && 8 * BPG <= max_blocks) nblk = 8 * BPG;
-    hipLaunchKernelGGL((rnn_row_kernel<CELL, H, NBL>), dim3(nblk), dim3(256), 0, s, p);
-    FTMI_CHECK_LAUNCH();
-  }
-  return FTMI_OK;
-}
-
 template <int CELL, int H, int U>
 int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
   constexpr int BPG = H / U;
@@ -1412,8 +1027,7 @@ int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
   return FTMI_OK;
 }
 
-template <int CELL, int H, int U, int WK, int MODE, bool FUSE = false, bool CST = false,
-          int NBL = NB>
+template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB>
 int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
   if (NBL != NB) {  // chunks of NBL sequences (the caller counted chunks of NB)
     nchunks = (p.B + NBL - 1) / NBL;
@@ -1440,7 +1054,7 @@ int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
     int nblk = p.ngroups * BPG;
     if (BPG > 1 && pad_env && p.xcd_local && p.ngroups < 8 && 8 * BPG <= max_blocks)
       nblk = 8 * BPG;
-    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, FUSE, CST, NBL>), dim3(nblk),
+    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, CST, NBL>), dim3(nblk),
                        dim3(BPG == 1 ? 256 : 320), 0, s, p);
     FTMI_CHECK_LAUNCH();
   }
@@ -1489,27 +1103,6 @@ static int rnn_units(int cell, int H, int mma) {
   return 16;
 }
 
-// FTMI_RNN_ROW=1: the f16x3 recurrences of H = 128 / 256 / 512 run on rnn_row_kernel (opt-in:
-// measured slower than rnn_bidir_kernel at c3 — LSTM 1.84-1.87 against 1.65-1.73 us/step,
-// postnet GRU 1.30-1.34 against 1.26 — its shared LDS h image makes the MFMA phase LDS-bound,
-// 4 waves x 32 KB of fragment reads per step; read per call: tests switch it)
-static bool row_path(int cell, int H, int mma) {
-  const char *v = getenv("FTMI_RNN_ROW");
-  const int env = v ? atoi(v) : 0;
-  return env && mma == 2 && ((cell == 1 && H == 512) || (cell == 0 && (H == 128 || H == 256)));
-}
-// live sequences per group of rnn_row_kernel: 16, or with FTMI_RNN_SPREAD the smallest of
-// 4 / 8 whose groups all fit the device at once (fewer h bytes per workgroup and step);
-// FTMI_RNN_NB (4, 8, 16) forces it
-static int row_nbl(int B, int H, bool spread, int maxb) {
-  const char *v = getenv("FTMI_RNN_NB");
-  if (v && (atoi(v) == 4 || atoi(v) == 8 || atoi(v) == 16)) return atoi(v);
-  if (!spread) return 16;
-  for (int nbl = 4; nbl <= 8; nbl *= 2)
-    if (2 * ((B + nbl - 1) / nbl) * (H / 16) <= maxb) return nbl;
-  return 16;
-}
-
 // FTMI_RNN_CSTORE=0 (read per call) keeps the comm wave's h stores: measured at c3, the
 // compute waves' own stores take the postnet GRU 1.315 -> 1.116 us/step, the LSTM 1.55 ->
 // 1.535 (barrier C and the stage read leave the hand-off's critical path)
@@ -1533,17 +1126,6 @@ extern "C" int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t m
   const bool spread = (mma & FTMI_RNN_SPREAD) != 0;
   mma &= 0xFF;
   if (gemv_path(cell, B, H)) return (xcd_local_env() ? 8 : 2) * (H / 16);  // launch_gemv
-  if (row_path(cell, H, mma)) {  // launch_row
-    const int maxb = device_cu_count(), bpg = H / 16;
-    const int nbl = row_nbl(B, H, spread, maxb);
-    const int max_groups = (maxb / bpg) & ~1;
-    if (max_groups < 2) return 0;
-    const int nchunks = (B + nbl - 1) / nbl;
-    const int ngroups = 2 * (nchunks < max_groups / 2 ? nchunks : max_groups / 2);
-    int nblk = ngroups * bpg;
-    if (xcd_local_env() && ngroups < 8 && 8 * bpg <= maxb) nblk = 8 * bpg;
-    return nblk;
-  }
   const int bpg = H / rnn_units(cell, H, mma);
   const int maxb = device_cu_count();
   const int max_groups = (maxb / bpg) & ~1;
@@ -1575,8 +1157,7 @@ extern "C" int64_t ftmi_rnn_error_offset(int32_t B) {
   return WS_ERR * (int64_t)sizeof(unsigned);
 }
 
-// the launch set-up shared by ftmi_rnn_bidir and ftmi_gru_bidir_fused: clears the
-// workspace (control words and the exchange buffer) and fills the common parameters
+// the launch set-up of ftmi_rnn_bidir: clears the workspace (control words and the exchange buffer) and fills the common parameters
 static int rnn_setup(RnnParams &p, int B, int T, int H, int cell, const float *w_hh,
                      const float *b_hh, const int32_t *lengths, float pad_value, float *y,
                      int64_t y_stride, uint32_t *status, void *sync, hipStream_t s,
@@ -1600,11 +1181,13 @@ static int rnn_setup(RnnParams &p, int B, int T, int H, int cell, const float *w
   p.hx = (float *)((char *)sync + ctl);
   p.status = status;
   p.spin_limit = g_spin_limit;
+#ifdef FTMI_DIAG
   static const int diag_env = [] {
     const char *v = getenv("FTMI_RNN_DIAG");
     return v ? atoi(v) : 0;
   }();
   p.diag = diag_env;
+#endif
   // s_sleep(1) count before a step's first h poll (rnn_bidir_kernel): the first poll then
   // lands after the producers' stores instead of a round trip before them.  Interleaved A/B
   // at c3 (tools/rnn_env_ab.py, two boxes): 3 -> LSTM 1.55 -> 1.52-1.54, postnet GRU 1.32 ->
@@ -1652,19 +1235,6 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
     if (H == 128) return launch_gemv<0, 128, 16>(p, maxb, s);
     return launch_gemv<0, 64, 16>(p, maxb, s);
   }
-  if (row_path(cell, H, mma)) {
-    const int nbl = row_nbl(B, H, spread, maxb);
-#define FTMI_ROW_NB(CELL_, H_)                                         \
-  switch (nbl) {                                                       \
-    case 4: return launch_row<CELL_, H_, 4>(p, maxb, s);               \
-    case 8: return launch_row<CELL_, H_, 8>(p, maxb, s);               \
-    default: return launch_row<CELL_, H_, 16>(p, maxb, s);             \
-  }
-    if (cell == 1) FTMI_ROW_NB(1, 512)
-    if (H == 256) FTMI_ROW_NB(0, 256)
-    FTMI_ROW_NB(0, 128)
-#undef FTMI_ROW_NB
-  }
 #define FTMI_RNN_MODES(CELL_, H_, U_, WKX_, WKF_)                                   \
   switch (mma) {                                                                    \
     case 2: return launch_rnn<CELL_, H_, U_, WKX_, 2>(p, nchunks, maxb, s);          \
@@ -1684,56 +1254,20 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   if (cell == 0 && H == 128) FTMI_RNN_MODES(0, 128, 16, 4, 4)
   // H = 256 / 512: 16 units per workgroup (32 units measured 1.84 against 1.19 us/step for
   // the H = 256 GRU; the LSTM's W_hh slice does not fit the VGPRs at 32 units)
-  // FTMI_RNN_WK=2 (timing experiments): the LSTM with a 2-way K split (two row halves per
-  // workgroup) on the f16x3 path instead of 4
-  static const int wk_env = [] {
-    const char *v = getenv("FTMI_RNN_WK");
-    return v ? atoi(v) : 4;
-  }();
   // f16x3, 16 units per workgroup: the compute waves store their own h (CST) and a spread
   // GRU runs 8 live sequences per group (legacy_nbl).  H = 128 keeps the form above (it
   // returned before this block since round 3; legacy_nbl agrees, so ftmi_rnn_blocks reports
   // the launch's real workgroup count)
   if (mma == 2 && cst_enabled() && ((cell == 1 && H == 512) || (cell == 0 && H == 256))) {
     const bool nb8 = legacy_nbl(cell, B, H, mma, spread, maxb) == 8;
-    if (cell == 1) return launch_rnn<1, 512, 16, 4, 2, false, true>(p, nchunks, maxb, s);
-    return nb8 ? launch_rnn<0, 256, 16, 4, 2, false, true, 8>(p, nchunks, maxb, s)
-               : launch_rnn<0, 256, 16, 4, 2, false, true>(p, nchunks, maxb, s);
+    if (cell == 1) return launch_rnn<1, 512, 16, 4, 2, true>(p, nchunks, maxb, s);
+    return nb8 ? launch_rnn<0, 256, 16, 4, 2, true, 8>(p, nchunks, maxb, s)
+               : launch_rnn<0, 256, 16, 4, 2, true>(p, nchunks, maxb, s);
   }
-  if (wk_env == 2 && mma == 2 && cell == 1 && H == 512)
-    return launch_rnn<1, 512, 16, 2, 2>(p, nchunks, maxb, s);
   if (cell == 0 && H == 256) FTMI_RNN_MODES(0, 256, 16, 4, 4)
   if (cell == 1 && H == 512) FTMI_RNN_MODES(1, 512, 16, 4, 4)
 #undef FTMI_RNN_MODES
   return FTMI_E_UNSUPPORTED;
-}
-
-extern "C" int ftmi_gru_bidir_fused(int32_t B, int32_t T, int32_t H, const float *x,
-                                    int64_t x_stride, int32_t Cin, const float *w_ih,
-                                    const float *b_ih, const float *w_hh, const float *b_hh,
-                                    const int32_t *lengths, float pad_value, float *y,
-                                    int64_t y_stride, uint32_t *status, void *sync,
-                                    ftmi_stream_t stream) {
-  if (!x || !w_ih || !b_ih || !w_hh || !b_hh || !y || !sync) return FTMI_E_ARG;
-  if (B <= 0 || T <= 0 || H <= 0 || Cin <= 0) return FTMI_E_ARG;
-  if (Cin != FUSE_CIN || (H != 128 && H != 256)) return FTMI_E_UNSUPPORTED;
-  if (!ftmi_aligned16(x) || (x_stride & 3) || !ftmi_aligned16(w_ih)) return FTMI_E_ALIGN;
-  if (!ftmi_aligned16(w_hh) || !ftmi_aligned16(sync)) return FTMI_E_ALIGN;
-  if (!ftmi_aligned16(y) || (y_stride & 3)) return FTMI_E_ALIGN;
-  hipStream_t s = ftmi_hs(stream);
-  RnnParams p = {};
-  int nchunks = 0;
-  const int rc = rnn_setup(p, B, T, H, 0, w_hh, b_hh, lengths, pad_value, y, y_stride, status,
-                           sync, s, nchunks);
-  if (rc != FTMI_OK) return rc;
-  p.T_src = T;
-  p.x = x;
-  p.x_stride = x_stride;
-  p.w_ih = w_ih;
-  p.b_ih = b_ih;
-  const int maxb = device_cu_count();
-  if (H == 128) return launch_rnn<0, 128, 16, 4, 2, true>(p, nchunks, maxb, s);
-  return launch_rnn<0, 256, 16, 4, 2, true>(p, nchunks, maxb, s);
 }
 
 #ifdef FTMI_RNN_STAMPS

@@ -338,7 +338,7 @@ extern "C" int ftmi_rowdot(const float *x, int64_t x_stride, int64_t M, int32_t 
   return FTMI_OK;
 }
 
-extern "C" int ftmi_abi_version(void) { return 17; }
+extern "C" int ftmi_abi_version(void) { return 18; }
 
 extern "C" const char *ftmi_strerror(int code) {
   switch (code) {

@@ -312,25 +312,15 @@ def split_bank_weights(w: torch.Tensor, K: int, Cin: int, Cout: int,
 def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, relu=False,
            bn=None, maxpool=False, residual=None, out=None, out_t=None, want_y=True,
            T_out: int = 0, mma: Optional[int] = None, w_split: Optional[torch.Tensor] = None,
-           x_split: bool = False, x_fin: Optional[torch.Tensor] = None):
+           x_split: bool = False):
     """Fused Conv1d (+bias, ReLU, BN, residual) on a channels-last (B, T, Cin) view.
 
     w: packed [N][k*Cin].  Returns (y, yt) where y is (B, T_out, N) (or `out`) and yt is
     the optional (B, N, T_out) transposed copy (`out_t`).  w_split: optional
     `split_weights(w)` (bf16x6 path without the per-call weight split).  x_split: x holds
     f16x3 split rows (include/ftmi.h, e.g. conv_bank(split_out=True)); f16x3 slab kernel
-    only (the C side refuses other shapes with FTMI_E_UNSUPPORTED).  x_fin: x is a
-    conv_bank(pair=True) output (2, B, T, Cin) and the operand is the bank's finish of its
-    two planes' sum, x_fin = (4, Cin) colscale / bias / BN scale / BN shift (few-row kernel
-    only: FTMI_E_UNSUPPORTED elsewhere).
+    only (the C side refuses other shapes with FTMI_E_UNSUPPORTED).
     """
-    x_plane = 0
-    if x_fin is not None:
-        if x.dim() != 4 or x.size(0) != 2:
-            raise ValueError('x_fin: a (2, B, T, C) bank pair expected')
-        _dev(x_fin)
-        x_plane = (x[1].data_ptr() - x[0].data_ptr()) // 4
-        x = x[0]
     _dev(x, w, bias, residual, out, out_t, w_split)
     B, T, Cin, xs = _rows(x)
     N = w.size(0)
@@ -360,8 +350,6 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
     a.mma, a.w_split = _gemm_mma(mma, w_split)
     a.status = status_word(x.device).data_ptr()
     a.x_split = int(x_split)
-    if x_fin is not None:
-        a.x_plane, a.x_fin = x_plane, x_fin.data_ptr()
     M = B * To
     if _skinny(a.mma, T, To, Cin, k, M, N):
         sk = _skinny_split(Cin)
@@ -371,10 +359,9 @@ def conv1d(x: torch.Tensor, w: torch.Tensor, k: int, pad: int, *, bias=None, rel
         part = torch.empty(sk * M * N, device=x.device, dtype=_f32)
         a.split_k, a.split_ws = sk, part.data_ptr()
     label = (f'conv1d[M={M},N={N},K={k * Cin}{",maxpool" if maxpool else ""}'
-             f'{",xsplit" if x_split else ""}{",xpair" if x_fin is not None else ""},mma={a.mma}]')
+             f'{",xsplit" if x_split else ""},mma={a.mma}]')
     launch('ftmi_conv1d', label, 2.0 * M * N * k * Cin,
-           4.0 * (B * T * Cin * (1 + (x_fin is not None)) + N * k * Cin
-                  + M * N * (1 + (residual is not None))),
+           4.0 * (B * T * Cin + N * k * Cin + M * N * (1 + (residual is not None))),
            ctypes.byref(a), _stream())
     return y, out_t
 
@@ -422,21 +409,17 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
               shift: torch.Tensor, mma: Optional[int] = None,
               w_split: Optional[torch.Tensor] = None, pool: bool = False,
               split_out: bool = False, x_split: bool = False,
-              w_image: Optional[torch.Tensor] = None, pair: bool = False) -> torch.Tensor:
+              w_image: Optional[torch.Tensor] = None) -> torch.Tensor:
     """CBHG conv bank, (B, T, Cin) -> (B, T, K*Cout); pool: the maxpool(2, 1) of it
     (common_layers.py:73,100), stored by the bank kernel (see bank_pools); split_out (with
     pool): stored as f16x3 split rows for proj1 (conv1d(x_split=True)); x_split: x holds
     split rows (split_rows); w_image: `bank_halves_image(w_split, ...)`, read instead of
-    w_split where the one-launch few-row kernel runs (same results bit for bit); pair
-    (`bank_pair_ok`): the few-row kernel without its finish — returns (2, B, T, K*Cout), the
-    two channel halves' raw sums, which conv1d(x_fin=...) finishes in its operand staging."""
+    w_split where the one-launch few-row kernel runs (same results bit for bit)."""
     if split_out and not pool:
         raise ValueError('split_out needs pool')
     _dev(x, w, scale, shift, w_split)
     B, T, Cin, xs = _rows(x)
-    if pair and not bank_pair_ok(x, K, Cout, mma, w_split):
-        raise ValueError('conv_bank(pair=True) needs the one-launch few-row kernel (bank_pair_ok)')
-    y = torch.empty((2,) * pair + (B, T, K * Cout), device=x.device, dtype=_f32)
+    y = torch.empty(B, T, K * Cout, device=x.device, dtype=_f32)
     M = B * T
     flops = 2.0 * M * Cout * Cin * K * (K + 1) / 2
     mma, wsp = _gemm_mma(mma, w_split)
@@ -448,18 +431,12 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
         if w_image is not None:
             _dev(w_image)
             wsp, last = w_image.data_ptr(), BANK_HALVES | BANK_IMAGE
-        if pair:
-            last |= BANK_PAIR
     elif not pool and _skinny(mma, T, T, Cin, K, M) and _skinny_split(Cin) > 1:
         sk = _skinny_split(Cin)  # weight-streaming kernel: partial sums, finished in order
-        if os.environ.get('FTMI_BANK_LAST', '0') != '0':
-            # tile counters + partials, finished in-kernel by each tile's last split block
-            part, last = _bank_workspace(sk * M * K * Cout, x.device), BANK_LAST
-        else:
-            part = torch.empty(sk * M * K * Cout, device=x.device, dtype=_f32)
+        part = torch.empty(sk * M * K * Cout, device=x.device, dtype=_f32)
     launch('ftmi_conv_bank_split', f'conv_bank[M={M},K={K},Cin={Cin},mma={mma}'
            f'{",pool" if pool else ""}{",split" if split_out else ""}{",xsplit" if x_split else ""}'
-           f'{",pair" if pair else ""}]',
+           ']',
            flops, 4.0 * (M * Cin + Cout * Cin * K * (K + 1) / 2 + M * K * Cout),
            x.data_ptr(), xs, B, T, Cin, w.data_ptr(), wsp, K, Cout,
            scale.data_ptr(), shift.data_ptr(), y.data_ptr(), y.stride(-2), mma,
@@ -468,21 +445,8 @@ def conv_bank(x: torch.Tensor, w: torch.Tensor, K: int, Cout: int, scale: torch.
     return y
 
 
-BANK_LAST, BANK_COUNTERS = 8, 4096  # include/ftmi.h FTMI_BANK_LAST, FTMI_BANK_COUNTERS
-BANK_HALVES, BANK_IMAGE, BANK_PAIR = 16, 32, 64  # include/ftmi.h FTMI_BANK_HALVES / _IMAGE / _PAIR
-# FTMI_BANK_PAIR=1 (read per call; default 0): the few-row bank leaves its two raw channel
-# halves and proj1's operand staging finishes them.  Measured at c2 (r4m, HIP graphs): bank
-# 14.7 us instead of 17.2, but proj1 20.2 instead of 17.7 us — the second plane's loads in
-# proj1's prologue cost what the exchange did (bank + proj1 34.9 us either way): off.
-
-
-def bank_pair_ok(x: torch.Tensor, K: int, Cout: int, mma: Optional[int] = None,
-                 w_split=None) -> bool:
-    """Whether conv_bank(pair=True) applies: the one-launch few-row kernel (_bank_halves) on
-    a plain (not split, not pooled) operand, FTMI_BANK_PAIR=1 (opt-in)."""
-    m, _ = _gemm_mma(mma, w_split)
-    return (os.environ.get('FTMI_BANK_PAIR', '0') != '0' and x.dim() == 3
-            and _bank_halves(m, x.size(0), x.size(1), x.size(2), K, Cout))
+BANK_COUNTERS = 4096  # include/ftmi.h FTMI_BANK_COUNTERS
+BANK_HALVES, BANK_IMAGE = 16, 32  # include/ftmi.h FTMI_BANK_HALVES / _IMAGE
 
 
 def _bank_halves(mma: int, B: int, T: int, Cin: int, K: int, Cout: int) -> bool:
@@ -498,7 +462,7 @@ _BANK_WS = {}
 
 
 def _bank_workspace(n_part: int, device) -> torch.Tensor:
-    """The FTMI_BANK_LAST workspace of the current stream: BANK_COUNTERS tile counters (zero
+    """The FTMI_BANK_HALVES workspace of the current stream: BANK_COUNTERS counters (zero
     once; every launch leaves them zero) followed by n_part floats of partial sums.  One per
     (device, stream) — launches on one stream are ordered, so they may share it — kept alive
     for graph replays that captured its address; grown (a new zeroed buffer) when too small."""
@@ -756,41 +720,6 @@ def rnn_bidir(cell: int, xp: torch.Tensor, H: int, w_hh: torch.Tensor, b_hh: Opt
         off = int(lib.ftmi_rnn_error_offset(B)) // 4
         if int(ws[off].item()) != 0:
             raise RnnTimeout('ftmi_rnn_bidir: a workgroup timed out waiting for its group')
-    return y
-
-
-# The fused form computes W_ih x_t inside each recurrence step (no (B, T, 6H) tensor).  It is
-# opt-in (FTMI_FUSED_GRU=1): measured at c3, the postnet GRU takes 2.59 ms fused against
-# 0.44 ms (input GEMM) + 1.72 ms (recurrence) in two calls — the extra per-step work lands on
-# the step's critical path instead of in the hand-off wait.
-FUSED_GRU = os.environ.get('FTMI_FUSED_GRU', '0') != '0'
-
-
-def gru_fused_ok(H: int, Cin: int) -> bool:
-    """Whether `gru_bidir_fused` takes this GRU (f16x3 path, Cin 256, H 128 / 256)."""
-    return FUSED_GRU and _rnn_mma() == 2 and Cin == 256 and H in (128, 256)
-
-
-def gru_bidir_fused(x: torch.Tensor, H: int, w_ih: torch.Tensor, b_ih: torch.Tensor,
-                    w_hh: torch.Tensor, b_hh: torch.Tensor, lengths: Optional[torch.Tensor] = None,
-                    pad_value: float = 0.0, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Bidirectional GRU over x (B, T, Cin) with the input projection computed inside the
-    recurrence (`ftmi_gru_bidir_fused`) -> (B, T, 2H).  w_ih [2*3H][Cin], b_ih [2*3H]."""
-    if lengths is not None:
-        lengths = lengths.to(device=x.device, dtype=torch.int32).contiguous()
-    _dev(x, w_ih, b_ih, w_hh, b_hh, lengths)
-    B, T, Cin, xs = _rows(x)
-    y = torch.empty(B, T, 2 * H, device=x.device, dtype=_f32)
-    lib = _lib.load()
-    need = int(lib.ftmi_rnn_workspace_bytes(B, H, 0)) // 4 + 4
-    if ws is None or ws.numel() < need:
-        ws = torch.empty(need, device=x.device, dtype=torch.int32)
-    launch('ftmi_gru_bidir_fused', f'gru_bidir_fused[B={B},T={T},H={H},Cin={Cin}]',
-           2.0 * B * T * 2 * 3 * H * (H + Cin),
-           4.0 * (B * T * Cin + 2 * 3 * H * (H + Cin) + B * T * 2 * H),
-           B, T, H, x.data_ptr(), xs, Cin, w_ih.data_ptr(), b_ih.data_ptr(), w_hh.data_ptr(),
-           b_hh.data_ptr(), _ptr(lengths), float(pad_value), y.data_ptr(), y.stride(1),
-           status_word(x.device).data_ptr(), ws.data_ptr(), _stream())
     return y
 
 

@@ -63,13 +63,6 @@ enum { FTMI_STATUS_F16_RANGE = 1, FTMI_STATUS_WHH_RANGE = 2, FTMI_STATUS_RNN_TIM
 enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
        FTMI_BANK_Y_SPLIT = 2, /* with FTMI_BANK_POOL: y as f16x3 split rows of K*Cout */
        FTMI_BANK_X_SPLIT = 4, /* x given as f16x3 split rows of Cin (FTMI_MMA_F16X3) */
-       FTMI_BANK_LAST = 8,    /* ABI 12, with split_k > 1: split_ws starts with
-                                 FTMI_BANK_COUNTERS 32-bit tile counters, zeroed once by the
-                                 caller and left zero by every launch; the partial sums follow.
-                                 The weight-streaming bank then finishes in-kernel (each tile's
-                                 last split block sums the splits in order) instead of a second
-                                 launch.  One workspace per stream: concurrent launches must not
-                                 share the counters. */
        FTMI_BANK_HALVES = 16, /* ABI 15 (alone, FTMI_MMA_F16X3): the few-row bank in ONE
                                  launch — a block per (group pair, 16-column set, half of the
                                  input channels), each wave's weight stream issued at once, the
@@ -79,20 +72,17 @@ enum { FTMI_BANK_POOL = 1,    /* y = CBHG maxpool(2, 1) of the bank output */
                                  ftmi_conv_bank_halves_ws_floats(B, T, K, Cout) floats, the first
                                  FTMI_BANK_COUNTERS zeroed once by the caller (every launch leaves
                                  them zero); split_k is ignored.  One workspace per stream. */
-       FTMI_BANK_IMAGE = 32,  /* ABI 16, with FTMI_BANK_HALVES: w_split is the bank's
+       FTMI_BANK_IMAGE = 32   /* ABI 16, with FTMI_BANK_HALVES: w_split is the bank's
                                  stream-order weight image (ftmi_conv_bank_halves_image), which
                                  the kernel reads as one contiguous 1 KB run per wave load;
-                                 same results bit for bit. */
-       FTMI_BANK_PAIR = 64    /* ABI 17, with FTMI_BANK_HALVES: no in-kernel finish — y holds
-                                 TWO planes, y and y + B*T*y_stride, the two channel halves'
-                                 raw sums (no colscale, ReLU or BN); the consumer finishes them
-                                 (ftmi_conv_args.x_fin: proj1's operand staging).  No exchange
-                                 workspace is read (split_ws still required). */ };
+                                 same results bit for bit. */ };
 enum { FTMI_BANK_COUNTERS = 4096 };
 
 /* ABI version; bumped on any signature change (14: ftmi_panel_proj_qkv, ftmi_attention_kv;
  * 15: FTMI_BANK_HALVES, ftmi_conv_bank_halves_ws_floats; 16: FTMI_BANK_IMAGE,
- * ftmi_conv_bank_halves_image[_bytes]; 17: FTMI_BANK_PAIR, ftmi_conv_args.x_plane / x_fin). */
+ * ftmi_conv_bank_halves_image[_bytes]; 17: FTMI_BANK_PAIR, ftmi_conv_args.x_plane / x_fin;
+ * 18: rejected variants removed — FTMI_BANK_LAST, FTMI_BANK_PAIR, ftmi_conv_args.x_plane /
+ * x_fin, ftmi_gru_bidir_fused). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
@@ -153,15 +143,6 @@ typedef struct ftmi_conv_args {
   int32_t x_split;     /* ABI 10: x holds f16x3 SPLIT ROWS (below) instead of floats; only
                           FTMI_MMA_F16X3 without maxpool on the slab kernel (B*T_out > 256
                           rows), else FTMI_E_UNSUPPORTED.  x_stride (floats) >= Cin. */
-  int64_t x_plane;     /* ABI 17, with x_fin: floats from x to the second plane */
-  const float *x_fin;  /* ABI 17: NULL, or x is a FTMI_BANK_PAIR bank output (two planes of
-                          raw half sums, x and x + x_plane) and the operand row is the bank's
-                          finish of their sum — relu(s * x_fin[c] + x_fin[Cin + c]) *
-                          x_fin[2 Cin + c] + x_fin[3 Cin + c] per channel c — before the
-                          maxpool: [4][Cin] floats (colscale, bias, BN scale, BN shift).
-                          Only the few-row kernel (B*T_out <= 256, FTMI_MMA_F16X3, one
-                          group), else FTMI_E_UNSUPPORTED; a non-finite sum sets status bit 0
-                          as the bank would. */
 } ftmi_conv_args;
 
 /* f16x3 split rows (ABI 10): the activation layout one f16x3 GEMM hands the next.  Row r
@@ -336,19 +317,6 @@ int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, const float *x
                    const float *xp_zero, const float *w_hh, const float *b_hh,
                    const int32_t *lengths, float pad_value, float *y, int64_t y_stride,
                    int32_t mma, uint32_t *status, void *sync, ftmi_stream_t stream);
-
-/* Bidirectional GRU with the input projection fused into the recurrence (f16x3 only):
- * the same result as ftmi_conv1d(x, W_ih, k=1, bias=b_ih) followed by ftmi_rnn_bidir, with
- * x (B, T, Cin) fp32 rows read directly (the (B, T, 6H) projection is never materialised;
- * each step's W_ih x_t is computed while the workgroup waits for the h hand-off).
- * w_ih [2][3H][Cin] (forward, reverse), b_ih [2*3H]; other arguments as ftmi_rnn_bidir.
- * Supported: Cin == 256, H in {128, 256} (FTMI_E_UNSUPPORTED otherwise: use the two-call
- * form).  Replaces nn.GRU's input GEMM + recurrence, models/common_layers.py:84,118
- * (CBHG) and models/forward_tacotron.py:39,53 (SeriesPredictor). */
-int ftmi_gru_bidir_fused(int32_t B, int32_t T, int32_t H, const float *x, int64_t x_stride,
-                         int32_t Cin, const float *w_ih, const float *b_ih, const float *w_hh,
-                         const float *b_hh, const int32_t *lengths, float pad_value, float *y,
-                         int64_t y_stride, uint32_t *status, void *sync, ftmi_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Duration post-processing of ForwardTacotron.generate + LengthRegulator counts:

@@ -79,8 +79,6 @@ int main() {
                         nullptr, a, nullptr), FTMI_E_ARG);
   EXPECT(ftmi_rnn_bidir(0, 1, 1, 64, a, 192, 1, nullptr, nullptr, mis, a, nullptr, 0.f, a, 128, 2,
                         nullptr, a, nullptr), FTMI_E_ALIGN);
-  EXPECT(ftmi_gru_bidir_fused(1, 1, 96, a, 256, 256, a, a, a, a, nullptr, 0.f, a, 192, nullptr, a,
-                              nullptr), FTMI_E_UNSUPPORTED);
   EXPECT(ftmi_attention(nullptr, 0, 1, 1, 1, 64, 0, 64, 128, nullptr, 1.f, nullptr, 0, 2, nullptr,
                         nullptr, 0, nullptr), FTMI_E_ARG);
   EXPECT(ftmi_attention(a, 192, 1, 1, 1, 96, 0, 96, 192, nullptr, 1.f, a, 96, 2, nullptr, nullptr,

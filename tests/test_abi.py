@@ -58,8 +58,6 @@ def test_strerror():
     (lambda L: L.ftmi_split_weights(None, 4, 4, None, None), 1001),
     (lambda L: L.ftmi_split_weights_f16(None, 4, 4, None, None), 1001),
     (lambda L: L.ftmi_rnn_bidir(0, 1, 1, 64, None, 0, 1, None, None, None, None, None, 0.0, None, 0, 2, None, None, None), 1001),
-    (lambda L: L.ftmi_gru_bidir_fused(1, 1, 128, None, 0, 256, None, None, None, None, None, 0.0, None, 0, None, None, None), 1001),
-    (lambda L: L.ftmi_gru_bidir_fused(1, 1, 96, ctypes.c_void_p(256), 256, 256, ctypes.c_void_p(256), ctypes.c_void_p(256), ctypes.c_void_p(256), ctypes.c_void_p(256), None, 0.0, ctypes.c_void_p(256), 192, None, ctypes.c_void_p(256), None), 1003),
     (lambda L: L.ftmi_duration_counts(None, 1, 1, 1, 2.0, None, None, None, None), 1001),
     (lambda L: L.ftmi_lr_index(None, 1, 1, 1, None, None), 1001),
     (lambda L: L.ftmi_length_regulate(None, 0, 1, 1, 4, None, 1, None, 0, None), 1001),
@@ -124,3 +122,13 @@ def test_build_id_tracks_flags():
     assert build_id() == source_hash() == _lib.load().ftmi_build_id().decode()
     assert build_id(['-DFTMI_X=1']) != build_id()
     assert build_id(['-DFTMI_X=1']).startswith(source_hash() + '+')
+
+
+def test_default_library_has_no_invalid_result_switches():
+    """the timing experiments that return invalid results with status 0
+    (FTMI_RNN_DIAG, FTMI_SLAB_DIAG, FTMI_SKINNY_DIAG, FTMI_BANK_HALVES_DIAG) exist only in the
+    diagnostic build (-DFTMI_DIAG, libftmi_stamps.so): the product library never reads them."""
+    data = (Path(_lib.__file__).parent / "libftmi.so").read_bytes()
+    for name in (b'FTMI_RNN_DIAG', b'FTMI_SLAB_DIAG', b'FTMI_SKINNY_DIAG',
+                 b'FTMI_BANK_HALVES_DIAG'):
+        assert name not in data, name

@@ -8,16 +8,10 @@ def test_rocprof_name_follows_the_gemv_rule(monkeypatch):
     monkeypatch.delenv('FTMI_RNN_GEMV', raising=False)
     assert bench.rocprof_name('rnn_bidir[lstm,B=1,T=816,H=512,mma=2]') == 'rnn_gemv_kernel<1, 512,'
     assert bench.rocprof_name('rnn_bidir[gru,B=4,T=816,H=256,mma=2]') == 'rnn_gemv_kernel<0, 256,'
-    monkeypatch.delenv('FTMI_RNN_ROW', raising=False)
     assert bench.rocprof_name('rnn_bidir[lstm,B=64,T=1368,H=512,mma=2]') == 'rnn_bidir_kernel<1, 512,'
     assert bench.rocprof_name('rnn_bidir[gru,B=1,T=816,H=32,mma=2]') == 'rnn_bidir_kernel<0, 32,'
     monkeypatch.setenv('FTMI_RNN_GEMV', '0')
     assert bench.rocprof_name('rnn_bidir[lstm,B=1,T=816,H=512,mma=2]') == 'rnn_bidir_kernel<1, 512,'
-    # the opt-in row kernel (FTMI_RNN_ROW=1): f16x3, H 128 / 256 / 512
-    monkeypatch.setenv('FTMI_RNN_ROW', '1')
-    assert bench.rocprof_name('rnn_bidir[lstm,B=64,T=1368,H=512,mma=2]') == 'rnn_row_kernel<1, 512,'
-    assert bench.rocprof_name('rnn_bidir[gru,B=64,T=1368,H=256,mma=2]') == 'rnn_row_kernel<0, 256,'
-    assert bench.rocprof_name('rnn_bidir[lstm,B=64,T=1368,H=512,mma=0]') == 'rnn_bidir_kernel<1, 512,'
     assert bench.rocprof_name('rnn_bidir[gru,B=64,T=200,H=64,mma=2]') == 'rnn_bidir_kernel<0, 64,'
     assert bench.rocprof_name('conv1d[M=12800,N=256,K=1280,mma=2]') is None
 

@@ -220,33 +220,6 @@ def test_conv_bank_pooled(K, Cin, B, T, rng, monkeypatch):
     close(yp, O.maxpool_k2_s1_p1(ref).transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
 
 
-def test_conv_bank_last_arriver_counters(rng, monkeypatch):
-    """FTMI_BANK_LAST (opt-in): every launch leaves the tile counters zero, so banks of
-    different split counts sharing the stream's workspace (prenet: 4 splits, postnet: 2) and
-    repeated calls give bit-identical results."""
-    from forwardtacotron_amd import ops
-    from forwardtacotron_amd.common_layers import pack_conv
-    monkeypatch.setenv('FTMI_BANK_LAST', '1')
-
-    def bank(K, Cin, T):
-        C = 256
-        x = dev(rng.normal(0, 1, (1, T, Cin)).astype(np.float32))
-        ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
-        wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
-        w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
-        sc = dev(rng.uniform(0.5, 1.5, K * C).astype(np.float32))
-        sh = dev(rng.normal(0, 0.1, K * C).astype(np.float32))
-        return lambda: ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3)
-
-    pre, post = bank(16, 256, 120), bank(8, 80, 100)
-    a0, b0 = host(pre()), host(post())
-    for _ in range(3):
-        assert np.array_equal(host(pre()), a0)
-        assert np.array_equal(host(post()), b0)
-    key = (torch.device('cuda', torch.cuda.current_device()), torch.cuda.current_stream().cuda_stream)
-    assert not ops._BANK_WS[key][:ops.BANK_COUNTERS].any()  # counters back to zero
-
-
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (16, 256, 1, 50), (8, 128, 2, 64),
                                      (4, 64, 1, 50)])
 def test_conv_bank_halves(K, Cin, B, T, rng, monkeypatch):
@@ -287,74 +260,6 @@ def test_conv_bank_halves(K, Cin, B, T, rng, monkeypatch):
     monkeypatch.setenv('FTMI_BANK_HALVES', '0')
     b0 = host(ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3))
     close(a0, b0, rtol=1e-5, atol=1e-5)
-
-
-@pytest.mark.parametrize('K,Cin,B,T,N', [(16, 256, 1, 120, 256), (16, 256, 1, 50, 256),
-                                       (8, 128, 2, 64, 128), (4, 64, 1, 33, 80)])
-def test_conv_bank_pair_proj1(K, Cin, B, T, N, rng, monkeypatch):
-    """FTMI_BANK_PAIR (opt-in): the halves bank leaves its two channel halves' raw sums and
-    proj1's operand staging (conv1d x_fin, the few-row kernel, maxpool fused) finishes them —
-    the proj1 output is bit-identical to proj1 (maxpool) on the bank's own in-kernel finish,
-    on repeated calls, with status 0; and the planes add up to the finished bank."""
-    monkeypatch.setenv('FTMI_BANK_PAIR', '1')
-    from forwardtacotron_amd import ops
-    from forwardtacotron_amd.common_layers import pack_conv
-    C = 256
-    x = dev(rng.normal(0, 1, (B, T, Cin)).astype(np.float32))
-    ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
-    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
-    w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
-    img = ops.bank_halves_image(w3, K, Cin, C)
-    sc = dev(rng.uniform(0.5, 1.5, K * C).astype(np.float32))
-    sh = dev(rng.normal(0, 0.1, K * C).astype(np.float32))
-    cs = img[img.numel() - 4 * K * C:].view(torch.float32)
-    fin = torch.stack([cs, torch.zeros_like(cs), sc, sh]).contiguous()
-    w1 = rng.normal(0, 1 / np.sqrt(K * C * 3), (N, K * C, 3)).astype(np.float32)
-    w1p = pack_conv(torch.from_numpy(w1)).cuda()
-    w13 = ops.split_weights_f16(w1p)
-    s1 = dev(rng.uniform(0.5, 1.5, N).astype(np.float32))
-    h1 = dev(rng.normal(0, 0.1, N).astype(np.float32))
-    assert ops.bank_pair_ok(x, K, C, 2, w3)
-    st = ops.status_word(x.device)
-    st.zero_()
-    yb = ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, w_image=img)
-    ref, _ = ops.conv1d(yb, w1p, 3, 1, relu=True, bn=(s1, h1), maxpool=True, mma=2, w_split=w13)
-    ref = host(ref)
-    for _ in range(3):
-        pr = ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, w_image=img, pair=True)
-        assert pr.shape == (2, B, T, K * C)
-        y, _ = ops.conv1d(pr, w1p, 3, 1, relu=True, bn=(s1, h1), maxpool=True, mma=2,
-                          w_split=w13, x_fin=fin)
-        np.testing.assert_array_equal(host(y), ref)
-    # the planes' sum, finished by torch (separate multiply and add: within rounding)
-    s = (pr[0] + pr[1]) * cs
-    np.testing.assert_allclose(host(torch.relu(s) * sc + sh), host(yb), rtol=1e-6, atol=1e-6)
-    assert int(st.item()) == 0
-    # the plane path (no image) as well
-    pr2 = ops.conv_bank(x, wp, K, C, sc, sh, mma=2, w_split=w3, pair=True)
-    np.testing.assert_array_equal(host(pr2), host(pr))
-
-
-def test_conv_bank_pair_status(rng):
-    """A non-finite bank sum reaching proj1's pair staging sets status bit 0, as the bank's
-    own finish would."""
-    from forwardtacotron_amd import ops
-    from forwardtacotron_amd.common_layers import pack_conv
-    K, Cin, C, T = 4, 64, 256, 40
-    ws = [rng.normal(0, 0.1, (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
-    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
-    w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
-    img = ops.bank_halves_image(w3, K, Cin, C)
-    cs = img[img.numel() - 4 * K * C:].view(torch.float32)
-    fin = torch.stack([cs, torch.zeros_like(cs), torch.ones_like(cs), torch.zeros_like(cs)]).contiguous()
-    pr = torch.zeros(2, 1, T, K * C, device='cuda')
-    pr[1, 0, 5, 300] = float('inf')
-    pr[0, 0, 5, 300] = float('-inf')  # inf + -inf = NaN: ReLU would hide it
-    w1p = pack_conv(torch.from_numpy(rng.normal(0, 0.01, (80, K * C, 3)).astype(np.float32))).cuda()
-    st = ops.status_word('cuda')
-    st.zero_()
-    ops.conv1d(pr, w1p, 3, 1, maxpool=True, mma=2, w_split=ops.split_weights_f16(w1p), x_fin=fin)
-    assert int(st.item()) & 1
 
 
 def test_conv_bank_halves_range_guard(rng):
@@ -430,8 +335,7 @@ def test_split_rows_bank_to_proj1(K, Cin, B, T, split_k, rng, monkeypatch):
         ops.conv1d(ys, w1, 3, 1, mma=0, x_split=True)
 
 
-@pytest.mark.parametrize('schedule', ['halves', 'halves-image', 'pairs', 'pairs-finish',
-                                      'quarters', 'quarters-finish', 'groups'])
+@pytest.mark.parametrize('schedule', ['halves', 'halves-image', 'pairs', 'groups'])
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (8, 80, 1, 100), (4, 64, 2, 50),
                                      (16, 256, 2, 64), (16, 256, 1, 37), (2, 32, 1, 128),
                                      (16, 256, 1, 129), (8, 128, 1, 128), (16, 192, 3, 40)])
@@ -439,20 +343,14 @@ def test_conv_bank_skinny_schedules(K, Cin, B, T, schedule, rng, monkeypatch):
     """The weight-streaming bank at batch-1 sizes on every block schedule: the one-launch
     channel-halves kernel (conv_bank_halves_kernel, the default where it applies: M <= 128,
     Cin % 64 == 0; other shapes fall through to the next), group pairs (k, K + 1 - k) per
-    block with one (unit, half) per wave, the same with each wave on a quarter of a heavy
-    and of a light unit (conv_bank_qb_kernel, FTMI_BANK_QB=1), one group per block
-    (FTMI_BANK_BALANCED=0); the split schedules with the in-kernel last-arriver finish
-    (FTMI_BANK_LAST=1) or the finish launch; f16x3, against the numpy oracle.  M = 129: two
-    row tiles, the second with one row.  halves-image: the halves kernel reading the
+    block with one (unit, half) per wave, one group per block (FTMI_BANK_BALANCED=0), the
+    split schedules finished by the finish launch; f16x3, against the numpy oracle.  M = 129:
+    two row tiles, the second with one row.  halves-image: the halves kernel reading the
     stream-order weight image (FTMI_BANK_IMAGE), bit-identical to it reading the planes."""
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import pack_conv
     monkeypatch.setenv('FTMI_BANK_HALVES', '1' if schedule.startswith('halves') else '0')
     monkeypatch.setenv('FTMI_BANK_BALANCED', '0' if schedule == 'groups' else '1')
-    monkeypatch.setenv('FTMI_BANK_QB', '1' if schedule.startswith('quarters') else '0')
-    # the tile's last split block finishes in-kernel (FTMI_BANK_LAST, default), or *-finish:
-    # the separate finish launch
-    monkeypatch.setenv('FTMI_BANK_LAST', '0' if schedule.endswith('-finish') else '1')
     C = 256
     x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
     ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
@@ -730,22 +628,16 @@ def _rnn_module(cell, fin, H, rng):
 
 
 RNN_MMAS = pytest.mark.parametrize('rnn_mma', [2, 1, 0], ids=['f16x3', 'bf16x6', 'f32'])
-# fused: the input projection inside the recurrence (ftmi_gru_bidir_fused) exists on the
-# f16x3 path for H 128 / 256 only — only those cells are generated
-GRU_CASES = [pytest.param(H, B, T, m, f, id=f'{"fused" if f else "two-call"}-{H}-{B}-{T}-{mid}')
+GRU_CASES = [pytest.param(H, B, T, m, id=f'{H}-{B}-{T}-{mid}')
              for H, B, T in [(64, 3, 40), (128, 2, 33), (256, 5, 60), (256, 17, 9)]
-             for m, mid in ((2, 'f16x3'), (1, 'bf16x6'), (0, 'f32'))
-             for f in (True, False) if not f or (m == 2 and H in (128, 256))]
+             for m, mid in ((2, 'f16x3'), (1, 'bf16x6'), (0, 'f32'))]
 
 
-@pytest.mark.parametrize('H,B,T,rnn_mma,fused', GRU_CASES)
-def test_gru_bidir(H, B, T, rng, rnn_mma, fused, monkeypatch):
-    """fused: the input projection inside the recurrence (ftmi_gru_bidir_fused, f16x3,
-    H 128 / 256); two-call: ftmi_conv1d + ftmi_rnn_bidir."""
+@pytest.mark.parametrize('H,B,T,rnn_mma', GRU_CASES)
+def test_gru_bidir(H, B, T, rng, rnn_mma, monkeypatch):
+    """ftmi_conv1d (input projection) + ftmi_rnn_bidir against the numpy oracle."""
     from forwardtacotron_amd import ops
     monkeypatch.setattr(ops, 'RNN_MMA', rnn_mma)
-    monkeypatch.setattr(ops, 'FUSED_GRU', fused)
-    assert not fused or ops.gru_fused_ok(H, 256)
     m, sd = _rnn_module('gru', 256, H, rng)
     x = rng.normal(0, 1, (B, T, 256)).astype(np.float32)
     ref = O.gru_bidir(sd, 'r', x, np.float32)
@@ -765,12 +657,10 @@ def test_lstm_bidir(rng, rnn_mma, monkeypatch):
 F16X3_SHAPES = [('lstm', 512, 1, 23), ('lstm', 512, 17, 12), ('lstm', 512, 64, 9),
                 ('gru', 256, 1, 31), ('gru', 256, 64, 7), ('gru', 256, 130, 5),
                 ('gru', 128, 20, 14), ('gru', 64, 64, 11), ('gru', 64, 1, 40)]
-# kernel variants: rnn_row_kernel (H 128 / 256 / 512, FTMI_RNN_ROW=1) with 16 / 8 / 4 live
-# sequences per group and with the spread choice; rnn_bidir_kernel (the default: compute-wave
-# h stores), with the comm wave's h stores (FTMI_RNN_CSTORE=0), and spread (GRU: 8 live
-# sequences per group); H = 64 always runs rnn_bidir_kernel — only the applicable cells are
-# generated
-ROW_VARIANTS = ['row16', 'row8', 'row4', 'rowspread', 'default', 'comm', 'spread']
+# kernel variants of rnn_bidir_kernel: the default (compute-wave h stores), the comm wave's
+# h stores (FTMI_RNN_CSTORE=0), and spread (GRU: 8 live sequences per group); H = 64 has the
+# default only
+ROW_VARIANTS = ['default', 'comm', 'spread']
 F16X3_CASES = [pytest.param(*shape, v, id=f'{shape[0]}{shape[1]}-B{shape[2]}-{v}')
                for shape in F16X3_SHAPES
                for v in (ROW_VARIANTS if shape[1] >= 128 else ['default'])]
@@ -785,13 +675,10 @@ def test_rnn_f16x3_kernels(cell, H, B, T, variant, rng, monkeypatch):
     from forwardtacotron_amd import ops
     monkeypatch.setattr(ops, 'RNN_MMA', 2)
     monkeypatch.setenv('FTMI_RNN_GEMV', '0')
-    monkeypatch.setenv('FTMI_RNN_ROW', '1' if variant.startswith('row') else '0')
     monkeypatch.setenv('FTMI_RNN_CSTORE', '0' if variant == 'comm' else '1')
-    if variant in ('row16', 'row8', 'row4'):
-        monkeypatch.setenv('FTMI_RNN_NB', variant[3:])
     fin = 512 if cell == 'lstm' else 256
     m, sd = _rnn_module(cell, fin, H, rng)
-    m.spread = variant in ('rowspread', 'spread')
+    m.spread = variant == 'spread'
     x = rng.normal(0, 1, (B, T, fin)).astype(np.float32)
     ref = (O.lstm_bidir if cell == 'lstm' else O.gru_bidir)(sd, 'r', x, np.float32)
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
@@ -829,15 +716,12 @@ def test_rnn_f16_weight_range_guard(rng, monkeypatch):
     assert int(st.item()) & 2
 
 
-@pytest.mark.parametrize('B,variant', [(2, 'gemv'), (9, 'row16'), (9, 'row4'), (9, 'default')])
+@pytest.mark.parametrize('B,variant', [(2, 'gemv'), (9, 'default'), (9, 'spread')])
 def test_lstm_through_lr_index_and_lengths(B, variant, rng, monkeypatch):
     """LSTM reading phoneme-rate projections through the LR index map == LSTM over the
     expanded sequence; with lengths it reproduces pack_padded / pad_packed semantics (B = 2:
-    the GEMV kernel; B = 9: the row kernel with 16 / 4 live sequences per group, legacy)."""
+    the GEMV kernel; B = 9: the MFMA kernel, compact and spread)."""
     from forwardtacotron_amd import ops
-    monkeypatch.setenv('FTMI_RNN_ROW', '1' if variant.startswith('row') else '0')
-    if variant.startswith('row'):
-        monkeypatch.setenv('FTMI_RNN_NB', variant[3:])
     m, sd = _rnn_module('lstm', 512, 512, rng)
     T = 11
     x = rng.normal(0, 1, (B, T, 512)).astype(np.float32)
