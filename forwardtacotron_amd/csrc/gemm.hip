@@ -2256,7 +2256,7 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   const int64_t planeh = (int64_t)GH.N * GH.Kpad, planel = (int64_t)GL.N * GL.Kpad;
   f16x8 rb0[NS], rb1[NS];
   auto wload = [&](int i) {
-    const int q = min(q0 + i, q1 - 1);
+    const int q = max(min(q0 + i, q1 - 1), 0);  // an empty range (q1 == q0 == 0) stays on step 0
     const bool hv = q < QH;
     const int qq = hv ? q : q - QH, j = qq / NCH, c = qq - j * NCH;
     const _Float16 *src = (hv ? wh : wl) + j * Cin + c * 32;
