@@ -146,9 +146,8 @@ def pmc_traffic_slab(label: str, path: str):
 
 def time_prenet_bank(model, x, reps: int = 20):
     """The prenet CBHG conv bank exactly as generate() issues it (same operand, packed
-    weights, pooled / split-output / pair choice; at c2 the one-launch halves kernel on the
-    stream-order weight image, leaving its two channel halves' raw sums for proj1's operand
-    staging to finish — `pair`; where the channel-split kernel runs, the bank + its finish
+    weights, pooled / split-output choice; at c2 the one-launch halves kernel on the
+    stream-order weight image; where the channel-split kernel runs, the bank + its finish
     launch), ms per call:
       warm  — `reps` calls captured in a HIP graph and replayed back to back (device time per
               call, kernel boundaries included, no host issue cost); the weights stay
@@ -156,26 +155,19 @@ def time_prenet_bank(model, x, reps: int = 20):
       eager — the same calls issued from the host one by one (ctypes + argument packing);
       cold  — each call behind a 512 MiB overwrite of another buffer (the weights come from
               HBM): graph [overwrite, call] x reps minus graph [overwrite] x reps;
-      finish — pair only: what finishing the bank costs proj1, graph [proj1 on the pair] minus
-              graph [proj1 on the finished bank output] (warm, per call), added to `warm`
-              for the bank's figure (bank plus its finishing work);
-      inkernel / planes — A/B in the same process: the halves kernel with its own in-kernel
-              finish (partner exchange), and that kernel reading the split planes."""
+      planes — A/B in the same process: the halves kernel reading the split planes."""
     from forwardtacotron_amd import ops
     cb = model.prenet
     h = ops.embedding(x, model.embedding.weight.detach())
-    bank_w, scale, shift, _, bank3, _, img, fin = cb.packed_weights()
+    bank_w, scale, shift, _, bank3, _, img = cb.packed_weights()
     pooled = ops.bank_pools(h, cb.K, cb.channels, w_split=bank3)
     if pooled or not ops._bank_halves(ops._gemm_mma(None, bank3)[0], h.size(0), h.size(1),
                                       h.size(2), cb.K, cb.channels):
         img = None  # the image serves the one-launch few-row kernel only
-    pair = (img is not None and fin is not None and ops.bank_pair_ok(h, cb.K, cb.channels, w_split=bank3)
-            and cb.conv_project1.takes_pair(h.size(0), h.size(1), cb.K * cb.channels))
 
-    def call(image=img, pr=pair):
+    def call(image=img):
         return ops.conv_bank(h, bank_w, cb.K, cb.channels, scale, shift, w_split=bank3,
-                             pool=pooled, split_out=pooled and ops.SPLIT_ROWS, w_image=image,
-                             pair=pr)
+                             pool=pooled, split_out=pooled and ops.SPLIT_ROWS, w_image=image)
 
     def timed(fn):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -193,13 +185,8 @@ def time_prenet_bank(model, x, reps: int = 20):
     graphs = {}
     bodies = [('warm', lambda: call()), ('flush', lambda: flush.fill_(1)),
               ('cold', lambda: (flush.fill_(1), call()))]
-    if img is not None:  # A/B: in-kernel finish, and that kernel on the split planes
-        bodies += [('inkernel', lambda: call(img, False)), ('planes', lambda: call(None, False))]
-    if pair:  # proj1 on the pair vs on the finished bank output: the finishing work
-        yp, yf = call(), call(img, False)
-        p1 = cb.conv_project1
-        bodies += [('proj1_pair', lambda: p1.forward_cl(yp, maxpool=True, x_fin=fin)),
-                   ('proj1_plain', lambda: p1.forward_cl(yf, maxpool=True))]
+    if img is not None:  # A/B: the same kernel on the split planes
+        bodies += [('planes', lambda: call(None))]
     for name, body in bodies:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -210,15 +197,9 @@ def time_prenet_bank(model, x, reps: int = 20):
     res = {'warm': timed(graphs['warm'].replay) / reps, 'eager': eager,
            'cold': (timed(graphs['cold'].replay) - timed(graphs['flush'].replay)) / reps,
            'weights': ('stream-order image' if img is not None
-                       else 'split planes (no few-row kernel at this size)'),
-           'pair': pair}
+                       else 'split planes (no few-row kernel at this size)')}
     if img is not None:
-        res['inkernel'] = timed(graphs['inkernel'].replay) / reps
         res['planes'] = timed(graphs['planes'].replay) / reps
-    if pair:
-        res['proj1_pair'] = timed(graphs['proj1_pair'].replay) / reps
-        res['proj1_plain'] = timed(graphs['proj1_plain'].replay) / reps
-        res['finish'] = res['proj1_pair'] - res['proj1_plain']
     del graphs, flush
     return res
 
@@ -481,8 +462,7 @@ def main():
         if pre:
             lab, v = pre[0]
             pb = prenet_bank_ms or {}
-            # pair: the bank plus the finishing work it leaves to proj1's staging
-            ms = pb.get('warm', v['avg_ms']) + max(pb.get('finish', 0.0), 0.0)
+            ms = pb.get('warm', v['avg_ms'])
             s_ = ms / 1e3
             frac = lambda t: round(v['bytes'] / (t / 1e3) / 1e9 / PEAK_HBM_GBS, 4)  # noqa: E731
             prenet = {'kernel': lab, 'avg_launch_ms': round(ms, 4),
@@ -502,9 +482,8 @@ def main():
                       'eager_single_call_ms': round(v['avg_ms'], 4)}
             if pb:
                 prenet['host_issued_ms'] = round(pb['eager'], 4)
-                fin_ms = max(pb.get('finish', 0.0), 0.0)
-                prenet['cold_ms'] = round(pb['cold'] + fin_ms, 4)
-                prenet['hbm_frac_cold'] = frac(pb['cold'] + fin_ms)
+                prenet['cold_ms'] = round(pb['cold'], 4)
+                prenet['hbm_frac_cold'] = frac(pb['cold'])
                 prenet['cold_basis'] = ('each call behind a 512 MiB overwrite of another buffer '
                                         '(weights from HBM): graph [overwrite, call] minus graph '
                                         '[overwrite], per call')
@@ -525,17 +504,7 @@ def main():
                             'source': os.path.relpath(pmc_path, ROOT), 'measured_on_tree': PMC_TREE,
                             'note': 'a prior PMC run of this workload, not this run'}
                 if 'planes' in pb:
-                    prenet['warm_ms_in_kernel_finish'] = round(pb['inkernel'], 4)
-                    prenet['warm_ms_in_kernel_finish_split_planes'] = round(pb['planes'], 4)
-                if pb['pair']:
-                    prenet['finish'] = (
-                        'pair: the bank stores its two channel halves\' raw sums and proj1\'s '
-                        'operand staging finishes them (sum, colscale, ReLU, BN, then maxpool); '
-                        'avg_launch_ms = bank warm + that finishing work')
-                    prenet['bank_warm_ms'] = round(pb['warm'], 4)
-                    prenet['finish_ms_in_proj1'] = round(pb['finish'], 4)
-                    prenet['proj1_ms_pair_vs_plain'] = [round(pb['proj1_pair'], 4),
-                                                       round(pb['proj1_plain'], 4)]
+                    prenet['warm_ms_split_planes'] = round(pb['planes'], 4)
         value = frames / elapsed
         # valid frames: frames of the non-pad phonemes (the rest of B * T_mel is padding)
         tok = (x_np != 0) if world == 1 else None

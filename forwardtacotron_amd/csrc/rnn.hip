@@ -128,7 +128,9 @@ struct RnnParams {
   unsigned *status;  // optional: bit 1 = a W_hh entry overflowed f16 (mode 2)
   unsigned spin_limit;  // bound of every spin (g_spin_limit at launch)
   int psleep;  // s_sleep(1) count before a step's first h poll (FTMI_RNN_PSLEEP; valid results)
-  int diag;  // timing experiments only (FTMI_RNN_DIAG, diagnostic build only): bit 0 =
+  int diag;  // timing experiments only (FTMI_RNN_DIAG, diagnostic build only; 32 = one MFMA
+             // per product, 64 = a quarter of the h loads, 128 = cell without
+             // transcendentals — rnn_bidir_kernel f16x3): bit 0 =
              // input projections from one L2-hot row, bit 1 = no hand-off waits,
              // bit 2 = no drain
 };
@@ -559,7 +561,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
       for (unsigned spins = 0;; ++spins) {
 #pragma unroll
         for (int i = 0; i < NL; ++i)
-          if (NBL == NB || hlive)
+          if ((NBL == NB || hlive) && !((RNN_DIAG(p) & 64) && i >= NL / 4))  // 64: a quarter
             hr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, hoff + i * 1024, soff, 16);
         // every tag equals want iff (want 1) the AND of all words has the tag bits set,
         // (want 0) their OR has none: a 3-input reduction instead of a test per word
@@ -624,8 +626,10 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
 #pragma unroll
         for (int i = 0; i < RBW; ++i) {
           f32x4 c = acc[i];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i][ks][1], hh, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i][ks][0], ht, c, 0, 0, 0);
+          if (!(RNN_DIAG(p) & 32)) {  // 32: the big term only (timing)
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i][ks][1], hh, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i][ks][0], ht, c, 0, 0, 0);
+          }
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[i][ks][0], hs, c, 0, 0, 0);
           acc[i] = c;
         }
@@ -683,7 +687,11 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         gi[g] = gx[j][g];
       }
       float hn;
-      if (CELL == 0) {
+      if (RNN_DIAG(p) & 128) {  // 128: no transcendentals (timing)
+        hn = 0.25f * (fmaf(gs[0], GSC, gi[0]) + fmaf(gs[1], GSC, gi[1]) +
+                      fmaf(gs[2], GSC, gi[2]) + (CELL ? fmaf(gs[G - 1], GSC, gi[G - 1]) : 0.f));
+        hn = fminf(fmaxf(hn, -0.9f), 0.9f);
+      } else if (CELL == 0) {
         // ATen GRU cell: r, z, n ; h' = n + z * (h - n)
         const float r = fast_sigmoid(gi[0] + fmaf(gs[0], GSC, bhh[j][0]));
         const float z = fast_sigmoid(gi[1] + fmaf(gs[1], GSC, bhh[j][1]));
