@@ -208,6 +208,22 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def dsp_kernel_table(kern):
+    """The audio kernels of a probe summary against the HBM roofline: algorithmic bytes per
+    launch (each input read once, each output written once) / the launch's average device
+    time, as a fraction of 8 TB/s."""
+    out = {}
+    for lab, v in kern.items():
+        if v['bytes'] <= 0 or v['avg_ms'] <= 0:
+            continue
+        gbs = v['bytes'] / (v['avg_ms'] / 1e3) / 1e9
+        out[lab] = {'launches': v['launches'], 'avg_ms': round(v['avg_ms'], 4),
+                    'algorithmic_bytes': v['bytes'], 'hbm_GBs': round(gbs, 1),
+                    'hbm_frac': round(gbs / PEAK_HBM_GBS, 4),
+                    'share_of_probe_ms': round(v['total_ms'] / sum(u['total_ms'] for u in kern.values()), 4)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -350,6 +366,8 @@ def main():
         from forwardtacotron_amd.dsp import DSP
         dsp = DSP.from_config(default_config())
 
+        last = {}
+
         def vstep():
             o = gen(x_host.to(dev))
             m = o['mel_post']
@@ -357,6 +375,7 @@ def main():
                 m.cpu()
                 return dsp.griffinlim(m[0]).cpu().numpy().shape[0]
             w, n = dsp.griffinlim_batch(m)
+            last['wav'] = w
             w.cpu()
             return int(n.sum().item()) if torch.is_tensor(n) else int(np.sum(n))
         vstep()
@@ -374,6 +393,26 @@ def main():
                        'as gen_forward.py:115-134 with the griffinlim vocoder (as forwardtacotron_'
                        'amd.gen_forward: the mel fetched to the host, Griffin-Lim started from the '
                        'device copy; the NNLS runs while the host draws the initial phases)'}
+        # the HIP STFT kernels of that step (BASELINE configs[4] "+ HIP STFT", utils/dsp.py:71-103)
+        # against the HBM roofline: one more step under the per-launch probe, and the analysis
+        # direction (wav_to_mel: reflect pad, window, FFT, |.|, mel filterbank, log) of the
+        # vocoded batch, HIP events over `reps` calls
+        with KernelProbe() as vprobe:
+            vstep()
+            torch.cuda.synchronize()
+        voc['kernels'] = dsp_kernel_table(vprobe.summary())
+        if 'wav' in last:
+            from forwardtacotron_amd.dsp import mel_spectrogram
+            wav = last['wav'].contiguous()
+            plan = dsp.plan(dev)
+            with KernelProbe() as mprobe:
+                for _ in range(10):
+                    mel_spectrogram(plan, wav)
+                torch.cuda.synchronize()
+            voc['wav_to_mel'] = dsp_kernel_table(mprobe.summary())
+            voc['wav_to_mel_what'] = (f'DSP.wav_to_mel of the vocoded batch: {wav.size(0)} rows x '
+                                      f'{wav.size(1)} samples -> {plan.frames(wav.size(1))} frames '
+                                      'each, one fused STFT + mel + log kernel')
     # The timed steps replay the phoneme phase as a HIP graph (forward_tacotron.GRAPH), whose
     # kernels the per-launch probe cannot see: one more generate() with the phase eager,
     # after the timed region, gives their per-kernel times (the prenet bank, --kernels).
@@ -531,6 +570,10 @@ def main():
                        'global_batch': args.batch * world, 'T_phonemes': int(x_np.shape[1]),
                        'T_mel': int(out['mel_post'].size(2)), 'parallelism': f'dp{world}'},
             'roofline': roof,
+            'value_basis': ('tokens resident in HBM when the timed region starts, mel_post left in '
+                            'HBM: the harness contract (PCIe-inclusive rates are never `value`); '
+                            'SURVEY 8(d)\'s per-call figure with the token H2D and the mel_post '
+                            'D2H is `host_to_host`'),
         }
         if valid is not None:
             line['valid_frames_per_step'] = valid

@@ -209,8 +209,13 @@ __device__ __forceinline__ void report_timeout(const RnnParams &p) {
 // NBL: live sequences per group (16, or 8 to spread a recurrence over twice the groups: every
 // workgroup then acquires and stores half the h bytes per step; the MFMA columns past NBL are
 // dead)
+// U = 8 (the LSTM, f16x3, CST; "two chains per CU"): a group spreads over twice the
+// workgroups (64 for H = 512) with half the W_hh rows each, and two workgroups share a CU —
+// each workgroup's step carries half the MFMAs, and the other workgroup's chain (another
+// group) fills the CU while this one waits for its h.  128 cells: waves 0-1 own them.
 template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB>
-__global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(const RnnParams p) {
+__global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bidir_kernel(
+    const RnnParams p) {
   constexpr bool X6 = MODE != 0;  // 16x16x32 fragment layout (bf16x6 and f16x3)
   constexpr bool H3 = MODE == 2;
   constexpr int G = CELL ? 4 : 3;
@@ -225,13 +230,16 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   constexpr int BPG = H / U;
   constexpr bool LOCAL = BPG == 1;
   constexpr int CELLS = U * NB;
-  constexpr int CPT = CELLS / 256;
-  static_assert(U % 16 == 0 && H % U == 0 && RB % WR == 0 && CELLS % 256 == 0, "shape");
+  constexpr bool HALFCELL = CELLS < 256;  // U = 8: threads 0..127 own the cells
+  constexpr int CPT = HALFCELL ? 1 : CELLS / 256;
+  static_assert(R % 16 == 0 && (U % 16 == 0 || U == 8) && H % U == 0 && RB % WR == 0 &&
+                    (CELLS % 256 == 0 || CELLS == 128), "shape");
   static_assert(X6 ? (KW % 32 == 0) : (KB % 4 == 0), "K split");
   // CST: the compute waves store their own tagged h chunks right after the cell update (each
   // wave's 16 chunks are its own cells: CPT == 1), the comm wave only the y rows — barrier C
   // and the comm wave's stage read leave the h hand-off's critical path
-  static_assert(!CST || (H3 && !LOCAL && CPT == 1 && U == 16), "compute-wave h stores");
+  static_assert(!CST || (H3 && !LOCAL && CPT == 1 && (U == 16 || U == 8)), "compute-wave h stores");
+  static_assert(U != 8 || (CST && NBL == NB), "U = 8: the CST form, 16 live sequences");
   static_assert(NBL == NB || (NBL == 8 && !LOCAL), "live sequences per group");
   constexpr int RR = R;                           // reduction rows
   constexpr float GSC = H3 ? H3_UNSCALE : 1.f;     // scale of the reduced W_hh h sums
@@ -306,8 +314,8 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
   if constexpr (!LOCAL) {
     if (wave == 4) {
       constexpr int F4 = CELLS / 4;  // float4s of the slice
-      constexpr int FPL = F4 / 64;   // per lane
-      static_assert(F4 % 64 == 0, "comm wave tiling");
+      constexpr int FPL = F4 < 64 ? 1 : F4 / 64;   // per lane (U = 8: lanes 0..31)
+      static_assert(F4 % 64 == 0 || F4 == 32, "comm wave tiling");
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.hx, (short)0, 0x7FFFFFF0, 0x00020000);
       const int hxp = p.ngroups_total * 16 * H * 4;  // bytes between the parity halves
       unsigned hofs[FPL];
@@ -320,7 +328,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
           const int bl = f / (U / 4);
           yb[i] = chunk * NBL + bl;
           k0s[i] = u0 + (f % (U / 4)) * 4;
-          ok[i] = bl < NBL && yb[i] < p.B;
+          ok[i] = f < F4 && bl < NBL && yb[i] < p.B;
         }
         if constexpr (H3) {  // h: 16-B chunk f = (seq, 8 units, plane) of f16 halves
           const int bl = f / (U / 4), rem = f % (U / 4), plane = rem & 1;
@@ -366,7 +374,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
         }
 #pragma unroll
         for (int i = 0; i < FPL; ++i) {
-          const f32x4 v = *(const f32x4 *)&ystage[(lane + 64 * i) * 4];
+          const f32x4 v = *(const f32x4 *)&ystage[((lane + 64 * i) % F4) * 4];
           if (ok[i]) *(f32x4 *)(p.y + ((size_t)yb[i] * p.T + tt) * p.y_stride + dir * H + k0s[i]) = v;
         }
       }
@@ -675,6 +683,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(co
     // cell update
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
+      if (HALFCELL && tid >= CELLS) continue;  // U = 8: waves 2-3 own no cells
       const int bl = cbl[j];
       float gs[G], gi[G];
 #pragma unroll
@@ -1129,11 +1138,28 @@ static int legacy_nbl(int cell, int B, int H, int mma, bool spread, int maxb) {
   return 2 * ((B + 7) / 8) * (H / 16) <= maxb ? 8 : NB;
 }
 
+// FTMI_RNN_U8=1 (read per call): the spread f16x3 LSTM on two workgroups of 8 units per CU
+// (rnn_bidir_kernel U = 8) instead of one of 16
+static bool u8_path(int cell, int H, int mma, bool spread) {
+  const char *v = getenv("FTMI_RNN_U8");
+  return v && atoi(v) == 1 && spread && mma == 2 && cell == 1 && H == 512 && cst_enabled();
+}
+
 extern "C" int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t mma) {
   if (B <= 0 || H <= 0 || H % 16 != 0) return 0;
   const bool spread = (mma & FTMI_RNN_SPREAD) != 0;
   mma &= 0xFF;
   if (gemv_path(cell, B, H)) return (xcd_local_env() ? 8 : 2) * (H / 16);  // launch_gemv
+  if (u8_path(cell, H, mma, spread)) {  // two workgroups per CU: CUs occupied
+    const int maxb = 2 * device_cu_count(), bpg = H / 8;
+    const int max_groups = (maxb / bpg) & ~1;
+    if (max_groups < 2) return 0;
+    const int nchunks = (B + NB - 1) / NB;
+    const int ngroups = 2 * (nchunks < max_groups / 2 ? nchunks : max_groups / 2);
+    int nblk = ngroups * bpg;
+    if (ngroups < 8 && 8 * bpg <= maxb) nblk = 8 * bpg;
+    return (nblk + 1) / 2;
+  }
   const int bpg = H / rnn_units(cell, H, mma);
   const int maxb = device_cu_count();
   const int max_groups = (maxb / bpg) & ~1;
@@ -1268,6 +1294,8 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   // the launch's real workgroup count)
   if (mma == 2 && cst_enabled() && ((cell == 1 && H == 512) || (cell == 0 && H == 256))) {
     const bool nb8 = legacy_nbl(cell, B, H, mma, spread, maxb) == 8;
+    if (cell == 1 && u8_path(cell, H, mma, spread))
+      return launch_rnn<1, 512, 8, 4, 2, true>(p, nchunks, 2 * maxb, s);
     if (cell == 1) return launch_rnn<1, 512, 16, 4, 2, true>(p, nchunks, maxb, s);
     return nb8 ? launch_rnn<0, 256, 16, 4, 2, true, 8>(p, nchunks, maxb, s)
                : launch_rnn<0, 256, 16, 4, 2, true>(p, nchunks, maxb, s);

@@ -660,10 +660,12 @@ F16X3_SHAPES = [('lstm', 512, 1, 23), ('lstm', 512, 17, 12), ('lstm', 512, 64, 9
 # kernel variants of rnn_bidir_kernel: the default (compute-wave h stores), the comm wave's
 # h stores (FTMI_RNN_CSTORE=0), and spread (GRU: 8 live sequences per group); H = 64 has the
 # default only
+# u8: the spread LSTM on two workgroups of 8 units per CU (FTMI_RNN_U8=1)
 ROW_VARIANTS = ['default', 'comm', 'spread']
 F16X3_CASES = [pytest.param(*shape, v, id=f'{shape[0]}{shape[1]}-B{shape[2]}-{v}')
                for shape in F16X3_SHAPES
-               for v in (ROW_VARIANTS if shape[1] >= 128 else ['default'])]
+               for v in (ROW_VARIANTS + ['u8'] * (shape[0] == 'lstm') if shape[1] >= 128
+                         else ['default'])]
 
 
 @pytest.mark.parametrize('cell,H,B,T,variant', F16X3_CASES)
@@ -676,9 +678,10 @@ def test_rnn_f16x3_kernels(cell, H, B, T, variant, rng, monkeypatch):
     monkeypatch.setattr(ops, 'RNN_MMA', 2)
     monkeypatch.setenv('FTMI_RNN_GEMV', '0')
     monkeypatch.setenv('FTMI_RNN_CSTORE', '0' if variant == 'comm' else '1')
+    monkeypatch.setenv('FTMI_RNN_U8', '1' if variant == 'u8' else '0')
     fin = 512 if cell == 'lstm' else 256
     m, sd = _rnn_module(cell, fin, H, rng)
-    m.spread = variant == 'spread'
+    m.spread = variant in ('spread', 'u8')
     x = rng.normal(0, 1, (B, T, fin)).astype(np.float32)
     ref = (O.lstm_bidir if cell == 'lstm' else O.gru_bidir)(sd, 'r', x, np.float32)
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
@@ -716,13 +719,17 @@ def test_rnn_f16_weight_range_guard(rng, monkeypatch):
     assert int(st.item()) & 2
 
 
-@pytest.mark.parametrize('B,variant', [(2, 'gemv'), (9, 'default'), (9, 'spread')])
+@pytest.mark.parametrize('B,variant', [(2, 'gemv'), (9, 'default'), (9, 'spread'), (9, 'u8'),
+                                       (40, 'u8')])
 def test_lstm_through_lr_index_and_lengths(B, variant, rng, monkeypatch):
     """LSTM reading phoneme-rate projections through the LR index map == LSTM over the
     expanded sequence; with lengths it reproduces pack_padded / pad_packed semantics (B = 2:
-    the GEMV kernel; B = 9: the MFMA kernel, compact and spread)."""
+    the GEMV kernel; B = 9: the MFMA kernel, compact and spread; u8: two workgroups of 8
+    units per CU)."""
     from forwardtacotron_amd import ops
+    monkeypatch.setenv('FTMI_RNN_U8', '1' if variant == 'u8' else '0')
     m, sd = _rnn_module('lstm', 512, 512, rng)
+    m.spread = variant in ('spread', 'u8')
     T = 11
     x = rng.normal(0, 1, (B, T, 512)).astype(np.float32)
     dur = rng.uniform(-0.5, 5.0, (B, T)).astype(np.float32)
