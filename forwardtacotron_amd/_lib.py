@@ -66,6 +66,10 @@ SIGNATURES = {
                                    c_int, P, P]),
     'ftmi_highway_stack': (c_int, [P, c_int64, c_int64, c_int, c_int, P, c_int, P, P, P, P, P,
                                    c_int, P, c_int64, P, c_int64, P, P]),
+    'ftmi_highway_stack_spread_ws_bytes': (c_int64, [c_int64]),
+    'ftmi_highway_stack_spread_blocks': (c_int, [c_int64]),
+    'ftmi_highway_stack_spread': (c_int, [P, c_int64, c_int64, c_int, c_int, P, c_int, P, P, P, P,
+                                          P, c_int, P, c_int64, P, c_int64, P, P, P]),
     'ftmi_split_weights_bytes': (c_int64, [c_int64, c_int64]),
     'ftmi_split_weights': (c_int, [P, c_int64, c_int64, P, P]),
     'ftmi_split_weights_f16_bytes': (c_int64, [c_int64, c_int64]),

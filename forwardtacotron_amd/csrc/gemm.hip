@@ -3032,6 +3032,196 @@ __global__ __launch_bounds__(512, 1) void highway_stack_kernel(const HwStackPara
   if (!(amax <= 65504.f) && p.status) atomicOr(p.status, 1u);
 }
 
+// ---- the CBHG tail for few rows, spread over the chip (c2: 120 / 816 rows) -------------
+// highway_stack_kernel gives one workgroup 64 rows x ALL 256 channels, so at batch 1 (120
+// prenet rows: 2 workgroups; 816 postnet rows: 13) a few CUs stream the whole 3-4 MB of
+// weight planes each (~100 us).  Here a row block is spread over HSS_P = 16 workgroups, each
+// owning 16 output channels of every layer (and n_out / 16 columns of the output
+// projection): it streams 1/16 of the weights, and the layers' activations are exchanged
+// between the 16 workgroups of a row block through memory after each layer.  Exchange
+// (MI355X_MICROARCH.md "Valid forms", first row of the sc1 table): a workgroup writes its
+// 64 x 16 slice of the layer's output, split into the f16 head / scaled-tail image layout,
+// with 16-B sc1 stores; every storing wave waits for its stores (vmcnt(0)); a barrier; one
+// lane adds to the row block's counter (agent scope) and polls it (sc1 loads, bounded) until
+// all 16 have added for this layer; a barrier; then every wave loads the full 64 x 256 image
+// with sc1 loads into LDS.  The image buffers alternate by layer parity: a workgroup writes
+// layer l + 2's slice only after all 16 have published layer l + 1, which each did after
+// reading layer l's image.  Per accumulator the k-step, product and epilogue order of
+// highway_stack_kernel (hs_gemm over the same fragment-major planes, one 16-row block per
+// wave): the results are bit-identical to it.  Every workgroup must be resident at once
+// (RB x 16 <= the CU count: the host checks); a spin past the bound sets the status word's
+// timeout bit (FTMI_STATUS_RNN_TIMEOUT) instead of hanging.
+constexpr int HSS_P = 16;       // workgroups (channel slices) per row block
+constexpr int HSS_MAXRB = 16;   // row blocks: M <= 1024
+constexpr int HSS_CNT = 32;     // words between row-block counters (one 128-B line each)
+
+struct HsSpread {
+  unsigned *cnt;    // [RB][HSS_CNT] arrival counters, zeroed before the launch
+  _Float16 *xb;     // [2][RB][2 planes][HS_BM][HS_P] exchange images
+  unsigned spin;    // poll bound
+};
+
+template <int NO>
+__global__ __launch_bounds__(512, 1) void highway_spread_kernel(const HwStackParams p,
+                                                               const HsSpread q) {
+  constexpr int IMG = HS_IMG;
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2 * IMG];           // head | tail
+  __shared__ __attribute__((aligned(16))) _Float16 pub[2 * HS_BM * 16];   // the slice, split
+  __shared__ int s_abort;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fs = lane >> 4;
+  const int s = blockIdx.x % HSS_P, rb = blockIdx.x / HSS_P;
+  const int m0 = rb * HS_BM, mi = wave & 3;
+  const int RB = (p.M + HS_BM - 1) / HS_BM;
+  auto bptr = [&](const _Float16 *base, int n0, int Kpad) -> const _Float16 * {
+    return base + (int64_t)(n0 >> 4) * (Kpad / 32) * 512 + lane * 8;
+  };
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(q.xb, (short)0, 0x7FFFFFF0, 0x00020000);
+  const int img_halves = 2 * HS_BM * HS_P;  // one (parity, row block) image
+  float amax = 0.f;
+  if (tid == 0) s_abort = 0;
+
+  // ---- the input rows -> the LDS image (as highway_stack_kernel)
+  const int q4 = p.kp_pre / 4;
+  for (int e = tid; e < HS_BM * q4; e += 512) {
+    const int r = e / q4, c = (e - r * q4) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (m0 + r < p.M && c < p.Cp) v = *(const f32x4 *)(p.x + (int64_t)(m0 + r) * p.x_stride + c);
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    f16x4 hh, tt;
+    split2h(v, hh, tt);
+    *(f16x4 *)(lds + r * HS_P + c) = hh;
+    *(f16x4 *)(lds + IMG + r * HS_P + c) = tt;
+  }
+  __syncthreads();
+  const _Float16 *Ah = lds + 16 * mi * HS_P, *At = lds + IMG + 16 * mi * HS_P;
+
+  // waves 0-3: rows 16 mi + 4 fs + i, channel 16 s + fr of the current activations (fp32)
+  f32x4 xs = {0.f, 0.f, 0.f, 0.f};
+  if (wave < 4) {  // pre_highway (no bias)
+    f32x4 acc[1][1];
+    const _Float16 *bp[1] = {bptr(p.w_pre, 16 * s, p.kp_pre)};
+    hs_gemm<1, 1>(acc, Ah, At, bp, (int64_t)HS_C * p.kp_pre, p.kp_pre / 32, fr, fs);
+    xs = acc[0][0] * p.cs_pre[16 * s + fr];
+  }
+
+  // publish xs as layer l's slice, wait for the row block's 16 slices, load the image
+  auto exchange = [&](int l) -> bool {
+    if (wave < 4) {  // the slice, split, into pub [plane][row][16]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = xs[i];
+        amax = fmaxf(amax, fabsf(v));
+        const _Float16 hh = (_Float16)v;
+        const int o = (16 * mi + 4 * fs + i) * 16 + fr;
+        pub[o] = hh;
+        pub[HS_BM * 16 + o] = (_Float16)((v - (float)hh) * H3_SCALE);
+      }
+    }
+    __syncthreads();
+    const int par = l & 1;
+    const int base = (par * RB + rb) * img_halves;  // halves
+    if (tid < 256) {  // 16-B chunk (plane, row, half of the 16 channels), write-through
+      const int pl = tid >> 7, row = (tid >> 1) & 63, c8 = tid & 1;
+      const u32x4 v = *(const u32x4 *)(pub + (pl * HS_BM + row) * 16 + 8 * c8);
+      const int off = (base + (pl * HS_BM + row) * HS_P + 16 * s + 8 * c8) * 2;
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16 /* sc1 */);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores done
+    __syncthreads();
+    if (tid == 0) {
+      unsigned *c = q.cnt + rb * HSS_CNT;
+      __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned want = (unsigned)HSS_P * (l + 1);
+      unsigned spins = 0;
+      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > q.spin) {
+          s_abort = 1;
+          if (p.status) atomicOr(p.status, FTMI_STATUS_RNN_TIMEOUT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (s_abort) return false;
+    u32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // chunk e = (plane, row, 16-B piece of the 256 channels)
+      const int e = tid + 512 * j, pl = e >> 11, row = (e >> 5) & 63, c = e & 31;
+      v[j] = __builtin_amdgcn_raw_buffer_load_b128(
+          rs, (base + (pl * HS_BM + row) * HS_P + 8 * c) * 2, 0, 16 /* sc1 */);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = tid + 512 * j, pl = e >> 11, row = (e >> 5) & 63, c = e & 31;
+      *(u32x4 *)(lds + pl * IMG + row * HS_P + 8 * c) = v[j];
+    }
+    __syncthreads();
+    return true;
+  };
+
+  // ---- highways: g = sigmoid(x W2^T + b2), x <- g relu(x W1^T + b1) + (1 - g) x
+  for (int l = 0; l < p.L; ++l) {
+    if (!exchange(l)) return;
+    if (wave < 4) {
+      const int cb = s >> 1, nj = s & 1;  // the stack kernel's (column block, half)
+      f32x4 acc[1][2];
+      const _Float16 *bp[2] = {bptr(p.w_hw[l], 64 * cb + 16 * nj, HS_C),
+                               bptr(p.w_hw[l], 64 * cb + 32 + 16 * nj, HS_C)};
+      hs_gemm<2, 1>(acc, Ah, At, bp, (int64_t)2 * HS_C * HS_C, HS_C / 32, fr, fs);
+      const int col = 16 * s + fr;
+      const float c1 = p.cs_hw[l][64 * cb + 16 * nj + fr];
+      const float c2 = p.cs_hw[l][64 * cb + 32 + 16 * nj + fr];
+      const float bb1 = p.b1[l][col], bb2 = p.b2[l][col];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float x1, x2;
+        {
+#pragma clang fp contract(off)
+          x1 = acc[0][0][i] * c1 + bb1;
+          x2 = acc[0][1][i] * c2 + bb2;
+        }
+        const float g = ftmi_sigmoid(x2);
+        xs[i] = highway_mix(g, x1, xs[i]);
+      }
+    }
+  }
+  if (p.h && wave < 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + 16 * mi + 4 * fs + i;
+      if (row < p.M) p.h[(int64_t)row * p.h_stride + 16 * s + fr] = xs[i];
+    }
+  }
+
+  // ---- output projection: columns [n_out / 16 s, + n_out / 16), two halves of NO tiles
+  if (p.w_out) {
+    if (!exchange(p.L)) return;
+    const int n0 = (p.n_out / HSS_P) * s + (wave >> 2) * 16 * NO;
+    f32x4 acc[1][NO];
+    const _Float16 *bp[NO];
+#pragma unroll
+    for (int ni = 0; ni < NO; ++ni) bp[ni] = bptr(p.w_out, n0 + 16 * ni, HS_C);
+    hs_gemm<NO, 1>(acc, Ah, At, bp, (int64_t)p.n_out * HS_C, HS_C / 32, fr, fs);
+#pragma unroll
+    for (int ni = 0; ni < NO; ++ni) {
+      const int col = n0 + 16 * ni + fr;
+      const float cs = p.cs_out[col], b = p.b_out ? p.b_out[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma clang fp contract(off)
+        const int row = m0 + 16 * mi + 4 * fs + i;
+        float v = acc[0][ni][i] * cs;
+        if (p.b_out) v += b;
+        if (row < p.M) p.y[(int64_t)row * p.y_stride + col] = v;
+      }
+    }
+  }
+  if (!(amax <= 65504.f) && p.status) atomicOr(p.status, 1u);
+}
+
 // ---- row-panel projection: y = [LayerNorm](x W^T + b [+ residual]) --------------------
 // The k = 1 contractions of a FastPitch FFT block (models/fast_pitch.py:56-91, the
 // reference's FFTBlock): self_attn.in_proj (K = d, N = 3d), out_proj + residual -> norm1
@@ -4004,13 +4194,13 @@ static const float *f16_colscale(const void *w3, int64_t N, int64_t K) {
   return (const float *)((const char *)w3 + 3 * N * Kpad * 2);
 }
 
-extern "C" int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, int32_t Cp,
-                                  int32_t C, const void *w_pre_split, int32_t L,
-                                  const void *const *w_hw_split, const float *const *b1,
-                                  const float *const *b2, const void *w_out_split,
-                                  const float *b_out, int32_t n_out, float *y, int64_t y_stride,
-                                  float *h, int64_t h_stride, uint32_t *status,
-                                  ftmi_stream_t stream) {
+// the parameters of ftmi_highway_stack[_spread] (FTMI_OK or the argument error)
+static int hs_params(HwStackParams &p, const float *x, int64_t x_stride, int64_t M, int32_t Cp,
+                     int32_t C, const void *w_pre_split, int32_t L,
+                     const void *const *w_hw_split, const float *const *b1,
+                     const float *const *b2, const void *w_out_split, const float *b_out,
+                     int32_t n_out, float *y, int64_t y_stride, float *h, int64_t h_stride,
+                     uint32_t *status) {
   if (!x || !w_pre_split || M <= 0 || Cp <= 0 || L < 0) return FTMI_E_ARG;
   if (L > 0 && (!w_hw_split || !b1 || !b2)) return FTMI_E_ARG;
   if (w_out_split ? (!y || n_out <= 0) : (n_out != 0 || y != nullptr)) return FTMI_E_ARG;
@@ -4020,7 +4210,7 @@ extern "C" int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, i
   if (!ftmi_aligned16(x) || (x_stride & 3) || !ftmi_aligned16(w_pre_split)) return FTMI_E_ALIGN;
   if (w_out_split && !ftmi_aligned16(w_out_split)) return FTMI_E_ALIGN;
   if ((const float *)x == y || (const float *)x == h) return FTMI_E_ARG;
-  HwStackParams p = {};
+  p = HwStackParams{};
   p.x = x;
   p.x_stride = x_stride;
   p.M = (int)M;
@@ -4047,6 +4237,20 @@ extern "C" int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, i
   p.h = h;
   p.h_stride = h_stride;
   p.status = status;
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, int32_t Cp,
+                                  int32_t C, const void *w_pre_split, int32_t L,
+                                  const void *const *w_hw_split, const float *const *b1,
+                                  const float *const *b2, const void *w_out_split,
+                                  const float *b_out, int32_t n_out, float *y, int64_t y_stride,
+                                  float *h, int64_t h_stride, uint32_t *status,
+                                  ftmi_stream_t stream) {
+  HwStackParams p;
+  const int rc = hs_params(p, x, x_stride, M, Cp, C, w_pre_split, L, w_hw_split, b1, b2,
+                           w_out_split, b_out, n_out, y, y_stride, h, h_stride, status);
+  if (rc != FTMI_OK) return rc;
   // 96 rows per workgroup once the grid still fills the chip (FTMI_HS_BM = 64 / 96, read per
   // call, forces one; 128 rows would need ~290 VGPRs and spills)
   const char *e = getenv("FTMI_HS_BM");
@@ -4057,6 +4261,55 @@ extern "C" int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, i
   } else {
     const unsigned blocks = (unsigned)((M + HS_BM - 1) / HS_BM);
     hipLaunchKernelGGL(highway_stack_kernel<64>, dim3(blocks), dim3(512), 0, ftmi_hs(stream), p);
+  }
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int64_t ftmi_highway_stack_spread_ws_bytes(int64_t M) {
+  if (M <= 0 || M > (int64_t)HSS_MAXRB * HS_BM) return 0;
+  const int64_t RB = (M + HS_BM - 1) / HS_BM;
+  return RB * HSS_CNT * 4 + 2 * RB * 2 * HS_BM * HS_P * 2;
+}
+
+extern "C" int32_t ftmi_highway_stack_spread_blocks(int64_t M) {
+  if (M <= 0 || M > (int64_t)HSS_MAXRB * HS_BM) return 0;
+  return (int32_t)((M + HS_BM - 1) / HS_BM * HSS_P);
+}
+
+extern "C" int ftmi_highway_stack_spread(const float *x, int64_t x_stride, int64_t M, int32_t Cp,
+                                         int32_t C, const void *w_pre_split, int32_t L,
+                                         const void *const *w_hw_split, const float *const *b1,
+                                         const float *const *b2, const void *w_out_split,
+                                         const float *b_out, int32_t n_out, float *y,
+                                         int64_t y_stride, float *h, int64_t h_stride,
+                                         uint32_t *status, void *ws, ftmi_stream_t stream) {
+  HwStackParams p;
+  const int rc = hs_params(p, x, x_stride, M, Cp, C, w_pre_split, L, w_hw_split, b1, b2,
+                           w_out_split, b_out, n_out, y, y_stride, h, h_stride, status);
+  if (rc != FTMI_OK) return rc;
+  if (!ws) return FTMI_E_ARG;
+  if (!ftmi_aligned16(ws)) return FTMI_E_ALIGN;
+  const int blocks = ftmi_highway_stack_spread_blocks(M);
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  // every workgroup resident at once (they wait on each other); n_out split in two halves
+  // of n_out / 512 16-column tiles per slice
+  if (blocks <= 0 || blocks > cus || (w_out_split && n_out > 3 * HS_NPASS)) return FTMI_E_UNSUPPORTED;
+  const int RB = blocks / HSS_P;
+  HsSpread q;
+  q.cnt = (unsigned *)ws;
+  q.xb = (_Float16 *)((char *)ws + (int64_t)RB * HSS_CNT * 4);
+  q.spin = 1u << 22;
+  hipStream_t s = ftmi_hs(stream);
+  hipError_t e = hipMemsetAsync(ws, 0, (size_t)RB * HSS_CNT * 4, s);
+  if (e != hipSuccess) return (int)e;
+  switch (w_out_split ? n_out / HS_NPASS : 1) {
+    case 1: hipLaunchKernelGGL(highway_spread_kernel<1>, dim3(blocks), dim3(512), 0, s, p, q); break;
+    case 2: hipLaunchKernelGGL(highway_spread_kernel<2>, dim3(blocks), dim3(512), 0, s, p, q); break;
+    default: hipLaunchKernelGGL(highway_spread_kernel<3>, dim3(blocks), dim3(512), 0, s, p, q);
   }
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;

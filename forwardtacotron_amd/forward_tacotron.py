@@ -278,14 +278,15 @@ class ForwardTacotron(nn.Module):
         return {'mel': x_mel, 'mel_post': x_post,
                 'dur': dur_hat, 'pitch': pitch_hat, 'energy': energy_hat}
 
-    def _side_streams(self, device, B: int):
+    def _side_streams(self, device, B: int, T: int = 0):
         """(pitch, energy, prenet) streams.  The prenet CBHG -> LSTM input projection is the
         phoneme phase's critical chain: its stream gets the higher priority
         (FTMI_PRENET_PRIORITY, default -1 = high; 0 = same as the others), so the
         predictors fill the CUs it leaves idle instead of delaying it.
         The four recurrences of the phase (three predictor GRUs, the prenet GRU) are
         persistent kernels whose workgroups wait on each other: run concurrently they must
-        fit the CUs together.  When they do not (large batches), every stream is the
+        fit the CUs together — with the prenet's spread CBHG tail at few rows
+        (ops.hs_spread_blocks: its workgroups wait on each other too).  When they do not (large batches), every stream is the
         caller's (the phase runs serialised) — never a co-residency timeout."""
         cache = self.__dict__.setdefault('_ftmi_streams', {})
         if device not in cache:
@@ -293,10 +294,11 @@ class ForwardTacotron(nn.Module):
             cache[device] = [torch.cuda.Stream(device=device), torch.cuda.Stream(device=device),
                              torch.cuda.Stream(device=device, priority=prio)]
         fits = self.__dict__.setdefault('_ftmi_concurrent', {})
-        key = (device, B, ops.RNN_MMA, bool(ops._FORCED))
+        key = (device, B, T, ops.RNN_MMA, bool(ops._FORCED))
         if key not in fits:
             rnns = (self.dur_pred.rnn, self.pitch_pred.rnn, self.energy_pred.rnn, self.prenet.rnn)
             need = sum(ops.rnn_blocks(r.cell, B, r.hidden) for r in rnns)
+            need += ops.hs_spread_blocks(B * T, 6 * self.prenet.channels)
             fits[key] = 0 < need <= ops._num_cus()
         if not fits[key]:
             main = torch.cuda.current_stream(device)
@@ -422,7 +424,7 @@ class ForwardTacotron(nn.Module):
         pitch_fn = energy_fn = None (capture only): the predictors' raw outputs are returned
         and xp does not carry their projections yet (the split graph of _phoneme_graph)."""
         main = torch.cuda.current_stream(x.device)
-        s_pitch, s_energy, s_prenet = self._side_streams(x.device, x.size(0))
+        s_pitch, s_energy, s_prenet = self._side_streams(x.device, x.size(0), x.size(1))
         for s in (s_pitch, s_energy, s_prenet):
             s.wait_stream(main)
         with torch.cuda.stream(s_prenet):

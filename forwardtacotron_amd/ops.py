@@ -551,13 +551,45 @@ def highway_stack(x: torch.Tensor, pre_split: torch.Tensor, C: int, hw_splits, b
     b2_arr = arr(*[b.data_ptr() for b in b2s])
     flops = 2.0 * M * C * (Cp + L * 2 * C + n_out)
     nbytes = 4.0 * M * (Cp + n_out + (C if want_h else 0))
-    launch('ftmi_highway_stack', f'highway_stack[M={M},Cp={Cp},L={L},N={n_out}]', flops, nbytes,
-           x.data_ptr(), xs, M, Cp, C, pre_split.data_ptr(), L, ctypes.addressof(w_arr),
-           ctypes.addressof(b1_arr), ctypes.addressof(b2_arr), _ptr(out_split), _ptr(b_out),
-           n_out if out_split is not None else 0, _ptr(y), y.stride(1) if y is not None else 0,
-           _ptr(h), h.stride(1) if h is not None else 0, status_word(x.device).data_ptr(),
-           _stream())
+    args = (x.data_ptr(), xs, M, Cp, C, pre_split.data_ptr(), L, ctypes.addressof(w_arr),
+            ctypes.addressof(b1_arr), ctypes.addressof(b2_arr), _ptr(out_split), _ptr(b_out),
+            n_out if out_split is not None else 0, _ptr(y), y.stride(1) if y is not None else 0,
+            _ptr(h), h.stride(1) if h is not None else 0, status_word(x.device).data_ptr())
+    if hs_spread_blocks(M, n_out if out_split is not None else 0) > 0:
+        ws = _spread_workspace(int(_lib.load().ftmi_highway_stack_spread_ws_bytes(M)), x.device)
+        launch('ftmi_highway_stack_spread', f'highway_stack_spread[M={M},Cp={Cp},L={L},N={n_out}]',
+               flops, nbytes, *args, ws.data_ptr(), _stream())
+    else:
+        launch('ftmi_highway_stack', f'highway_stack[M={M},Cp={Cp},L={L},N={n_out}]', flops,
+               nbytes, *args, _stream())
     return y, h
+
+
+def hs_spread_blocks(M: int, n_out: int = 0) -> int:
+    """Workgroups of the spread CBHG tail (`ftmi_highway_stack_spread`) for M rows, or 0 when
+    `highway_stack` runs the one-workgroup-per-64-rows kernel: M <= 1024 rows, n_out <= 1536,
+    all of them resident at once.  FTMI_HS_SPREAD=0 (read per call) keeps that kernel."""
+    if os.environ.get('FTMI_HS_SPREAD', '1') == '0' or n_out > 1536:
+        return 0
+    n = int(_lib.load().ftmi_highway_stack_spread_blocks(M))
+    return n if 0 < n <= _num_cus() else 0
+
+
+_SPREAD_WS = {}
+
+
+def _spread_workspace(nbytes: int, device) -> torch.Tensor:
+    """The spread tail's exchange workspace of the current stream (one per (device, stream):
+    launches on one stream are ordered), kept alive for graph replays that captured its
+    address; grown when too small."""
+    stream = torch.cuda.current_stream(device)
+    key = (torch.device(device), stream.cuda_stream)
+    t = _SPREAD_WS.get(key)
+    if t is None or t.numel() < nbytes:
+        if t is not None:
+            _BANK_OLD.append(t)  # a captured graph may still replay the old buffer
+        t = _SPREAD_WS[key] = torch.zeros(max(nbytes, 16), device=device, dtype=torch.uint8)
+    return t
 
 
 PANEL_N = 256  # gemm.hip panel_proj_kernel: output columns per panel (LayerNorm width)

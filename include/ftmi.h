@@ -82,7 +82,7 @@ enum { FTMI_BANK_COUNTERS = 4096 };
  * 15: FTMI_BANK_HALVES, ftmi_conv_bank_halves_ws_floats; 16: FTMI_BANK_IMAGE,
  * ftmi_conv_bank_halves_image[_bytes]; 17: FTMI_BANK_PAIR, ftmi_conv_args.x_plane / x_fin;
  * 18: rejected variants removed — FTMI_BANK_LAST, FTMI_BANK_PAIR, ftmi_conv_args.x_plane /
- * x_fin, ftmi_gru_bidir_fused). */
+ * x_fin, ftmi_gru_bidir_fused; ftmi_highway_stack_spread[_ws_bytes|_blocks] added). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
@@ -271,6 +271,26 @@ int ftmi_highway_stack(const float *x, int64_t x_stride, int64_t M, int32_t Cp, 
                        const void *w_out_split, const float *b_out, int32_t n_out, float *y,
                        int64_t y_stride, float *h, int64_t h_stride, uint32_t *status,
                        ftmi_stream_t stream);
+
+/* The same CBHG tail for few rows (ABI 18; batch-1 generation, BASELINE config c2: the
+ * prenet's 120 and the postnet's 816 rows), spread over the chip: each 64-row block over 16
+ * workgroups that own 16 channels of every layer (and n_out / 16 output columns) and exchange
+ * the layers' activations through `ws` — bit-identical to ftmi_highway_stack.  M <= 1024,
+ * n_out <= 1536, and the ftmi_highway_stack_spread_blocks(M) workgroups must all be resident
+ * at once (<= the CU count; they wait on each other: run it where no other persistent kernel
+ * holds the CUs it needs), else FTMI_E_UNSUPPORTED.  ws: 16-B aligned device workspace of
+ * ftmi_highway_stack_spread_ws_bytes(M) bytes, one per stream (its counters are zeroed by
+ * the call).  A workgroup that waits past its spin bound sets FTMI_STATUS_RNN_TIMEOUT.
+ * Replaces common_layers.py:110-118 (pre_highway, highways, the GRU's input GEMM). */
+int64_t ftmi_highway_stack_spread_ws_bytes(int64_t M);
+int32_t ftmi_highway_stack_spread_blocks(int64_t M);
+int ftmi_highway_stack_spread(const float *x, int64_t x_stride, int64_t M, int32_t Cp,
+                              int32_t C, const void *w_pre_split, int32_t L,
+                              const void *const *w_hw_split, const float *const *b1,
+                              const float *const *b2, const void *w_out_split,
+                              const float *b_out, int32_t n_out, float *y, int64_t y_stride,
+                              float *h, int64_t h_stride, uint32_t *status, void *ws,
+                              ftmi_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * Bidirectional single-layer GRU / LSTM recurrence, PyTorch semantics, h0 = c0 = 0,

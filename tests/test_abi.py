@@ -67,6 +67,9 @@ def test_strerror():
     (lambda L: L.ftmi_highway_stack(ctypes.c_void_p(256), 80, 10, 80, 128, ctypes.c_void_p(256), 0, None, None, None, None, None, 0, None, 0, ctypes.c_void_p(512), 256, None, None), 1002),
     (lambda L: L.ftmi_highway_stack(ctypes.c_void_p(256), 80, 10, 78, 256, ctypes.c_void_p(256), 0, None, None, None, None, None, 0, None, 0, ctypes.c_void_p(512), 256, None, None), 1002),
     (lambda L: L.ftmi_highway_stack(ctypes.c_void_p(256), 80, 10, 80, 256, ctypes.c_void_p(256), 0, None, None, None, ctypes.c_void_p(256), None, 500, ctypes.c_void_p(1024), 500, None, 0, None, None), 1002),
+    # ftmi_highway_stack_spread: no workspace; more rows than one launch of resident workgroups
+    (lambda L: L.ftmi_highway_stack_spread(ctypes.c_void_p(256), 80, 10, 80, 256, ctypes.c_void_p(256), 0, None, None, None, None, None, 0, None, 0, ctypes.c_void_p(512), 256, None, None, None), 1001),
+    (lambda L: L.ftmi_highway_stack_spread(ctypes.c_void_p(256), 80, 2000, 80, 256, ctypes.c_void_p(256), 0, None, None, None, None, None, 0, None, 0, ctypes.c_void_p(512), 256, None, ctypes.c_void_p(1024), None), 1003),
     (lambda L: L.ftmi_highway_stack(ctypes.c_void_p(260), 80, 10, 80, 256, ctypes.c_void_p(256), 0, None, None, None, None, None, 0, None, 0, ctypes.c_void_p(512), 256, None, None), 1004),
     (lambda L: L.ftmi_split_weights_f16_frag(None, 16, 4, None, None), 1001),
     (lambda L: L.ftmi_split_weights_f16_frag(ctypes.c_void_p(256), 20, 4, ctypes.c_void_p(256), None), 1002),
@@ -132,3 +135,14 @@ def test_default_library_has_no_invalid_result_switches():
     for name in (b'FTMI_RNN_DIAG', b'FTMI_SLAB_DIAG', b'FTMI_SKINNY_DIAG',
                  b'FTMI_BANK_HALVES_DIAG'):
         assert name not in data, name
+
+
+def test_highway_stack_spread_sizes():
+    """The spread CBHG tail's workgroup count and workspace: 16 workgroups per 64-row block up
+    to 1024 rows, none beyond."""
+    lib = _lib.load()
+    assert lib.ftmi_highway_stack_spread_blocks(120) == 32
+    assert lib.ftmi_highway_stack_spread_blocks(816) == 13 * 16
+    assert lib.ftmi_highway_stack_spread_blocks(1025) == 0
+    assert lib.ftmi_highway_stack_spread_ws_bytes(120) == 2 * 32 * 4 + 2 * 2 * 2 * 64 * 272 * 2
+    assert lib.ftmi_highway_stack_spread_ws_bytes(0) == 0

@@ -460,6 +460,43 @@ def test_highway_stack_rows96_bit_identical(B, T, rng, monkeypatch):
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize('B,T,Cp,L,out', [(1, 120, 256, 4, True), (1, 816, 80, 4, True),
+                                          (1, 50, 80, 2, False), (2, 64, 256, 4, True),
+                                          (1, 1024, 80, 4, True), (3, 43, 80, 0, True)])
+def test_highway_stack_spread_bit_identical(B, T, Cp, L, out, rng, monkeypatch):
+    """The few-row CBHG tail spread over 16 workgroups per 64-row block
+    (ftmi_highway_stack_spread: c2's prenet 120 and postnet 816 rows) against the
+    one-workgroup-per-block kernel: the same per-accumulator order, bit for bit — the
+    projection, the last highway's output, ragged row blocks, no highway layers (L = 0),
+    h only (no projection) — repeatedly (the exchange counters are re-zeroed per call)."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import CBHG
+    C = 256
+    torch.manual_seed(7)
+    m = CBHG(K=2, in_channels=Cp, channels=C, proj_channels=[C, Cp], num_highways=L)
+    with torch.no_grad():
+        for hw in m.highways:
+            hw.W1.bias.normal_(0, 0.1)
+    m = m.cuda()
+    xd = dev(rng.normal(0, 1, (B, T, Cp)).astype(np.float32))
+    _, b_in, _, _, _ = m.rnn.packed_weights()
+    pre_f, hw_f, b1s, b2s, ih_f, _, n_out = m._stack_pack()
+    st = ops.status_word('cuda')
+    st.zero_()
+    args = (xd, pre_f, C, hw_f, b1s, b2s) + ((ih_f, b_in, n_out) if out else (None, None, 0))
+    assert ops.hs_spread_blocks(B * T, n_out if out else 0) == -(-B * T // 64) * 16
+    res = []
+    for sp in ('1', '1', '0'):
+        monkeypatch.setenv('FTMI_HS_SPREAD', sp)
+        y, h = ops.highway_stack(*args, want_h=True)
+        res.append((None if y is None else host(y), host(h)))
+    for r in res[:2]:
+        if out:
+            np.testing.assert_array_equal(r[0], res[2][0])
+        np.testing.assert_array_equal(r[1], res[2][1])
+    assert int(st.item()) == 0
+
+
 def test_highway_stack_range_guard(rng):
     from forwardtacotron_amd import ops
     from forwardtacotron_amd.common_layers import CBHG
