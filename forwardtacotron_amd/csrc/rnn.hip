@@ -220,7 +220,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
   constexpr bool H3 = MODE == 2;
   constexpr int G = CELL ? 4 : 3;
   constexpr int R = G * U;
-  constexpr int RB = R / 16;
+  constexpr int RB = (R + 15) / 16;  // the GRU at U = 8: 24 rows in 2 row blocks, 8 dead
   constexpr int WR = 4 / WK;
   constexpr int RBW = RB / WR;  // row blocks per wave
   constexpr int KW = H / WK;    // K range per wave
@@ -232,16 +232,16 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
   constexpr int CELLS = U * NB;
   constexpr bool HALFCELL = CELLS < 256;  // U = 8: threads 0..127 own the cells
   constexpr int CPT = HALFCELL ? 1 : CELLS / 256;
-  static_assert(R % 16 == 0 && (U % 16 == 0 || U == 8) && H % U == 0 && RB % WR == 0 &&
-                    (CELLS % 256 == 0 || CELLS == 128), "shape");
+  static_assert((R % 16 == 0 || U == 8) && (U % 16 == 0 || U == 8) && H % U == 0 &&
+                    RB % WR == 0 && (CELLS % 256 == 0 || CELLS == 128), "shape");
   static_assert(X6 ? (KW % 32 == 0) : (KB % 4 == 0), "K split");
   // CST: the compute waves store their own tagged h chunks right after the cell update (each
   // wave's 16 chunks are its own cells: CPT == 1), the comm wave only the y rows — barrier C
   // and the comm wave's stage read leave the h hand-off's critical path
   static_assert(!CST || (H3 && !LOCAL && CPT == 1 && (U == 16 || U == 8)), "compute-wave h stores");
-  static_assert(U != 8 || (CST && NBL == NB), "U = 8: the CST form, 16 live sequences");
+  static_assert(U != 8 || CST, "U = 8: the CST form");
   static_assert(NBL == NB || (NBL == 8 && !LOCAL), "live sequences per group");
-  constexpr int RR = R;                           // reduction rows
+  constexpr int RR = RB * 16;                     // reduction rows (dead ones included)
   constexpr float GSC = H3 ? H3_UNSCALE : 1.f;     // scale of the reduced W_hh h sums
 
   __shared__ __attribute__((aligned(16))) float red[WK * RR * RED_STRIDE];
@@ -392,7 +392,9 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
   bool wbad = false;
 #pragma unroll
   for (int i = 0; i < RBW; ++i) {
-    const int lrow = (wr * RBW + i) * 16 + lc;
+    const int lrow0 = (wr * RBW + i) * 16 + lc;
+    const bool rlive = lrow0 < R;  // a dead row (R % 16 != 0) multiplies zeros
+    const int lrow = rlive ? lrow0 : 0;
     const int grow = (lrow / U) * H + u0 + (lrow % U);
     const float *src = wdir + (size_t)grow * H + wk * KW;
     if constexpr (X6) {
@@ -403,6 +405,9 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
         const f32x4 b = *(const f32x4 *)(src + ks * 32 + 8 * ls + 4);
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
         v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        if (!rlive)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = 0.f;
         if constexpr (H3) {
           split2h8(v, wh[i][ks][0], wh[i][ks][1]);
 #pragma unroll
@@ -1138,12 +1143,20 @@ static int legacy_nbl(int cell, int B, int H, int mma, bool spread, int maxb) {
   return 2 * ((B + 7) / 8) * (H / 16) <= maxb ? 8 : NB;
 }
 
-// FTMI_RNN_U8=1 (read per call): the spread f16x3 LSTM on two workgroups of 8 units per CU
-// (rnn_bidir_kernel U = 8) instead of one of 16
-static bool u8_path(int cell, int H, int mma, bool spread) {
+// FTMI_RNN_U8 (bits, read per call): spread f16x3 recurrences on workgroups of 8 units
+// (rnn_bidir_kernel U = 8: half the W_hh rows and MFMAs per workgroup, two workgroups per
+// CU) instead of 16 — bit 0: the LSTM (H 512); bit 1: the GRU (H 256) with 8 live sequences
+// per group (512 workgroups); bit 2: the GRU with 16 (256 workgroups).  0 for the others.
+static int u8_bits() {
   const char *v = getenv("FTMI_RNN_U8");
-  return v && atoi(v) == 1 && spread && mma == 2 && cell == 1 && H == 512 && cst_enabled();
+  return v ? atoi(v) : 0;
 }
+static bool u8_path(int cell, int H, int mma, bool spread) {
+  if (!spread || mma != 2 || !cst_enabled()) return false;
+  const int b = u8_bits();
+  return cell == 1 ? (H == 512 && (b & 1)) : (H == 256 && (b & 6));
+}
+static int u8_nbl(int cell) { return cell == 0 && (u8_bits() & 2) ? 8 : NB; }
 
 extern "C" int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t mma) {
   if (B <= 0 || H <= 0 || H % 16 != 0) return 0;
@@ -1151,10 +1164,10 @@ extern "C" int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t m
   mma &= 0xFF;
   if (gemv_path(cell, B, H)) return (xcd_local_env() ? 8 : 2) * (H / 16);  // launch_gemv
   if (u8_path(cell, H, mma, spread)) {  // two workgroups per CU: CUs occupied
-    const int maxb = 2 * device_cu_count(), bpg = H / 8;
+    const int maxb = 2 * device_cu_count(), bpg = H / 8, nbl = u8_nbl(cell);
     const int max_groups = (maxb / bpg) & ~1;
     if (max_groups < 2) return 0;
-    const int nchunks = (B + NB - 1) / NB;
+    const int nchunks = (B + nbl - 1) / nbl;
     const int ngroups = 2 * (nchunks < max_groups / 2 ? nchunks : max_groups / 2);
     int nblk = ngroups * bpg;
     if (ngroups < 8 && 8 * bpg <= maxb) nblk = 8 * bpg;
@@ -1294,8 +1307,11 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   // the launch's real workgroup count)
   if (mma == 2 && cst_enabled() && ((cell == 1 && H == 512) || (cell == 0 && H == 256))) {
     const bool nb8 = legacy_nbl(cell, B, H, mma, spread, maxb) == 8;
-    if (cell == 1 && u8_path(cell, H, mma, spread))
-      return launch_rnn<1, 512, 8, 4, 2, true>(p, nchunks, 2 * maxb, s);
+    if (u8_path(cell, H, mma, spread)) {
+      if (cell == 1) return launch_rnn<1, 512, 8, 4, 2, true>(p, nchunks, 2 * maxb, s);
+      return u8_nbl(cell) == 8 ? launch_rnn<0, 256, 8, 4, 2, true, 8>(p, nchunks, 2 * maxb, s)
+                               : launch_rnn<0, 256, 8, 4, 2, true>(p, nchunks, 2 * maxb, s);
+    }
     if (cell == 1) return launch_rnn<1, 512, 16, 4, 2, true>(p, nchunks, maxb, s);
     return nb8 ? launch_rnn<0, 256, 16, 4, 2, true, 8>(p, nchunks, maxb, s)
                : launch_rnn<0, 256, 16, 4, 2, true>(p, nchunks, maxb, s);

@@ -697,12 +697,15 @@ F16X3_SHAPES = [('lstm', 512, 1, 23), ('lstm', 512, 17, 12), ('lstm', 512, 64, 9
 # kernel variants of rnn_bidir_kernel: the default (compute-wave h stores), the comm wave's
 # h stores (FTMI_RNN_CSTORE=0), and spread (GRU: 8 live sequences per group); H = 64 has the
 # default only
-# u8: the spread LSTM on two workgroups of 8 units per CU (FTMI_RNN_U8=1)
+# u8*: spread recurrences on workgroups of 8 units (FTMI_RNN_U8 bits: 1 the LSTM, 2 the GRU
+# H 256 with 8 live sequences per group, 4 the GRU with 16)
 ROW_VARIANTS = ['default', 'comm', 'spread']
+U8_BITS = {'u8': 1, 'u8g8': 2, 'u8g16': 4}
 F16X3_CASES = [pytest.param(*shape, v, id=f'{shape[0]}{shape[1]}-B{shape[2]}-{v}')
                for shape in F16X3_SHAPES
-               for v in (ROW_VARIANTS + ['u8'] * (shape[0] == 'lstm') if shape[1] >= 128
-                         else ['default'])]
+               for v in (ROW_VARIANTS + (['u8'] if shape[0] == 'lstm' else
+                                         ['u8g8', 'u8g16'] if shape[1] == 256 else [])
+                         if shape[1] >= 128 else ['default'])]
 
 
 @pytest.mark.parametrize('cell,H,B,T,variant', F16X3_CASES)
@@ -715,10 +718,10 @@ def test_rnn_f16x3_kernels(cell, H, B, T, variant, rng, monkeypatch):
     monkeypatch.setattr(ops, 'RNN_MMA', 2)
     monkeypatch.setenv('FTMI_RNN_GEMV', '0')
     monkeypatch.setenv('FTMI_RNN_CSTORE', '0' if variant == 'comm' else '1')
-    monkeypatch.setenv('FTMI_RNN_U8', '1' if variant == 'u8' else '0')
+    monkeypatch.setenv('FTMI_RNN_U8', str(U8_BITS.get(variant, 0)))
     fin = 512 if cell == 'lstm' else 256
     m, sd = _rnn_module(cell, fin, H, rng)
-    m.spread = variant in ('spread', 'u8')
+    m.spread = variant == 'spread' or variant in U8_BITS
     x = rng.normal(0, 1, (B, T, fin)).astype(np.float32)
     ref = (O.lstm_bidir if cell == 'lstm' else O.gru_bidir)(sd, 'r', x, np.float32)
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
