@@ -213,7 +213,13 @@ __device__ __forceinline__ void report_timeout(const RnnParams &p) {
 // workgroups (64 for H = 512) with half the W_hh rows each, and two workgroups share a CU —
 // each workgroup's step carries half the MFMAs, and the other workgroup's chain (another
 // group) fills the CU while this one waits for its h.  128 cells: waves 0-1 own them.
-template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB>
+// OB (one barrier per step; CST form): the K-split partials and the y stage are double
+// buffered by step parity, so barrier C goes — a compute wave's cell(t) reads red[t & 1]
+// after barrier B(t) and the next write of that buffer is step t + 2's, after barrier B(t + 1),
+// which every wave reaches only past its cell(t); the comm wave stores y(t - 1) after B(t)
+// (and y(T - 1) after a closing barrier).
+template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB,
+          bool OB = false>
 __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bidir_kernel(
     const RnnParams p) {
   constexpr bool X6 = MODE != 0;  // 16x16x32 fragment layout (bf16x6 and f16x3)
@@ -240,16 +246,18 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
   // and the comm wave's stage read leave the h hand-off's critical path
   static_assert(!CST || (H3 && !LOCAL && CPT == 1 && (U == 16 || U == 8)), "compute-wave h stores");
   static_assert(U != 8 || CST, "U = 8: the CST form");
+  static_assert(!OB || CST, "one barrier per step: the CST form");
+  constexpr int NPAR = OB ? 2 : 1;  // parity buffers of red / ystage
   static_assert(NBL == NB || (NBL == 8 && !LOCAL), "live sequences per group");
   constexpr int RR = RB * 16;                     // reduction rows (dead ones included)
   constexpr float GSC = H3 ? H3_UNSCALE : 1.f;     // scale of the reduced W_hh h sums
 
-  __shared__ __attribute__((aligned(16))) float red[WK * RR * RED_STRIDE];
+  __shared__ __attribute__((aligned(16))) float red[NPAR * WK * RR * RED_STRIDE];
   __shared__ __attribute__((aligned(16))) float hloc[LOCAL ? 2 * 16 * H : 4];
   // multi-workgroup groups: the new h slice and y values of this workgroup, handed from the
   // compute waves to the comm wave (cell c = seq * U + unit; float4 f = 4 units)
   __shared__ __attribute__((aligned(16))) float hstage[LOCAL ? 4 : CELLS];
-  __shared__ __attribute__((aligned(16))) float ystage[LOCAL ? 4 : CELLS];
+  __shared__ __attribute__((aligned(16))) float ystage[LOCAL ? 4 : NPAR * CELLS];
   __shared__ int s_abort, s_group, s_bi, s_mode;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -354,6 +362,25 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
         }
       }
       __syncthreads();  // the compute waves' set-up barrier
+      if constexpr (OB) {
+        auto store_y = [&](int t) {  // y(t) from its parity buffer
+          const int tt = dir ? (p.T - 1 - t) : t;
+          const float *ys = ystage + (t & 1) * CELLS;
+#pragma unroll
+          for (int i = 0; i < FPL; ++i) {
+            const f32x4 v = *(const f32x4 *)&ys[((lane + 64 * i) % F4) * 4];
+            if (ok[i]) *(f32x4 *)(p.y + ((size_t)yb[i] * p.T + tt) * p.y_stride + dir * H + k0s[i]) = v;
+          }
+        };
+        for (int t = 0; t < p.T; ++t) {
+          __syncthreads();  // B(t): every cell(t - 1) is done
+          if (s_abort) break;
+          if (t > 0) store_y(t - 1);
+        }
+        __syncthreads();  // closing barrier: cell(T - 1) is done
+        if (!s_abort) store_y(p.T - 1);
+        return;
+      }
       for (int t = 0; t < p.T; ++t) {
         const int tt = dir ? (p.T - 1 - t) : t;
         __syncthreads();  // B
@@ -533,6 +560,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
   auto step = [&](int t, const float (&gx)[CPT][G], float (&gnext)[CPT][G],
                   const int (&inext)[CPT], int (&iload)[CPT]) -> bool {
     const int tt = frame(t);
+    const int rpar = OB ? (t & 1) * WK * RR * RED_STRIDE : 0;  // red parity buffer
     STAMP(0);
     // h_{t-1} operand: NL float4 per lane (fragment order), zero at t = 0.  f16x3 groups of
     // several workgroups exchange h pre-split: hr[2 ks] = 8 heads, hr[2 ks + 1] = 8 scaled
@@ -680,7 +708,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
     for (int i = 0; i < RBW; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        red[(wk * RR + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] = acc[i][e];
+        red[rpar + (wk * RR + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] = acc[i][e];
     __syncthreads();
     if (!LOCAL && s_abort) return false;  // a wave timed out acquiring h_{t-1}
     STAMP(3);
@@ -694,9 +722,9 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int row = g * U + cu[j];
-        float sum = red[row * RED_STRIDE + bl];
+        float sum = red[rpar + row * RED_STRIDE + bl];
 #pragma unroll
-        for (int w = 1; w < WK; ++w) sum += red[(w * RR + row) * RED_STRIDE + bl];
+        for (int w = 1; w < WK; ++w) sum += red[rpar + (w * RR + row) * RED_STRIDE + bl];
         gs[g] = sum;  // H3: 2^11 (W_hh h)
         gi[g] = gx[j][g];
       }
@@ -756,7 +784,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
       } else {  // to the comm wave: cell c = bl * U + unit is also its float4 order
         const int c = bl * U + cu[j];
         if constexpr (!HSPLIT) hstage[c] = hn;
-        ystage[c] = yout;
+        ystage[(OB ? (t & 1) * CELLS : 0) + c] = yout;
       }
     }
     if constexpr (CST) {
@@ -774,7 +802,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
       }
     }
     STAMP(4);
-    __syncthreads();  // LOCAL: h_t visible in LDS; else: staged for the comm wave
+    if constexpr (!OB) __syncthreads();  // LOCAL: h_t visible in LDS; else: staged for the comm wave
     STAMP(5);
     return true;
   };
@@ -784,6 +812,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
     if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1)) break;
     if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2)) break;
   }
+  if constexpr (OB) __syncthreads();  // the comm wave's closing barrier
 #ifdef FTMI_RNN_STAMPS
   if (tid == 0)
     for (int i = 0; i < 6; ++i) ftmi_rnn_stamps[blockIdx.x * 8 + i] = st_acc[i];
@@ -1049,7 +1078,8 @@ int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
   return FTMI_OK;
 }
 
-template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB>
+template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB,
+          bool OB = false>
 int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
   if (NBL != NB) {  // chunks of NBL sequences (the caller counted chunks of NB)
     nchunks = (p.B + NBL - 1) / NBL;
@@ -1076,7 +1106,7 @@ int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
     int nblk = p.ngroups * BPG;
     if (BPG > 1 && pad_env && p.xcd_local && p.ngroups < 8 && 8 * BPG <= max_blocks)
       nblk = 8 * BPG;
-    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, CST, NBL>), dim3(nblk),
+    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, CST, NBL, OB>), dim3(nblk),
                        dim3(BPG == 1 ? 256 : 320), 0, s, p);
     FTMI_CHECK_LAUNCH();
   }
@@ -1307,14 +1337,21 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   // the launch's real workgroup count)
   if (mma == 2 && cst_enabled() && ((cell == 1 && H == 512) || (cell == 0 && H == 256))) {
     const bool nb8 = legacy_nbl(cell, B, H, mma, spread, maxb) == 8;
+    // FTMI_RNN_ONEBAR=1 (read per call): one barrier per step (rnn_bidir_kernel OB)
+    const char *ob = getenv("FTMI_RNN_ONEBAR");
+    const bool one = ob && atoi(ob) == 1;
+#define FTMI_CST(CELL_, H_, U_, NBL_, MB_)                                                   \
+  return one ? launch_rnn<CELL_, H_, U_, 4, 2, true, NBL_, true>(p, nchunks, MB_, s)         \
+             : launch_rnn<CELL_, H_, U_, 4, 2, true, NBL_>(p, nchunks, MB_, s);
     if (u8_path(cell, H, mma, spread)) {
-      if (cell == 1) return launch_rnn<1, 512, 8, 4, 2, true>(p, nchunks, 2 * maxb, s);
-      return u8_nbl(cell) == 8 ? launch_rnn<0, 256, 8, 4, 2, true, 8>(p, nchunks, 2 * maxb, s)
-                               : launch_rnn<0, 256, 8, 4, 2, true>(p, nchunks, 2 * maxb, s);
+      if (cell == 1) FTMI_CST(1, 512, 8, NB, 2 * maxb)
+      if (u8_nbl(cell) == 8) FTMI_CST(0, 256, 8, 8, 2 * maxb)
+      FTMI_CST(0, 256, 8, NB, 2 * maxb)
     }
-    if (cell == 1) return launch_rnn<1, 512, 16, 4, 2, true>(p, nchunks, maxb, s);
-    return nb8 ? launch_rnn<0, 256, 16, 4, 2, true, 8>(p, nchunks, maxb, s)
-               : launch_rnn<0, 256, 16, 4, 2, true>(p, nchunks, maxb, s);
+    if (cell == 1) FTMI_CST(1, 512, 16, NB, maxb)
+    if (nb8) FTMI_CST(0, 256, 16, 8, maxb)
+    FTMI_CST(0, 256, 16, NB, maxb)
+#undef FTMI_CST
   }
   if (cell == 0 && H == 256) FTMI_RNN_MODES(0, 256, 16, 4, 4)
   if (cell == 1 && H == 512) FTMI_RNN_MODES(1, 512, 16, 4, 4)
