@@ -209,18 +209,13 @@ __device__ __forceinline__ void report_timeout(const RnnParams &p) {
 // NBL: live sequences per group (16, or 8 to spread a recurrence over twice the groups: every
 // workgroup then acquires and stores half the h bytes per step; the MFMA columns past NBL are
 // dead)
-// U = 8 (the LSTM, f16x3, CST; "two chains per CU"): a group spreads over twice the
-// workgroups (64 for H = 512) with half the W_hh rows each, and two workgroups share a CU —
-// each workgroup's step carries half the MFMAs, and the other workgroup's chain (another
-// group) fills the CU while this one waits for its h.  128 cells: waves 0-1 own them.
-// OB (one barrier per step; CST form): the K-split partials and the y stage are double
-// buffered by step parity, so barrier C goes — a compute wave's cell(t) reads red[t & 1]
-// after barrier B(t) and the next write of that buffer is step t + 2's, after barrier B(t + 1),
-// which every wave reaches only past its cell(t); the comm wave stores y(t - 1) after B(t)
-// (and y(T - 1) after a closing barrier).
-template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB,
-          bool OB = false>
-__global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bidir_kernel(
+// U = 8 (the spread postnet GRU, H = 256, f16x3, CST): a group of 16 live sequences spreads
+// over 32 workgroups of 8 units (24 W_hh rows in 2 row blocks, 8 dead): the same 256
+// workgroups at B = 64 as 16 units with 8 live sequences (legacy_nbl), with two thirds of
+// the MFMAs per wave and 128 cells per workgroup (waves 0-1 own them).  Measured at B = 64,
+// T = 1368: 1.11-1.12 against 1.39 us/step (tools/rnn_diag.py, profiles/r5_rnn_diag.txt).
+template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB>
+__global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(
     const RnnParams p) {
   constexpr bool X6 = MODE != 0;  // 16x16x32 fragment layout (bf16x6 and f16x3)
   constexpr bool H3 = MODE == 2;
@@ -245,19 +240,17 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
   // wave's 16 chunks are its own cells: CPT == 1), the comm wave only the y rows — barrier C
   // and the comm wave's stage read leave the h hand-off's critical path
   static_assert(!CST || (H3 && !LOCAL && CPT == 1 && (U == 16 || U == 8)), "compute-wave h stores");
-  static_assert(U != 8 || CST, "U = 8: the CST form");
-  static_assert(!OB || CST, "one barrier per step: the CST form");
-  constexpr int NPAR = OB ? 2 : 1;  // parity buffers of red / ystage
+  static_assert(U != 8 || (CST && CELL == 0 && NBL == NB), "U = 8: the spread GRU's CST form");
   static_assert(NBL == NB || (NBL == 8 && !LOCAL), "live sequences per group");
   constexpr int RR = RB * 16;                     // reduction rows (dead ones included)
   constexpr float GSC = H3 ? H3_UNSCALE : 1.f;     // scale of the reduced W_hh h sums
 
-  __shared__ __attribute__((aligned(16))) float red[NPAR * WK * RR * RED_STRIDE];
+  __shared__ __attribute__((aligned(16))) float red[WK * RR * RED_STRIDE];
   __shared__ __attribute__((aligned(16))) float hloc[LOCAL ? 2 * 16 * H : 4];
   // multi-workgroup groups: the new h slice and y values of this workgroup, handed from the
   // compute waves to the comm wave (cell c = seq * U + unit; float4 f = 4 units)
   __shared__ __attribute__((aligned(16))) float hstage[LOCAL ? 4 : CELLS];
-  __shared__ __attribute__((aligned(16))) float ystage[LOCAL ? 4 : NPAR * CELLS];
+  __shared__ __attribute__((aligned(16))) float ystage[LOCAL ? 4 : CELLS];
   __shared__ int s_abort, s_group, s_bi, s_mode;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -362,25 +355,6 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
         }
       }
       __syncthreads();  // the compute waves' set-up barrier
-      if constexpr (OB) {
-        auto store_y = [&](int t) {  // y(t) from its parity buffer
-          const int tt = dir ? (p.T - 1 - t) : t;
-          const float *ys = ystage + (t & 1) * CELLS;
-#pragma unroll
-          for (int i = 0; i < FPL; ++i) {
-            const f32x4 v = *(const f32x4 *)&ys[((lane + 64 * i) % F4) * 4];
-            if (ok[i]) *(f32x4 *)(p.y + ((size_t)yb[i] * p.T + tt) * p.y_stride + dir * H + k0s[i]) = v;
-          }
-        };
-        for (int t = 0; t < p.T; ++t) {
-          __syncthreads();  // B(t): every cell(t - 1) is done
-          if (s_abort) break;
-          if (t > 0) store_y(t - 1);
-        }
-        __syncthreads();  // closing barrier: cell(T - 1) is done
-        if (!s_abort) store_y(p.T - 1);
-        return;
-      }
       for (int t = 0; t < p.T; ++t) {
         const int tt = dir ? (p.T - 1 - t) : t;
         __syncthreads();  // B
@@ -560,7 +534,6 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
   auto step = [&](int t, const float (&gx)[CPT][G], float (&gnext)[CPT][G],
                   const int (&inext)[CPT], int (&iload)[CPT]) -> bool {
     const int tt = frame(t);
-    const int rpar = OB ? (t & 1) * WK * RR * RED_STRIDE : 0;  // red parity buffer
     STAMP(0);
     // h_{t-1} operand: NL float4 per lane (fragment order), zero at t = 0.  f16x3 groups of
     // several workgroups exchange h pre-split: hr[2 ks] = 8 heads, hr[2 ks + 1] = 8 scaled
@@ -600,6 +573,10 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
       const bool want1 = h_tag(t - 1) != 0u;  // uniform
       const bool hlive = (lane & 15) < NBL;  // this lane's h column is a live sequence
       for (unsigned spins = 0;; ++spins) {
+        // a compiler memory barrier: the loop stores nothing, so without it LICM hoists the
+        // loads out and the loop spins on the first values (it did once the timing switches
+        // left the product build)
+        asm volatile("" ::: "memory");
 #pragma unroll
         for (int i = 0; i < NL; ++i)
           if ((NBL == NB || hlive) && !((RNN_DIAG(p) & 64) && i >= NL / 4))  // 64: a quarter
@@ -708,7 +685,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
     for (int i = 0; i < RBW; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        red[rpar + (wk * RR + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] = acc[i][e];
+        red[(wk * RR + (wr * RBW + i) * 16 + ls * 4 + e) * RED_STRIDE + lc] = acc[i][e];
     __syncthreads();
     if (!LOCAL && s_abort) return false;  // a wave timed out acquiring h_{t-1}
     STAMP(3);
@@ -722,9 +699,9 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int row = g * U + cu[j];
-        float sum = red[rpar + row * RED_STRIDE + bl];
+        float sum = red[row * RED_STRIDE + bl];
 #pragma unroll
-        for (int w = 1; w < WK; ++w) sum += red[rpar + (w * RR + row) * RED_STRIDE + bl];
+        for (int w = 1; w < WK; ++w) sum += red[(w * RR + row) * RED_STRIDE + bl];
         gs[g] = sum;  // H3: 2^11 (W_hh h)
         gi[g] = gx[j][g];
       }
@@ -784,7 +761,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
       } else {  // to the comm wave: cell c = bl * U + unit is also its float4 order
         const int c = bl * U + cu[j];
         if constexpr (!HSPLIT) hstage[c] = hn;
-        ystage[(OB ? (t & 1) * CELLS : 0) + c] = yout;
+        ystage[c] = yout;
       }
     }
     if constexpr (CST) {
@@ -802,7 +779,7 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
       }
     }
     STAMP(4);
-    if constexpr (!OB) __syncthreads();  // LOCAL: h_t visible in LDS; else: staged for the comm wave
+    __syncthreads();  // LOCAL: h_t visible in LDS; else: staged for the comm wave
     STAMP(5);
     return true;
   };
@@ -812,7 +789,6 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, U == 8 ? 3 : 1) void rnn_bi
     if (t + 1 >= p.T || !step(t + 1, g1, g0, i0, i1)) break;
     if (t + 2 >= p.T || !step(t + 2, g2, g1, i1, i2)) break;
   }
-  if constexpr (OB) __syncthreads();  // the comm wave's closing barrier
 #ifdef FTMI_RNN_STAMPS
   if (tid == 0)
     for (int i = 0; i < 6; ++i) ftmi_rnn_stamps[blockIdx.x * 8 + i] = st_acc[i];
@@ -948,6 +924,7 @@ __global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * GV_KSEG) void rnn_gem
         const unsigned off = (unsigned)(((dir * NBV + b) * H + k) * 4);
         const int soff = ((t - 1) & 1) * par_bytes;
         for (unsigned spins = 0;; ++spins) {
+          asm volatile("" ::: "memory");  // keep the load in the loop (see rnn_bidir_kernel)
           typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
           const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, soff, 16);
           const bool fresh = want ? ((r.x & r.y & r.z & r.w) & 1u) != 0u
@@ -1078,8 +1055,7 @@ int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
   return FTMI_OK;
 }
 
-template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB,
-          bool OB = false>
+template <int CELL, int H, int U, int WK, int MODE, bool CST = false, int NBL = NB>
 int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
   if (NBL != NB) {  // chunks of NBL sequences (the caller counted chunks of NB)
     nchunks = (p.B + NBL - 1) / NBL;
@@ -1106,7 +1082,7 @@ int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
     int nblk = p.ngroups * BPG;
     if (BPG > 1 && pad_env && p.xcd_local && p.ngroups < 8 && 8 * BPG <= max_blocks)
       nblk = 8 * BPG;
-    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, CST, NBL, OB>), dim3(nblk),
+    hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, CST, NBL>), dim3(nblk),
                        dim3(BPG == 1 ? 256 : 320), 0, s, p);
     FTMI_CHECK_LAUNCH();
   }
@@ -1173,35 +1149,30 @@ static int legacy_nbl(int cell, int B, int H, int mma, bool spread, int maxb) {
   return 2 * ((B + 7) / 8) * (H / 16) <= maxb ? 8 : NB;
 }
 
-// FTMI_RNN_U8 (bits, read per call): spread f16x3 recurrences on workgroups of 8 units
-// (rnn_bidir_kernel U = 8: half the W_hh rows and MFMAs per workgroup, two workgroups per
-// CU) instead of 16 — bit 0: the LSTM (H 512); bit 1: the GRU (H 256) with 8 live sequences
-// per group (512 workgroups); bit 2: the GRU with 16 (256 workgroups).  0 for the others.
-static int u8_bits() {
+// The spread postnet GRU (H 256, f16x3, CST) on workgroups of 8 units (rnn_bidir_kernel
+// U = 8) while every group's workgroups fit one per CU (B <= 64 on 256 CUs: 8 groups x 32);
+// FTMI_RNN_U8=0 (read per call: tests switch it) keeps 16 units.  Rejected this round and
+// removed: U = 8 for the LSTM (64 workgroups per group, two per CU — both of the same group
+// under the census layout, so no MFMA time is saved, and five-wave workgroups at 150 VGPRs
+// were not reliably co-resident two per CU: the census timed out), the GRU at U = 8 with 8
+// live sequences (1.48 against 1.39 us/step) and one barrier per step (parity-buffered
+// partials: LSTM 1.59 against 1.53, GRU at U = 8 1.18 against 1.11).
+static bool u8_path(int cell, int B, int H, int mma, bool spread, int maxb) {
+  if (!spread || mma != 2 || !cst_enabled() || cell != 0 || H != 256) return false;
   const char *v = getenv("FTMI_RNN_U8");
-  return v ? atoi(v) : 0;
+  if (v && atoi(v) == 0) return false;
+  const int ngroups = 2 * ((B + NB - 1) / NB);
+  return (ngroups < 8 ? 8 : ngroups) * (H / 8) <= maxb;
 }
-static bool u8_path(int cell, int H, int mma, bool spread) {
-  if (!spread || mma != 2 || !cst_enabled()) return false;
-  const int b = u8_bits();
-  return cell == 1 ? (H == 512 && (b & 1)) : (H == 256 && (b & 6));
-}
-static int u8_nbl(int cell) { return cell == 0 && (u8_bits() & 2) ? 8 : NB; }
 
 extern "C" int32_t ftmi_rnn_blocks(int32_t cell, int32_t B, int32_t H, int32_t mma) {
   if (B <= 0 || H <= 0 || H % 16 != 0) return 0;
   const bool spread = (mma & FTMI_RNN_SPREAD) != 0;
   mma &= 0xFF;
   if (gemv_path(cell, B, H)) return (xcd_local_env() ? 8 : 2) * (H / 16);  // launch_gemv
-  if (u8_path(cell, H, mma, spread)) {  // two workgroups per CU: CUs occupied
-    const int maxb = 2 * device_cu_count(), bpg = H / 8, nbl = u8_nbl(cell);
-    const int max_groups = (maxb / bpg) & ~1;
-    if (max_groups < 2) return 0;
-    const int nchunks = (B + nbl - 1) / nbl;
-    const int ngroups = 2 * (nchunks < max_groups / 2 ? nchunks : max_groups / 2);
-    int nblk = ngroups * bpg;
-    if (ngroups < 8 && 8 * bpg <= maxb) nblk = 8 * bpg;
-    return (nblk + 1) / 2;
+  if (u8_path(cell, B, H, mma, spread, device_cu_count())) {  // launch_rnn U = 8: one group
+    const int ngroups = 2 * ((B + NB - 1) / NB);                // pass, padded to 8 groups
+    return (ngroups < 8 && xcd_local_env() ? 8 : ngroups) * (H / 8);
   }
   const int bpg = H / rnn_units(cell, H, mma);
   const int maxb = device_cu_count();
@@ -1337,21 +1308,10 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   // the launch's real workgroup count)
   if (mma == 2 && cst_enabled() && ((cell == 1 && H == 512) || (cell == 0 && H == 256))) {
     const bool nb8 = legacy_nbl(cell, B, H, mma, spread, maxb) == 8;
-    // FTMI_RNN_ONEBAR=1 (read per call): one barrier per step (rnn_bidir_kernel OB)
-    const char *ob = getenv("FTMI_RNN_ONEBAR");
-    const bool one = ob && atoi(ob) == 1;
-#define FTMI_CST(CELL_, H_, U_, NBL_, MB_)                                                   \
-  return one ? launch_rnn<CELL_, H_, U_, 4, 2, true, NBL_, true>(p, nchunks, MB_, s)         \
-             : launch_rnn<CELL_, H_, U_, 4, 2, true, NBL_>(p, nchunks, MB_, s);
-    if (u8_path(cell, H, mma, spread)) {
-      if (cell == 1) FTMI_CST(1, 512, 8, NB, 2 * maxb)
-      if (u8_nbl(cell) == 8) FTMI_CST(0, 256, 8, 8, 2 * maxb)
-      FTMI_CST(0, 256, 8, NB, 2 * maxb)
-    }
-    if (cell == 1) FTMI_CST(1, 512, 16, NB, maxb)
-    if (nb8) FTMI_CST(0, 256, 16, 8, maxb)
-    FTMI_CST(0, 256, 16, NB, maxb)
-#undef FTMI_CST
+    if (u8_path(cell, B, H, mma, spread, maxb)) return launch_rnn<0, 256, 8, 4, 2, true>(p, nchunks, maxb, s);
+    if (cell == 1) return launch_rnn<1, 512, 16, 4, 2, true>(p, nchunks, maxb, s);
+    return nb8 ? launch_rnn<0, 256, 16, 4, 2, true, 8>(p, nchunks, maxb, s)
+               : launch_rnn<0, 256, 16, 4, 2, true>(p, nchunks, maxb, s);
   }
   if (cell == 0 && H == 256) FTMI_RNN_MODES(0, 256, 16, 4, 4)
   if (cell == 1 && H == 512) FTMI_RNN_MODES(1, 512, 16, 4, 4)

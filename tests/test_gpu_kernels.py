@@ -695,19 +695,14 @@ F16X3_SHAPES = [('lstm', 512, 1, 23), ('lstm', 512, 17, 12), ('lstm', 512, 64, 9
                 ('gru', 256, 1, 31), ('gru', 256, 64, 7), ('gru', 256, 130, 5),
                 ('gru', 128, 20, 14), ('gru', 64, 64, 11), ('gru', 64, 1, 40)]
 # kernel variants of rnn_bidir_kernel: the default (compute-wave h stores), the comm wave's
-# h stores (FTMI_RNN_CSTORE=0), and spread (GRU: 8 live sequences per group); H = 64 has the
-# default only
-# u8*: spread recurrences on workgroups of 8 units (FTMI_RNN_U8 bits: 1 the LSTM, 2 the GRU
-# H 256 with 8 live sequences per group, 4 the GRU with 16)
+# h stores (FTMI_RNN_CSTORE=0), and spread (the GRU H 256: 8 units per workgroup while the
+# groups fit one workgroup per CU, spread-u16 the 16-unit form with 8 live sequences per
+# group); H = 64 has the default only
 ROW_VARIANTS = ['default', 'comm', 'spread']
-U8_BITS = {'u8': 1, 'u8g8': 2, 'u8g16': 4}
-# +ob: one barrier per step (FTMI_RNN_ONEBAR=1, the compute-wave-store forms)
 F16X3_CASES = [pytest.param(*shape, v, id=f'{shape[0]}{shape[1]}-B{shape[2]}-{v}')
                for shape in F16X3_SHAPES
-               for v0 in (ROW_VARIANTS + (['u8'] if shape[0] == 'lstm' else
-                                          ['u8g8', 'u8g16'] if shape[1] == 256 else [])
-                          if shape[1] >= 128 else ['default'])
-               for v in ([v0, v0 + '+ob'] if v0 != 'comm' and shape[1] >= 256 else [v0])]
+               for v in ((ROW_VARIANTS + (['spread-u16'] if shape[1] == 256 else []))
+                         if shape[1] >= 128 else ['default'])]
 
 
 @pytest.mark.parametrize('cell,H,B,T,variant', F16X3_CASES)
@@ -720,12 +715,10 @@ def test_rnn_f16x3_kernels(cell, H, B, T, variant, rng, monkeypatch):
     monkeypatch.setattr(ops, 'RNN_MMA', 2)
     monkeypatch.setenv('FTMI_RNN_GEMV', '0')
     monkeypatch.setenv('FTMI_RNN_CSTORE', '0' if variant == 'comm' else '1')
-    monkeypatch.setenv('FTMI_RNN_ONEBAR', '1' if variant.endswith('+ob') else '0')
-    variant = variant.split('+')[0]
-    monkeypatch.setenv('FTMI_RNN_U8', str(U8_BITS.get(variant, 0)))
+    monkeypatch.setenv('FTMI_RNN_U8', '0' if variant == 'spread-u16' else '1')
     fin = 512 if cell == 'lstm' else 256
     m, sd = _rnn_module(cell, fin, H, rng)
-    m.spread = variant == 'spread' or variant in U8_BITS
+    m.spread = variant.startswith('spread')
     x = rng.normal(0, 1, (B, T, fin)).astype(np.float32)
     ref = (O.lstm_bidir if cell == 'lstm' else O.gru_bidir)(sd, 'r', x, np.float32)
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
@@ -763,19 +756,14 @@ def test_rnn_f16_weight_range_guard(rng, monkeypatch):
     assert int(st.item()) & 2
 
 
-@pytest.mark.parametrize('B,variant', [(2, 'gemv'), (9, 'default'), (9, 'spread'), (9, 'u8'),
-                                       (40, 'u8'), (40, 'u8+ob'), (9, 'spread+ob')])
+@pytest.mark.parametrize('B,variant', [(2, 'gemv'), (9, 'default'), (9, 'spread'), (40, 'spread')])
 def test_lstm_through_lr_index_and_lengths(B, variant, rng, monkeypatch):
     """LSTM reading phoneme-rate projections through the LR index map == LSTM over the
     expanded sequence; with lengths it reproduces pack_padded / pad_packed semantics (B = 2:
-    the GEMV kernel; B = 9: the MFMA kernel, compact and spread; u8: two workgroups of 8
-    units per CU)."""
+    the GEMV kernel; B = 9 / 40: the MFMA kernel, compact and spread)."""
     from forwardtacotron_amd import ops
-    monkeypatch.setenv('FTMI_RNN_ONEBAR', '1' if variant.endswith('+ob') else '0')
-    variant = variant.split('+')[0]
-    monkeypatch.setenv('FTMI_RNN_U8', '1' if variant == 'u8' else '0')
     m, sd = _rnn_module('lstm', 512, 512, rng)
-    m.spread = variant in ('spread', 'u8')
+    m.spread = variant == 'spread'
     T = 11
     x = rng.normal(0, 1, (B, T, 512)).astype(np.float32)
     dur = rng.uniform(-0.5, 5.0, (B, T)).astype(np.float32)
