@@ -81,12 +81,12 @@ PEAK_X3_TFLOPS = PEAK_BF16_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 
-PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r4_pmc_traffic.json')        # c3
-PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r4c2_pmc_traffic.json')   # c2 (--config c2)
-PMC_PROFILE_C5 = os.path.join(ROOT, 'profiles', 'r4c5_pmc_traffic.json')   # c5 (--model fast_pitch)
+PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r5_pmc_traffic.json')        # c3
+PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r5c2_pmc_traffic.json')   # c2 (--config c2)
+PMC_PROFILE_C5 = os.path.join(ROOT, 'profiles', 'r5c5_pmc_traffic.json')   # c5 (--model fast_pitch)
 # the PMC files are a prior run of the same workload (separate FETCH_SIZE / WRITE_SIZE passes
 # cannot share the timed run), taken on this tree
-PMC_TREE = 'cf0df58 (round 4, tools/gpu_r4_measure.sh pmc)'
+PMC_TREE = 'ce09a8d (round 5, tools/gpu_r5_measure.sh pmc)'
 
 
 def rocprof_name(label: str):
@@ -142,6 +142,38 @@ def pmc_traffic_slab(label: str, path: str):
             'read_bytes_corrected': v['read_bytes_corrected'], 'write_bytes': v['write_bytes'],
             'kernel_grid': k, 'source': os.path.relpath(path, ROOT), 'measured_on_tree': PMC_TREE,
             'note': 'a prior PMC run of this workload, not this run'}
+
+
+PMC_MFMA = os.path.join(ROOT, 'profiles', 'r5_pmc_mfma.json')  # tools/pmc_mfma.py
+
+
+def pmc_mfma(label: str, cfg: str):
+    """MFMA-busy share of the dominant kernel from the committed SQ_VALU_MFMA_BUSY_CYCLES /
+    GRBM_GUI_ACTIVE pass of the same workload (tools/gpu_r5_measure.sh mfma), or None."""
+    if not os.path.exists(PMC_MFMA):
+        return None
+    ks = json.load(open(PMC_MFMA)).get('configs', {}).get(cfg, {}).get('kernels', {})
+    pref = rocprof_name(label)
+    if pref is not None:
+        hit = [(k, v) for k, v in ks.items() if k.startswith(pref)]
+    elif label.startswith('conv1d['):
+        f = dict(kv.split('=') for kv in label[7:-1].split(',') if '=' in kv)
+        M, N = int(f['M']), int(f['N'])
+        mt = -(-M // 256)
+        nblk = (mt if mt < 8 else -(-mt // 8) * 8) * -(-N // 128)
+        hit = [(k, v) for k, v in ks.items() if k.startswith('conv_gemm_slab')
+               and int(k.rsplit('|', 1)[1]) in (nblk * 768, nblk * 512)]
+    else:
+        return None
+    if len(hit) != 1 or 'mfma_busy' not in hit[0][1]:
+        return None
+    k, v = hit[0]
+    return {'mfma_busy': v['mfma_busy'], 'kernel_grid': k,
+            'definition': 'SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs): '
+                          'the share of the dispatch\'s active cycles an average SIMD\'s matrix '
+                          'pipe was busy (16 cycles per v_mfma_f32_16x16x32_f16)',
+            'source': os.path.relpath(PMC_MFMA, ROOT),
+            'note': 'a separate --pmc run of this workload on this round\'s tree, not this run'}
 
 
 def time_prenet_bank(model, x, reps: int = 20):
@@ -336,9 +368,13 @@ def main():
         from forwardtacotron_amd.host_io import PinnedD2H
         d2h = PinnedD2H(dev)
         x_pin = x_host.pin_memory()
-        o = gen(x_pin.to(dev, non_blocking=True))  # the pinned ring's buffers, untimed
-        if o is not None:
-            d2h.submit(o['mel_post'])
+        # every slot of the pinned ring allocated untimed: a slot's first submit page-locks a
+        # fresh 28 MB host buffer (c3), ~8 ms — inside the timed loop that one allocation was
+        # the 5.5 % (20 steps) vs 17 % (5 steps) spread of this figure in round 4
+        for _ in range(d2h.depth):
+            o = gen(x_pin.to(dev, non_blocking=True))
+            if o is not None:
+                d2h.submit(o['mel_post'])
         d2h.synchronize()
         barrier()
         h0 = time.perf_counter()
@@ -487,6 +523,12 @@ def main():
             if tr is not None:
                 roof['traffic'] = tr['bytes_per_launch']
                 roof['traffic_detail'] = tr
+            cfg = {(64, 50, 200): 'c3', (1, 120, 120): 'c2'}.get(shape) if args.model == 'forward_tacotron' \
+                else ('c5' if shape == (64, 50, 200) else None)
+            mb = pmc_mfma(dom_label, cfg) if cfg and world == 1 else None
+            if mb is not None:
+                roof['mfma_busy'] = mb['mfma_busy']
+                roof['mfma_busy_detail'] = mb
         else:
             achieved = dom['bytes'] / s / 1e9
             roof = {'kernel': dom_label, 'bound': 'hbm', 'achieved': round(achieved, 1),

@@ -10,7 +10,8 @@ the share of the dispatch's active cycles in which an average SIMD's matrix pipe
 SQ_VALU_MFMA_BUSY_CYCLES counts cycles, 16 per v_mfma_f32_16x16x32_f16: § Per-instruction
 cycle constants), and the clock the dispatch ran at, GRBM_GUI_ACTIVE / 8 / duration, where
 the kernel trace of the same run gives the duration.
-usage: python tools/pmc_mfma.py DIR OUT.json [label=name-prefix ...]"""
+usage: python tools/pmc_mfma.py OUT.json CONFIG=DIR [CONFIG=DIR ...]
+(the named kernels of each config: NAMED below, kernel-name prefix [| grid])"""
 import csv
 import glob
 import json
@@ -50,25 +51,53 @@ def load(src):
     return out
 
 
+# the kernels the north star names, per bench config (prefix of "name|grid" keys)
+NAMED = {
+    'c3': {'decoder_lstm': 'rnn_bidir_kernel<1, 512,',
+           'postnet_gru': 'rnn_bidir_kernel<0, 256, 8,',
+           'prenet_gru': 'rnn_bidir_kernel<0, 256, 16,',
+           'prenet_bank': 'conv_gemm_slab_kernel<0, false, true>|1376256',
+           'postnet_bank': 'conv_gemm_slab_kernel<0, false, true>|4227072',
+           'postnet_proj1': 'conv_gemm_slab_kernel<0, false, true>|528384',
+           'postnet_highway_stack': 'highway_stack_kernel<96>',
+           'prenet_highway_stack': 'highway_stack_kernel<64>',
+           'lstm_input_projection': 'conv_gemm_slabp_kernel<0>|917504'},
+    'c2': {'decoder_lstm': 'rnn_gemv_kernel<1, 512,', 'postnet_gru': 'rnn_gemv_kernel<0, 256,',
+           'prenet_bank': 'conv_bank_halves_kernel',
+           'postnet_highway_stack': 'highway_spread_kernel<3>|106496',
+           'prenet_highway_stack': 'highway_spread_kernel<3>|16384'},
+    'c5': {'ffn_conv_k9': 'conv_gemm_slab_kernel<0, false, true>|2162688',
+           'attention': 'attention_t3_kernel<128, true>',
+           'postnet_conv': 'conv_gemm_slab_kernel<0, false, true>|344064'},
+}
+KEEP = ('mfma_busy', 'SQ_VALU_MFMA_BUSY_CYCLES', 'SQ_BUSY_CYCLES', 'GRBM_GUI_ACTIVE', 'dispatches',
+        'sq_wait_any_share', 'sq_active_inst_any_share')
+
+
+def short_key(k):  # the attention kernel's name stays mangled in the counter CSV
+    if k.startswith('_ZN12_GLOBAL__N_119attention_t3_kernelILi128ELb1E'):
+        return 'attention_t3_kernel<128, true>' + k[k.index('|'):]
+    return k
+
+
 def main():
-    src, dst = sys.argv[1], sys.argv[2]
-    labels = dict(a.split('=', 1) for a in sys.argv[3:])
-    ks = load(src)
-    doc = {'what': __doc__.split('\n\n')[0], 'source_dir': src, 'kernels': ks}
-    if labels:  # friendly names: the heaviest dispatch group whose key starts with the prefix
+    dst = sys.argv[1]
+    doc = {'what': __doc__.split('\n\n')[0], 'configs': {}}
+    for arg in sys.argv[2:]:
+        cfg, src = arg.split('=', 1)
+        ks = load(src)
         named = {}
-        for name, pref in labels.items():
-            hit = [(k, v) for k, v in ks.items() if k.startswith(pref)]
+        for name, pref in NAMED.get(cfg, {}).items():
+            hit = [(k, v) for k, v in ks.items() if short_key(k).startswith(pref)]
             if hit:
                 k, v = max(hit, key=lambda kv: kv[1].get('GRBM_GUI_ACTIVE', 0))
-                named[name] = {'kernel': k, **{c: v[c] for c in v if c in (
-                    'mfma_busy', 'SQ_VALU_MFMA_BUSY_CYCLES', 'GRBM_GUI_ACTIVE', 'dispatches',
-                    'sq_wait_any_share', 'sq_active_inst_any_share')}}
-        doc['named'] = named
+                named[name] = {'kernel': k, **{c: v[c] for c in v if c in KEEP}}
+        doc['configs'][cfg] = {'source_dir': src, 'named': named, 'kernels': ks}
+        print(f'== {cfg}')
+        for name, v in named.items():
+            print(f'  {name:24s} busy {v.get("mfma_busy", float("nan")):6.3f}  {v["kernel"][:80]}')
     os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
     json.dump(doc, open(dst, 'w'), indent=1, sort_keys=True)
-    for k, v in sorted(ks.items(), key=lambda kv: -kv[1].get('GRBM_GUI_ACTIVE', 0))[:25]:
-        print(f'{k[:90]:90s} busy {v.get("mfma_busy", float("nan")):7.3f}  gui {v.get("GRBM_GUI_ACTIVE", 0):12.0f}')
 
 
 if __name__ == '__main__':
