@@ -285,8 +285,10 @@ class ForwardTacotron(nn.Module):
         predictors fill the CUs it leaves idle instead of delaying it.
         The four recurrences of the phase (three predictor GRUs, the prenet GRU) are
         persistent kernels whose workgroups wait on each other: run concurrently they must
-        fit the CUs together — with the prenet's spread CBHG tail at few rows
-        (ops.hs_spread_blocks: its workgroups wait on each other too).  When they do not (large batches), every stream is the
+        fit the CUs together.  The prenet stream's two persistent kernels — the spread CBHG
+        tail at few rows (ops.hs_spread_blocks: its workgroups wait on each other too), then
+        the prenet GRU — run one after the other, so the larger of them counts beside the
+        predictors' three.  When they do not fit (large batches), every stream is the
         caller's (the phase runs serialised) — never a co-residency timeout."""
         cache = self.__dict__.setdefault('_ftmi_streams', {})
         if device not in cache:
@@ -296,10 +298,13 @@ class ForwardTacotron(nn.Module):
         fits = self.__dict__.setdefault('_ftmi_concurrent', {})
         key = (device, B, T, ops.RNN_MMA, bool(ops._FORCED))
         if key not in fits:
-            rnns = (self.dur_pred.rnn, self.pitch_pred.rnn, self.energy_pred.rnn, self.prenet.rnn)
-            need = sum(ops.rnn_blocks(r.cell, B, r.hidden) for r in rnns)
-            need += ops.hs_spread_blocks(B * T, 6 * self.prenet.channels)
-            fits[key] = 0 < need <= ops._num_cus()
+            preds = (self.dur_pred.rnn, self.pitch_pred.rnn, self.energy_pred.rnn)
+            need = sum(ops.rnn_blocks(r.cell, B, r.hidden) for r in preds)
+            # the prenet stream's persistent kernels (the spread CBHG tail, then the prenet
+            # GRU) run one after the other on it: the larger of the two beside the predictors
+            pre = ops.rnn_blocks(self.prenet.rnn.cell, B, self.prenet.rnn.hidden)
+            need += max(pre, ops.hs_spread_blocks(B * T, 6 * self.prenet.channels))
+            fits[key] = 0 < need <= ops._num_cus() and pre > 0
         if not fits[key]:
             main = torch.cuda.current_stream(device)
             return [main, main, main]
