@@ -1240,12 +1240,20 @@ static int rnn_setup(RnnParams &p, int B, int T, int H, int cell, const float *w
   // lands after the producers' stores instead of a round trip before them.  Interleaved A/B
   // at c3 (tools/rnn_env_ab.py, two boxes): 3 -> LSTM 1.55 -> 1.52-1.54, postnet GRU 1.32 ->
   // 1.27 us/step; 6 made the LSTM slower again (1.58-1.61)
+  // (-1 = unset: 3, and 6 for the spread postnet GRU on 8-unit workgroups — its producers
+  // store later in the step: 1.12-1.13 -> 1.08 us/step at c3, round 5, profiles/r5_rnn_diag.txt)
   static const int psleep_env = [] {
     const char *v = getenv("FTMI_RNN_PSLEEP");
-    return v ? atoi(v) : 3;
+    return v ? atoi(v) : -1;
   }();
-  p.psleep = psleep_env;
+  p.psleep = psleep_env < 0 ? 3 : psleep_env;
   return FTMI_OK;
+}
+
+// first-poll delay of the U = 8 spread GRU (see rnn_setup)
+static int u8_psleep() {
+  const char *v = getenv("FTMI_RNN_PSLEEP");
+  return v ? atoi(v) : 6;
 }
 
 extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, const float *xp,
@@ -1308,7 +1316,10 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   // the launch's real workgroup count)
   if (mma == 2 && cst_enabled() && ((cell == 1 && H == 512) || (cell == 0 && H == 256))) {
     const bool nb8 = legacy_nbl(cell, B, H, mma, spread, maxb) == 8;
-    if (u8_path(cell, B, H, mma, spread, maxb)) return launch_rnn<0, 256, 8, 4, 2, true>(p, nchunks, maxb, s);
+    if (u8_path(cell, B, H, mma, spread, maxb)) {
+      p.psleep = u8_psleep();
+      return launch_rnn<0, 256, 8, 4, 2, true>(p, nchunks, maxb, s);
+    }
     if (cell == 1) return launch_rnn<1, 512, 16, 4, 2, true>(p, nchunks, maxb, s);
     return nb8 ? launch_rnn<0, 256, 16, 4, 2, true, 8>(p, nchunks, maxb, s)
                : launch_rnn<0, 256, 16, 4, 2, true>(p, nchunks, maxb, s);
