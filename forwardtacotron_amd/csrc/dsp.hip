@@ -253,7 +253,8 @@ constexpr int NNLS_MAX_MELS = 512;
 // filterbank (each bin feeds at most two mel rows), started like librosa's nnls from the
 // clipped minimum-norm least-squares solution pinv(A) m.  Everything stays in LDS /
 // registers across the iterations; HBM sees only m in and x out.
-template <int NJ>
+// NR: mel rows per lane (n_mels <= 64 NR)
+template <int NJ, int NR>
 __global__ __launch_bounds__(64) void nnls_kernel(const NnlsParams p) {
   extern __shared__ float dyn[];  // m[n_mels] r[n_mels] y[nb] vals[nnz]
   float *m_s = dyn, *r_s = dyn + p.n_mels, *y_s = r_s + p.n_mels, *v_s = y_s + p.nb;
@@ -294,14 +295,36 @@ __global__ __launch_bounds__(64) void nnls_kernel(const NnlsParams p) {
     }
     yv[j] = x[j];
   }
+  // the lane's mel rows (lane, lane + 64, ...: n_mels <= 512) and their sparse supports,
+  // read once: inside the iteration loop they were three dependent global loads per row and
+  // step.  The row sums keep their order (q ascending, one fmaf chain per row); the loop is
+  // unrolled so a row's LDS reads issue back to back instead of one latency per term.
+  int rlo[NR], ro[NR], rc[NR];
+#pragma unroll
+  for (int u = 0; u < NR; ++u) {
+    const int i = lane + 64 * u;
+    rlo[u] = ro[u] = rc[u] = 0;
+    if (i < p.n_mels) {
+      rlo[u] = p.rowlo[i];
+      ro[u] = p.rowptr[i];
+      rc[u] = p.rowptr[i + 1] - ro[u];
+    }
+  }
   float t = 1.f;
   for (int it = 0; it < p.iters; ++it) {
     __syncthreads();
-    for (int i = lane; i < p.n_mels; i += 64) {
-      const int lo = p.rowlo[i], o = p.rowptr[i], cnt = p.rowptr[i + 1] - o;
-      float acc = 0.f;
-      for (int q = 0; q < cnt; ++q) acc = fmaf(v_s[o + q], y_s[lo + q], acc);
-      r_s[i] = acc - m_s[i];
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const int i = lane + 64 * u;
+      if (64 * u >= p.n_mels) break;  // uniform
+      if (i < p.n_mels) {
+        const float *vr = v_s + ro[u], *yr = y_s + rlo[u];
+        const int cnt = rc[u];
+        float acc = 0.f;
+#pragma unroll 8
+        for (int q = 0; q < cnt; ++q) acc = fmaf(vr[q], yr[q], acc);
+        r_s[i] = acc - m_s[i];
+      }
     }
     __syncthreads();
     const float tn = 0.5f * (1.f + sqrtf(1.f + 4.f * t * t));
@@ -443,16 +466,23 @@ extern "C" int ftmi_mel_nnls(const float *mel, int32_t B, int32_t F, const int32
   const int nj = (n_bins + 63) / 64;
   const dim3 grid((unsigned)((int64_t)B * F)), block(64);
   const size_t sm = (size_t)(2 * n_mels + n_bins + nnz) * sizeof(float);
-  if (nj <= 3)
-    hipLaunchKernelGGL(nnls_kernel<3>, grid, block, sm, s, p);
-  else if (nj <= 5)
-    hipLaunchKernelGGL(nnls_kernel<5>, grid, block, sm, s, p);
-  else if (nj <= 9)
-    hipLaunchKernelGGL(nnls_kernel<9>, grid, block, sm, s, p);
-  else if (nj <= 17)
-    hipLaunchKernelGGL(nnls_kernel<17>, grid, block, sm, s, p);
-  else
-    hipLaunchKernelGGL(nnls_kernel<33>, grid, block, sm, s, p);
+#define FTMI_NNLS_NJ(NR_)                                                       \
+  if (nj <= 3)                                                                  \
+    hipLaunchKernelGGL((nnls_kernel<3, NR_>), grid, block, sm, s, p);           \
+  else if (nj <= 5)                                                             \
+    hipLaunchKernelGGL((nnls_kernel<5, NR_>), grid, block, sm, s, p);           \
+  else if (nj <= 9)                                                             \
+    hipLaunchKernelGGL((nnls_kernel<9, NR_>), grid, block, sm, s, p);           \
+  else if (nj <= 17)                                                            \
+    hipLaunchKernelGGL((nnls_kernel<17, NR_>), grid, block, sm, s, p);          \
+  else                                                                          \
+    hipLaunchKernelGGL((nnls_kernel<33, NR_>), grid, block, sm, s, p);
+  if (n_mels <= 128) {  // the model's 80 mels: two rows per lane
+    FTMI_NNLS_NJ(2)
+  } else {
+    FTMI_NNLS_NJ(NNLS_MAX_MELS / 64)
+  }
+#undef FTMI_NNLS_NJ
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
 }
