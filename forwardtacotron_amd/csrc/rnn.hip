@@ -811,24 +811,26 @@ __global__ __launch_bounds__(H / U == 1 ? 256 : 320, 1) void rnn_bidir_kernel(
 constexpr int GV_KSEG = 8;  // k-segments per row (lanes summed by shuffles)
 constexpr int GV_RPT = 2;   // rows per thread
 
-template <int CELL, int H, int U, int NBV>
-__global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * GV_KSEG) void rnn_gemv_kernel(
+// KSEG: k-segments per row (GV_KSEG, or 16 — the default for H = 512 / 256: twice the
+// threads, half the FMA chain per thread, one more shuffle stage)
+template <int CELL, int H, int U, int NBV, int KSEG = GV_KSEG>
+__global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * KSEG) void rnn_gemv_kernel(
     const RnnParams p) {
   constexpr int G = CELL ? 4 : 3;
   constexpr int R = G * U;
-  constexpr int NT = R / GV_RPT * GV_KSEG;  // threads
-  constexpr int SEG = H / GV_KSEG;
+  constexpr int NT = R / GV_RPT * KSEG;  // threads
+  constexpr int SEG = H / KSEG;
   constexpr int SEGP = SEG + 4;             // LDS pitch of a segment: conflict-free b128 reads
   constexpr int BPG = H / U;
   constexpr int HF4 = H / 4;                // float4 of one sequence's h
   static_assert(R % GV_RPT == 0 && SEG % 4 == 0 && U * NBV <= NT && NT % 64 == 0, "shape");
   static_assert(BPG <= FLAGS_PER_GROUP, "group size");
-  __shared__ __attribute__((aligned(16))) float hl[2][NBV * GV_KSEG * SEGP];
+  __shared__ __attribute__((aligned(16))) float hl[2][NBV * KSEG * SEGP];
   __shared__ float red[R][NBV];
   __shared__ int s_abort, s_group, s_bi, s_mode;
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int ks = tid % GV_KSEG, rg = tid / GV_KSEG;
+  const int ks = tid % KSEG, rg = tid / KSEG;
 
   // ---- group (= direction) assignment: the census of the MFMA kernel ----------------
   if (tid == 0) {
@@ -940,12 +942,12 @@ __global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * GV_KSEG) void rnn_gem
           }
         }
       }
-      *(f32x4 *)&hb[b * GV_KSEG * SEGP + (k / SEG) * SEGP + k % SEG] = v;
+      *(f32x4 *)&hb[b * KSEG * SEGP + (k / SEG) * SEGP + k % SEG] = v;
     }
     // sequences past B (NBV > B): zero segments
     for (int f = nf4 + tid; f < NBV * HF4; f += NT) {
       const int b = f / HF4, k = (f - b * HF4) * 4;
-      *(f32x4 *)&hb[b * GV_KSEG * SEGP + (k / SEG) * SEGP + k % SEG] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      *(f32x4 *)&hb[b * KSEG * SEGP + (k / SEG) * SEGP + k % SEG] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();
     if (s_abort) return false;
@@ -961,7 +963,7 @@ __global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * GV_KSEG) void rnn_gem
       for (int b = 0; b < NBV; ++b) acc[i][b] = 0.f;
 #pragma unroll
     for (int b = 0; b < NBV; ++b) {
-      const float *hs = hb + b * GV_KSEG * SEGP + ks * SEGP;
+      const float *hs = hb + b * KSEG * SEGP + ks * SEGP;
 #pragma unroll
       for (int j = 0; j < SEG; j += 4) {
         const f32x4 hv = *(const f32x4 *)(hs + j);
@@ -982,6 +984,7 @@ __global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * GV_KSEG) void rnn_gem
         v += __shfl_xor(v, 1);
         v += __shfl_xor(v, 2);
         v += __shfl_xor(v, 4);
+        if constexpr (KSEG == 16) v += __shfl_xor(v, 8);
         acc[i][b] = v;
       }
     if (ks < GV_RPT)
@@ -1032,10 +1035,10 @@ __global__ __launch_bounds__((CELL ? 4 : 3) * U / GV_RPT * GV_KSEG) void rnn_gem
   }
 }
 
-template <int CELL, int H, int U>
+template <int CELL, int H, int U, int KSEG = GV_KSEG>
 int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
   constexpr int BPG = H / U;
-  constexpr int NT = (CELL ? 4 : 3) * U / GV_RPT * GV_KSEG;
+  constexpr int NT = (CELL ? 4 : 3) * U / GV_RPT * KSEG;
   if (8 * BPG > max_blocks) return FTMI_E_UNSUPPORTED;
   p.chunk0 = 0;
   p.ngroups = 2;
@@ -1043,7 +1046,7 @@ int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
   // other XCDs' workgroups retire after the census barrier)
   const int nblk = p.xcd_local ? 8 * BPG : 2 * BPG;
 #define FTMI_GEMV_LAUNCH(NBV_)                                                           \
-  hipLaunchKernelGGL((rnn_gemv_kernel<CELL, H, U, NBV_>), dim3(nblk), dim3(NT), 0, s, p); \
+  hipLaunchKernelGGL((rnn_gemv_kernel<CELL, H, U, NBV_, KSEG>), dim3(nblk), dim3(NT), 0, s, p); \
   break;
   switch (p.B) {
     case 1: FTMI_GEMV_LAUNCH(1)
@@ -1286,8 +1289,14 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   const int maxb = device_cu_count();
   // small batches: exact fp32 GEMV recurrence (any mma: it is exact)
   if (gemv_path(cell, B, H)) {
-    if (cell == 1) return launch_gemv<1, 512, 16>(p, maxb, s);
-    if (H == 256) return launch_gemv<0, 256, 16>(p, maxb, s);
+    // H = 512 / 256: 16 k-segments per row (512 / 384 threads, half the FMA chain per thread):
+    // c2 LSTM 1.26 -> 1.17-1.18, postnet GRU 1.01 -> 0.96-0.97 us/step (tools/rnn_diag.py,
+    // two interleaved rounds; 32 segments: 1.32-1.34 / 1.07-1.08).  FTMI_RNN_GEMV_KSEG=8 (read
+    // per call) keeps 8.
+    const char *kv = getenv("FTMI_RNN_GEMV_KSEG");
+    const bool k8 = kv && atoi(kv) == 8;
+    if (cell == 1) return k8 ? launch_gemv<1, 512, 16>(p, maxb, s) : launch_gemv<1, 512, 16, 16>(p, maxb, s);
+    if (H == 256) return k8 ? launch_gemv<0, 256, 16>(p, maxb, s) : launch_gemv<0, 256, 16, 16>(p, maxb, s);
     if (H == 128) return launch_gemv<0, 128, 16>(p, maxb, s);
     return launch_gemv<0, 64, 16>(p, maxb, s);
   }

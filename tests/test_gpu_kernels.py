@@ -724,14 +724,18 @@ def test_rnn_f16x3_kernels(cell, H, B, T, variant, rng, monkeypatch):
     close(host(m.forward_cl(dev(x))), ref, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize('cell,H,B,T', [('lstm', 512, 1, 37), ('lstm', 512, 2, 20),
-                                        ('lstm', 512, 4, 15), ('gru', 256, 1, 50),
-                                        ('gru', 256, 3, 21), ('gru', 128, 1, 33),
-                                        ('gru', 128, 4, 17), ('gru', 64, 1, 40),
-                                        ('gru', 64, 2, 25)])
-def test_rnn_gemv(cell, H, B, T, rng, monkeypatch):
+GEMV_CASES = [('lstm', 512, 1, 37), ('lstm', 512, 2, 20), ('lstm', 512, 4, 15), ('gru', 256, 1, 50),
+              ('gru', 256, 3, 21), ('gru', 128, 1, 33), ('gru', 128, 4, 17), ('gru', 64, 1, 40),
+              ('gru', 64, 2, 25)]
+
+
+@pytest.mark.parametrize('cell,H,B,T,kseg', [c + (8,) for c in GEMV_CASES] +
+                         [c + (16,) for c in GEMV_CASES if c[1] >= 256])
+def test_rnn_gemv(cell, H, B, T, kseg, rng, monkeypatch):
     """B <= 4: the exact-fp32 GEMV recurrence against the numpy oracle in fp64 (a tighter
-    bound than the f16x3 kernels') and against the MFMA kernel."""
+    bound than the f16x3 kernels') and against the MFMA kernel; kseg: k-segments per row
+    (FTMI_RNN_GEMV_KSEG, 16 for H = 512 / 256)."""
+    monkeypatch.setenv('FTMI_RNN_GEMV_KSEG', str(kseg))
     fin = 512 if cell == 'lstm' else 256
     m, sd = _rnn_module(cell, fin, H, rng)
     x = rng.normal(0, 1, (B, T, fin)).astype(np.float32)
