@@ -195,9 +195,15 @@ def _split_k(M: int, N: int, K: int, mma: int, slab: bool = False, Cin: int = 0)
         nch = -(-Cin // 32)
         k = K // Cin if Cin else 1
 
+        # the round trip as measured in the model's phoneme phase (round 5, r5_timeline_c3:
+        # 24-39 us for 2 splits of 12,800 x 256 beside the other streams — the old 5 TB/s +
+        # 5 us model priced it at 15 us and split proj2 / the predictor convs where the
+        # finish costs more than it saves): 1 TB/s + 20 us.  Interleaved A/B (5 / 3 rounds,
+        # profiles/r5_ab_splitk*.jsonl): c3 8.12-8.20 -> 8.01-8.15, c5 11.33-11.40 ->
+        # 11.19-11.26 ms/step, c2 unchanged (2.59-2.65 / 2.60-2.68)
         def t_us(sp):
             run = -(-tiles * sp // cus) * -(-nch // sp) * k * 1.8
-            return run + (sp * M * N * 8 / 5e6 + 5.0 if sp > 1 else 0.0)
+            return run + (sp * M * N * 8 / 1e6 + 20.0 if sp > 1 else 0.0)
         return int(min(range(1, min(8, nch) + 1), key=t_us))
     if mma == 0 or K < 2048:
         return 1
