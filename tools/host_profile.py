@@ -38,7 +38,9 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / n
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats('tottime').print_stats(30)
+    st = pstats.Stats(pr, stream=s)
+    st.sort_stats('tottime').print_stats(30)
+    st.sort_stats('cumulative').print_stats(45)
     print(f'{cfg}: {dt * 1e3:.3f} ms per call (wall, profiled)')
     print(s.getvalue())
 
