@@ -1832,6 +1832,378 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slabp_kernel(const GemmParam
   slab_epilogue<EPI, NTHR>(p, G, tile, m0, n0, tid);
 }
 
+// ---- conv bank walk: the pooled bank of a narrow input (the CBHG postnet: Cin = 80) -------
+// The slab kernel gives every (group, column tile) its own block, so the c3 postnet bank ran
+// 16 blocks per 255-row tile, each re-staging the same 80-channel slab and paying its own
+// prologue and LDS-tile epilogue for 3 k steps of MFMAs (0.64-0.66 ms, 24 % of the f16x3
+// ceiling).  Here one block owns a (255-row pooled tile, 128-column tile) and WALKS every group
+// over a slab staged once: all 3 chunks of the input rows (f16 head / scaled tail, 101 KB) stay
+// in LDS for the whole walk, the B planes of step s + 1 are staged under step s (2 buffers) and
+// the group loop holds no epilogue state.  A group's epilogue works on the accumulators in
+// registers: the maxpool's previous row is the lane 16 below (ds_bpermute), the block of 16
+// rows above, or — for a wave's first row — the last row of the wave above through a 4 KB LDS
+// halo; neighbouring column pairs are exchanged by DPP and byte-permuted so each lane stores
+// 4 B of two columns.  Same MFMA order and operands as the slab kernel (bit-identical output).
+// Measured (tools/bank_walk_ab.py, c3 postnet bank): 0.54 ms against the slab kernel's 0.64-0.65
+// = 29 % of the ceiling; with no epilogue 0.43, with neither MFMAs nor epilogue 0.22 (the
+// step skeleton: fragment reads, B staging, barrier) — the MFMAs do not overlap the skeleton.
+// Not kept: fragment prefetch across steps (10 VGPR spills, 0.60 ms), two B register sets
+// (0.59 ms).  Limits: Cin <= 96, K <= 8, T >= 4, N % 128 == 0, groups k = K .. 1 heaviest
+// first with pad k / 2.
+constexpr int BW_MAXK = 8;
+constexpr int BW_MAXCH = 3;                    // 32-channel chunks resident (Cin <= 96)
+constexpr int BW_SR = SL_BM + BW_MAXK - 1;     // slab rows
+constexpr int BW_ZROW = BW_SR;                 // the all-zero row (masked taps)
+constexpr int BW_AIMG = (BW_SR + 1) * SP_ROW;  // halves per (chunk, plane) slab image
+constexpr int BW_NBUF = 2;                     // B buffers
+
+__global__ __launch_bounds__(512, 1) void conv_bank_walk_kernel(const GemmParams p) {
+  constexpr int NTHR = 512;
+  constexpr int BSLOTS = 1024 / NTHR;
+  constexpr int NGRAN = BW_MAXCH * 8;                      // 4-channel granules per slab row
+  constexpr int ASLOTS = (BW_SR * NGRAN + NTHR - 1) / NTHR;  // slab granules per thread
+  __shared__ __attribute__((aligned(16))) _Float16 lds[BW_MAXCH * 2 * BW_AIMG + BW_NBUF * 2 * SP_BIMG];
+  __shared__ float halo[2][4][SL_BN];  // [walk parity][wave row][column]: a wave's last row
+  _Float16 *const lds_a = lds;
+  _Float16 *const lds_b = lds + BW_MAXCH * 2 * BW_AIMG;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  constexpr int TS = SL_BM - 1;  // pooled rows a tile produces (row 0 is the halo row)
+  const int MT = (p.M + TS - 1) / TS, NT = p.g[0].ntiles;
+  int mt, nt;
+  slab_tile(blockIdx.x, MT, NT, 0, mt, nt);  // a row tile's column tiles on one XCD
+  if (mt >= MT) return;                      // the grid is padded to whole XCD rounds
+  const int m0 = mt * TS - 1, n0 = nt * SL_BN;
+  const int Cin = p.Cin, nch = (Cin + 31) / 32, NG = p.ngroups, N = p.g[0].N;
+  const int PMAX = NG / 2;  // the heaviest group's halo: slab row 0 = input row m0 - PMAX
+#ifdef FTMI_DIAG
+  // timing experiments (FTMI_SLAB_DIAG, results invalid): bit 0 = every B load from the first
+  // step's (L2-hot) lines, bit 1 = no MFMAs, bit 2 = no epilogue (finish / stores),
+  // bit 3 = no epilogue stores (split rows)
+  const int diag = p.diag;
+#else
+  constexpr int diag = 0;
+#endif
+  // Group g has k = NG - g taps (pad k / 2); its f16x3 block (ftmi_split_weights_f16 layout:
+  // 3 planes [N][Kpad], then N column scales, 16-B padded) sits right before group g - 1's, the
+  // BN affine at (k - 1) N — all arithmetic, so the walk issues no scalar loads per step (their
+  // waits would also drain the LDS reads); bank_walk_ok checks the layout on the host.
+  auto kpad = [&](int k) { return (k * Cin + 31) & ~31; };
+  auto block_bytes = [&](int k) { return (int64_t)6 * N * kpad(k) + ((4 * N + 15) & ~15); };
+  const char *const wblk0 = (const char *)p.g[0].w3;
+  const float *const bnsc = p.g[NG - 1].scale, *const bnsh = p.g[NG - 1].shift;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 3, wn = wave >> 2;
+  const int fr = lane & 15, fs = lane >> 4;
+
+  // ---- the slab, once: item = (slab row, 4-channel granule); channels >= Cin are zero ----
+  const int SR = SL_BM + NG - 1;
+  float amax = 0.f;
+  {
+    f32x4 v[ASLOTS];
+#pragma unroll
+    for (int i = 0; i < ASLOTS; ++i) {
+      const int it = tid + NTHR * i, sr = it / NGRAN, q = it - sr * NGRAN;
+      int mp = m0 - PMAX + sr;
+      mp = mp < 0 ? 0 : (mp >= p.M ? p.M - 1 : mp);  // clamped rows only feed masked taps
+      const bool ok = sr < SR && q * 4 < Cin;
+      v[i] = ok ? *(const f32x4 *)(p.x + (int64_t)mp * p.x_stride + q * 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < ASLOTS; ++i) {
+      const int it = tid + NTHR * i, sr = it / NGRAN, q = it - sr * NGRAN;
+      if (sr >= SR) continue;
+      amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
+      f16x4 h, t;
+      split2h(v[i], h, t);
+      _Float16 *dst = lds_a + (q >> 3) * 2 * BW_AIMG + sp_off(sr, (q & 7) >> 1) + (q & 1) * 4;
+      *(f16x4 *)dst = h;
+      *(f16x4 *)(dst + BW_AIMG) = t;
+    }
+    if (tid < BW_MAXCH * 2 * (SP_ROW / 8)) {  // the zero row of every chunk and plane
+      const int img = tid / (SP_ROW / 8), part = tid % (SP_ROW / 8);
+      *(u32x4 *)(lds_a + img * BW_AIMG + BW_ZROW * SP_ROW + part * 8) = (u32x4){0u, 0u, 0u, 0u};
+    }
+  }
+
+  // ---- B: item = (plane, row n, 16-B segment); the walk's steps are (group, chunk, tap) ----
+  int bdst[BSLOTS], brow[BSLOTS];
+#pragma unroll
+  for (int i = 0; i < BSLOTS; ++i) {
+    const int idx = tid + NTHR * i, pl = idx >> 9, rem = idx & 511, nl = rem >> 2, seg = rem & 3;
+    const int n = n0 + nl < N ? n0 + nl : N - 1;
+    brow[i] = pl * N + n;
+    bdst[i] = pl * SP_BIMG + sp_off(nl, seg);
+  }
+  struct BRaw {
+    u32x4 v[BSLOTS];
+    bool ok;
+  };
+  // The walk order k0, k0 - 1, .., 1, NG, .., k0 + 1 with k0 rotating over the blocks of an
+  // XCD: blocks that run together reach their epilogues (130 KB of stores each, drained before
+  // the next B staging: the loads wait on the same counter) at different times instead of
+  // all at once.  Any order gives the same bits (each group owns its accumulators).
+  const int k0 = NG - (int)((blockIdx.x >> 3) % NG);
+  const char *wk0 = wblk0;
+  for (int k = NG - 1; k >= k0; --k) wk0 -= block_bytes(k);
+  int bk = k0, bc = 0, bj = 0, bn = 0;  // taps (group) / chunk / tap of the next B load, groups done
+  const char *bw = wk0;                  // that group's block
+  auto loadB = [&](BRaw &rb) {           // past the last step: a harmless re-read
+    rb.ok = bc * 32 + (tid & 3) * 8 < Cin;
+    const _Float16 *w16 = (const _Float16 *)((diag & 1) ? wblk0 : bw) +
+                          ((diag & 1) ? 0 : bj * Cin + (rb.ok ? bc * 32 : 0)) + (tid & 3) * 8;
+    const int kp = kpad(bk);
+#pragma unroll
+    for (int i = 0; i < BSLOTS; ++i) rb.v[i] = *(const u32x4 *)(w16 + (int64_t)brow[i] * kp);
+    if (bn < NG && ++bj == bk) {
+      bj = 0;
+      if (++bc == nch) {
+        bc = 0;
+        ++bn;
+        if (bk == 1) {
+          bk = NG;
+          bw = wblk0;
+        } else {
+          bw -= block_bytes(--bk);
+        }
+      }
+    }
+  };
+  auto storeB = [&](const BRaw &rb, int buf) {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < BSLOTS; ++i)
+      *(u32x4 *)(lds_b + buf * 2 * SP_BIMG + bdst[i]) = rb.ok ? rb.v[i] : z;
+  };
+
+  // rows of this lane's A fragments: in range, and their frame within the sequence
+  int tfr[4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + wm * 64 + mi * 16 + fr;
+    // rows outside [0, M) get a frame no tap offset brings into [0, T): one unsigned compare
+    tfr[mi] = m >= 0 && m < p.M ? m % p.T : -(1 << 20);
+  }
+  struct Frag {
+    f16x8 ah[4], at[4], b0[4], b1[4];
+  };
+  auto read_frags = [&](Frag &f, int k, int c, int j, int bbuf) {
+    const int d = j - k / 2;  // the tap's row offset
+    const _Float16 *Ab = lds_a + c * 2 * BW_AIMG;
+    const _Float16 *Bb = lds_b + bbuf * 2 * SP_BIMG;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const bool ok = (unsigned)(tfr[mi] + d) < (unsigned)p.T;
+      const int o = sp_off(ok ? wm * 64 + mi * 16 + fr + d + PMAX : BW_ZROW, fs);
+      f.ah[mi] = *(const f16x8 *)(Ab + o);
+      f.at[mi] = *(const f16x8 *)(Ab + BW_AIMG + o);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int o = sp_off(wn * 64 + ni * 16 + fr, fs);
+      f.b0[ni] = *(const f16x8 *)(Bb + o);
+      f.b1[ni] = *(const f16x8 *)(Bb + SP_BIMG + o);
+    }
+  };
+  f32x4 acc[4][4];
+  auto zero_acc = [&] {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  };
+  zero_acc();
+  auto mfma_frags = [&](const Frag &f) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const f16x8 bh = f.b0[ni] * (_Float16)(1.0f / H3_SCALE);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {  // small terms first (the slab kernel's order)
+        f32x4 c = acc[mi][ni];
+        c = mma16(f.at[mi], bh, c);
+        c = mma16(f.ah[mi], f.b1[ni], c);
+        c = mma16(f.ah[mi], f.b0[ni], c);
+        acc[mi][ni] = c;
+      }
+    }
+  };
+
+  // ---- a group's epilogue (VALU-lean: a wave64 VALU op costs 4 cycles, the epilogue runs 8
+  // times per block; the first form, ~3,100 instructions, cost 7 us per group) ---------------
+  // Per lane: frame of its first output row of block mi (row -1, tile 0's halo row, as frame
+  // T - 1 so that row 0 is a sequence start), and bit 4 mi + i = row 4 fs + i of block mi is
+  // stored (not the halo row, inside [0, M)).  Rows outside [0, M) hold exact zeros and the
+  // clamped columns do not exist (N % 128 == 0), so the range guards need no masks.
+  int tst[4];
+  unsigned vrow = 0;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int R = wm * 64 + mi * 16 + 4 * fs, r = m0 + R;
+    tst[mi] = r >= 0 ? r % p.T : p.T - 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) vrow |= (unsigned)(R + i > 0 && r + i < p.M) << (4 * mi + i);
+  }
+  // part 1 (before a barrier): colscale, range guard, ReLU / BN in place, and the wave's last
+  // row into the halo
+  float nf = 0.f;  // NaN once an accumulator was not finite (x * 0 + nf)
+  auto finish = [&](const float (&cs)[4], const float (&sc)[4], const float (&sh)[4], int par) {
+    // opaque copies: without them LICM hoists the epilogue's group-invariant row / column
+    // terms out of the walk and keeps them live across it (256 VGPRs + spills)
+    int ln = lane, wv = wave;
+    asm volatile("" : "+v"(ln), "+s"(wv));
+    const int efr = ln & 15, efs = ln >> 4, ewm = wv & 3, ewn = wv >> 2;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          nf = fmaf(acc[mi][ni][i], 0.f, nf);
+          float v = acc[mi][ni][i] * cs[ni];  // (a bank has no bias: bank_walk_ok)
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (bnsc) v = v * sc[ni] + sh[ni];
+          acc[mi][ni][i] = v;
+        }
+      if (efs == 3) halo[par][ewm][ewn * 64 + ni * 16 + efr] = acc[3][ni][3];
+    }
+  };
+  // part 2 (after the barrier): y[t] = max(v[t - 1], v[t]) within a sequence, stored
+  float ymax = 0.f;
+  auto store_pooled = [&](int k, int par) {
+    int ln = lane, wv = wave, mb = m0;
+    asm volatile("" : "+v"(ln), "+s"(wv), "+s"(mb));
+    const int efr = ln & 15, efs = ln >> 4, ewm = wv & 3, ewn = wv >> 2;
+    const int ycol0 = (k - 1) * N, cw = n0 + ewn * 64;  // the wave's first column
+    const bool ev = (efr & 1) == 0;
+    float up[4];  // per ni: row 15 of the block above (lanes fs = 0 take it)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) up[ni] = ewm > 0 ? halo[par][ewm - 1][ewn * 64 + ni * 16 + efr] : 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      // the sequence start among the lane's 4 rows (T >= 4: at most one): position 0..3, or 4
+      const int zp = tst[mi] ? p.T - tst[mi] : 0;
+      bool st[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st[i] = zp == i;
+      f32x4 o[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const float s3 = __shfl(acc[mi][ni][3], (ln - 16) & 63);
+        const float prev0 = efs ? s3 : up[ni];
+        up[ni] = s3;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float a = acc[mi][ni][i], pv = i ? acc[mi][ni][i - 1] : prev0;
+          o[ni][i] = st[i] ? a : fmaxf(a, pv);
+          ymax = fmaxf(ymax, fabsf(o[ni][i]));
+        }
+      }
+      const int R0 = ewm * 64 + mi * 16 + 4 * efs;
+      if (p.y_split_c) {
+        // column pairs (fr even: rows 0 / 1 of columns fr, fr + 1; fr odd: rows 2 / 3 of
+        // fr - 1, fr): each lane sends its partner the word the partner stores (DPP lane ^ 1),
+        // then two byte permutes build its own rows, the even column's half first
+        unsigned hw[2][4], tw[2][4];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          f16x4 h, tl;
+          split2h(o[ni], h, tl);
+          const u32x2 hb = __builtin_bit_cast(u32x2, h), tb = __builtin_bit_cast(u32x2, tl);
+          const unsigned hx = __builtin_amdgcn_mov_dpp(ev ? hb.y : hb.x, 0xB1, 0xF, 0xF, false);
+          const unsigned tx = __builtin_amdgcn_mov_dpp(ev ? tb.y : tb.x, 0xB1, 0xF, 0xF, false);
+          const unsigned ha = ev ? hb.x : hx, hbv = ev ? hx : hb.y;
+          const unsigned ta = ev ? tb.x : tx, tbv = ev ? tx : tb.y;
+          hw[0][ni] = __builtin_amdgcn_perm(hbv, ha, 0x05040100u);
+          hw[1][ni] = __builtin_amdgcn_perm(hbv, ha, 0x07060302u);
+          tw[0][ni] = __builtin_amdgcn_perm(tbv, ta, 0x05040100u);
+          tw[1][ni] = __builtin_amdgcn_perm(tbv, ta, 0x07060302u);
+        }
+        const int ra = ev ? 0 : 2;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (!((vrow >> (4 * mi + ra + q)) & 1u)) continue;
+          _Float16 *yr = (_Float16 *)(p.y + (int64_t)(mb + R0 + ra + q) * p.y_stride) + ycol0 + cw +
+                         (efr & ~1);
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            if (diag & 8) continue;
+            *(unsigned *)(yr + ni * 16) = hw[q][ni];
+            *(unsigned *)(yr + p.y_split_c + ni * 16) = tw[q][ni];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (!((vrow >> (4 * mi + i)) & 1u)) continue;
+          float *yr = p.y + (int64_t)(mb + R0 + i) * p.y_stride + ycol0 + cw + efr;
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) yr[ni * 16] = o[ni][i];
+        }
+      }
+    }
+  };
+
+  // ---- the walk: groups, each c outer / j inner as the slab kernel -------------------------
+  // Step s (global over the walk) reads B buffer s & 1, stored in step s - 1 from registers
+  // loaded in step s - 2; its fragments are read at the step's top (the other wave of the SIMD
+  // covers that wait with its MFMAs).  The epilogue sits between the groups' step loops, so
+  // none of its values is live in them; the group's column scales and BN affine are loaded
+  // before its steps.
+  const int S = nch * NG * (NG + 1) / 2;
+  BRaw rb;
+  loadB(rb);
+  storeB(rb, 0);
+  loadB(rb);  // step 1
+  __syncthreads();
+  int s = 0, kc = k0;
+  const char *ew = wk0;  // the group's block
+  for (int gn = 0; gn < NG; ++gn) {
+    float cs[4], sc[4], sh[4];
+    {
+      const float *colscale = (const float *)(ew + (int64_t)6 * N * kpad(kc));
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int cc = n0 + wn * 64 + ni * 16 + fr;
+        cs[ni] = colscale[cc];
+        sc[ni] = bnsc ? bnsc[(kc - 1) * N + cc] : 1.f;
+        sh[ni] = bnsc ? bnsh[(kc - 1) * N + cc] : 0.f;
+      }
+    }
+    const int ng = nch * kc;
+    int u = 0, c = 0, j = 0;
+    auto step = [&](BRaw &rs) {  // rs holds B(s + 1)
+      Frag f;
+      read_frags(f, kc, c, j, s & 1);
+      if (s + 1 < S) {
+        storeB(rs, (s + 1) & 1);
+        loadB(rs);  // step s + 2 (clamped)
+      }
+      if (!(diag & 2)) mfma_frags(f);
+      __syncthreads();
+      ++s;
+      ++u;
+      if (++j == kc) {
+        j = 0;
+        ++c;
+      }
+    };
+    while (u < ng) step(rb);
+    if (!(diag & 4)) finish(cs, sc, sh, gn & 1);
+    __syncthreads();  // the halo
+    if (!(diag & 4)) store_pooled(kc, gn & 1);
+    zero_acc();
+    if (kc == 1) {
+      kc = NG;
+      ew = wblk0;
+    } else {
+      ew -= block_bytes(--kc);
+    }
+  }
+  const bool bad = nf != 0.f || !(amax <= 65504.f) || (p.y_split_c && !(ymax <= 65504.f));
+  if (bad && p.status) atomicOr(p.status, 1u);
+}
+
 // ---- skinny kernel: few output rows (M <= SK_MMAX, e.g. batch 1), the weight stream binds --
 // At B = 1 (BASELINE config c2: T = 120 phonemes) a conv moves its whole weight block for a
 // handful of rows: the prenet bank reads 35.65 MB of weight planes for 120 x 4096 outputs, so
@@ -3782,6 +4154,55 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
   return FTMI_OK;
 }
 
+// conv_bank_walk_kernel: a pooled f16x3 bank on fp32 input rows of at most 96 channels, groups
+// k = K .. 1 (K <= 8, pad k / 2) of equal widths (16-column multiples), no split.
+// By default only with at least BW_MIN_BLOCKS blocks (two per CU of the 256: the walk has
+// one block per row and column tile, the slab kernel 16 per row tile, so a few-tile bank —
+// c2's postnet, 4 row tiles — would leave the chip idle); FTMI_BANK_WALK (read per call) = 0
+// never, 1 at any size.
+constexpr int BW_MIN_BLOCKS = 512;
+int64_t split_block_bytes(int64_t N, int64_t K, int mma);
+static bool bank_walk_ok(const GemmParams &p) {
+  const char *e = getenv("FTMI_BANK_WALK");
+  if (e && atoi(e) == 0) return false;
+  const int64_t blocks = (p.M + SL_BM - 2) / (SL_BM - 1) * ((p.g[0].N + SL_BN - 1) / SL_BN);
+  if (!e && blocks < BW_MIN_BLOCKS) return false;
+  if (!p.pool_out || p.x_split || p.residual || p.yt || !p.y || p.split_req > 1) return false;
+  if (p.Cin <= 0 || p.Cin > BW_MAXCH * 32 || p.Cin % 16 || p.To != p.T || p.M <= 0) return false;
+  if (p.T < 4 || p.ngroups < 2 || p.ngroups > BW_MAXK || p.g[0].N % SL_BN) return false;
+  // the layout the kernel derives from group 0 (set_bank_groups, ftmi_split_weights_f16)
+  const int NG = p.ngroups, N = p.g[0].N;
+  const GemmGroup &g1 = p.g[NG - 1];  // k = 1: BN affine of column block 0
+  const char *blk = (const char *)p.g[0].w3;
+  for (int i = 0; i < NG; ++i) {
+    const GemmGroup &g = p.g[i];
+    const int k = NG - i, kp = (k * p.Cin + 31) / 32 * 32;
+    if (i > 0) blk -= split_block_bytes(N, (int64_t)k * p.Cin, 2);
+    if (g.k != k || g.pad != k / 2 || g.N != N || g.Kpad != kp || g.ycol0 != (k - 1) * N)
+      return false;
+    if ((const char *)g.w3 != blk || (const char *)g.colscale != blk + (int64_t)6 * N * kp)
+      return false;
+    if (g.bias || (g.scale != (g1.scale ? g1.scale + (int64_t)(k - 1) * N : nullptr)) ||
+        (g.shift != (g1.scale ? g1.shift + (int64_t)(k - 1) * N : nullptr)) || !g.shift != !g.scale)
+      return false;
+  }
+  return true;
+}
+
+static int launch_bank_walk(const GemmParams &p, hipStream_t s) {
+  GemmParams q = p;
+  q.g[0].ntiles = (q.g[0].N + SL_BN - 1) / SL_BN;
+#ifdef FTMI_DIAG
+  const char *de = getenv("FTMI_SLAB_DIAG");
+  q.diag = de ? atoi(de) : 0;
+#endif
+  const int MT = (q.M + SL_BM - 2) / (SL_BM - 1);
+  const int nblk = (MT < 8 ? MT : (MT + 7) / 8 * 8) * q.g[0].ntiles;  // whole XCD rounds
+  hipLaunchKernelGGL(conv_bank_walk_kernel, dim3(nblk), dim3(512), 0, s, q);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
 int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hipStream_t s) {
   if (nblocks <= 0) return FTMI_OK;
   dim3 grid(nblocks), block(256);
@@ -3795,6 +4216,7 @@ int launch(const GemmParams &p, int epi, bool maxpool, int nblocks, int mma, hip
     if (!(mma == 2 && presplit && epi == EPI_CONV && !maxpool && !p.residual && !p.yt &&
           p.y && slab_ok(q, epi)))
       return FTMI_E_UNSUPPORTED;
+    if (bank_walk_ok(q)) return launch_bank_walk(q, s);
     return launch_slab(q, epi, false, s);
   }
   if (p.y_split_c) return FTMI_E_UNSUPPORTED;  // split output rows: pool_out only

@@ -220,6 +220,49 @@ def test_conv_bank_pooled(K, Cin, B, T, rng, monkeypatch):
     close(yp, O.maxpool_k2_s1_p1(ref).transpose(0, 2, 1), rtol=5e-5, atol=5e-5)
 
 
+@pytest.mark.parametrize('K,Cin,B,T', [(8, 80, 3, 200), (8, 80, 16, 1368), (8, 96, 2, 300),
+                                     (4, 48, 7, 5), (4, 48, 5, 3), (2, 16, 3, 40),
+                                     (3, 64, 5, 61)])
+def test_conv_bank_walk(K, Cin, B, T, rng, monkeypatch):
+    """The walking bank (gemm.hip conv_bank_walk_kernel: one block per pooled row tile and
+    column tile, every group over one resident slab, the epilogue from registers) gives the
+    slab kernel's pooled bank bit for bit — fp32 rows and f16x3 split rows — including tiles
+    that hold sequence starts, sequences shorter than the taps (T = 5, k = 4; T = 3 takes the
+    slab kernel: the walk needs T >= 4) and 86 row tiles (the XCD-ordered grid); status stays
+    0, and inputs or outputs beyond the f16 range set bit 0."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import pack_conv
+    C = 256
+    x = rng.normal(0, 1, (B, T, Cin)).astype(np.float32)
+    ws = [rng.normal(0, 1 / np.sqrt(Cin * k), (C, Cin, k)).astype(np.float32) for k in range(1, K + 1)]
+    sc = dev(rng.uniform(0.5, 1.5, K * C).astype(np.float32))
+    sh = dev(rng.normal(0, 0.1, K * C).astype(np.float32))
+    wp = torch.cat([pack_conv(torch.from_numpy(w)).reshape(-1) for w in ws]).cuda()
+    w3 = ops.split_bank_weights(wp, K, Cin, C, 2)
+    xd = dev(x)
+    st = ops.status_word(xd.device)
+    st.zero_()
+    out = {}
+    for walk in ('1', '0'):
+        monkeypatch.setenv('FTMI_BANK_WALK', walk)
+        out[walk] = [host(ops.conv_bank(xd, wp, K, C, sc, sh, mma=2, w_split=w3, pool=True,
+                                        split_out=so)) for so in (False, True)]
+    for a, b in zip(out['1'], out['0']):
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert int(st.item()) == 0
+    monkeypatch.setenv('FTMI_BANK_WALK', '1')
+    xb = x.copy()
+    xb[B - 1, T - 1, Cin - 1] = 1e5  # the last row's last channel
+    ops.conv_bank(dev(xb), wp, K, C, sc, sh, mma=2, w_split=w3, pool=True)
+    assert int(st.item()) & 1
+    st.zero_()
+    ops.conv_bank(xd, wp, K, C, sc * 1e5, sh, mma=2, w_split=w3, pool=True)  # fp32 rows: fine
+    assert int(st.item()) == 0
+    ops.conv_bank(xd, wp, K, C, sc * 1e5, sh, mma=2, w_split=w3, pool=True, split_out=True)
+    assert int(st.item()) & 1
+    st.zero_()
+
+
 @pytest.mark.parametrize('K,Cin,B,T', [(16, 256, 1, 120), (16, 256, 1, 50), (8, 128, 2, 64),
                                      (4, 64, 1, 50)])
 def test_conv_bank_halves(K, Cin, B, T, rng, monkeypatch):
