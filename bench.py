@@ -86,7 +86,7 @@ PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r5c2_pmc_traffic.json')   # c2 
 PMC_PROFILE_C5 = os.path.join(ROOT, 'profiles', 'r5c5_pmc_traffic.json')   # c5 (--model fast_pitch)
 # the PMC files are a prior run of the same workload (separate FETCH_SIZE / WRITE_SIZE passes
 # cannot share the timed run), taken on this tree
-PMC_TREE = 'd3ccbd7 (round 5, tools/gpu_r5_measure.sh pmc)'
+PMC_TREE = '6eb8293 (round 5, tools/gpu_r5_measure.sh pmc / mfma)'
 
 
 def rocprof_name(label: str):

@@ -1848,7 +1848,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slabp_kernel(const GemmParam
 // = 29 % of the ceiling; with no epilogue 0.43, with neither MFMAs nor epilogue 0.22 (the
 // step skeleton: fragment reads, B staging, barrier) — the MFMAs do not overlap the skeleton.
 // Not kept: fragment prefetch across steps (10 VGPR spills, 0.60 ms), two B register sets
-// (0.59 ms).  Limits: Cin <= 96, K <= 8, T >= 4, N % 128 == 0, groups k = K .. 1 heaviest
+// (0.59 ms), per-wave B fragments from L2 without LDS staging or per-step barriers (0.82 ms).  Limits: Cin <= 96, K <= 8, T >= 4, N % 128 == 0, groups k = K .. 1 heaviest
 // first with pad k / 2.
 constexpr int BW_MAXK = 8;
 constexpr int BW_MAXCH = 3;                    // 32-channel chunks resident (Cin <= 96)

@@ -57,7 +57,7 @@ NAMED = {
            'postnet_gru': 'rnn_bidir_kernel<0, 256, 8,',
            'prenet_gru': 'rnn_bidir_kernel<0, 256, 16,',
            'prenet_bank': 'conv_gemm_slab_kernel<0, false, true>|1376256',
-           'postnet_bank': 'conv_gemm_slab_kernel<0, false, true>|4227072',
+           'postnet_bank': 'conv_bank_walk_kernel|352256',
            'postnet_proj1': 'conv_gemm_slab_kernel<0, false, true>|528384',
            'postnet_highway_stack': 'highway_stack_kernel<96>',
            'prenet_highway_stack': 'highway_stack_kernel<64>',
