@@ -21,7 +21,7 @@ _lib = None
 
 c_int, c_int64, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 P = c_void_p  # every device pointer travels as void*
-ABI_VERSION = 18
+ABI_VERSION = 19
 MMA_F32, MMA_BF16X6, MMA_F16X3 = 0, 1, 2
 
 
@@ -47,11 +47,20 @@ class WaveRNNArgs(ctypes.Structure):
             'n_classes', 'mol', 'rnn_dims', 'fc_dims', 'feat_dims', 'aux_dims')]
 
 
+class NnlsArgs(ctypes.Structure):
+    """Mirror of ftmi_nnls_lbfgsb_args (include/ftmi.h)."""
+    _fields_ = [('mel', P)] + [(n, c_int) for n in ('B', 'F', 'n_mels', 'n_bins', 'denorm')] + [
+        ('blocks', P)] + [(n, c_int) for n in ('n_blocks', 'groups', 'm', 'max_frames')] + [
+        (n, P) for n in ('rowvals', 'rowptr', 'rowlo', 'bin_rows', 'bin_w', 'pinv', 'workspace', 'S',
+                         'active')]
+
+
 # name -> (restype, argtypes); the exact export list of include/ftmi.h
 SIGNATURES = {
     'ftmi_abi_version': (c_int, []),
     'ftmi_build_id': (ctypes.c_char_p, []),
     'ftmi_strerror': (ctypes.c_char_p, [c_int]),
+    'ftmi_set_resident_cu_limit': (c_int, [c_int]),
     'ftmi_embedding': (c_int, [P, c_int64, P, c_int64, c_int64, P, P, P]),
     'ftmi_conv1d': (c_int, [ctypes.POINTER(ConvArgs), P]),
     'ftmi_conv_bank': (c_int, [P, c_int64, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P, c_int64,
@@ -111,6 +120,9 @@ SIGNATURES = {
     'ftmi_unit_phases': (c_int, [P, c_int, c_int, c_int, P, P]),
     'ftmi_istft_workspace_bytes': (c_int64, [c_int, c_int, c_int]),
     'ftmi_istft': (c_int, [P, c_int, c_int, P, c_int, c_int, P, P, P, P, P, c_int64, c_int64, P]),
+    'ftmi_griffinlim_iter': (c_int, [P, P, P, P, c_int, c_int, P, c_int, c_int, P, P, P, c_float,
+                                     c_int, P]),
+    'ftmi_istft_fused': (c_int, [P, c_int, c_int, P, c_int, c_int, P, P, P, P, c_int64, c_int64, P]),
     'ftmi_wr_stretch_conv': (c_int, [P, c_int64, c_int, c_int, c_int, c_int, P, P, c_int64, c_int,
                                      c_int, P]),
     'ftmi_wavernn_workspace_bytes': (c_int64, []),
@@ -119,6 +131,10 @@ SIGNATURES = {
     'ftmi_wr_unfold': (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     'ftmi_mel_nnls': (c_int, [P, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P,
                               c_float, c_int, P, P]),
+    'ftmi_nnls_lbfgsb_workspace_bytes': (c_int64, [c_int, c_int, c_int, c_int, c_int]),
+    'ftmi_nnls_lbfgsb_start': (c_int, [ctypes.POINTER(NnlsArgs), P]),
+    'ftmi_nnls_lbfgsb_cycles': (c_int, [ctypes.POINTER(NnlsArgs), c_int, P]),
+    'ftmi_nnls_lbfgsb_finish': (c_int, [ctypes.POINTER(NnlsArgs), P, P, P]),
 }
 
 

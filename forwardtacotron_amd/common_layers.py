@@ -336,16 +336,27 @@ class CBHG(Packed):
             self.__dict__['_ftmi_stack'] = cache
         return cache[1]
 
+    def spread_blocks(self, M: int) -> int:
+        """Workgroups the spread CBHG tail would hold resident for M rows (0: the fused
+        stack does not apply or runs the one-workgroup-per-64-rows kernel)."""
+        Cp = self.channels  # the tail's input: proj2's output (common_layers.py:104-109)
+        if not ops.highway_stack_ok(M, Cp, self.channels, len(self.highways), 6 * self.channels,
+                                    (self.packed_weights()[5],)):
+            return 0
+        return ops.hs_spread_blocks(M, 6 * self.channels)
+
     def _highway_stack(self, y: torch.Tensor) -> Optional[torch.Tensor]:
         """pre_highway -> highways -> the GRU's input projection in one launch (the GRU input
-        rows, or None where ops.highway_stack does not apply)."""
+        rows, or None where ops.highway_stack does not apply).  `allow_spread` (set per call
+        by the model's co-residency check) = False keeps the stack kernel."""
         M, Cp = y.size(0) * y.size(1), y.size(2)
         n_out = 6 * self.channels
         if not ops.highway_stack_ok(M, Cp, self.channels, len(self.highways), n_out,
                                     (self.packed_weights()[5],)):
             return None
         pre_f, hw_f, b1s, b2s, ih_f, b_in, n_out = self._stack_pack()
-        xp, _ = ops.highway_stack(y, pre_f, self.channels, hw_f, b1s, b2s, ih_f, b_in, n_out)
+        xp, _ = ops.highway_stack(y, pre_f, self.channels, hw_f, b1s, b2s, ih_f, b_in, n_out,
+                                  spread=getattr(self, 'allow_spread', True))
         return xp
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

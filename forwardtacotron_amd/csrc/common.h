@@ -18,4 +18,21 @@ static inline bool ftmi_aligned16(const void *p) { return ((uintptr_t)p & 15u) =
 
 static inline hipStream_t ftmi_hs(ftmi_stream_t s) { return (hipStream_t)s; }
 
+// CUs a persistent grid may count on: the device's, or fewer when a test lowers it
+// (ftmi_set_resident_cu_limit; defined in seq.hip)
+__attribute__((visibility("hidden"))) int ftmi_resident_cus(void);
+
+// Persistent-launch guard (rnn_bidir, rnn_gemv, highway_stack_spread, wavernn: workgroups
+// that wait on each other).  Every workgroup of the grid must be resident at once, so the
+// kernel's occupancy at this block size / LDS times the CU count must cover the grid;
+// otherwise the caller returns FTMI_E_UNSUPPORTED before launching anything (instead of
+// relying on a spin bound to turn the deadlock into a status bit).
+static inline int ftmi_resident_ok(const void *kernel, int grid, int block, size_t smem) {
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, smem) != hipSuccess ||
+      per <= 0)
+    return FTMI_E_UNSUPPORTED;
+  return (int64_t)per * ftmi_resident_cus() >= grid ? FTMI_OK : FTMI_E_UNSUPPORTED;
+}
+
 __device__ __forceinline__ float ftmi_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }

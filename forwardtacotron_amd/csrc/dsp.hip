@@ -537,3 +537,297 @@ extern "C" int ftmi_unit_phases(const double *u, int32_t B, int32_t n_bins, int3
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
 }
+
+// ==========================================================================================
+// The fused Griffin-Lim iteration (round 6): one launch per iteration instead of the ISTFT
+// frame kernel (fp64 frames through HBM: (B, F, 1024) x 8 B), the overlap-add kernel and the
+// analysis kernel.  A workgroup owns a tile of GL_TF consecutive frames of one item:
+//   1. synthesis: the inverse rFFT of every frame whose support reaches the tile's analysis
+//      windows (the tile +- GL_HALO frames: n_fft / hop = 4, plus the reflect padding at the
+//      signal's ends), two real frames per complex fp64 FFT, each wave one pair;
+//   2. overlap-add into a float32 segment in LDS in the reference's frame order (float32
+//      rounding after every add, librosa 0.7.2 istft), then the division by the float32
+//      window sum-square (its own frame-order accumulation) — the audio the tile's frames
+//      analyse, never written to HBM;
+//   3. analysis (center=True reflect padding) of the tile's frames, two per FFT, and the
+//      fast-GL update (momentum, normalise, S * angles) — X to a second buffer (the halo
+//      frames of the neighbouring tiles still read this iteration's X), tprev in place.
+// The final ISTFT is the same kernel with the analysis replaced by the store of the tile's
+// audio samples.  Specialised to the reference configuration n_fft = 1024, hop = 256
+// (config.yaml); other sizes keep the three-kernel path.
+//
+// The FFT: 1024 points per wave, 16 per lane: a radix-16 DFT in registers over stride 64,
+// twiddles, an LDS transpose, a radix-16 DFT in registers, twiddles, a radix-4 DFT across
+// each quad of lanes (DPP quad permutes) — two LDS passes where the radix-2 Stockham
+// kernels above make ten.  fp64 throughout, like numpy.fft under librosa.
+namespace {
+
+constexpr int GLN = 1024, GLHOP = 256, GLNB = GLN / 2 + 1;
+constexpr int GL_TF = 16;    // analysis frames per tile
+constexpr int GL_HALO = 4;   // synthesis frames beyond the tile on each side
+constexpr int GL_SEG = (GL_TF + 2 * GL_HALO - 1) * GLHOP + GLN;  // segment samples
+constexpr int GL_BUF = 1040;  // per-wave LDS buffer (double2): transpose rows of 65
+
+// exp(-2 pi i j / 1024), j in [0, 1024), from the n/2-entry table
+__device__ __forceinline__ double2 gl_tw(const double2 *tw, int j) {
+  double2 w = tw[j & 511];
+  if (j & 512) {
+    w.x = -w.x;
+    w.y = -w.y;
+  }
+  return w;
+}
+
+// 16-point DFT in registers: V[q] = sum_m v[m] w16^(mq) (radix-2 DIF, reordered)
+__device__ __forceinline__ void gl_dft16(double2 (&v)[16]) {
+  const double C1 = 0.92387953251128674, S1 = 0.38268343236508977, C2 = 0.70710678118654752;
+  const double2 W[8] = {make_double2(1.0, 0.0),  make_double2(C1, -S1),  make_double2(C2, -C2),
+                        make_double2(S1, -C1),   make_double2(0.0, -1.0), make_double2(-S1, -C1),
+                        make_double2(-C2, -C2), make_double2(-C1, -S1)};
+#pragma unroll
+  for (int h = 8; h >= 1; h >>= 1) {
+#pragma unroll
+    for (int b = 0; b < 16; b += 2 * h) {
+#pragma unroll
+      for (int j = 0; j < h; ++j) {
+        const double2 u = v[b + j], t = v[b + j + h];
+        v[b + j] = cadd(u, t);
+        v[b + j + h] = (j == 0) ? csub(u, t) : cmul(csub(u, t), W[j * (8 / h)]);
+      }
+    }
+  }
+  constexpr int rev[16] = {0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15};
+  double2 r[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) r[k] = v[rev[k]];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = r[k];
+}
+
+template <int CTRL>
+__device__ __forceinline__ double gl_dpp(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ double2 gl_dpp2(double2 v) {
+  return make_double2(gl_dpp<CTRL>(v.x), gl_dpp<CTRL>(v.y));
+}
+
+// natural-order index k of the FFT output in a wave buffer (a 4-element gap every 256)
+__device__ __forceinline__ int gl_pk(int k) { return k + ((k >> 8) << 2); }
+
+// forward FFT of z[lane + 64 m] = v[m]; the result in buf (gl_pk order).  Every thread of
+// the workgroup calls it (the exchanges use workgroup barriers).
+__device__ void gl_fft1024(double2 (&v)[16], double2 *buf, const double2 *tw) {
+  const int lane = threadIdx.x & 63;
+  gl_dft16(v);
+#pragma unroll
+  for (int q = 1; q < 16; ++q) v[q] = cmul(v[q], gl_tw(tw, lane * q));
+#pragma unroll
+  for (int q = 0; q < 16; ++q) buf[q * 65 + lane] = v[q];
+  __syncthreads();
+  const int q = lane >> 2, l2 = lane & 3;
+#pragma unroll
+  for (int l1 = 0; l1 < 16; ++l1) v[l1] = buf[q * 65 + 4 * l1 + l2];
+  __syncthreads();
+  gl_dft16(v);
+#pragma unroll
+  for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], gl_tw(tw, 16 * l2 * k1));
+  // 4-point DFT over l2 across the quad: lanes (0, 1, 2, 3) end with Y[0], Y[2], Y[1], Y[3]
+#pragma unroll
+  for (int k1 = 0; k1 < 16; ++k1) {
+    const double2 p = gl_dpp2<0x4E>(v[k1]);  // lane ^ 2
+    double2 r = (l2 < 2) ? cadd(v[k1], p) : csub(p, v[k1]);
+    if (l2 == 3) r = make_double2(r.y, -r.x);  // (-i) (x1 - x3)
+    const double2 p2 = gl_dpp2<0xB1>(r);       // lane ^ 1
+    v[k1] = (l2 & 1) ? csub(p2, r) : cadd(r, p2);
+  }
+  const int k2 = ((l2 & 1) << 1) | (l2 >> 1);
+#pragma unroll
+  for (int k1 = 0; k1 < 16; ++k1) buf[gl_pk(q + 16 * k1 + 256 * k2)] = v[k1];
+  __syncthreads();
+}
+
+struct GlParams {
+  const float2 *Xin;
+  float2 *Xout;
+  const float *S;
+  float2 *tprev;
+  int B, F, tiles;
+  const int32_t *frames;
+  const double *window, *win_sq;
+  const double2 *tw;
+  float c;
+  int first;
+  float *y;
+  int64_t y_stride, y_len;
+};
+
+template <int W, bool FINAL>
+__global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
+  __shared__ float seg[GL_SEG];
+  __shared__ double2 bufs[W][GL_BUF];
+  const int b = blockIdx.x / p.tiles, t = blockIdx.x - b * p.tiles;
+  const int Fb = p.frames ? min(p.frames[b], p.F) : p.F;
+  const int f0 = t * GL_TF;
+  if (f0 >= Fb) return;
+  const int f1 = min(f0 + GL_TF, Fb);
+  const int a0 = max(0, f0 - GL_HALO), a1 = min(Fb, f1 + GL_HALO);
+  const int64_t sb = (int64_t)a0 * GLHOP;                  // segment start (uncropped samples)
+  const int slen = (a1 - 1 - a0) * GLHOP + GLN;
+  const int64_t L = (int64_t)GLHOP * (Fb - 1);             // istft length of item b
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const double scale = 1.0 / GLN;
+  double2 *buf = bufs[w];
+  for (int i = threadIdx.x; i < slen; i += 64 * W) seg[i] = 0.f;
+
+  // ---- 1 + 2: synthesis and overlap-add, W frame pairs per round
+  const int nsyn = a1 - a0;
+  for (int r0 = 0; r0 < nsyn; r0 += 2 * W) {
+    const int fa = a0 + r0 + 2 * w, fb = fa + 1;
+    const bool va = fa < a1, vb = fb < a1;
+    double2 v[16];
+    const float2 *XA = p.Xin + ((int64_t)b * p.F + fa) * GLNB;
+    const float2 *XB = XA + GLNB;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int k = lane + 64 * m;
+      const bool mirror = k > GLN / 2;
+      const int kk = mirror ? GLN - k : k;
+      const float2 a32 = va ? XA[kk] : make_float2(0.f, 0.f);
+      const float2 b32 = vb ? XB[kk] : make_float2(0.f, 0.f);
+      double ar = a32.x, ai = a32.y, br = b32.x, bi = b32.y;
+      if (kk == 0 || kk == GLN / 2) ai = bi = 0.0;  // c2r ignores imag of DC / Nyquist
+      if (mirror) {
+        ai = -ai;
+        bi = -bi;
+      }
+      // conj(A_full + i B_full): the inverse FFT as conj(FFT(conj z))
+      v[m] = make_double2(ar - bi, -(ai + br));
+    }
+    gl_fft1024(v, buf, p.tw);
+    // overlap-add of this round's frames, each sample's frames in increasing order
+    const int rf0 = a0 + r0, rf1 = min(a1, rf0 + 2 * W);
+    const int s_lo = rf0 * GLHOP, s_hi = (rf1 - 1) * GLHOP + GLN;
+    for (int s = s_lo + threadIdx.x; s < s_hi; s += 64 * W) {
+      float acc = seg[s - sb];
+      const int ihi = min(rf1 - 1, s / GLHOP);
+      const int ilo = max(rf0, (s - GLN + GLHOP) / GLHOP);
+      for (int i = ilo; i <= ihi; ++i) {
+        const int off = s - i * GLHOP;
+        const double2 z = bufs[(i - rf0) >> 1][gl_pk(off)];
+        const double part = ((i - rf0) & 1) ? -z.y : z.x;
+        acc = (float)((double)acc + p.window[off] * (part * scale));
+      }
+      seg[s - sb] = acc;
+    }
+    __syncthreads();
+  }
+  // window sum-square (float32, frame order over every frame of the item), division
+  for (int i = threadIdx.x; i < slen; i += 64 * W) {
+    const int64_t s = sb + i;
+    const int ihi = (int)min((int64_t)Fb - 1, s / GLHOP);
+    const int ilo = (int)max((int64_t)0, (s - GLN + GLHOP) / GLHOP);
+    float w2 = 0.f;
+    for (int k = ilo; k <= ihi; ++k) w2 = (float)((double)w2 + p.win_sq[s - (int64_t)k * GLHOP]);
+    const float v = seg[i];
+    seg[i] = (w2 > 1.17549435e-38f) ? (v / w2) : v;
+  }
+  __syncthreads();
+
+  if constexpr (FINAL) {
+    // the tile's audio samples (cropped by n/2), zeros past the item's length
+    const int64_t j0 = (int64_t)f0 * GLHOP;
+    const int64_t j1 = (f1 == Fb) ? p.y_len : min((int64_t)f1 * GLHOP, p.y_len);
+    float *yb = p.y + (int64_t)b * p.y_stride;
+    for (int64_t j = j0 + threadIdx.x; j < j1; j += 64 * W)
+      yb[j] = (j < L) ? seg[j + GLN / 2 - sb] : 0.f;
+    return;
+  } else {
+    // ---- 3: analysis of the tile's frames and the fast-GL update
+    for (int r0 = 0; r0 < f1 - f0; r0 += 2 * W) {
+      const int fa = f0 + r0 + 2 * w, fb = fa + 1;
+      const bool va = fa < f1, vb = fb < f1;
+      double2 v[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int i = lane + 64 * m;
+        const double wi = p.window[i];
+        const int64_t ja = (int64_t)fa * GLHOP + i - GLN / 2;
+        const double xa = va ? (double)seg[reflect_index(ja, L) + GLN / 2 - sb] : 0.0;
+        const double xb = vb ? (double)seg[reflect_index(ja + GLHOP, L) + GLN / 2 - sb] : 0.0;
+        v[m] = make_double2(wi * xa, vb ? wi * xb : 0.0);
+      }
+      gl_fft1024(v, buf, p.tw);
+      for (int k = lane; k < GLNB; k += 64) {
+        const double2 zk = buf[gl_pk(k)], zn = buf[gl_pk((GLN - k) & (GLN - 1))];
+        const float2 A = make_float2((float)(0.5 * (zk.x + zn.x)), (float)(0.5 * (zk.y - zn.y)));
+        const float2 Bq = make_float2((float)(0.5 * (zk.y + zn.y)), (float)(-0.5 * (zk.x - zn.x)));
+#pragma unroll
+        for (int fr = 0; fr < 2; ++fr) {
+          if (!(fr ? vb : va)) continue;
+          const float2 vv = fr ? Bq : A;
+          const int64_t o = ((int64_t)b * p.F + fa + fr) * GLNB + k;
+          float2 an = vv;
+          if (!p.first) {
+            const float2 tp = p.tprev[o];
+            an.x = (vv.x - (p.c * tp.x));
+            an.y = (vv.y - (p.c * tp.y));
+          }
+          const float d = (cabs_rn(an.x, an.y) + 1e-16f);
+          const float scl = (1.0f / d);
+          an.x = (an.x * scl);
+          an.y = (an.y * scl);
+          const float sv = p.S[o];
+          p.tprev[o] = vv;
+          p.Xout[o] = make_float2((sv * an.x), (sv * an.y));
+        }
+      }
+      __syncthreads();  // buf is the next round's FFT buffer
+    }
+  }
+}
+
+int gl_check(int32_t n_fft, int32_t hop, const double *window, const double *win_sq, const void *tw) {
+  if (!window || !win_sq || !tw) return FTMI_E_ARG;
+  if (n_fft != GLN || hop != GLHOP) return FTMI_E_UNSUPPORTED;
+  return FTMI_OK;
+}
+
+}  // namespace
+
+extern "C" int ftmi_griffinlim_iter(const void *Xin, void *Xout, const float *S, void *tprev,
+                                    int32_t B, int32_t F, const int32_t *frames, int32_t n_fft,
+                                    int32_t hop, const double *window, const double *win_sq,
+                                    const void *twiddle, float c, int32_t first,
+                                    ftmi_stream_t stream) {
+  if (!Xin || !Xout || !S || !tprev || B <= 0 || F <= 0 || Xin == Xout) return FTMI_E_ARG;
+  if (int rc = gl_check(n_fft, hop, window, win_sq, twiddle)) return rc;
+  GlParams p{};
+  p.Xin = (const float2 *)Xin, p.Xout = (float2 *)Xout, p.S = S, p.tprev = (float2 *)tprev;
+  p.B = B, p.F = F, p.tiles = (F + GL_TF - 1) / GL_TF, p.frames = frames;
+  p.window = window, p.win_sq = win_sq, p.tw = (const double2 *)twiddle;
+  p.c = c, p.first = first;
+  hipLaunchKernelGGL((gl_fused_kernel<4, false>), dim3(B * p.tiles), dim3(256), 0, ftmi_hs(stream), p);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
+extern "C" int ftmi_istft_fused(const void *X, int32_t B, int32_t F, const int32_t *frames,
+                                int32_t n_fft, int32_t hop, const double *window,
+                                const double *win_sq, const void *twiddle, float *y,
+                                int64_t y_stride, int64_t y_len, ftmi_stream_t stream) {
+  if (!X || !y || B <= 0 || F <= 0 || y_len < 0 || y_stride < y_len) return FTMI_E_ARG;
+  if (int rc = gl_check(n_fft, hop, window, win_sq, twiddle)) return rc;
+  GlParams p{};
+  p.Xin = (const float2 *)X;
+  p.B = B, p.F = F, p.tiles = (F + GL_TF - 1) / GL_TF, p.frames = frames;
+  p.window = window, p.win_sq = win_sq, p.tw = (const double2 *)twiddle;
+  p.y = y, p.y_stride = y_stride, p.y_len = y_len;
+  hipLaunchKernelGGL((gl_fused_kernel<4, true>), dim3(B * p.tiles), dim3(256), 0, ftmi_hs(stream), p);
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}

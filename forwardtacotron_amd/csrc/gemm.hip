@@ -4720,6 +4720,13 @@ extern "C" int ftmi_highway_stack_spread(const float *x, int64_t x_stride, int64
   // every workgroup resident at once (they wait on each other); n_out split in two halves
   // of n_out / 512 16-column tiles per slice
   if (blocks <= 0 || blocks > cus || (w_out_split && n_out > 3 * HS_NPASS)) return FTMI_E_UNSUPPORTED;
+  {
+    const int nk = w_out_split ? n_out / HS_NPASS : 1;
+    const void *k = nk == 1 ? (const void *)highway_spread_kernel<1>
+                  : nk == 2 ? (const void *)highway_spread_kernel<2>
+                            : (const void *)highway_spread_kernel<3>;
+    if (int rc2 = ftmi_resident_ok(k, blocks, 512, 0)) return rc2;
+  }
   const int RB = blocks / HSS_P;
   HsSpread q;
   q.cnt = (unsigned *)ws;

@@ -1045,7 +1045,9 @@ int launch_gemv(RnnParams p, int max_blocks, hipStream_t s) {
   // one direction's BPG workgroups per XCD (the census seats direction x on XCD x; the
   // other XCDs' workgroups retire after the census barrier)
   const int nblk = p.xcd_local ? 8 * BPG : 2 * BPG;
-#define FTMI_GEMV_LAUNCH(NBV_)                                                           \
+#define FTMI_GEMV_LAUNCH(NBV_)                                                             \
+  if (int rc = ftmi_resident_ok((const void *)rnn_gemv_kernel<CELL, H, U, NBV_, KSEG>, nblk, NT, 0)) \
+    return rc;                                                                               \
   hipLaunchKernelGGL((rnn_gemv_kernel<CELL, H, U, NBV_, KSEG>), dim3(nblk), dim3(NT), 0, s, p); \
   break;
   switch (p.B) {
@@ -1085,6 +1087,9 @@ int launch_rnn(RnnParams p, int nchunks, int max_blocks, hipStream_t s) {
     int nblk = p.ngroups * BPG;
     if (BPG > 1 && pad_env && p.xcd_local && p.ngroups < 8 && 8 * BPG <= max_blocks)
       nblk = 8 * BPG;
+    if (int rc = ftmi_resident_ok((const void *)rnn_bidir_kernel<CELL, H, U, WK, MODE, CST, NBL>,
+                                  nblk, BPG == 1 ? 256 : 320, 0))
+      return rc;
     hipLaunchKernelGGL((rnn_bidir_kernel<CELL, H, U, WK, MODE, CST, NBL>), dim3(nblk),
                        dim3(BPG == 1 ? 256 : 320), 0, s, p);
     FTMI_CHECK_LAUNCH();

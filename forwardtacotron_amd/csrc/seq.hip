@@ -338,7 +338,28 @@ extern "C" int ftmi_rowdot(const float *x, int64_t x_stride, int64_t M, int32_t 
   return FTMI_OK;
 }
 
-extern "C" int ftmi_abi_version(void) { return 18; }
+extern "C" int ftmi_abi_version(void) { return 19; }
+
+static int g_cu_limit = 0;
+
+extern "C" int32_t ftmi_set_resident_cu_limit(int32_t cus) {
+  const int prev = g_cu_limit;
+  g_cu_limit = cus > 0 ? cus : 0;
+  return prev;
+}
+
+__attribute__((visibility("hidden"))) int ftmi_resident_cus(void) {
+  static int dev_cus = 0;
+  if (dev_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      dev_cus = n;
+    else
+      return 0;  // no device: nothing can be resident
+  }
+  return (g_cu_limit > 0 && g_cu_limit < dev_cus) ? g_cu_limit : dev_cus;
+}
 
 extern "C" const char *ftmi_strerror(int code) {
   switch (code) {

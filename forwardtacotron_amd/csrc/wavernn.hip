@@ -234,6 +234,9 @@ __device__ __forceinline__ void acquire_vec(const WrParams &p, WrShared<NBV, NI>
     if (((tid + i * NT) >> 7) < p.B) stale |= 1u << i;
   }
   for (unsigned spins = 0; stale; ++spins) {
+    // compiler memory barrier: the poll stores nothing, so LICM could hoist the loads out
+    // and spin on stale values (as rnn.hip's polls once did)
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int i = 0; i < PER; ++i)
       if (stale & (1u << i))
@@ -298,6 +301,7 @@ __device__ __forceinline__ void acquire_sample(const WrParams &p, WrShared<NBV, 
     if (b < p.B && part * 2 + 16 * i < np) stale |= 1u << i;
   }
   for (unsigned spins = 0; stale; ++spins) {
+    asm volatile("" ::: "memory");  // keep the poll's loads in the loop (see above)
 #pragma unroll
     for (int i = 0; i < PER; ++i)
       if (stale & (1u << i))
@@ -1016,8 +1020,12 @@ extern "C" int ftmi_wavernn(const ftmi_wavernn_args *a, ftmi_stream_t stream) {
     const int bi = (p.B + ni - 1) / ni;
     hipError_t e = hipMemsetAsync(a->workspace, 0, (size_t)ftmi_wavernn_workspace_bytes(), s);
     if (e != hipSuccess) return (int)e;
-#define FTMI_WR_LAUNCH(NBV_, NI_)                                                         \
-  hipLaunchKernelGGL((wavernn_kernel<NBV_, NI_>), dim3(WR_GRID), dim3(WR_NT * NI_), 0, s, p)
+#define FTMI_WR_LAUNCH(NBV_, NI_)                                                            \
+  do {                                                                                       \
+    if (int rc = ftmi_resident_ok((const void *)wavernn_kernel<NBV_, NI_>, WR_GRID, WR_NT * NI_, 0)) \
+      return rc;                                                                             \
+    hipLaunchKernelGGL((wavernn_kernel<NBV_, NI_>), dim3(WR_GRID), dim3(WR_NT * NI_), 0, s, p); \
+  } while (0)
     if (ni == 1) {
       p.B = p.B < WR_NBMAX ? p.B : WR_NBMAX;  // one instance: <= 32 folds per launch
       if (p.B <= 8) FTMI_WR_LAUNCH(8, 1);

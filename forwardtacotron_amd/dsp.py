@@ -17,6 +17,7 @@ Not carried over (outside the hot path, need absent libraries): ``load_wav`` res
 from __future__ import annotations
 
 import ctypes
+import os
 import wave
 from pathlib import Path
 from typing import Any, Dict, Optional, Tuple, Union
@@ -115,7 +116,11 @@ class DspPlan:
         self.nnz = int(rowptr[-1])
         self.rowvals, self.rowptr, self.rowlo = t(vals), t(rowptr), t(lo)
         self.bin_rows, self.bin_w = t(bin_rows), t(bin_w)
-        self.pinv = t(np.linalg.pinv(A64).astype(np.float32))
+        pinv64 = np.linalg.pinv(A64)
+        self.pinv = t(pinv64.astype(np.float32))
+        self.pinv64 = t(pinv64)
+        # librosa util.nnls block width: MAX_MEM_BLOCK // (n_bins * itemsize of float32)
+        self.nnls_cols = max(1, (2 ** 8 * 2 ** 10) // (self.nb * 4))
 
     def frames(self, n_samples: int) -> int:
         return 1 + n_samples // self.hop
@@ -185,14 +190,31 @@ def istft(plan: DspPlan, X: torch.Tensor, frames: Optional[torch.Tensor] = None,
     return y[:, :y_len]
 
 
+NNLS_METHODS = ('lbfgsb', 'fista')
+NNLS_GROUPS = 32  # workgroups per L-BFGS-B block (fixed: the sums, hence S, do not depend on
+                  # how many blocks share a launch)
+NNLS_WS_CAP = 4 << 30  # workspace bytes per launch chunk
+
+
 def mel_to_stft(plan: DspPlan, mel: torch.Tensor, frames: Optional[torch.Tensor] = None,
-                denorm: bool = True, iters: int = 200) -> torch.Tensor:
+                denorm: bool = True, iters: int = 200, method: str = 'lbfgsb') -> torch.Tensor:
     """librosa feature.inverse.mel_to_stft(power=1) of (B, n_mels, F) (log-)mels:
-    (B, F, nb) float32 non-negative magnitudes, frame-major."""
+    (B, F, nb) float32 non-negative magnitudes, frame-major.
+
+    method 'lbfgsb' (default) runs the reference's own NNLS on the device — util.nnls'
+    L-BFGS-B over 127-frame blocks, same iterates to rounding (ftmi_nnls_lbfgsb_*) — so S is
+    the reference's S.  'fista' is the fast per-frame solver (`iters` FISTA steps): a
+    minimiser of the same objective, but the minimiser is not unique, so its S (and the
+    Griffin-Lim wav built on it) is NOT the reference's (tests/test_gpu_dsp.py states by how
+    much)."""
     _need_cuda(mel, frames)
     if mel.dtype != torch.float32 or not mel.is_contiguous() or mel.size(1) != plan.n_mels:
         raise ValueError('contiguous (B, n_mels, F) float32 expected')
+    if method not in NNLS_METHODS:
+        raise ValueError(f'method must be one of {NNLS_METHODS}')
     B, _, F = mel.shape
+    if method == 'lbfgsb':
+        return _nnls_lbfgsb(plan, mel, frames, denorm)
     S = torch.empty(B, F, plan.nb, device=mel.device)
     launch('ftmi_mel_nnls', f'mel_nnls[B={B},F={F},iters={iters}]', 0,
            4.0 * B * F * (plan.n_mels + plan.nb),
@@ -200,6 +222,65 @@ def mel_to_stft(plan: DspPlan, mel: torch.Tensor, frames: Optional[torch.Tensor]
            plan.rowvals.data_ptr(), plan.rowptr.data_ptr(), plan.rowlo.data_ptr(),
            plan.bin_rows.data_ptr(), plan.bin_w.data_ptr(), plan.pinv.data_ptr(),
            ctypes.c_float(plan.inv_L), iters, S.data_ptr(), _stream())
+    return S
+
+
+def _nnls_lbfgsb(plan: DspPlan, mel: torch.Tensor, frames: Optional[torch.Tensor],
+                 denorm: bool) -> torch.Tensor:
+    """The host loop around ftmi_nnls_lbfgsb_* — what scipy's fmin_l_bfgs_b driver is around
+    setulb: start, then cycles (every block advances one L-BFGS-B iteration or one extra
+    line-search evaluation per cycle) until the device's count of running blocks reads 0.
+    Blocks as librosa 0.7.2 util.nnls cuts them (127 frames of each item's mel)."""
+    lib = _lib.load()
+    B, _, F = mel.shape
+    dev = mel.device
+    fr = [F] * B if frames is None else [min(int(v), F) for v in frames.cpu().tolist()]
+    nc = plan.nnls_cols
+    blocks = [(b, s0, min(nc, fb - s0), 0) for b, fb in enumerate(fr) for s0 in range(0, fb, nc)]
+    S = torch.empty(B, F, plan.nb, device=dev)
+    fr_dev = None if frames is None else frames.to(device=dev, dtype=torch.int32)
+    if not blocks:
+        S.zero_()
+        return S
+    stream = _stream()
+    m = 32
+    i = 0
+    while i < len(blocks):
+        per = lib.ftmi_nnls_lbfgsb_workspace_bytes(1, plan.nb, nc, m, NNLS_GROUPS)
+        nblk = max(1, min(len(blocks) - i, NNLS_WS_CAP // per))
+        chunk = blocks[i:i + nblk]
+        ws = torch.empty(per * nblk, dtype=torch.uint8, device=dev)
+        bt = torch.tensor(chunk, dtype=torch.int32, device=dev)
+        active = torch.full((1,), nblk, dtype=torch.int32, device=dev)
+        status = torch.zeros(2, dtype=torch.int32, device=dev)
+        a = _lib.NnlsArgs(mel.data_ptr(), B, F, plan.n_mels, plan.nb, int(denorm), bt.data_ptr(),
+                          nblk, NNLS_GROUPS, m, nc, plan.rowvals.data_ptr(), plan.rowptr.data_ptr(),
+                          plan.rowlo.data_ptr(), plan.bin_rows.data_ptr(), plan.bin_w.data_ptr(),
+                          plan.pinv64.data_ptr(), ws.data_ptr(), S.data_ptr(), active.data_ptr())
+        ap = ctypes.byref(a)
+        launch('ftmi_nnls_lbfgsb_start', f'nnls_lbfgsb_start[blocks={nblk}]', 0, 0, ap, stream)
+        cycles, step = 0, 4
+        while True:
+            launch('ftmi_nnls_lbfgsb_cycles', f'nnls_lbfgsb_cycles[blocks={nblk}]', 0, 0, ap, step,
+                   stream)
+            cycles += step
+            if int(active.item()) == 0:
+                break
+            if cycles > 20 * 15000:
+                raise RuntimeError('L-BFGS-B NNLS did not finish')
+            step = min(2 * step, 64)
+        launch('ftmi_nnls_lbfgsb_finish', f'nnls_lbfgsb_finish[blocks={nblk}]', 0, 0, ap,
+               _p(fr_dev), status.data_ptr(), stream)
+        st = status.cpu().tolist()
+        if st[0] & 4 and m < plan.nb:
+            # history full (more than 32 updates: the synthetic-weights mels of the tests take
+            # ~150): rerun the chunk with the reference's whole history, m = n_bins
+            m = plan.nb
+            continue
+        if st[0]:
+            raise RuntimeError(f'L-BFGS-B NNLS failed (status {st[0]}: 2 abnormal line search, '
+                               '4 history wrap, 8 equal breakpoints, 16 maxiter)')
+        i += nblk
     return S
 
 
@@ -213,6 +294,13 @@ def griffinlim_from_stft(plan: DspPlan, S: torch.Tensor, angles: torch.Tensor, n
     return _gl_loop(plan, S, angles, n_iter, frames, momentum)
 
 
+def _gl_fused(plan: DspPlan) -> bool:
+    """The one-launch-per-iteration kernels (ftmi_griffinlim_iter / ftmi_istft_fused) cover the
+    reference configuration n_fft = 1024, hop = 256; FTMI_GL_FUSED=0 keeps the three-kernel
+    path (A/B runs)."""
+    return plan.n_fft == 1024 and plan.hop == 256 and os.environ.get('FTMI_GL_FUSED', '1') != '0'
+
+
 def _gl_loop(plan: DspPlan, S: torch.Tensor, angles: torch.Tensor, n_iter: int,
              frames: Optional[torch.Tensor], momentum: float) -> torch.Tensor:
     B, F, nb = S.shape
@@ -221,11 +309,26 @@ def _gl_loop(plan: DspPlan, S: torch.Tensor, angles: torch.Tensor, n_iter: int,
     launch('ftmi_spec_mul', f'spec_mul[n={S.numel()}]', 0, 20.0 * S.numel(),
            S.data_ptr(), angles.data_ptr(), S.numel(), X.data_ptr(), _stream())
     tprev = torch.empty_like(X)
+    L = plan.hop * (F - 1)
+    c = float(np.float32(momentum / (1 + momentum)))
+    if _gl_fused(plan):
+        # X read (+ the halo frames) and written to the other buffer, S read, tprev r/w
+        X2 = torch.empty_like(X)
+        for it in range(n_iter):
+            launch('ftmi_griffinlim_iter', f'gl_iter[B={B},F={F}]', 0, 44.0 * S.numel(),
+                   X.data_ptr(), X2.data_ptr(), S.data_ptr(), tprev.data_ptr(), B, F, _p(frames),
+                   plan.n_fft, plan.hop, plan.window.data_ptr(), plan.win_sq.data_ptr(),
+                   plan.twiddle.data_ptr(), ctypes.c_float(c), int(it == 0), _stream())
+            X, X2 = X2, X
+        y = torch.empty(B, max(L, 1), device=dev)
+        launch('ftmi_istft_fused', f'istft_fused[B={B},F={F}]', 0, 8.0 * S.numel() + 4.0 * B * L,
+               X.data_ptr(), B, F, _p(frames), plan.n_fft, plan.hop, plan.window.data_ptr(),
+               plan.win_sq.data_ptr(), plan.twiddle.data_ptr(), y.data_ptr(), y.stride(0), L,
+               _stream())
+        return y[:, :L]
     work = torch.empty(_lib.load().ftmi_istft_workspace_bytes(B, F, plan.n_fft), dtype=torch.uint8,
                        device=dev)
-    L = plan.hop * (F - 1)
     lengths = None if frames is None else (plan.hop * (frames - 1)).to(torch.int32)
-    c = float(np.float32(momentum / (1 + momentum)))
     for it in range(n_iter):
         y = istft(plan, X, frames, L, work)
         launch('ftmi_griffinlim_stft', f'gl_stft[B={B},F={F}]', 0, 4.0 * B * L + 28.0 * S.numel(),
@@ -267,6 +370,9 @@ class DSP:
         self.voc_mode = voc_mode
         self._plans: Dict[Any, DspPlan] = {}
         self.nnls_iters = 200
+        # 'lbfgsb': the reference's NNLS (librosa util.nnls), reproduced; 'fista': the fast
+        # per-frame solver (another minimiser of the same objective, not the reference's S)
+        self.nnls = 'lbfgsb'
 
     @classmethod
     def from_config(cls, config: Dict[str, Any]) -> 'DSP':
@@ -332,12 +438,14 @@ class DSP:
         rng = np.random if random_state is None else np.random.RandomState(random_state)
         return rng.rand(self.n_fft // 2 + 1, T)
 
-    def griffinlim(self, mel, n_iter: int = 32, angles=None, random_state=None, uniforms=None):
+    def griffinlim(self, mel, n_iter: int = 32, angles=None, random_state=None, uniforms=None,
+                   nnls: Optional[str] = None):
         """exp -> mel_to_stft (NNLS) -> fast Griffin-Lim (32 iterations, momentum 0.99).
         numpy (n_mels, T) -> numpy wav of hop * (T - 1) samples.  The initial phases are
         exp(2 pi i U[0,1)) drawn like librosa (np.random, or RandomState(random_state)),
         shape (n_bins, T); pass `uniforms` (draw_uniforms) to use a draw made ahead, or
-        `angles` to fix the phases."""
+        `angles` to fix the phases.  nnls: 'lbfgsb' (the reference's magnitudes; default
+        self.nnls) or 'fista' (fast, another minimiser)."""
         is_t = isinstance(mel, torch.Tensor)
         m = mel if is_t else torch.from_numpy(np.ascontiguousarray(mel, dtype=np.float32)).cuda()
         _need_cuda(m)
@@ -345,7 +453,8 @@ class DSP:
         T = m.shape[-1]
         # the NNLS magnitudes first: queued on the device, they run while the host draws the
         # initial phases below (the draw does not depend on them)
-        S = mel_to_stft(plan, m.float().reshape(1, plan.n_mels, T).contiguous(), iters=self.nnls_iters)
+        S = mel_to_stft(plan, m.float().reshape(1, plan.n_mels, T).contiguous(), iters=self.nnls_iters,
+                        method=nnls or self.nnls)
         if angles is None:
             # the reference's draw (librosa: np.random.rand(n_bins, T)); exp(2 pi i u) and the
             # frame-major layout on the device (ftmi_unit_phases: the host exp of 420 k
@@ -366,8 +475,8 @@ class DSP:
         return wav if is_t else wav.cpu().numpy()
 
     def griffinlim_batch(self, mel: torch.Tensor, frames: Optional[torch.Tensor] = None,
-                         n_iter: int = 32, generator: Optional[torch.Generator] = None
-                         ) -> Tuple[torch.Tensor, torch.Tensor]:
+                         n_iter: int = 32, generator: Optional[torch.Generator] = None,
+                         nnls: Optional[str] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Batched Griffin-Lim of (B, n_mels, F) device mels (item b uses its first
         frames[b] frames): returns (wav (B, hop*(F-1)), samples per item).  Initial phases
         from torch's generator on the device."""
@@ -379,7 +488,7 @@ class DSP:
         angles = torch.empty(B, F, plan.nb, dtype=torch.complex64, device=mel.device)
         launch('ftmi_unit_phases', f'unit_phases[B={B},T={F}]', 0, 16.0 * B * plan.nb * F,
                u.data_ptr(), B, plan.nb, F, angles.data_ptr(), _stream())
-        S = mel_to_stft(plan, mel.float().contiguous(), fr, iters=self.nnls_iters)
+        S = mel_to_stft(plan, mel.float().contiguous(), fr, iters=self.nnls_iters, method=nnls or self.nnls)
         wav = griffinlim_from_stft(plan, S, angles, n_iter, fr)
         n = plan.hop * ((fr if fr is not None else torch.full((B,), F, device=mel.device)) - 1)
         return wav, n

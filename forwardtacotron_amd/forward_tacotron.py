@@ -296,16 +296,24 @@ class ForwardTacotron(nn.Module):
             cache[device] = [torch.cuda.Stream(device=device), torch.cuda.Stream(device=device),
                              torch.cuda.Stream(device=device, priority=prio)]
         fits = self.__dict__.setdefault('_ftmi_concurrent', {})
-        key = (device, B, T, ops.RNN_MMA, bool(ops._FORCED))
+        key = (device, B, T, ops.RNN_MMA, bool(ops._FORCED), os.environ.get('FTMI_HS_SPREAD', '1'))
         if key not in fits:
             preds = (self.dur_pred.rnn, self.pitch_pred.rnn, self.energy_pred.rnn)
             need = sum(ops.rnn_blocks(r.cell, B, r.hidden) for r in preds)
             # the prenet stream's persistent kernels (the spread CBHG tail, then the prenet
-            # GRU) run one after the other on it: the larger of the two beside the predictors
+            # GRU) run one after the other on it: the larger of the two beside the predictors.
+            # The spread tail counts only where it would run (the fused stack applies and
+            # spreads at this row count); where predictors + spread tail would not fit, the
+            # tail takes the one-workgroup-per-64-rows stack kernel (nothing to co-schedule)
+            # and the phase stays concurrent (~900 prenet rows)
             pre = ops.rnn_blocks(self.prenet.rnn.cell, B, self.prenet.rnn.hidden)
-            need += max(pre, ops.hs_spread_blocks(B * T, 6 * self.prenet.channels))
-            fits[key] = 0 < need <= ops._num_cus() and pre > 0
-        if not fits[key]:
+            spread = self.prenet.spread_blocks(B * T)
+            cus = ops._num_cus()
+            use_spread = spread > 0 and need + max(pre, spread) <= cus
+            fits[key] = (0 < need + pre <= cus and pre > 0, use_spread)
+        concurrent, use_spread = fits[key]
+        self.prenet.allow_spread = use_spread
+        if not concurrent:
             main = torch.cuda.current_stream(device)
             return [main, main, main]
         return cache[device]

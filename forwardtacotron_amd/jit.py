@@ -87,15 +87,39 @@ def device_model(config: str, weights: List[torch.Tensor]) -> nn.Module:
                                f'{len(keys)} state_dict keys')
         from .forward_tacotron import ForwardTacotron
         m = ForwardTacotron(**cfg['kwargs'])
-        sd = dict(zip(keys, weights))
-        sd['step'] = m.step
-        m.load_state_dict(sd)
-        m = m.to(dev).eval()
+        if all(w.device == dev for w in weights):
+            # the weights already live on the compute device (a scripted GPU model): build the
+            # device model AROUND them — its parameters / buffers share their storage, so the
+            # device holds one copy (load_state_dict + .to() made a second one)
+            own = dict(m.named_parameters())
+            own.update(m.named_buffers())
+            for k, w in zip(keys, weights):
+                t = own[k]
+                if t.shape != w.shape or t.dtype != w.dtype:
+                    raise RuntimeError(f'ftmi TorchScript archive: {k} is {tuple(w.shape)} '
+                                       f'{w.dtype}, the model expects {tuple(t.shape)} {t.dtype}')
+                t.data = w
+            m = m.to(dev).eval()  # moves only `step`; the shared tensors are already there
+        else:
+            sd = dict(zip(keys, weights))
+            sd['step'] = m.step
+            m.load_state_dict(sd)
+            m = m.to(dev).eval()
         ent = (list(weights), m)
         while len(_CACHE) >= CACHE_SIZE:
             _CACHE.popitem(last=False)
     _CACHE[key] = ent  # most recently used last
     return ent[1]
+
+
+def clear_cache() -> None:
+    """Drop the cached device models (their weight packs and HIP graphs).  Storage sharing
+    has the limits of any TorchScript attribute: the scripted module holds the tensors it was
+    scripted with, so re-assigning the eager model's parameters afterwards (`.to()`,
+    `param.data = ...`) leaves the scripted module on the old tensors — script again after
+    moving a model; in-place updates of the shared tensors ARE seen (the cache key carries
+    each tensor's version)."""
+    _CACHE.clear()
 
 
 def _outputs(out: Dict[str, torch.Tensor], device) -> Tuple[torch.Tensor, ...]:

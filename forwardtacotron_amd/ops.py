@@ -189,7 +189,8 @@ def _split_k(M: int, N: int, K: int, mma: int, slab: bool = False, Cin: int = 0)
     if slab:
         # one workgroup per CU: model the time as (rounds of workgroups) x (steps per
         # workgroup, ~1.8 us each) + the partial-sum round trip of a split (sp x M x N fp32
-        # written and read back at ~5 TB/s, plus the finishing launch)
+        # written and read back, priced at 1 TB/s, plus 20 us for the finishing launch —
+        # calibrated below)
         tiles = -(-M // 256) * -(-N // 128)
         cus = _num_cus()
         nch = -(-Cin // 32)
@@ -540,11 +541,13 @@ def highway_stack_ok(M: int, Cp: int, C: int, L: int, n_out: int, splits) -> boo
 
 def highway_stack(x: torch.Tensor, pre_split: torch.Tensor, C: int, hw_splits, b1s, b2s,
                   out_split: Optional[torch.Tensor], b_out: Optional[torch.Tensor], n_out: int,
-                  want_h: bool = False):
+                  want_h: bool = False, spread: bool = True):
     """CBHG pre_highway -> highways -> GRU input projection in one launch
     (`ftmi_highway_stack`; models/common_layers.py:110-115).  x: (B, T, Cp) channels-last;
-    every weight block is `split_weights_f16(w, frag=True)`.  Returns (y (B, T, n_out) or
-    None, h (B, T, C) or None)."""
+    every weight block is `split_weights_f16(w, frag=True)`.  spread=False keeps the
+    one-workgroup-per-64-rows kernel where the spread one would apply (its workgroups must
+    be co-resident: the caller decides).  Returns (y (B, T, n_out) or None, h (B, T, C) or
+    None)."""
     _dev(x, pre_split, out_split, b_out, *hw_splits, *b1s, *b2s)
     B, T, Cp, xs = _rows(x)
     M = B * T
@@ -561,7 +564,7 @@ def highway_stack(x: torch.Tensor, pre_split: torch.Tensor, C: int, hw_splits, b
             ctypes.addressof(b1_arr), ctypes.addressof(b2_arr), _ptr(out_split), _ptr(b_out),
             n_out if out_split is not None else 0, _ptr(y), y.stride(1) if y is not None else 0,
             _ptr(h), h.stride(1) if h is not None else 0, status_word(x.device).data_ptr())
-    if hs_spread_blocks(M, n_out if out_split is not None else 0) > 0:
+    if spread and hs_spread_blocks(M, n_out if out_split is not None else 0) > 0:
         ws = _spread_workspace(int(_lib.load().ftmi_highway_stack_spread_ws_bytes(M)), x.device)
         launch('ftmi_highway_stack_spread', f'highway_stack_spread[M={M},Cp={Cp},L={L},N={n_out}]',
                flops, nbytes, *args, ws.data_ptr(), _stream())

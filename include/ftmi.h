@@ -82,7 +82,8 @@ enum { FTMI_BANK_COUNTERS = 4096 };
  * 15: FTMI_BANK_HALVES, ftmi_conv_bank_halves_ws_floats; 16: FTMI_BANK_IMAGE,
  * ftmi_conv_bank_halves_image[_bytes]; 17: FTMI_BANK_PAIR, ftmi_conv_args.x_plane / x_fin;
  * 18: rejected variants removed — FTMI_BANK_LAST, FTMI_BANK_PAIR, ftmi_conv_args.x_plane /
- * x_fin, ftmi_gru_bidir_fused; ftmi_highway_stack_spread[_ws_bytes|_blocks] added). */
+ * x_fin, ftmi_gru_bidir_fused; ftmi_highway_stack_spread[_ws_bytes|_blocks] added;
+ * 19: ftmi_nnls_lbfgsb_*, ftmi_set_resident_cu_limit, the persistent-launch guard). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
@@ -90,6 +91,12 @@ int ftmi_abi_version(void);
 const char *ftmi_build_id(void);
 /* Static string for an error code (FTMI_E_* or hipError_t). */
 const char *ftmi_strerror(int code);
+/* Persistent kernels (ftmi_rnn_bidir, ftmi_highway_stack_spread, ftmi_wavernn) hold every
+ * workgroup of their grid resident while they wait on each other: each checks, before it
+ * launches anything, that the kernel's occupancy times the CU count covers its grid, and
+ * returns FTMI_E_UNSUPPORTED otherwise (ABI 19).  This sets the CU count the check assumes
+ * (0 = the device's; a test hook for the refusal path); returns the previous setting. */
+int32_t ftmi_set_resident_cu_limit(int32_t cus);
 
 /* ------------------------------------------------------------------------------------
  * Embedding gather.  out[n, :] = table[ids[n], :]
@@ -449,6 +456,24 @@ int ftmi_istft(const void *X, int32_t B, int32_t F, const int32_t *frames, int32
                int32_t hop, const double *window, const double *win_sq, const void *twiddle,
                void *work, float *y, int64_t y_stride, int64_t y_len, ftmi_stream_t stream);
 
+/* One fast Griffin-Lim iteration in ONE launch (ABI 19; librosa 0.7.2 core.griffinlim loop
+ * body, utils/dsp.py:91-102): rebuilt = stft(istft(Xin)); angles = rebuilt - c * tprev
+ * (first: rebuilt); angles /= |angles| + 1e-16; Xout = S * angles; tprev = rebuilt — the
+ * ISTFT (fp64 irfft, float32 overlap-add in frame order, window sum-square division,
+ * center crop) and the STFT (reflect padding) of ftmi_istft / ftmi_griffinlim_stft, fused
+ * per tile of 16 frames with the audio kept on chip.  Xin != Xout (neighbouring tiles read
+ * Xin's halo frames); spectra (B, F, n_fft/2+1) complex64 frame-major, item b's first
+ * frames[b] frames (NULL: F).  n_fft = 1024, hop = 256 only (else FTMI_E_UNSUPPORTED).
+ * window / win_sq: [n_fft] float64, twiddle: [n_fft/2] complex128 (the ftmi_stft plan). */
+int ftmi_griffinlim_iter(const void *Xin, void *Xout, const float *S, void *tprev, int32_t B,
+                         int32_t F, const int32_t *frames, int32_t n_fft, int32_t hop,
+                         const double *window, const double *win_sq, const void *twiddle,
+                         float c, int32_t first, ftmi_stream_t stream);
+/* ftmi_istft in one launch, no workspace (ABI 19; same sizes as ftmi_griffinlim_iter). */
+int ftmi_istft_fused(const void *X, int32_t B, int32_t F, const int32_t *frames, int32_t n_fft,
+                     int32_t hop, const double *window, const double *win_sq, const void *twiddle,
+                     float *y, int64_t y_stride, int64_t y_len, ftmi_stream_t stream);
+
 /* mel -> linear magnitude (librosa feature.inverse.mel_to_stft, power=1, via util.nnls):
  * per frame min ||A x - m||^2, x >= 0, m = exp(mel) when denorm (DSP.denormalize
  * :109-110).  Solved by FISTA (`iters` steps of 1/L = inv_L) from the clipped
@@ -461,6 +486,42 @@ int ftmi_mel_nnls(const float *mel, int32_t B, int32_t F, const int32_t *frames,
                   const int32_t *rowptr, const int32_t *rowlo, const int32_t *bin_rows,
                   const float *bin_w, const float *pinv, float inv_L, int32_t iters, float *S,
                   ftmi_stream_t stream);
+
+/* The reference's NNLS itself (ABI 19): librosa 0.7.2 util.nnls — scipy fmin_l_bfgs_b
+ * (L-BFGS-B 3.0, m = n_bins, pgtol 1e-5, factr 1e7, maxls 20) on blocks of up to
+ * `max_frames` frames (127 for n_fft 1024: MAX_MEM_BLOCK // (n_bins * 4)), started from the
+ * float32 least-squares solution clipped at 0 — so S is the reference's to rounding, not
+ * just another minimiser (librosa/util/utils.py nnls, _nnls_lbfgs_block).
+ * blocks: device [n_blocks][4] int32 (item, first frame, frames, 0); groups: workgroups per
+ * block for the sweeps (1..64); m: history columns the workspace holds (the reference keeps
+ * n_bins; a block that needs more stops with bit 4 in status[0]: rerun with a larger m);
+ * pinv: [n_bins][n_mels] float64; active: device int32 the caller sets to n_blocks before
+ * ftmi_nnls_lbfgsb_start — each block decrements it when done.  Drive it like scipy's
+ * driver loop: start, then ftmi_nnls_lbfgsb_cycles (one cycle advances every block by one
+ * L-BFGS-B iteration or one extra line-search evaluation) until *active reads 0, then
+ * ftmi_nnls_lbfgsb_finish (writes S (B, F, n_bins), zero past frames[b]; status: device
+ * int32[2] the caller zeroes: [0] |= failure bits of any block (2 abnormal line search,
+ * 4 history full, 8 > 1024 equal breakpoints, 16 maxiter), [1] = max iterations). */
+typedef struct {
+  const float *mel; /* (B, n_mels, F) */
+  int32_t B, F, n_mels, n_bins, denorm;
+  const int32_t *blocks;
+  int32_t n_blocks, groups, m, max_frames;
+  const float *rowvals;
+  const int32_t *rowptr, *rowlo, *bin_rows;
+  const float *bin_w;
+  const double *pinv;
+  void *workspace; /* ftmi_nnls_lbfgsb_workspace_bytes(n_blocks, n_bins, max_frames, m, groups) */
+  float *S;
+  int32_t *active;
+} ftmi_nnls_lbfgsb_args;
+int64_t ftmi_nnls_lbfgsb_workspace_bytes(int32_t n_blocks, int32_t n_bins, int32_t max_frames,
+                                         int32_t m, int32_t groups);
+int ftmi_nnls_lbfgsb_start(const ftmi_nnls_lbfgsb_args *args, ftmi_stream_t stream);
+int ftmi_nnls_lbfgsb_cycles(const ftmi_nnls_lbfgsb_args *args, int32_t cycles,
+                            ftmi_stream_t stream);
+int ftmi_nnls_lbfgsb_finish(const ftmi_nnls_lbfgsb_args *args, const int32_t *frames,
+                            int32_t *status, ftmi_stream_t stream);
 
 /* ====================================================================================
  * FastPitch transformer (models/fast_pitch.py).  Activations channels-last (B, T, C).

@@ -146,3 +146,33 @@ def test_highway_stack_spread_sizes():
     assert lib.ftmi_highway_stack_spread_blocks(1025) == 0
     assert lib.ftmi_highway_stack_spread_ws_bytes(120) == 2 * 32 * 4 + 2 * 2 * 2 * 64 * 272 * 2
     assert lib.ftmi_highway_stack_spread_ws_bytes(0) == 0
+
+
+@pytest.mark.gpu
+def test_persistent_launch_refused_when_not_resident():
+    """The persistent-launch guard (ABI 19): a spread CBHG tail of 1024 rows needs 256
+    workgroups resident at once; with the CUs the check may count lowered to 8, the entry
+    point returns FTMI_E_UNSUPPORTED before its counter memset or its launch (the status word
+    stays clean: no spin timeout), and runs once the limit is lifted."""
+    import torch
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.common_layers import CBHG
+    torch.manual_seed(3)
+    m = CBHG(K=2, in_channels=256, channels=256, proj_channels=[256, 256], num_highways=4).cuda()
+    x = torch.randn(1, 1024, 256, device='cuda')
+    pre_f, hw_f, b1s, b2s, ih_f, b_in, n_out = m._stack_pack()
+    assert ops.hs_spread_blocks(1024, n_out) == 256
+    lib = _lib.load()
+    st = ops.status_word('cuda')
+    st.zero_()
+    prev = lib.ftmi_set_resident_cu_limit(8)
+    try:
+        with pytest.raises(_lib.FtmiError, match='status 1003'):
+            ops.highway_stack(x, pre_f, 256, hw_f, b1s, b2s, ih_f, b_in, n_out)
+        torch.cuda.synchronize()
+        assert int(st.item()) == 0
+    finally:
+        lib.ftmi_set_resident_cu_limit(prev)
+    y, _ = ops.highway_stack(x, pre_f, 256, hw_f, b1s, b2s, ih_f, b_in, n_out)
+    torch.cuda.synchronize()
+    assert y is not None and torch.isfinite(y).all() and int(st.item()) == 0

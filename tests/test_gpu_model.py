@@ -387,20 +387,6 @@ def test_split_graph_gen_forward_lambdas(gpu_model, monkeypatch):
             assert torch.equal(e[k], o[k]), k
 
 
-def test_bank_pair_generate_bit_identical(gpu_model, monkeypatch):
-    """FTMI_BANK_PAIR=1 (the prenet bank's halves finished in proj1's operand staging) gives
-    generate() the same bits as the default in-kernel finish at batch 1 (the few-row path)."""
-    from forwardtacotron_amd import forward_tacotron as FT
-    x = torch.from_numpy(load_golden('gen_b3')['x'][:1]).cuda()
-    monkeypatch.setattr(FT, 'GRAPH', False)
-    monkeypatch.setenv('FTMI_BANK_PAIR', '0')
-    a = gpu_model.generate(x)
-    monkeypatch.setenv('FTMI_BANK_PAIR', '1')
-    b = gpu_model.generate(x)
-    for k in ('mel', 'mel_post', 'dur', 'pitch', 'energy'):
-        assert torch.equal(a[k], b[k]), k
-
-
 def test_range_guard_rerun_is_checked(monkeypatch, synth_sd):
     """the exact-path rerun triggered by a range bit is status-checked like the
     first pass — a recurrence timeout during the rerun raises RnnTimeout (spin bound 1 in
