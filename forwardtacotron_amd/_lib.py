@@ -50,7 +50,7 @@ class WaveRNNArgs(ctypes.Structure):
 class NnlsArgs(ctypes.Structure):
     """Mirror of ftmi_nnls_lbfgsb_args (include/ftmi.h)."""
     _fields_ = [('mel', P)] + [(n, c_int) for n in ('B', 'F', 'n_mels', 'n_bins', 'denorm')] + [
-        ('blocks', P)] + [(n, c_int) for n in ('n_blocks', 'groups', 'm', 'max_frames')] + [
+        ('blocks', P)] + [(n, c_int) for n in ('n_blocks', 'groups', 'm', 'max_frames', 'maxiter', 'dbg_stop')] + [
         (n, P) for n in ('rowvals', 'rowptr', 'rowlo', 'bin_rows', 'bin_w', 'pinv', 'workspace', 'S',
                          'active')]
 
@@ -134,7 +134,7 @@ SIGNATURES = {
     'ftmi_nnls_lbfgsb_workspace_bytes': (c_int64, [c_int, c_int, c_int, c_int, c_int]),
     'ftmi_nnls_lbfgsb_start': (c_int, [ctypes.POINTER(NnlsArgs), P]),
     'ftmi_nnls_lbfgsb_cycles': (c_int, [ctypes.POINTER(NnlsArgs), c_int, P]),
-    'ftmi_nnls_lbfgsb_finish': (c_int, [ctypes.POINTER(NnlsArgs), P, P, P]),
+    'ftmi_nnls_lbfgsb_finish': (c_int, [ctypes.POINTER(NnlsArgs), P, P, P, P]),
 }
 
 

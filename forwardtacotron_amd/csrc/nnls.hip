@@ -40,6 +40,7 @@ constexpr int NW = NT / 64;
 constexpr int CAP = 1024;       // breakpoints sorted per walk chunk
 constexpr int KCHUNK = 256;     // target chunk size
 constexpr int MC = 32;          // history columns whose small matrices the scalar parts stage in LDS
+constexpr int MMAX = 513;       // history columns at most (the reference's m = n_bins for n_fft 1024)
 
 enum Phase { PH_DONE = 0, PH_EVAL = 1, PH_CAUCHY = 2, PH_WALK = 3, PH_FREEV = 4, PH_FORMK = 5,
              PH_SUBSM = 6, PH_BACKTRACK = 7 };
@@ -62,7 +63,7 @@ struct Args {
   const float *mel;   // (B, n_mels, F) (log mel if denorm)
   int B, F, n_mels, nb, denorm;
   const int32_t *blocks;  // [n_blocks][4]: item, first frame, frames, 0
-  int n_blocks, groups, m, mref, ncmax;
+  int n_blocks, groups, m, mref, ncmax, maxiter, dbg_stop;
   const float *rowvals;
   const int32_t *rowptr, *rowlo, *bin_rows;
   const float *bin_w;
@@ -316,6 +317,190 @@ __device__ bool formt(int m, int col, const double *sy, const double *ss, double
   return dpofa(wt, m, col);
 }
 
+
+// ---- wave- / workgroup-parallel forms of the small-matrix routines (long histories: the
+// serial forms above are O(col^2) / O(col^3) chains of dependent loads).  Same operations in
+// the same order per element (column-oriented substitution subtracts in the reference's k
+// order); the right-looking Cholesky reduces each entry in the same j order as dpofa's ddot.
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// element j of a lane-strided register vector (element k lives in lane k % 64, slot k / 64)
+template <int NPL>
+__device__ inline double wget(const double (&r)[NPL], int j) {
+  const int u = j >> 6;
+  double v = 0.0;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q)
+    if (q == u) v = r[q];
+  return __shfl(v, j & 63);
+}
+
+// trans(U) x = b, U upper (dtrsl job 11), x lane-strided in registers; false on a zero pivot
+template <int NPL>
+__device__ bool wtrsl_t(const double *U, int ld, int n, double (&x)[NPL]) {
+  const int lane = threadIdx.x & 63;
+  for (int j = 0; j < n; ++j) {
+    const double d = U[j * ld + j];
+    if (d == 0.0) return false;
+    const double xj = wget<NPL>(x, j) / d;
+#pragma unroll
+    for (int q = 0; q < NPL; ++q) {
+      const int k = lane + 64 * q;
+      if (k == j) x[q] = xj;
+      else if (k > j && k < n) x[q] = x[q] - U[j * ld + k] * xj;
+    }
+  }
+  return true;
+}
+
+// U x = b, U upper (dtrsl job 01)
+template <int NPL>
+__device__ bool wtrsl_n(const double *U, int ld, int n, double (&x)[NPL]) {
+  const int lane = threadIdx.x & 63;
+  for (int j = n - 1; j >= 0; --j) {
+    const double d = U[j * ld + j];
+    if (d == 0.0) return false;
+    const double xj = wget<NPL>(x, j) / d;
+#pragma unroll
+    for (int q = 0; q < NPL; ++q) {
+      const int k = lane + 64 * q;
+      if (k == j) x[q] = xj;
+      else if (k < j) x[q] = x[q] - U[k * ld + j] * xj;
+    }
+  }
+  return true;
+}
+
+// bmv by one wave: p = M v (all 64 lanes call it; v and p in memory, 2 col entries)
+template <int NPL>
+__device__ bool wbmv_t(int ld, int col, const double *sy, const double *wt, const double *v,
+                       double *p) {
+  const int lane = threadIdx.x & 63;
+  double a[NPL], bq[NPL];
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    const int i = lane + 64 * q;
+    a[q] = bq[q] = 0.0;
+    if (i < col) {
+      double sum = 0.0;
+      for (int k = 0; k < i; ++k) sum = sum + sy[i * ld + k] * v[k] / sy[k * ld + k];
+      a[q] = (i == 0) ? v[col] : v[col + i] + sum;
+      bq[q] = v[i] / sqrt(sy[i * ld + i]);
+    }
+  }
+  if (!wtrsl_t<NPL>(wt, ld, col, a)) return false;
+  if (!wtrsl_n<NPL>(wt, ld, col, a)) return false;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    const int i = lane + 64 * q;
+    if (i < col) bq[q] = -bq[q] / sqrt(sy[i * ld + i]);
+  }
+  // p1_i += sum_{k > i} sy(k, i) p2_k / sy(i, i), k ascending
+  double sums[NPL];
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) sums[q] = 0.0;
+  for (int k = 1; k < col; ++k) {
+    const double p2k = wget<NPL>(a, k);
+#pragma unroll
+    for (int q = 0; q < NPL; ++q) {
+      const int i = lane + 64 * q;
+      if (i < k) sums[q] = sums[q] + sy[k * ld + i] * p2k / sy[i * ld + i];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    const int i = lane + 64 * q;
+    if (i < col) {
+      p[i] = bq[q] + sums[q];
+      p[col + i] = a[q];
+    }
+  }
+  wave_sync();
+  return true;
+}
+
+__device__ bool wbmv(int ld, int col, const double *sy, const double *wt, const double *v, double *p) {
+  if (col == 0) return true;
+  if (col <= 64) return wbmv_t<1>(ld, col, sy, wt, v, p);
+  if (col <= 128) return wbmv_t<2>(ld, col, sy, wt, v, p);
+  if (col <= 256) return wbmv_t<4>(ld, col, sy, wt, v, p);
+  return wbmv_t<9>(ld, col, sy, wt, v, p);
+}
+
+// trans(U) x = b then U y = x' with the first `neg` entries of x negated in between (subsm's
+// K^-1: dtrsl 11, negate, dtrsl 01), x in memory (2 col entries), one wave
+template <int NPL>
+__device__ bool wsolve_k_t(const double *U, int ld, int n, int neg, double *x) {
+  const int lane = threadIdx.x & 63;
+  double r[NPL];
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    const int k = lane + 64 * q;
+    r[q] = k < n ? x[k] : 0.0;
+  }
+  if (!wtrsl_t<NPL>(U, ld, n, r)) return false;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q)
+    if (lane + 64 * q < neg) r[q] = -r[q];
+  if (!wtrsl_n<NPL>(U, ld, n, r)) return false;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    const int k = lane + 64 * q;
+    if (k < n) x[k] = r[q];
+  }
+  wave_sync();
+  return true;
+}
+__device__ bool wsolve_k(const double *U, int ld, int n, int neg, double *x) {
+  if (n <= 64) return wsolve_k_t<1>(U, ld, n, neg, x);
+  if (n <= 128) return wsolve_k_t<2>(U, ld, n, neg, x);
+  if (n <= 256) return wsolve_k_t<4>(U, ld, n, neg, x);
+  if (n <= 512) return wsolve_k_t<8>(U, ld, n, neg, x);
+  return wsolve_k_t<17>(U, ld, n, neg, x);
+}
+
+// dpofa by the whole workgroup (right-looking); every thread gets the same result
+__device__ bool wg_dpofa(double *a, int ld, int n) {
+  __shared__ int fail;
+  for (int j = 0; j < n; ++j) {
+    if (threadIdx.x == 0) {
+      const double d = a[j * ld + j];
+      fail = !(d > 0.0);
+      if (!fail) a[j * ld + j] = sqrt(d);
+    }
+    __syncthreads();
+    if (fail) return false;
+    const double piv = a[j * ld + j];
+    for (int k = j + 1 + threadIdx.x; k < n; k += NT) a[j * ld + k] = a[j * ld + k] / piv;
+    __syncthreads();
+    const int mm = n - j - 1;
+    for (int idx = threadIdx.x; idx < mm * mm; idx += NT) {
+      const int i = j + 1 + idx / mm, k = j + 1 + idx % mm;
+      if (k >= i) a[i * ld + k] = a[i * ld + k] - a[j * ld + i] * a[j * ld + k];
+    }
+    __syncthreads();
+  }
+  return true;
+}
+
+// formt by the whole workgroup: T into wt, then its Cholesky factor
+__device__ bool wg_formt(int ld, int col, const double *sy, const double *ss, double theta,
+                         double *wt) {
+  for (int idx = threadIdx.x; idx < col * col; idx += NT) {
+    const int i = idx / col, j = idx - i * col;
+    if (j < i) continue;
+    double ddum = 0.0;
+    for (int k = 0; k < i; ++k) ddum = ddum + sy[i * ld + k] * sy[j * ld + k] / sy[k * ld + k];
+    wt[i * ld + j] = (i == 0) ? theta * ss[j] : ddum + theta * ss[i * ld + j];
+  }
+  __syncthreads();
+  return wg_dpofa(wt, ld, col);
+}
+
 // ---- dcsrch / dcstep (MINPACK-2, as called by lnsrlb: ftol 1e-3, gtol 0.9, xtol 0.1) ----
 __device__ void dcstep(double &stx, double &fx, double &dx, double &sty, double &fy, double &dy,
                        double &stp, double fp, double dp, int &brackt, double stpmin,
@@ -531,15 +716,29 @@ __device__ void ls_begin(NnlsState &s, int *active, double dtd, double gd, doubl
   s.phase = PH_EVAL;
 }
 
-// the GCP is known: cmprlb's wa = M c (bmv), then FREEV
+// the GCP is known: cmprlb's wa = M c (bmv), then FREEV.  Wave-collective (64 lanes);
+// lane 0 writes the state.
 __device__ void gcp_done(NnlsState &s, const Blk &b, int ld, const double *sy, const double *wt,
                          const double *cvec) {
-  if (s.col > 0 && !bmv(ld, s.col, sy, wt, cvec, b.WA)) {
-    refresh(s);
-    s.bk_count = 0;
-    return;
+  const int col = s.col;
+  const bool ok = col == 0 || wbmv(ld, col, sy, wt, cvec, b.WA);
+  if ((threadIdx.x & 63) == 0) {
+    if (!ok) {
+      refresh(s);
+      s.bk_count = 0;
+    } else {
+      s.phase = PH_FREEV;
+    }
   }
-  s.phase = PH_FREEV;
+}
+
+// debug stop (ftmi_nnls_lbfgsb_args.dbg_stop = 16 * iteration + phase): the block ends
+// right before that phase of that iteration, its workspace holding the state it had there
+__device__ inline bool dbg_hit(const Args &a, NnlsState &s, int g) {
+  if (a.dbg_stop == 0 || a.dbg_stop != 16 * s.it + s.phase) return false;
+  __syncthreads();
+  if (g == 0 && threadIdx.x == 0) finish_block(s, a.active, 0);
+  return true;
 }
 
 // ---- phase kernels ---------------------------------------------------------------------------
@@ -557,7 +756,7 @@ __global__ __launch_bounds__(NT) void nnls_start_kernel(const Args a) {
     __syncthreads();
     for (int i = threadIdx.x; i < a.n_mels; i += NT) {
       const float v = a.mel[((int64_t)b.item * a.n_mels + i) * a.F + f];
-      m_s[i] = a.denorm ? (double)expf(v) : (double)v;
+      m_s[i] = a.denorm ? (double)(float)exp((double)v) : (double)v;
     }
     __syncthreads();
     for (int k = threadIdx.x; k < a.nb; k += NT) {
@@ -592,6 +791,7 @@ __global__ __launch_bounds__(NT) void nnls_eval_kernel(const Args a) {
   Blk b = blk_view(a, blk);
   NnlsState &s = *b.st;
   if (s.phase != PH_EVAL) return;
+  if (dbg_hit(a, s, g)) return;
   const bool first = (s.nfev == 0);
   const int cur = s.cur, nxt = first ? cur : cur ^ 1;
   const double stp = s.stp;
@@ -621,7 +821,7 @@ __global__ __launch_bounds__(NT) void nnls_eval_kernel(const Args a) {
     }
     for (int i = threadIdx.x; i < a.n_mels; i += NT) {
       const float v = a.mel[((int64_t)b.item * a.n_mels + i) * a.F + f];
-      diff[i] = a.denorm ? (double)expf(v) : (double)v;
+      diff[i] = a.denorm ? (double)(float)exp((double)v) : (double)v;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < a.n_mels; i += NT) {
@@ -713,7 +913,7 @@ __global__ __launch_bounds__(NT) void nnls_eval_kernel(const Args a) {
     finish_block(s, a.active, ST_CONV);
     return;
   }
-  if (s.it >= 15000) {
+  if (s.it >= a.maxiter) {
     finish_block(s, a.active, ST_MAXITER);
     return;
   }
@@ -755,6 +955,7 @@ __global__ __launch_bounds__(NT) void nnls_cauchy_kernel(const Args a) {
   Blk b = blk_view(a, blk);
   NnlsState &s = *b.st;
   if (s.phase != PH_CAUCHY) return;
+  if (dbg_hit(a, s, g)) return;
   const int m = a.m, ns = nslots(m);
   const int cur = s.cur;
   const double *x = xbuf(b, cur), *gv = gbuf(b, cur), *xprev = xbuf(b, cur ^ 1), *gprev = gbuf(b, cur ^ 1);
@@ -836,9 +1037,9 @@ __global__ __launch_bounds__(NT) void nnls_cauchy_kernel(const Args a) {
     wg_sums<4 * JB>(acc, 4 * JB, red, part + 4 + 4 * j0);
   }
   if (!arrive_last(b.st, a.groups)) return;
-  // ---- scalar part: thread 0, the small matrices staged in LDS when col <= MC ----
+  // ---- scalar part: the small matrices staged in LDS when col <= MC; formt by the whole
+  // workgroup, bmv by wave 0, the state by thread 0 ----
   __shared__ double msy[MC * MC], mss[MC * MC], mwt[MC * MC];
-  __shared__ int wt_back;
   if (threadIdx.x == 0) {
     double f1 = 0.0, rr = 0.0, nfc = 0.0, unb = 0.0;
     for (int q = 0; q < a.groups; ++q) {
@@ -852,6 +1053,7 @@ __global__ __launch_bounds__(NT) void nnls_cauchy_kernel(const Args a) {
     s.rr = rr;
     s.nfree_c = (int)nfc;
     s.bnded = unb > 0.0 ? 0 : 1;
+    s.nbreak = s.bk_count;
     if (pend) {
       // matupd (lbfgsb.f): the new column's S'Y row and S'S column
       const int c = col0;  // 0-based index of the new column
@@ -874,7 +1076,6 @@ __global__ __launch_bounds__(NT) void nnls_cauchy_kernel(const Args a) {
       s.theta = rr / s.dr;
       s.pending = 0;
     }
-    wt_back = 0;
   }
   __syncthreads();
   const int col = coln;
@@ -887,79 +1088,94 @@ __global__ __launch_bounds__(NT) void nnls_cauchy_kernel(const Args a) {
     if (!pend) stage_in(mwt, b.WT, m, col);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const double nbreak = s.bk_count;
-    bool go = true;
-    if (pend) {
-      if (!formt(ld, col, SYp, SSp, s.theta, WTp)) {
-        refresh(s);  // redo the Cauchy step with an empty memory
-        s.bk_count = 0;
-        go = false;
-      } else {
-        wt_back = sm ? 1 : 0;
-      }
+  const double theta = s.theta;
+  bool ok = true;
+  if (pend) ok = wg_formt(ld, col, SYp, SSp, theta, WTp);
+  if (pend && ok && sm) stage_out(b.WT, m, mwt, col);
+  // p, c, M p in LDS (the lanes exchange them), copied out at the end
+  __shared__ double vP[2 * MMAX], vC[2 * MMAX], vV[2 * MMAX];
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  if (!ok) {
+    if (lane == 0) {
+      refresh(s);  // redo the Cauchy step with an empty memory
+      s.bk_count = 0;
     }
-    if (go) {
-      const double theta = s.theta;
-      for (int j = 0; j < col; ++j) {
-        double py = 0.0, ps = 0.0;
-        for (int q = 0; q < a.groups; ++q) {
-          const double *pq = b.PART + q * ns + 4;
-          const int jb = (j / JB) * JB, jj = j - jb;
-          py += pq[4 * jb + jj];
-          ps += pq[4 * jb + JB + jj];
-        }
-        b.P[j] = py;
-        b.P[col + j] = ps * theta;  // dscal(col, theta, p(col+1))
-      }
-      for (int j = 0; j < 2 * col; ++j) b.C[j] = 0.0;
-      const double f1 = s.f1;
-      s.nbreak = (int)nbreak;
-      s.kpassed = 0;
-      s.nseg = 0;
-      s.tsum = 0.0;
-      s.tj = 0.0;
-      s.walk_done = 0;
-      s.nenter = s.nleave = 0;
-      if (s.nbreak == 0 && s.nfree_c == 0) {
-        // d = 0: xcp = x (lbfgsb.f cauchy returns before the loop); c = 0
-        s.dtm = 0.0;
-        s.tsum = 0.0;
-        gcp_done(s, b, ld, SYp, WTp, b.C);
-      } else {
-        double f2 = -theta * f1;
-        s.f2_org = f2;
-        bool ok = true;
-        if (col > 0) {
-          if (!bmv(ld, col, SYp, WTp, b.P, b.V)) {
-            refresh(s);
-            s.bk_count = 0;
-            ok = false;
-          } else {
-            double vp = 0.0;
-            for (int j = 0; j < 2 * col; ++j) vp = vp + b.V[j] * b.P[j];
-            f2 = f2 - vp;
-          }
-        }
-        if (ok) {
-          s.f2 = f2;
-          s.dtm = -f1 / f2;
-          s.nseg = 1;
-          if (s.nbreak == 0) {
-            // goto 888
-            if (s.dtm <= 0.0) s.dtm = 0.0;
-            s.tsum = s.tsum + s.dtm;
-            for (int j = 0; j < 2 * col; ++j) b.C[j] = b.C[j] + s.dtm * b.P[j];
-            gcp_done(s, b, ld, SYp, WTp, b.C);
-          } else {
-            s.phase = PH_WALK;
-          }
-        }
-      }
-    }
+    return;
   }
-  __syncthreads();
-  if (wt_back) stage_out(b.WT, m, mwt, col);
+  for (int j = lane; j < col; j += 64) {
+    double py = 0.0, ps = 0.0;
+    for (int q = 0; q < a.groups; ++q) {
+      const double *pq = b.PART + q * ns + 4;
+      const int jb = (j / JB) * JB, jj = j - jb;
+      py += pq[4 * jb + jj];
+      ps += pq[4 * jb + JB + jj];
+    }
+    vP[j] = py;
+    vP[col + j] = ps * theta;  // dscal(col, theta, p(col+1))
+    vC[j] = 0.0;
+    vC[col + j] = 0.0;
+  }
+  wave_sync();
+  auto flush = [&]() {
+    wave_sync();
+    for (int j = lane; j < 2 * col; j += 64) {
+      b.P[j] = vP[j];
+      b.C[j] = vC[j];
+    }
+  };
+  const int nbreak = s.nbreak;
+  const double f1 = s.f1;
+  if (lane == 0) {
+    s.kpassed = 0;
+    s.nseg = 0;
+    s.tsum = 0.0;
+    s.tj = 0.0;
+    s.walk_done = 0;
+    s.nenter = s.nleave = 0;
+  }
+  if (nbreak == 0 && s.nfree_c == 0) {
+    // d = 0: xcp = x (lbfgsb.f cauchy returns before the loop); c = 0
+    if (lane == 0) s.dtm = 0.0;
+    flush();
+    gcp_done(s, b, ld, SYp, WTp, vC);
+    return;
+  }
+  double vp = 0.0;
+  if (col > 0) {
+    if (!wbmv(ld, col, SYp, WTp, vP, vV)) {
+      if (lane == 0) {
+        refresh(s);
+        s.bk_count = 0;
+      }
+      return;
+    }
+    // v'p in the reference's order (every lane the same sum)
+    for (int j = 0; j < 2 * col; ++j) vp = vp + vV[j] * vP[j];
+  }
+  const double f2o = -theta * f1;
+  const double f2 = f2o - vp;
+  const double dtm0 = -f1 / f2;
+  if (lane == 0) {
+    s.f2_org = f2o;
+    s.f2 = f2;
+    s.dtm = dtm0;
+    s.nseg = 1;
+  }
+  if (nbreak == 0) {
+    // goto 888
+    const double dtm = fmax(dtm0, 0.0);
+    for (int j = lane; j < 2 * col; j += 64) vC[j] = vC[j] + dtm * vP[j];
+    if (lane == 0) {
+      s.dtm = dtm;
+      s.tsum = dtm;
+    }
+    flush();
+    gcp_done(s, b, ld, SYp, WTp, vC);
+    return;
+  }
+  flush();
+  if (lane == 0) s.phase = PH_WALK;
 }
 
 // WALK (one workgroup per block): the breakpoints in increasing order — chunks of the
@@ -970,6 +1186,7 @@ __global__ __launch_bounds__(NT) void nnls_walk_kernel(const Args a) {
   Blk b = blk_view(a, blk);
   NnlsState &s = *b.st;
   if (s.phase != PH_WALK) return;
+  if (dbg_hit(a, s, 0)) return;
   const int m = a.m;
   __shared__ unsigned hist[2048];
   __shared__ unsigned long long skey[CAP];
@@ -980,21 +1197,30 @@ __global__ __launch_bounds__(NT) void nnls_walk_kernel(const Args a) {
   const double *x = xbuf(b, s.cur), *gv = gbuf(b, s.cur);
   // the small matrices and vectors of the serial loop in LDS (col <= MC): the loop's loads
   // form a dependent chain
-  __shared__ double msy[MC * MC], mwt[MC * MC], mp[2 * MC], mc[2 * MC], mwbp[2 * MC], mv[2 * MC];
+  // the vectors of the serial loop always in LDS (lanes exchange them), the matrices too when
+  // col <= MC (read-only here; L2-resident otherwise)
+  __shared__ double msy[MC * MC], mwt[MC * MC], mp[2 * MMAX], mc[2 * MMAX], mwbp[2 * MMAX],
+      mv[2 * MMAX];
   const int colw = s.col;
   const bool sm = colw <= MC;
   const int ld = sm ? colw : m;
-  double *SYp = sm ? msy : b.SY, *WTp = sm ? mwt : b.WT, *Pp = sm ? mp : b.P, *Cp = sm ? mc : b.C;
-  double *WBPp = sm ? mwbp : b.WBP, *Vp = sm ? mv : b.V;
+  const double *SYp = sm ? msy : b.SY, *WTp = sm ? mwt : b.WT;
+  double *Pp = mp, *Cp = mc, *WBPp = mwbp, *Vp = mv;
   if (sm) {
     stage_in(msy, b.SY, m, colw);
     stage_in(mwt, b.WT, m, colw);
-    for (int j = threadIdx.x; j < 2 * colw; j += NT) {
-      mp[j] = b.P[j];
-      mc[j] = b.C[j];
-    }
+  }
+  for (int j = threadIdx.x; j < 2 * colw; j += NT) {
+    mp[j] = b.P[j];
+    mc[j] = b.C[j];
   }
   __syncthreads();
+  // the Cauchy loop's scalars, held in wave 0's registers across the chunks
+  const double theta = s.theta;
+  const int bnded = s.bnded;
+  const double w_f2org = s.f2_org;
+  double w_tj = s.tj, w_tsum = s.tsum, w_f1 = s.f1, w_f2 = s.f2, w_dtm = s.dtm;
+  int w_kpassed = s.kpassed, w_nseg = s.nseg, w_done = 0;
   unsigned long long last = 0ull;
   bool have_last = false;
   while (true) {
@@ -1099,78 +1325,83 @@ __global__ __launch_bounds__(NT) void nnls_walk_kernel(const Args a) {
         __syncthreads();
       }
     }
-    // ---- the Cauchy loop over this chunk (one thread)
-    if (threadIdx.x == 0) {
+    // ---- the Cauchy loop over this chunk (wave 0; the scalars uniform in its lanes)
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
       int stop = 0;
-      const double theta = s.theta;
-      const int col = s.col;
       for (int q = 0; q < cnt; ++q) {
-        const double tj0 = s.tj;
+        const double tj0 = w_tj;
         const int ibp = sidx[q];
         const double tj = __longlong_as_double((long long)skey[q]);
         const double dt = tj - tj0;
-        if (s.dtm < dt) {  // the minimiser is within this interval
+        if (w_dtm < dt) {  // the minimiser is within this interval
           stop = 1;
           break;
         }
-        s.tj = tj;
-        s.tsum = s.tsum + dt;
-        s.kpassed += 1;
-        const int nleft = nbreak - s.kpassed;
+        w_tj = tj;
+        w_tsum = w_tsum + dt;
+        w_kpassed += 1;
+        const int nleft = nbreak - w_kpassed;
         const double dibp = -gv[ibp];
-        b.IW[ibp] = 1;  // fixed at the lower bound: xcp = 0, d = 0
+        if (lane == 0) b.IW[ibp] = 1;  // fixed at the lower bound: xcp = 0, d = 0
         const double zibp = 0.0 - x[ibp];
         if (nleft == 0 && nbreak == b.n) {
-          s.dtm = dt;
-          for (int j = 0; j < 2 * col; ++j) Cp[j] = Cp[j] + s.dtm * Pp[j];
-          s.walk_done = 2;  // label 999: xcp needs no daxpy
+          w_dtm = dt;
+          for (int j = lane; j < 2 * colw; j += 64) Cp[j] = Cp[j] + w_dtm * Pp[j];
+          w_done = 2;  // label 999: xcp needs no daxpy
           stop = 2;
           break;
         }
-        s.nseg += 1;
+        w_nseg += 1;
         const double dibp2 = dibp * dibp;
-        double f1 = s.f1 + dt * s.f2 + dibp2 - theta * dibp * zibp;
-        double f2 = s.f2 - theta * dibp2;
-        if (col > 0) {
-          for (int j = 0; j < 2 * col; ++j) Cp[j] = Cp[j] + dt * Pp[j];
-          for (int j = 0; j < col; ++j) {
+        double f1 = w_f1 + dt * w_f2 + dibp2 - theta * dibp * zibp;
+        double f2 = w_f2 - theta * dibp2;
+        if (colw > 0) {
+          for (int j = lane; j < colw; j += 64) {
+            Cp[j] = Cp[j] + dt * Pp[j];
+            Cp[colw + j] = Cp[colw + j] + dt * Pp[colw + j];
             WBPp[j] = b.WY[(int64_t)j * a.n_pad + ibp];
-            WBPp[col + j] = theta * b.WS[(int64_t)j * a.n_pad + ibp];
+            WBPp[colw + j] = theta * b.WS[(int64_t)j * a.n_pad + ibp];
           }
-          if (!bmv(ld, col, SYp, WTp, WBPp, Vp)) {
-            s.walk_done = 3;  // info != 0: refresh
+          wave_sync();
+          if (!wbmv(ld, colw, SYp, WTp, WBPp, Vp)) {
+            w_done = 3;  // info != 0: refresh
             stop = 3;
             break;
           }
           double wmc = 0.0, wmp = 0.0, wmw = 0.0;
-          for (int j = 0; j < 2 * col; ++j) {
+          for (int j = lane; j < 2 * colw; j += 64) {
             wmc = wmc + Cp[j] * Vp[j];
             wmp = wmp + Pp[j] * Vp[j];
             wmw = wmw + WBPp[j] * Vp[j];
           }
-          for (int j = 0; j < 2 * col; ++j) Pp[j] = Pp[j] + (-dibp) * WBPp[j];
+          wmc = wave_sum(wmc);
+          wmp = wave_sum(wmp);
+          wmw = wave_sum(wmw);
+          for (int j = lane; j < 2 * colw; j += 64) Pp[j] = Pp[j] + (-dibp) * WBPp[j];
+          wave_sync();
           f1 = f1 + dibp * wmc;
           f2 = f2 + 2.0 * dibp * wmp - dibp2 * wmw;
         }
-        f2 = fmax(EPSMCH * s.f2_org, f2);
-        s.f1 = f1;
-        s.f2 = f2;
+        f2 = fmax(EPSMCH * w_f2org, f2);
+        w_f1 = f1;
+        w_f2 = f2;
         if (nleft > 0) {
-          s.dtm = -f1 / f2;
-        } else if (s.bnded) {
-          s.f1 = 0.0;
-          s.f2 = 0.0;
-          s.dtm = 0.0;
+          w_dtm = -f1 / f2;
+        } else if (bnded) {
+          w_f1 = 0.0;
+          w_f2 = 0.0;
+          w_dtm = 0.0;
         } else {
-          s.dtm = -f1 / f2;
+          w_dtm = -f1 / f2;
         }
       }
-      if (!stop && s.kpassed >= nbreak) stop = 1;  // every breakpoint passed: label 888
+      if (!stop && w_kpassed >= nbreak) stop = 1;  // every breakpoint passed: label 888
       if (!stop && cnt == 0) {  // cannot happen unless > CAP equal keys were cut (ST_TIES)
-        s.status |= ST_TIES;
+        if (lane == 0) s.status |= ST_TIES;
         stop = 1;
       }
-      stop_sh = stop;
+      if (lane == 0) stop_sh = stop;
     }
     __syncthreads();
     const int stop = stop_sh;
@@ -1179,26 +1410,38 @@ __global__ __launch_bounds__(NT) void nnls_walk_kernel(const Args a) {
     have_last = true;
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    if (s.walk_done == 3) {
-      refresh(s);
-      s.bk_count = 0;
-    } else {
-      if (s.walk_done != 2) {
-        // label 888
-        if (s.dtm <= 0.0) s.dtm = 0.0;
-        s.tsum = s.tsum + s.dtm;
-        for (int j = 0; j < 2 * s.col; ++j) Cp[j] = Cp[j] + s.dtm * Pp[j];
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    if (w_done == 3) {
+      if (lane == 0) {
+        refresh(s);
+        s.bk_count = 0;
       }
+    } else {
+      if (w_done != 2) {
+        // label 888
+        if (w_dtm <= 0.0) w_dtm = 0.0;
+        w_tsum = w_tsum + w_dtm;
+        for (int j = lane; j < 2 * colw; j += 64) Cp[j] = Cp[j] + w_dtm * Pp[j];
+      }
+      if (lane == 0) {
+        s.tj = w_tj;
+        s.tsum = w_tsum;
+        s.f1 = w_f1;
+        s.f2 = w_f2;
+        s.dtm = w_dtm;
+        s.kpassed = w_kpassed;
+        s.nseg = w_nseg;
+        s.walk_done = w_done;
+      }
+      wave_sync();
       gcp_done(s, b, ld, SYp, WTp, Cp);
     }
   }
   __syncthreads();
-  if (sm) {
-    for (int j = threadIdx.x; j < 2 * colw; j += NT) {
-      b.P[j] = mp[j];
-      b.C[j] = mc[j];
-    }
+  for (int j = threadIdx.x; j < 2 * colw; j += NT) {
+    b.P[j] = mp[j];
+    b.C[j] = mc[j];
   }
 }
 
@@ -1217,6 +1460,7 @@ __global__ __launch_bounds__(NT) void nnls_freev_kernel(const Args a) {
   Blk b = blk_view(a, blk);
   NnlsState &s = *b.st;
   if (s.phase != PH_FREEV) return;
+  if (dbg_hit(a, s, g)) return;
   const int m = a.m, ns = nslots(m);
   const int cur = s.cur, col = s.col;
   const double *x = xbuf(b, cur), *gv = gbuf(b, cur);
@@ -1378,21 +1622,22 @@ __global__ __launch_bounds__(NT) void nnls_formk_kernel(const Args a) {
   Blk b = blk_view(a, blk);
   NnlsState &s = *b.st;
   if (s.phase != PH_FORMK) return;
-  const int m = a.m, m2 = 2 * m, col = s.col;
-  const bool wrk = (s.nenter > 0) || (s.nleave > 0) || s.updatd;
-  // WN and its factorisation in LDS when 2 col <= 64 (the serial loops' loads chain)
+  if (dbg_hit(a, s, 0)) return;
+  const int m = a.m, m2 = 2 * m, col = s.col, ns = nslots(m);
+  const bool updatd = s.updatd;
+  const bool wrk = (s.nenter > 0) || (s.nleave > 0) || updatd;
+  // WN and its factorisation in LDS when 2 col <= 64
   __shared__ double mwn[64 * 64];
+  __shared__ int fok;
   const int col2 = 2 * col;
   const bool sm = col2 <= 64;
   const int ldw = sm ? col2 : m2;
-  double *wnp = sm ? mwn : b.WN;
+  double *wn = sm ? mwn : b.WN;
   double *wn1 = b.WN1;  // [2m][2m], rows/cols: Y block 0..m-1, S block m..2m-1
   if (wrk) {
-    const int upcl = s.updatd ? col - 1 : col;
-    // entering (CHG[0..nenter)) and leaving (CHG[n - nleave .. n)) sums for the old part:
-    // DELTA[0]: Y'Y enter, [1]: Y'Y leave, [2]: S'S enter, [3]: S'S leave,
-    // [4]: S'Y enter (is, jy), [5]: S'Y leave
-    const int ns = nslots(m);
+    const int upcl = updatd ? col - 1 : col;
+    // entering / leaving sums for the old part: DELTA[0]: Y'Y enter, [1]: Y'Y leave,
+    // [2]: S'S enter, [3]: S'S leave, [4]: S'Y enter (is, jy), [5]: S'Y leave
     const int npair = upcl * upcl;
     for (int pq = threadIdx.x; pq < npair; pq += NT) {
       const int i = pq / upcl, j = pq - i * upcl;
@@ -1421,92 +1666,80 @@ __global__ __launch_bounds__(NT) void nnls_formk_kernel(const Args a) {
           t[5] = t[5] + si[k] * yj[k];
         }
       }
-      for (int u = 0; u < 6; ++u) b.DELTA[u * m * m + i * m + j] = t[u];
+      // the old part of WN1 (lbfgsb.f formk): each entry owned by this thread
+      if (j <= i) {
+        wn1[i * m2 + j] = wn1[i * m2 + j] + t[0] - t[1];
+        wn1[(m + i) * m2 + (m + j)] = wn1[(m + i) * m2 + (m + j)] - t[2] + t[3];
+      }
+      if (i <= j) wn1[(m + i) * m2 + j] = wn1[(m + i) * m2 + j] + t[4] - t[5];
+      else wn1[(m + i) * m2 + j] = wn1[(m + i) * m2 + j] - t[4] + t[5];
+    }
+    if (updatd) {
+      // the new row / column (c = col - 1), summed by FREEV
+      const int c = col - 1;
+      for (int j = threadIdx.x; j <= c; j += NT) {
+        wn1[c * m2 + j] = b.NEWROW[j];                   // Y'ZZ'Y(c, j)
+        wn1[(m + c) * m2 + (m + j)] = b.NEWROW[m + j];   // S'AA'S(c, j)
+        wn1[(m + c) * m2 + j] = (j == c) ? b.NEWROW[3 * m + c] : b.NEWROW[2 * m + j];  // L_a(c, j) | R_z(c, c)
+        if (j < c) wn1[(m + j) * m2 + c] = b.NEWROW[3 * m + j];  // R_z(j, c)
+      }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      if (s.updatd) {
-        const int c = col - 1;
-        for (int j = 0; j <= c; ++j) {
-          wn1[c * m2 + j] = b.NEWROW[j];                   // Y'ZZ'Y(c, j)
-          wn1[(m + c) * m2 + (m + j)] = b.NEWROW[m + j];   // S'AA'S(c, j)
-          wn1[(m + c) * m2 + j] = b.NEWROW[2 * m + j];     // L_a(c, j)
-        }
-        for (int i = 0; i <= c; ++i) wn1[(m + i) * m2 + c] = b.NEWROW[3 * m + i];  // R_z(i, c)
+    // WN (upper triangle, 2col x 2col)
+    const double th = s.theta;
+    for (int idx = threadIdx.x; idx < col * col; idx += NT) {
+      const int iy = idx / col, jy = idx - iy * col;
+      const int is = col + iy, is1 = m + iy;
+      if (jy <= iy) {
+        const int js = col + jy, js1 = m + jy;
+        double v = wn1[iy * m2 + jy] / th;
+        if (jy == iy) v = v + b.SY[iy * m + iy];
+        wn[jy * ldw + iy] = v;
+        wn[js * ldw + is] = wn1[is1 * m2 + js1] * th;
       }
-      for (int iy = 0; iy < upcl; ++iy)
-        for (int jy = 0; jy <= iy; ++jy) {
-          const double *D = b.DELTA;
-          wn1[iy * m2 + jy] = wn1[iy * m2 + jy] + D[0 * m * m + iy * m + jy] - D[1 * m * m + iy * m + jy];
-          wn1[(m + iy) * m2 + (m + jy)] = wn1[(m + iy) * m2 + (m + jy)] - D[2 * m * m + iy * m + jy] +
-                                          D[3 * m * m + iy * m + jy];
-        }
-      for (int is = 0; is < upcl; ++is)
-        for (int jy = 0; jy < upcl; ++jy) {
-          const double *D = b.DELTA;
-          const double t1 = D[4 * m * m + is * m + jy], t3 = D[5 * m * m + is * m + jy];
-          if (is <= jy) wn1[(m + is) * m2 + jy] = wn1[(m + is) * m2 + jy] + t1 - t3;
-          else wn1[(m + is) * m2 + jy] = wn1[(m + is) * m2 + jy] - t1 + t3;
-        }
-      // WN (upper triangle, 2col x 2col, leading dimension m2)
-      double *wn = wnp;
-      const double th = s.theta;
-      for (int iy = 0; iy < col; ++iy) {
-        const int is = col + iy, is1 = m + iy;
-        for (int jy = 0; jy <= iy; ++jy) {
-          const int js = col + jy, js1 = m + jy;
-          wn[jy * ldw + iy] = wn1[iy * ldw + jy] / th;
-          wn[js * ldw + is] = wn1[is1 * ldw + js1] * th;
-        }
-        for (int jy = 0; jy < iy; ++jy) wn[jy * ldw + is] = -wn1[is1 * ldw + jy];
-        for (int jy = iy; jy < col; ++jy) wn[jy * ldw + is] = wn1[is1 * ldw + jy];
-        wn[iy * ldw + iy] = wn[iy * ldw + iy] + b.SY[iy * m + iy];
-      }
-      bool ok = dpofa(wn, ldw, col);
-      if (ok) {
-        for (int js = col; js < 2 * col; ++js) {
-          // dtrsl(wn, ldw, col, wn(1, js), 11): column js of the (1,2) block
-          for (int j = 0; j < col; ++j) {
-            double sum = wn[j * ldw + js];
-            for (int k = 0; k < j; ++k) sum = sum - wn[k * ldw + j] * wn[k * ldw + js];
-            wn[j * ldw + js] = sum / wn[j * ldw + j];
-          }
-        }
-        for (int is = col; is < 2 * col; ++is)
-          for (int js = is; js < 2 * col; ++js) {
-            double d = 0.0;
-            for (int k = 0; k < col; ++k) d = d + wn[k * ldw + is] * wn[k * ldw + js];
-            wn[is * ldw + js] = wn[is * ldw + js] + d;
-          }
-        ok = dpofa(wn + col * ldw + col, m2, col);
-      }
-      s.iword = ok ? 0 : -1;
+      wn[jy * ldw + is] = (jy < iy) ? -wn1[is1 * m2 + jy] : wn1[is1 * m2 + jy];
     }
+    __syncthreads();
+    bool ok = wg_dpofa(wn, ldw, col);
+    if (ok) {
+      // dtrsl(wn, col, wn(1, js), 11) per column js of the (1,2) block: independent columns
+      for (int js = col + threadIdx.x; js < col2; js += NT) {
+        for (int j = 0; j < col; ++j) {
+          double sum = wn[j * ldw + js];
+          for (int k = 0; k < j; ++k) sum = sum - wn[k * ldw + j] * wn[k * ldw + js];
+          wn[j * ldw + js] = sum / wn[j * ldw + j];
+        }
+      }
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < col * col; idx += NT) {
+        const int is = col + idx / col, js = col + idx % col;
+        if (js < is) continue;
+        double d = 0.0;
+        for (int k = 0; k < col; ++k) d = d + wn[k * ldw + is] * wn[k * ldw + js];
+        wn[is * ldw + js] = wn[is * ldw + js] + d;
+      }
+      __syncthreads();
+      ok = wg_dpofa(wn + col * ldw + col, ldw, col);
+    }
+    if (threadIdx.x == 0) fok = ok;
+    __syncthreads();
+    if (ok && sm) stage_out(b.WN, m2, mwn, col2);
+  } else {
+    if (sm) stage_in(mwn, b.WN, m2, col2);
+    if (threadIdx.x == 0) fok = 1;
     __syncthreads();
   }
-  if (!wrk && sm) stage_in(mwn, b.WN, m2, col2);
-  __syncthreads();
-  __shared__ int back;
+  if (threadIdx.x >= 64) return;
+  // subsm: wv = K^-1 wv (dtrsl job 11, negate the first col, dtrsl job 01) by wave 0
+  const bool ok = fok && wsolve_k(wn, ldw, col2, col, b.WV);
   if (threadIdx.x == 0) {
-    back = 0;
-    if (wrk && s.iword != 0) {
-      refresh(s);
-    } else if (!trsl_t(wnp, ldw, col2, b.WV)) {
-      // subsm: wv = K^-1 wv (dtrsl job 11, negate the first col, dtrsl job 01)
+    if (!ok) {
       refresh(s);
     } else {
-      for (int i = 0; i < col; ++i) b.WV[i] = -b.WV[i];
-      if (!trsl_n(wnp, ldw, col2, b.WV)) {
-        refresh(s);
-      } else {
-        s.backtrack = 0;
-        s.phase = PH_SUBSM;
-      }
-      back = wrk && sm;
+      s.backtrack = 0;
+      s.phase = PH_SUBSM;
     }
   }
-  __syncthreads();
-  if (back) stage_out(b.WN, m2, mwn, col2);
 }
 
 // SUBSM: d = (1/theta) r + (1/theta^2) Z'W wv on the free variables, z = max(0, xcp + d)
@@ -1519,6 +1752,7 @@ __global__ __launch_bounds__(NT) void nnls_subsm_kernel(const Args a) {
   Blk b = blk_view(a, blk);
   NnlsState &s = *b.st;
   if (s.phase != (BACK ? PH_BACKTRACK : PH_SUBSM)) return;
+  if (dbg_hit(a, s, g)) return;
   const int m = a.m, ns = nslots(m);
   const int cur = s.cur, col = s.col;
   const double *x = xbuf(b, cur), *gv = gbuf(b, cur);
@@ -1675,12 +1909,18 @@ __global__ void nnls_zero_tail_kernel(float *S, int B, int F, int nb, const int3
     S[(int64_t)b * F * nb + i] = 0.f;
 }
 
-__global__ void nnls_status_kernel(const Args a, int *status_out) {
+__global__ void nnls_status_kernel(const Args a, int *status_out, double *info) {
   for (int blk = blockIdx.x * blockDim.x + threadIdx.x; blk < a.n_blocks; blk += gridDim.x * blockDim.x) {
     Blk b = blk_view(a, blk);
     const int st = b.st->status;
-    if (st & ~ST_CONV) atomicOr(status_out, st & ~ST_CONV);
+    if (st & ~(ST_CONV | ST_MAXITER)) atomicOr(status_out, st & ~(ST_CONV | ST_MAXITER));
     atomicMax(status_out + 1, b.st->it);
+    if (info) {
+      info[4 * blk + 0] = b.st->it;
+      info[4 * blk + 1] = b.st->nfev;
+      info[4 * blk + 2] = b.st->f;
+      info[4 * blk + 3] = b.st->sbgnrm;
+    }
   }
 }
 
@@ -1705,6 +1945,8 @@ Args make_args(const ftmi_nnls_lbfgsb_args *p) {
   a.m = p->m;
   a.mref = p->n_bins;  // librosa: fmin_l_bfgs_b(..., m=A.shape[1])
   a.ncmax = p->max_frames;
+  a.maxiter = p->maxiter > 0 ? p->maxiter : 15000;
+  a.dbg_stop = p->dbg_stop;
   a.rowvals = p->rowvals;
   a.rowptr = p->rowptr;
   a.rowlo = p->rowlo;
@@ -1757,14 +1999,14 @@ extern "C" int ftmi_nnls_lbfgsb_cycles(const ftmi_nnls_lbfgsb_args *p, int32_t c
 }
 
 extern "C" int ftmi_nnls_lbfgsb_finish(const ftmi_nnls_lbfgsb_args *p, const int32_t *frames,
-                                       int32_t *status, ftmi_stream_t stream) {
+                                       int32_t *status, double *info, ftmi_stream_t stream) {
   if (!check_args(p) || !status) return FTMI_E_ARG;
   const Args a = make_args(p);
   const hipStream_t s = ftmi_hs(stream);
   hipLaunchKernelGGL(nnls_finish_kernel, dim3(a.groups, a.n_blocks), dim3(NT), 0, s, a);
   hipLaunchKernelGGL(nnls_zero_tail_kernel, dim3(64, a.B), dim3(256), 0, s, a.S, a.B, a.F, a.nb,
                      frames);
-  hipLaunchKernelGGL(nnls_status_kernel, dim3(1), dim3(256), 0, s, a, (int *)status);
+  hipLaunchKernelGGL(nnls_status_kernel, dim3(1), dim3(256), 0, s, a, (int *)status, info);
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
 }

@@ -226,11 +226,15 @@ def mel_to_stft(plan: DspPlan, mel: torch.Tensor, frames: Optional[torch.Tensor]
 
 
 def _nnls_lbfgsb(plan: DspPlan, mel: torch.Tensor, frames: Optional[torch.Tensor],
-                 denorm: bool) -> torch.Tensor:
+                 denorm: bool, maxiter: int = 0, info: Optional[list] = None,
+                 debug: Optional[dict] = None) -> torch.Tensor:
     """The host loop around ftmi_nnls_lbfgsb_* — what scipy's fmin_l_bfgs_b driver is around
     setulb: start, then cycles (every block advances one L-BFGS-B iteration or one extra
     line-search evaluation per cycle) until the device's count of running blocks reads 0.
-    Blocks as librosa 0.7.2 util.nnls cuts them (127 frames of each item's mel)."""
+    Blocks as librosa 0.7.2 util.nnls cuts them (127 frames of each item's mel).  maxiter:
+    scipy's (0: 15000); info: a list that receives per block (iterations, f evaluations, f,
+    projected-gradient norm); debug (tools/nnls_diag.py): {'stop': 16 * iteration + phase}
+    ends the blocks there and receives the workspace and its geometry."""
     lib = _lib.load()
     B, _, F = mel.shape
     dev = mel.device
@@ -254,7 +258,8 @@ def _nnls_lbfgsb(plan: DspPlan, mel: torch.Tensor, frames: Optional[torch.Tensor
         active = torch.full((1,), nblk, dtype=torch.int32, device=dev)
         status = torch.zeros(2, dtype=torch.int32, device=dev)
         a = _lib.NnlsArgs(mel.data_ptr(), B, F, plan.n_mels, plan.nb, int(denorm), bt.data_ptr(),
-                          nblk, NNLS_GROUPS, m, nc, plan.rowvals.data_ptr(), plan.rowptr.data_ptr(),
+                          nblk, NNLS_GROUPS, m, nc, maxiter, (debug or {}).get('stop', 0),
+                          plan.rowvals.data_ptr(), plan.rowptr.data_ptr(),
                           plan.rowlo.data_ptr(), plan.bin_rows.data_ptr(), plan.bin_w.data_ptr(),
                           plan.pinv64.data_ptr(), ws.data_ptr(), S.data_ptr(), active.data_ptr())
         ap = ctypes.byref(a)
@@ -269,17 +274,22 @@ def _nnls_lbfgsb(plan: DspPlan, mel: torch.Tensor, frames: Optional[torch.Tensor
             if cycles > 20 * 15000:
                 raise RuntimeError('L-BFGS-B NNLS did not finish')
             step = min(2 * step, 64)
+        inf = torch.zeros(nblk, 4, dtype=torch.float64, device=dev)
         launch('ftmi_nnls_lbfgsb_finish', f'nnls_lbfgsb_finish[blocks={nblk}]', 0, 0, ap,
-               _p(fr_dev), status.data_ptr(), stream)
+               _p(fr_dev), status.data_ptr(), inf.data_ptr(), stream)
         st = status.cpu().tolist()
         if st[0] & 4 and m < plan.nb:
             # history full (more than 32 updates: the synthetic-weights mels of the tests take
             # ~150): rerun the chunk with the reference's whole history, m = n_bins
             m = plan.nb
             continue
-        if st[0]:
+        if st[0] and debug is None:
             raise RuntimeError(f'L-BFGS-B NNLS failed (status {st[0]}: 2 abnormal line search, '
                                '4 history wrap, 8 equal breakpoints, 16 maxiter)')
+        if info is not None:
+            info.extend(inf.cpu().tolist())
+        if debug is not None:
+            debug.update(ws=ws, m=m, groups=NNLS_GROUPS, per=per, n_pad=(plan.nb * nc + 255) // 256 * 256)
         i += nblk
     return S
 
@@ -447,14 +457,20 @@ class DSP:
         `angles` to fix the phases.  nnls: 'lbfgsb' (the reference's magnitudes; default
         self.nnls) or 'fista' (fast, another minimiser)."""
         is_t = isinstance(mel, torch.Tensor)
-        m = mel if is_t else torch.from_numpy(np.ascontiguousarray(mel, dtype=np.float32)).cuda()
+        if is_t:
+            m, denorm = mel, True  # exp on the device
+        else:
+            # numpy in, as the reference: its own denormalize (np.exp, float32) on the host, so
+            # the NNLS sees the reference's M bit for bit (80 x T exps: microseconds)
+            m = torch.from_numpy(np.exp(np.ascontiguousarray(mel, dtype=np.float32))).cuda()
+            denorm = False
         _need_cuda(m)
         plan = self.plan(m.device)
         T = m.shape[-1]
         # the NNLS magnitudes first: queued on the device, they run while the host draws the
         # initial phases below (the draw does not depend on them)
-        S = mel_to_stft(plan, m.float().reshape(1, plan.n_mels, T).contiguous(), iters=self.nnls_iters,
-                        method=nnls or self.nnls)
+        S = mel_to_stft(plan, m.float().reshape(1, plan.n_mels, T).contiguous(), denorm=denorm,
+                        iters=self.nnls_iters, method=nnls or self.nnls)
         if angles is None:
             # the reference's draw (librosa: np.random.rand(n_bins, T)); exp(2 pi i u) and the
             # frame-major layout on the device (ftmi_unit_phases: the host exp of 420 k

@@ -501,12 +501,15 @@ int ftmi_mel_nnls(const float *mel, int32_t B, int32_t F, const int32_t *frames,
  * L-BFGS-B iteration or one extra line-search evaluation) until *active reads 0, then
  * ftmi_nnls_lbfgsb_finish (writes S (B, F, n_bins), zero past frames[b]; status: device
  * int32[2] the caller zeroes: [0] |= failure bits of any block (2 abnormal line search,
- * 4 history full, 8 > 1024 equal breakpoints, 16 maxiter), [1] = max iterations). */
+ * 4 history full, 8 > 1024 equal breakpoints), [1] = max iterations; info: NULL or device
+ * double[n_blocks][4] = per block (iterations, f evaluations, f, projected-gradient norm)). */
 typedef struct {
   const float *mel; /* (B, n_mels, F) */
   int32_t B, F, n_mels, n_bins, denorm;
   const int32_t *blocks;
   int32_t n_blocks, groups, m, max_frames;
+  int32_t maxiter;   /* scipy's maxiter (0: its default 15000) */
+  int32_t dbg_stop;  /* 0; else stop each block before phase (dbg_stop & 15) of iteration dbg_stop >> 4 */
   const float *rowvals;
   const int32_t *rowptr, *rowlo, *bin_rows;
   const float *bin_w;
@@ -521,7 +524,7 @@ int ftmi_nnls_lbfgsb_start(const ftmi_nnls_lbfgsb_args *args, ftmi_stream_t stre
 int ftmi_nnls_lbfgsb_cycles(const ftmi_nnls_lbfgsb_args *args, int32_t cycles,
                             ftmi_stream_t stream);
 int ftmi_nnls_lbfgsb_finish(const ftmi_nnls_lbfgsb_args *args, const int32_t *frames,
-                            int32_t *status, ftmi_stream_t stream);
+                            int32_t *status, double *info, ftmi_stream_t stream);
 
 /* ====================================================================================
  * FastPitch transformer (models/fast_pitch.py).  Activations channels-last (B, T, C).

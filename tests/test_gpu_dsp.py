@@ -121,19 +121,46 @@ def _speech_mel(frames, seed):
 NNLS_RTOL = 1e-6
 
 
-@pytest.mark.parametrize('kind,frames,seed', [('ref', 40, 0), ('speech', 127, 12), ('speech', 60, 3),
-                                              ('rand', 24, 5)])
+@pytest.mark.parametrize('kind,frames,seed', [('ref', 40, 0), ('speech', 127, 12), ('speech', 60, 3)])
 def test_mel_to_stft_lbfgsb_is_the_reference(dsp, kind, frames, seed):
     """The device L-BFGS-B (the reference's util.nnls) returns the oracle's S — not just a
     minimiser of the same objective."""
     from forwardtacotron_amd import dsp as G
     mel = REF_MEL if kind == 'ref' else (_speech_mel(frames, seed) if kind == 'speech' else _rand_mel(frames, seed))
-    ref = D.mel_to_stft(np.exp(mel))
-    S = G.mel_to_stft(dsp.plan(), torch.from_numpy(np.ascontiguousarray(mel)).cuda()[None])[0].cpu().numpy().T
+    M = np.exp(mel)  # the reference's denormalize (numpy float32 exp), as DSP.griffinlim does
+    ref = D.mel_to_stft(M)
+    S = G.mel_to_stft(dsp.plan(), torch.from_numpy(np.ascontiguousarray(M)).cuda()[None],
+                      denorm=False)[0].cpu().numpy().T
     assert S.shape == ref.shape and S.dtype == np.float32 and (S >= 0).all()
     rel = np.linalg.norm(S.astype(np.float64) - ref) / np.linalg.norm(ref)
     assert rel <= NNLS_RTOL, rel
     assert np.abs(S - ref).max() <= NNLS_RTOL * 10 * np.abs(ref).max()
+
+
+def test_mel_to_stft_lbfgsb_long_history(dsp):
+    """A non-speech mel: ~280 L-BFGS-B iterations, histories past the 32 columns the scalar
+    parts stage in LDS, line searches of several evaluations.  The device's iterates are
+    scipy's: after 60 iterations S agrees to 1e-6 (measured 2.8e-8, the float32 output
+    rounding).  Over hundreds of iterations on this degenerate problem (its minimisers form a
+    face of a polytope) rounding-level differences in the sums steer the two runs apart
+    (measured: 272 against 283 iterations, 1.6e-2 apart), so the full run is held to the
+    reference's objective: within 1e-4 relative."""
+    import scipy.optimize
+    from forwardtacotron_amd import dsp as G
+    M = np.exp(_rand_mel(24, 5))
+    A = D.mel_filters(22050, 1024, 80, 0, 8000)
+    x0 = np.clip(np.linalg.lstsq(A, M, rcond=None)[0], 0, None)
+    md = torch.from_numpy(np.ascontiguousarray(M)).cuda()[None]
+    ref, f_ref, _ = scipy.optimize.fmin_l_bfgs_b(D._nnls_obj, x0, args=(x0.shape, A, M),
+                                                 bounds=[(0, None)] * x0.size, m=513, maxiter=60)
+    info = []
+    S = G._nnls_lbfgsb(dsp.plan(), md, None, False, maxiter=60, info=info)[0].cpu().numpy().T
+    assert info[0][0] == 60 and abs(info[0][2] - f_ref) <= 1e-9 * f_ref
+    assert np.linalg.norm(S - ref.reshape(x0.shape)) / np.linalg.norm(ref) <= NNLS_RTOL
+    full = D.mel_to_stft(M)
+    S = G.mel_to_stft(dsp.plan(), md, denorm=False)[0].cpu().numpy().T
+    obj = lambda x: 0.5 * np.sum((A.astype(np.float64) @ x - M) ** 2)  # noqa: E731
+    assert (S >= 0).all() and abs(obj(S) - obj(full)) <= 1e-4 * obj(full)
 
 
 def test_mel_to_stft_lbfgsb_c2_length_and_batch(dsp):
@@ -142,19 +169,20 @@ def test_mel_to_stft_lbfgsb_c2_length_and_batch(dsp):
     same S bit for bit (the solver's sums do not depend on the batch)."""
     from forwardtacotron_amd import dsp as G
     plan = dsp.plan()
-    mel = _speech_mel(C2_FRAMES, 21)
-    ref = D.mel_to_stft(np.exp(mel))
-    S = G.mel_to_stft(plan, torch.from_numpy(mel).cuda()[None])[0].cpu().numpy().T
+    M = np.exp(_speech_mel(C2_FRAMES, 21))
+    ref = D.mel_to_stft(M)
+    S = G.mel_to_stft(plan, torch.from_numpy(M).cuda()[None], denorm=False)[0].cpu().numpy().T
     assert np.linalg.norm(S.astype(np.float64) - ref) / np.linalg.norm(ref) <= NNLS_RTOL
-    other = _speech_mel(300, 22)
+    other = np.exp(_speech_mel(300, 22))
     batch = np.zeros((2, 80, C2_FRAMES), np.float32)
-    batch[0] = mel
+    batch[0] = M
     batch[1, :, :300] = other
     frames = torch.tensor([C2_FRAMES, 300], dtype=torch.int32, device='cuda')
-    Sb = G.mel_to_stft(plan, torch.from_numpy(batch).cuda(), frames).cpu().numpy()
+    Sb = G.mel_to_stft(plan, torch.from_numpy(batch).cuda(), frames, denorm=False).cpu().numpy()
     np.testing.assert_array_equal(Sb[0].T, S)
     assert not Sb[1, 300:].any()
-    S1 = G.mel_to_stft(plan, torch.from_numpy(np.ascontiguousarray(other)).cuda()[None])[0].cpu().numpy()
+    S1 = G.mel_to_stft(plan, torch.from_numpy(np.ascontiguousarray(other)).cuda()[None],
+                       denorm=False)[0].cpu().numpy()
     np.testing.assert_array_equal(Sb[1, :300], S1)
 
 
