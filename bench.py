@@ -276,6 +276,11 @@ def main():
                     help='gen_forward: pitch_function = lambda x: x * amp, energy_function = '
                          'lambda x: x, as gen_forward.py:103-104 passes them')
     ap.add_argument('--amp', type=float, default=1.0, help='gen_forward.py --amp')
+    ap.add_argument('--nnls', choices=['lbfgsb', 'fista'], default='lbfgsb',
+                    help='the vocoder leg\'s mel pseudo-inverse: lbfgsb = the reference\'s util.nnls '
+                         '(L-BFGS-B, its S), fista = the fast per-frame solver (another minimiser)')
+    ap.add_argument('--vocoder-steps', type=int, default=0,
+                    help='timed steps of the vocoder leg (0: --steps)')
     ap.add_argument('--vocoder', choices=['none', 'griffinlim'], default='none',
                     help='griffinlim: also time generate + Griffin-Lim per step (gen_forward.py)')
     ap.add_argument('--no-host-loop', action='store_true',
@@ -409,21 +414,23 @@ def main():
             m = o['mel_post']
             if m.size(0) == 1:  # as forwardtacotron_amd.gen_forward: D2H, GL from the device mel
                 m.cpu()
-                return dsp.griffinlim(m[0]).cpu().numpy().shape[0]
-            w, n = dsp.griffinlim_batch(m)
+                return dsp.griffinlim(m[0], nnls=args.nnls).cpu().numpy().shape[0]
+            w, n = dsp.griffinlim_batch(m, nnls=args.nnls)
             last['wav'] = w
             w.cpu()
             return int(n.sum().item()) if torch.is_tensor(n) else int(np.sum(n))
         vstep()
         torch.cuda.synchronize()
+        vsteps = args.vocoder_steps or args.steps
         v0 = time.perf_counter()
         nsamp = 0
-        for _ in range(args.steps):
+        for _ in range(vsteps):
             nsamp += vstep()
         torch.cuda.synchronize()
         velapsed = time.perf_counter() - v0
-        voc = {'name': 'griffinlim', 'ms_per_step': round(velapsed / args.steps * 1e3, 3),
-               'mel_frames_per_s': round(frames / velapsed, 1),
+        voc = {'name': 'griffinlim', 'nnls': args.nnls, 'steps': vsteps,
+               'ms_per_step': round(velapsed / vsteps * 1e3, 3),
+               'mel_frames_per_s': round(frames / args.steps * vsteps / velapsed, 1),
                'audio_samples_per_s': round(nsamp / velapsed, 1),
                'what': 'generate() + mel_post D2H + DSP.griffinlim (numpy wav out) per step, '
                        'as gen_forward.py:115-134 with the griffinlim vocoder (as forwardtacotron_'

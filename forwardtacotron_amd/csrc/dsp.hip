@@ -541,7 +541,7 @@ extern "C" int ftmi_unit_phases(const double *u, int32_t B, int32_t n_bins, int3
 // ==========================================================================================
 // The fused Griffin-Lim iteration (round 6): one launch per iteration instead of the ISTFT
 // frame kernel (fp64 frames through HBM: (B, F, 1024) x 8 B), the overlap-add kernel and the
-// analysis kernel.  A workgroup owns a tile of GL_TF consecutive frames of one item:
+// analysis kernel.  A workgroup owns a tile of TF consecutive frames of one item:
 //   1. synthesis: the inverse rFFT of every frame whose support reaches the tile's analysis
 //      windows (the tile +- GL_HALO frames: n_fft / hop = 4, plus the reflect padding at the
 //      signal's ends), two real frames per complex fp64 FFT, each wave one pair;
@@ -563,19 +563,20 @@ extern "C" int ftmi_unit_phases(const double *u, int32_t B, int32_t n_bins, int3
 namespace {
 
 constexpr int GLN = 1024, GLHOP = 256, GLNB = GLN / 2 + 1;
-constexpr int GL_TF = 16;    // analysis frames per tile
-constexpr int GL_HALO = 4;   // synthesis frames beyond the tile on each side
-constexpr int GL_SEG = (GL_TF + 2 * GL_HALO - 1) * GLHOP + GLN;  // segment samples
-constexpr int GL_BUF = 1040;  // per-wave LDS buffer (double2): transpose rows of 65
+constexpr int GL_HALO = 3;   // synthesis frames beyond the tile on each side (4 at the item's
+                             // end when its last tile has one frame: reflect padding)
+constexpr int gl_seg(int tf) { return (tf + 2 * GL_HALO) * GLHOP + GLN; }  // segment samples
+constexpr int GL_ROW = 68;    // transpose row pitch (double2): rows 16 banks apart, conflict-free
+constexpr int GL_BUF = 16 * GL_ROW;  // per-wave LDS buffer (double2)
 
-// exp(-2 pi i j / 1024), j in [0, 1024), from the n/2-entry table
-__device__ __forceinline__ double2 gl_tw(const double2 *tw, int j) {
-  double2 w = tw[j & 511];
-  if (j & 512) {
-    w.x = -w.x;
-    w.y = -w.y;
-  }
-  return w;
+// stage twiddles, laid out so a wave's 64 reads are consecutive (no bank conflicts):
+// twA[(q - 1) * 64 + lane] = w^(lane q), q = 1..15; twB[l2 * 16 + k1] = w^(16 l2 k1)
+constexpr int GL_TWA = 15 * 64, GL_TWB = 64;
+
+// complex product with fused multiply-adds (the FFT's internal rounding: its outputs are
+// rounded to float32, where a 1e-16-level change of the fp64 intermediates shows nowhere)
+__device__ __forceinline__ double2 gl_cmul(double2 a, double2 b) {
+  return make_double2(__fma_rn(a.x, b.x, -(a.y * b.y)), __fma_rn(a.x, b.y, a.y * b.x));
 }
 
 // 16-point DFT in registers: V[q] = sum_m v[m] w16^(mq) (radix-2 DIF, reordered)
@@ -592,7 +593,7 @@ __device__ __forceinline__ void gl_dft16(double2 (&v)[16]) {
       for (int j = 0; j < h; ++j) {
         const double2 u = v[b + j], t = v[b + j + h];
         v[b + j] = cadd(u, t);
-        v[b + j + h] = (j == 0) ? csub(u, t) : cmul(csub(u, t), W[j * (8 / h)]);
+        v[b + j + h] = (j == 0) ? csub(u, t) : gl_cmul(csub(u, t), W[j * (8 / h)]);
       }
     }
   }
@@ -619,36 +620,45 @@ __device__ __forceinline__ double2 gl_dpp2(double2 v) {
 // natural-order index k of the FFT output in a wave buffer (a 4-element gap every 256)
 __device__ __forceinline__ int gl_pk(int k) { return k + ((k >> 8) << 2); }
 
-// forward FFT of z[lane + 64 m] = v[m]; the result in buf (gl_pk order).  Every thread of
-// the workgroup calls it (the exchanges use workgroup barriers).
-__device__ void gl_fft1024(double2 (&v)[16], double2 *buf, const double2 *tw) {
+__device__ __forceinline__ void gl_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// forward FFT of z[lane + 64 m] = v[m]; the result in buf (gl_pk order).  One wave, its own
+// buffer: the exchanges are wave-local (no workgroup barrier), so the waves of a workgroup
+// run their FFTs independently.
+__device__ void gl_fft1024(double2 (&v)[16], double2 *buf, const double2 *twA, const double2 *twB) {
   const int lane = threadIdx.x & 63;
   gl_dft16(v);
 #pragma unroll
-  for (int q = 1; q < 16; ++q) v[q] = cmul(v[q], gl_tw(tw, lane * q));
+  for (int q = 1; q < 16; ++q) v[q] = gl_cmul(v[q], twA[(q - 1) * 64 + lane]);
 #pragma unroll
-  for (int q = 0; q < 16; ++q) buf[q * 65 + lane] = v[q];
-  __syncthreads();
+  for (int q = 0; q < 16; ++q) buf[q * GL_ROW + lane] = v[q];
+  gl_wave_sync();
   const int q = lane >> 2, l2 = lane & 3;
 #pragma unroll
-  for (int l1 = 0; l1 < 16; ++l1) v[l1] = buf[q * 65 + 4 * l1 + l2];
-  __syncthreads();
+  for (int l1 = 0; l1 < 16; ++l1) v[l1] = buf[q * GL_ROW + 4 * l1 + l2];
+  gl_wave_sync();
   gl_dft16(v);
 #pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], gl_tw(tw, 16 * l2 * k1));
-  // 4-point DFT over l2 across the quad: lanes (0, 1, 2, 3) end with Y[0], Y[2], Y[1], Y[3]
+  for (int k1 = 1; k1 < 16; ++k1) v[k1] = gl_cmul(v[k1], twB[l2 * 16 + k1]);
+  // 4-point DFT over l2 across the quad: lanes (0, 1, 2, 3) end with Y[0], Y[2], Y[1], Y[3].
+  // Each step is partner +- own value: one fma per component with a per-lane sign.
+  const double sg1 = (l2 < 2) ? 1.0 : -1.0, sg2 = (l2 & 1) ? -1.0 : 1.0;
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) {
     const double2 p = gl_dpp2<0x4E>(v[k1]);  // lane ^ 2
-    double2 r = (l2 < 2) ? cadd(v[k1], p) : csub(p, v[k1]);
+    double2 r = make_double2(__fma_rn(sg1, v[k1].x, p.x), __fma_rn(sg1, v[k1].y, p.y));
     if (l2 == 3) r = make_double2(r.y, -r.x);  // (-i) (x1 - x3)
     const double2 p2 = gl_dpp2<0xB1>(r);       // lane ^ 1
-    v[k1] = (l2 & 1) ? csub(p2, r) : cadd(r, p2);
+    v[k1] = make_double2(__fma_rn(sg2, r.x, p2.x), __fma_rn(sg2, r.y, p2.y));
   }
   const int k2 = ((l2 & 1) << 1) | (l2 >> 1);
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) buf[gl_pk(q + 16 * k1 + 256 * k2)] = v[k1];
-  __syncthreads();
+  gl_wave_sync();
 }
 
 struct GlParams {
@@ -666,40 +676,75 @@ struct GlParams {
   int64_t y_stride, y_len;
 };
 
-template <int W, bool FINAL>
+template <int W, int TF, bool FINAL>
 __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
-  __shared__ float seg[GL_SEG];
+  __shared__ float seg[gl_seg(TF)];
   __shared__ double2 bufs[W][GL_BUF];
+  __shared__ double win[GLN];
+  __shared__ double2 twA[GL_TWA], twB[GL_TWB];
+  __shared__ float wss_int[GLHOP];
   const int b = blockIdx.x / p.tiles, t = blockIdx.x - b * p.tiles;
   const int Fb = p.frames ? min(p.frames[b], p.F) : p.F;
-  const int f0 = t * GL_TF;
+  const int f0 = t * TF;
   if (f0 >= Fb) return;
-  const int f1 = min(f0 + GL_TF, Fb);
-  const int a0 = max(0, f0 - GL_HALO), a1 = min(Fb, f1 + GL_HALO);
-  const int64_t sb = (int64_t)a0 * GLHOP;                  // segment start (uncropped samples)
+  const int f1 = min(f0 + TF, Fb);
+  // synthesis frames whose support reaches the tile's analysis windows: [f0 - 3, f1 + 3);
+  // the reflect padding at the item's end reaches frame Fb - 5 from the last frame
+  const int a0 = max(0, f0 - GL_HALO - ((f1 == Fb && f1 - f0 < 2) ? 1 : 0));
+  const int a1 = min(Fb, f1 + GL_HALO);
+  const int sb = a0 * GLHOP;                  // segment start (uncropped samples)
   const int slen = (a1 - 1 - a0) * GLHOP + GLN;
-  const int64_t L = (int64_t)GLHOP * (Fb - 1);             // istft length of item b
+  const int L = GLHOP * (Fb - 1);             // istft length of item b
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const double scale = 1.0 / GLN;
   double2 *buf = bufs[w];
   for (int i = threadIdx.x; i < slen; i += 64 * W) seg[i] = 0.f;
+  for (int i = threadIdx.x; i < GLN; i += 64 * W) win[i] = p.window[i];
+  for (int i = threadIdx.x; i < GL_TWA + GL_TWB; i += 64 * W) {
+    const int j = i < GL_TWA ? (i & 63) * (i / 64 + 1) : 16 * ((i - GL_TWA) >> 4) * ((i - GL_TWA) & 15);
+    const double2 t = p.tw[j & (GLN / 2 - 1)];  // w^(j + 512) = -w^j
+    const double2 v = (j & (GLN / 2)) ? make_double2(-t.x, -t.y) : t;
+    if (i < GL_TWA) twA[i] = v;
+    else twB[i - GL_TWA] = v;
+  }
+  __syncthreads();
+  // the window sum-square of a sample covered by four frames, accumulated in frame order
+  // (offsets r + 768, r + 512, r + 256, r): the same for every interior sample
+  for (int r = threadIdx.x; r < GLHOP; r += 64 * W) {
+    float w2 = 0.f;
+    for (int k = 3; k >= 0; --k) {
+      const double wv = win[r + k * GLHOP];
+      w2 = (float)((double)w2 + wv * wv);
+    }
+    wss_int[r] = w2;
+  }
 
-  // ---- 1 + 2: synthesis and overlap-add, W frame pairs per round
+  // ---- 1 + 2: synthesis and overlap-add, W frame pairs per round.  The next round's spectra
+  // are loaded (registers) while this round's frames are overlap-added.
   const int nsyn = a1 - a0;
-  for (int r0 = 0; r0 < nsyn; r0 += 2 * W) {
+  float2 xa[16], xb[16];
+  auto load_pair = [&](int r0) {
     const int fa = a0 + r0 + 2 * w, fb = fa + 1;
     const bool va = fa < a1, vb = fb < a1;
-    double2 v[16];
     const float2 *XA = p.Xin + ((int64_t)b * p.F + fa) * GLNB;
     const float2 *XB = XA + GLNB;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int k = lane + 64 * m;
+      const int kk = k > GLN / 2 ? GLN - k : k;
+      xa[m] = va ? XA[kk] : make_float2(0.f, 0.f);
+      xb[m] = vb ? XB[kk] : make_float2(0.f, 0.f);
+    }
+  };
+  load_pair(0);
+  for (int r0 = 0; r0 < nsyn; r0 += 2 * W) {
+    double2 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int k = lane + 64 * m;
       const bool mirror = k > GLN / 2;
       const int kk = mirror ? GLN - k : k;
-      const float2 a32 = va ? XA[kk] : make_float2(0.f, 0.f);
-      const float2 b32 = vb ? XB[kk] : make_float2(0.f, 0.f);
-      double ar = a32.x, ai = a32.y, br = b32.x, bi = b32.y;
+      double ar = xa[m].x, ai = xa[m].y, br = xb[m].x, bi = xb[m].y;
       if (kk == 0 || kk == GLN / 2) ai = bi = 0.0;  // c2r ignores imag of DC / Nyquist
       if (mirror) {
         ai = -ai;
@@ -708,7 +753,9 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
       // conj(A_full + i B_full): the inverse FFT as conj(FFT(conj z))
       v[m] = make_double2(ar - bi, -(ai + br));
     }
-    gl_fft1024(v, buf, p.tw);
+    gl_fft1024(v, buf, twA, twB);
+    __syncthreads();
+    if (r0 + 2 * W < nsyn) load_pair(r0 + 2 * W);
     // overlap-add of this round's frames, each sample's frames in increasing order
     const int rf0 = a0 + r0, rf1 = min(a1, rf0 + 2 * W);
     const int s_lo = rf0 * GLHOP, s_hi = (rf1 - 1) * GLHOP + GLN;
@@ -718,9 +765,9 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
       const int ilo = max(rf0, (s - GLN + GLHOP) / GLHOP);
       for (int i = ilo; i <= ihi; ++i) {
         const int off = s - i * GLHOP;
-        const double2 z = bufs[(i - rf0) >> 1][gl_pk(off)];
-        const double part = ((i - rf0) & 1) ? -z.y : z.x;
-        acc = (float)((double)acc + p.window[off] * (part * scale));
+        const double *zc = (const double *)&bufs[(i - rf0) >> 1][gl_pk(off)];
+        const double part = ((i - rf0) & 1) ? -zc[1] : zc[0];
+        acc = (float)((double)acc + win[off] * (part * scale));
       }
       seg[s - sb] = acc;
     }
@@ -728,11 +775,19 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
   }
   // window sum-square (float32, frame order over every frame of the item), division
   for (int i = threadIdx.x; i < slen; i += 64 * W) {
-    const int64_t s = sb + i;
-    const int ihi = (int)min((int64_t)Fb - 1, s / GLHOP);
-    const int ilo = (int)max((int64_t)0, (s - GLN + GLHOP) / GLHOP);
-    float w2 = 0.f;
-    for (int k = ilo; k <= ihi; ++k) w2 = (float)((double)w2 + p.win_sq[s - (int64_t)k * GLHOP]);
+    const int s = sb + i;
+    const int ihi = min(Fb - 1, s / GLHOP);
+    const int ilo = max(0, (s - GLN + GLHOP) / GLHOP);
+    float w2;
+    if (ihi - ilo == 3) {
+      w2 = wss_int[s & (GLHOP - 1)];
+    } else {
+      w2 = 0.f;
+      for (int k = ilo; k <= ihi; ++k) {
+        const double wv = win[s - k * GLHOP];
+        w2 = (float)((double)w2 + wv * wv);
+      }
+    }
     const float v = seg[i];
     seg[i] = (w2 > 1.17549435e-38f) ? (v / w2) : v;
   }
@@ -747,22 +802,48 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
       yb[j] = (j < L) ? seg[j + GLN / 2 - sb] : 0.f;
     return;
   } else {
-    // ---- 3: analysis of the tile's frames and the fast-GL update
+    // ---- 3: analysis of the tile's frames and the fast-GL update (each wave its own pairs)
     for (int r0 = 0; r0 < f1 - f0; r0 += 2 * W) {
       const int fa = f0 + r0 + 2 * w, fb = fa + 1;
       const bool va = fa < f1, vb = fb < f1;
       double2 v[16];
+      const int ja = fa * GLHOP - GLN / 2;  // first sample of frame fa (cropped coordinates)
+      const bool inner = ja >= 0 && ja + GLHOP + GLN - 1 < L;
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int i = lane + 64 * m;
-        const double wi = p.window[i];
-        const int64_t ja = (int64_t)fa * GLHOP + i - GLN / 2;
-        const double xa = va ? (double)seg[reflect_index(ja, L) + GLN / 2 - sb] : 0.0;
-        const double xb = vb ? (double)seg[reflect_index(ja + GLHOP, L) + GLN / 2 - sb] : 0.0;
-        v[m] = make_double2(wi * xa, vb ? wi * xb : 0.0);
+        const double wi = win[i];
+        double xa, xb;
+        if (inner) {
+          xa = (double)seg[ja + i + GLN / 2 - sb];
+          xb = (double)seg[ja + GLHOP + i + GLN / 2 - sb];
+        } else {
+          xa = va ? (double)seg[reflect_index(ja + i, L) + GLN / 2 - sb] : 0.0;
+          xb = vb ? (double)seg[reflect_index(ja + GLHOP + i, L) + GLN / 2 - sb] : 0.0;
+        }
+        v[m] = make_double2(va ? wi * xa : 0.0, vb ? wi * xb : 0.0);
       }
-      gl_fft1024(v, buf, p.tw);
-      for (int k = lane; k < GLNB; k += 64) {
+      // this pair's S and tprev (9 bins per lane per frame), loaded before the FFT so their
+      // latency hides behind it
+      float sv[2][9];
+      float2 tp[2][9];
+#pragma unroll
+      for (int fr = 0; fr < 2; ++fr) {
+        const bool vf = fr ? vb : va;
+        const int64_t ob = ((int64_t)b * p.F + fa + fr) * GLNB;
+#pragma unroll
+        for (int u = 0; u < 9; ++u) {
+          const int k = lane + 64 * u;
+          const bool ok = vf && k < GLNB;
+          sv[fr][u] = ok ? p.S[ob + k] : 0.f;
+          tp[fr][u] = (ok && !p.first) ? p.tprev[ob + k] : make_float2(0.f, 0.f);
+        }
+      }
+      gl_fft1024(v, buf, twA, twB);
+#pragma unroll
+      for (int u = 0; u < 9; ++u) {
+        const int k = lane + 64 * u;
+        if (k >= GLNB) continue;
         const double2 zk = buf[gl_pk(k)], zn = buf[gl_pk((GLN - k) & (GLN - 1))];
         const float2 A = make_float2((float)(0.5 * (zk.x + zn.x)), (float)(0.5 * (zk.y - zn.y)));
         const float2 Bq = make_float2((float)(0.5 * (zk.y + zn.y)), (float)(-0.5 * (zk.x - zn.x)));
@@ -773,23 +854,33 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
           const int64_t o = ((int64_t)b * p.F + fa + fr) * GLNB + k;
           float2 an = vv;
           if (!p.first) {
-            const float2 tp = p.tprev[o];
-            an.x = (vv.x - (p.c * tp.x));
-            an.y = (vv.y - (p.c * tp.y));
+            an.x = (vv.x - (p.c * tp[fr][u].x));
+            an.y = (vv.y - (p.c * tp[fr][u].y));
           }
           const float d = (cabs_rn(an.x, an.y) + 1e-16f);
           const float scl = (1.0f / d);
           an.x = (an.x * scl);
           an.y = (an.y * scl);
-          const float sv = p.S[o];
           p.tprev[o] = vv;
-          p.Xout[o] = make_float2((sv * an.x), (sv * an.y));
+          p.Xout[o] = make_float2((sv[fr][u] * an.x), (sv[fr][u] * an.y));
         }
       }
-      __syncthreads();  // buf is the next round's FFT buffer
+      gl_wave_sync();  // buf is this wave's next FFT buffer
     }
   }
 }
+
+// the tile shape: W waves (one FFT pair each at a time), TF analysis frames per tile.  c5
+// (B = 64, F = 1400) per iteration, tools/gl_bench.py: 4 x 16 1.34 ms before the
+// conflict-free twiddle tables / fma quad stage, 1.10 after; 8 x 10 (162 KB of LDS, two waves
+// per SIMD) 1.42; 4 x 32 (the halo 19 % of the synthesis instead of 38 %) 0.97-1.03 ms (the
+// three-kernel path: 1.47).  What bounds it (PMC, profiles/r6_pmc_gl.txt): one wave per SIMD
+// — every in-flight fp64 FFT holds a 17 KB LDS exchange buffer, so LDS, not VGPRs, caps the
+// CU at four — and 33 % of wave cycles parked at waitcnt / barriers
+#ifndef GL_IW
+#define GL_IW 4
+#define GL_ITF 32
+#endif
 
 int gl_check(int32_t n_fft, int32_t hop, const double *window, const double *win_sq, const void *tw) {
   if (!window || !win_sq || !tw) return FTMI_E_ARG;
@@ -808,10 +899,11 @@ extern "C" int ftmi_griffinlim_iter(const void *Xin, void *Xout, const float *S,
   if (int rc = gl_check(n_fft, hop, window, win_sq, twiddle)) return rc;
   GlParams p{};
   p.Xin = (const float2 *)Xin, p.Xout = (float2 *)Xout, p.S = S, p.tprev = (float2 *)tprev;
-  p.B = B, p.F = F, p.tiles = (F + GL_TF - 1) / GL_TF, p.frames = frames;
+  p.B = B, p.F = F, p.tiles = (F + GL_ITF - 1) / GL_ITF, p.frames = frames;
   p.window = window, p.win_sq = win_sq, p.tw = (const double2 *)twiddle;
   p.c = c, p.first = first;
-  hipLaunchKernelGGL((gl_fused_kernel<4, false>), dim3(B * p.tiles), dim3(256), 0, ftmi_hs(stream), p);
+  hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_ITF, false>), dim3(B * p.tiles), dim3(64 * GL_IW), 0,
+                     ftmi_hs(stream), p);
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
 }
@@ -824,10 +916,11 @@ extern "C" int ftmi_istft_fused(const void *X, int32_t B, int32_t F, const int32
   if (int rc = gl_check(n_fft, hop, window, win_sq, twiddle)) return rc;
   GlParams p{};
   p.Xin = (const float2 *)X;
-  p.B = B, p.F = F, p.tiles = (F + GL_TF - 1) / GL_TF, p.frames = frames;
+  p.B = B, p.F = F, p.tiles = (F + GL_ITF - 1) / GL_ITF, p.frames = frames;
   p.window = window, p.win_sq = win_sq, p.tw = (const double2 *)twiddle;
   p.y = y, p.y_stride = y_stride, p.y_len = y_len;
-  hipLaunchKernelGGL((gl_fused_kernel<4, true>), dim3(B * p.tiles), dim3(256), 0, ftmi_hs(stream), p);
+  hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_ITF, true>), dim3(B * p.tiles), dim3(64 * GL_IW), 0,
+                     ftmi_hs(stream), p);
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;
 }

@@ -322,10 +322,11 @@ def _gl_loop(plan: DspPlan, S: torch.Tensor, angles: torch.Tensor, n_iter: int,
     L = plan.hop * (F - 1)
     c = float(np.float32(momentum / (1 + momentum)))
     if _gl_fused(plan):
-        # X read (+ the halo frames) and written to the other buffer, S read, tprev r/w
+        # algorithmic bytes per iteration: X read, S read, tprev read + written, X written
+        # (36 B per bin; the halo frames' re-reads of X are not counted)
         X2 = torch.empty_like(X)
         for it in range(n_iter):
-            launch('ftmi_griffinlim_iter', f'gl_iter[B={B},F={F}]', 0, 44.0 * S.numel(),
+            launch('ftmi_griffinlim_iter', f'gl_iter[B={B},F={F}]', 0, 36.0 * S.numel(),
                    X.data_ptr(), X2.data_ptr(), S.data_ptr(), tprev.data_ptr(), B, F, _p(frames),
                    plan.n_fft, plan.hop, plan.window.data_ptr(), plan.win_sq.data_ptr(),
                    plan.twiddle.data_ptr(), ctypes.c_float(c), int(it == 0), _stream())
