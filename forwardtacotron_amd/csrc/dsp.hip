@@ -882,6 +882,25 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
 #define GL_ITF 32
 #endif
 
+// 32-frame tiles where the batch fills the chip (c5: 2,816 tiles), 8-frame tiles below one
+// tile per CU (c2's 821-frame sentence: 26 tiles of 32 would leave 230 CUs idle; 103 of 8)
+constexpr int GL_SMALL_TF = 8;
+
+template <bool FINAL>
+int gl_launch(GlParams p, hipStream_t s) {
+  const int big = (p.F + GL_ITF - 1) / GL_ITF;
+  if ((int64_t)p.B * big >= 256) {
+    p.tiles = big;
+    hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_ITF, FINAL>), dim3(p.B * p.tiles), dim3(64 * GL_IW), 0, s, p);
+  } else {
+    p.tiles = (p.F + GL_SMALL_TF - 1) / GL_SMALL_TF;
+    hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_SMALL_TF, FINAL>), dim3(p.B * p.tiles), dim3(64 * GL_IW), 0, s,
+                       p);
+  }
+  FTMI_CHECK_LAUNCH();
+  return FTMI_OK;
+}
+
 int gl_check(int32_t n_fft, int32_t hop, const double *window, const double *win_sq, const void *tw) {
   if (!window || !win_sq || !tw) return FTMI_E_ARG;
   if (n_fft != GLN || hop != GLHOP) return FTMI_E_UNSUPPORTED;
@@ -899,13 +918,10 @@ extern "C" int ftmi_griffinlim_iter(const void *Xin, void *Xout, const float *S,
   if (int rc = gl_check(n_fft, hop, window, win_sq, twiddle)) return rc;
   GlParams p{};
   p.Xin = (const float2 *)Xin, p.Xout = (float2 *)Xout, p.S = S, p.tprev = (float2 *)tprev;
-  p.B = B, p.F = F, p.tiles = (F + GL_ITF - 1) / GL_ITF, p.frames = frames;
+  p.B = B, p.F = F, p.frames = frames;
   p.window = window, p.win_sq = win_sq, p.tw = (const double2 *)twiddle;
   p.c = c, p.first = first;
-  hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_ITF, false>), dim3(B * p.tiles), dim3(64 * GL_IW), 0,
-                     ftmi_hs(stream), p);
-  FTMI_CHECK_LAUNCH();
-  return FTMI_OK;
+  return gl_launch<false>(p, ftmi_hs(stream));
 }
 
 extern "C" int ftmi_istft_fused(const void *X, int32_t B, int32_t F, const int32_t *frames,
@@ -916,11 +932,8 @@ extern "C" int ftmi_istft_fused(const void *X, int32_t B, int32_t F, const int32
   if (int rc = gl_check(n_fft, hop, window, win_sq, twiddle)) return rc;
   GlParams p{};
   p.Xin = (const float2 *)X;
-  p.B = B, p.F = F, p.tiles = (F + GL_ITF - 1) / GL_ITF, p.frames = frames;
+  p.B = B, p.F = F, p.frames = frames;
   p.window = window, p.win_sq = win_sq, p.tw = (const double2 *)twiddle;
   p.y = y, p.y_stride = y_stride, p.y_len = y_len;
-  hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_ITF, true>), dim3(B * p.tiles), dim3(64 * GL_IW), 0,
-                     ftmi_hs(stream), p);
-  FTMI_CHECK_LAUNCH();
-  return FTMI_OK;
+  return gl_launch<true>(p, ftmi_hs(stream));
 }

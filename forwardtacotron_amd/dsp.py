@@ -197,13 +197,14 @@ NNLS_WS_CAP = 4 << 30  # workspace bytes per launch chunk
 
 
 def mel_to_stft(plan: DspPlan, mel: torch.Tensor, frames: Optional[torch.Tensor] = None,
-                denorm: bool = True, iters: int = 200, method: str = 'lbfgsb') -> torch.Tensor:
+                denorm: bool = True, iters: int = 32, method: str = 'lbfgsb') -> torch.Tensor:
     """librosa feature.inverse.mel_to_stft(power=1) of (B, n_mels, F) (log-)mels:
     (B, F, nb) float32 non-negative magnitudes, frame-major.
 
     method 'lbfgsb' (default) runs the reference's own NNLS on the device — util.nnls'
     L-BFGS-B over 127-frame blocks, same iterates to rounding (ftmi_nnls_lbfgsb_*) — so S is
-    the reference's S.  'fista' is the fast per-frame solver (`iters` FISTA steps): a
+    the reference's S.  'fista' is the fast per-frame solver (`iters` FISTA steps, default
+    32): a
     minimiser of the same objective, but the minimiser is not unique, so its S (and the
     Griffin-Lim wav built on it) is NOT the reference's (tests/test_gpu_dsp.py states by how
     much)."""
@@ -380,7 +381,9 @@ class DSP:
         self.mu_law = mu_law
         self.voc_mode = voc_mode
         self._plans: Dict[Any, DspPlan] = {}
-        self.nnls_iters = 200
+        # FISTA steps of the fast solver: 32 fit the mel 100x closer than the reference's own
+        # L-BFGS-B stops (relative residual ~3e-7 against ~4e-5 on speech; 200 steps: 1e-14)
+        self.nnls_iters = 32
         # 'lbfgsb': the reference's NNLS (librosa util.nnls), reproduced; 'fista': the fast
         # per-frame solver (another minimiser of the same objective, not the reference's S)
         self.nnls = 'lbfgsb'
