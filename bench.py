@@ -31,8 +31,11 @@ ranks hold the shards (64 utterances each, seed = rank) of ONE global batch and 
 forwardtacotron_amd.sharded.generate_sharded(gather='rank0'): global phoneme padding, the
 batch-global fill-2 rule and T_mel by scalar RCCL all-reduces, mel_post gathered to rank 0
 only (result collection) — the reference's output for the global batch (weak scaling:
-per-GPU work fixed).  Barrier + synchronize around the K timed steps, max elapsed over
-ranks, value = frames of the global mel_post / that time.
+per-GPU work fixed).  The gather runs on its own communicator and is left in flight while
+the next step runs (--gather-overlap off: blocking).  Barrier + synchronize around the K
+timed steps, max elapsed over ranks, value = frames of the global mel_post / that time.
+`collectives` in the line: per-collective RCCL times (HIP events, max over ranks) from one
+more loop with the gather blocking, the weights broadcast, and every rank's step time.
 
 The JSON line also carries
   roofline     the dominant kernel (largest device time inside the timed steps, measured
@@ -68,7 +71,8 @@ from forwardtacotron_amd import forward_tacotron as ft_module  # noqa: E402
 from forwardtacotron_amd.fast_pitch import FastPitch  # noqa: E402
 from forwardtacotron_amd.forward_tacotron import ForwardTacotron  # noqa: E402
 from forwardtacotron_amd.probe import KernelProbe  # noqa: E402
-from forwardtacotron_amd.sharded import broadcast_state, generate_sharded  # noqa: E402
+from forwardtacotron_amd.sharded import (CollectiveTimer, broadcast_state,  # noqa: E402
+                                         generate_sharded)
 from forwardtacotron_amd.synthetic import default_config, synthetic_state_dict, synthetic_tokens  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA == vector rate), MI355X_MICROARCH.md
@@ -283,6 +287,9 @@ def main():
                     help='timed steps of the vocoder leg (0: --steps)')
     ap.add_argument('--vocoder', choices=['none', 'griffinlim'], default='none',
                     help='griffinlim: also time generate + Griffin-Lim per step (gen_forward.py)')
+    ap.add_argument('--gather-overlap', choices=('auto', 'on', 'off'), default='auto',
+                    help='N > 1: the rank-0 gather of step i in flight during step i + 1 (auto: '
+                         'on with nccl; off in the gloo rehearsal, whose ranks share one GPU)')
     ap.add_argument('--no-host-loop', action='store_true',
                     help='skip the second (host-to-host, PCIe-inclusive) timed loop')
     args = ap.parse_args()
@@ -320,8 +327,11 @@ def main():
         sd = synthetic_state_dict(model, seed=0, model=args.model)
         model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     model = model.to(dev).eval()
+    bcast_timer = CollectiveTimer()
+    ggroup = None
     if world > 1:
-        broadcast_state(model, src=0)
+        broadcast_state(model, src=0, timer=bcast_timer)
+        ggroup = dist.new_group()  # the result collection's own communicator (RCCL stream)
     x_np = synthetic_tokens(args.batch, args.tmax, seed=rank, min_len=args.tmin)
     x_host = torch.from_numpy(x_np)
     x = x_host.to(dev)
@@ -333,9 +343,19 @@ def main():
         cb = dict(pitch_function=lambda v: v * amp, energy_function=lambda v: v)
     else:
         cb = {}
+    # auto: pipelined with RCCL (one rank per GPU).  In the gloo rehearsal the ranks share a
+    # GPU and pipelining unlocks their step phase, so two processes' all-CU persistent
+    # recurrences can meet on the one device (a spin timeout and compact rerun, seconds):
+    # blocking there (tools/c4_overlap_diag.py)
+    overlap = world > 1 and (args.gather_overlap == 'on'
+                             or (args.gather_overlap == 'auto' and backend == 'nccl'))
     if world > 1:  # c4: one global batch sharded over the ranks (reference-identical result),
         # the result collected on rank 0 (SURVEY 8(e) "result collection")
         gen = lambda xx: generate_sharded(model, xx, gather='rank0', **cb)
+        # timed loop: step i's rank-0 gather in flight on its own communicator while step
+        # i + 1 runs; waited on after step i + 1 is issued
+        gen_async = lambda xx: generate_sharded(model, xx, gather='rank0', gather_group=ggroup,
+                                                async_gather=True, **cb)
     else:
         gen = lambda xx: model.generate(xx, **cb)
     for _ in range(args.warmup):
@@ -349,11 +369,25 @@ def main():
 
     frames = 0
     out = None
+    if overlap:  # the pipelined form once untimed (the gather communicator's first use)
+        gen_async(x).wait()
+        torch.cuda.synchronize()
     with KernelProbe() as probe:
         barrier()
         t0 = time.perf_counter()
+        pending = None
         for _ in range(args.steps):
-            o = gen(x)  # N > 1: rank 0 holds the global batch's result
+            if overlap:
+                p = gen_async(x)
+                o = pending.wait() if pending is not None else None
+                pending = p
+            else:
+                o = gen(x)  # N > 1: rank 0 holds the global batch's result
+            if o is not None:
+                out = o
+                frames += out['mel_post'].size(0) * out['mel_post'].size(2)
+        if pending is not None:
+            o = pending.wait()
             if o is not None:
                 out = o
                 frames += out['mel_post'].size(0) * out['mel_post'].size(2)
@@ -362,6 +396,21 @@ def main():
         t1 = time.perf_counter()
     elapsed = t1 - t0
     kern = probe.summary()
+
+    # c4: the communication share.  One more loop of `steps` calls with the blocking
+    # rank-0 gather and every collective bracketed by HIP events (sharded.CollectiveTimer),
+    # after the timed region; per-collective averages are maxed over ranks below.
+    comm = None
+    if world > 1:
+        ctimer = CollectiveTimer()
+        barrier()
+        c0 = time.perf_counter()
+        for _ in range(args.steps):
+            generate_sharded(model, x, gather='rank0', timer=ctimer, **cb)
+        torch.cuda.synchronize()
+        barrier()
+        comm = {'elapsed': time.perf_counter() - c0, 'per_call': ctimer.summary(),
+                'broadcast': bcast_timer.summary()}
 
     # Second loop, PCIe-inclusive, as gen_forward.py:111-120 runs a call: token ids H2D,
     # generate(), mel_post D2H — through pinned buffers, the D2H stream-ordered on a side
@@ -481,6 +530,37 @@ def main():
                       else None)
 
     if world > 1:
+        rank_ms = torch.zeros(world, dtype=torch.float64, device=cdev)
+        dist.all_gather_into_tensor(rank_ms, torch.tensor([elapsed / args.steps * 1e3],
+                                                          dtype=torch.float64, device=cdev))
+        names = ['shard_sizes all_gather', 'fill_rule all_reduce SUM', 't_mel all_reduce MAX',
+                 'status all_reduce MAX', 'result gather to rank 0']
+        pc = comm['per_call']
+        vec = [pc.get(n, {}).get('avg_ms', 0.0) for n in names]
+        vec += [pc.get(n, {}).get('total_ms', 0.0) / args.steps for n in names]
+        bc = comm['broadcast'].get('weights broadcast', {'total_ms': 0.0, 'calls': 0})
+        vec += [bc['total_ms'], comm['elapsed']]
+        cv = torch.tensor(vec, dtype=torch.float64, device=cdev)
+        dist.all_reduce(cv, op=dist.ReduceOp.MAX)
+        cv = cv.tolist()
+        nn = len(names)
+        comm_line = {
+            'per_collective': {n: {'calls_per_step': round(pc.get(n, {}).get('calls', 0) / args.steps, 2),
+                                   'avg_ms': round(cv[i], 4), 'ms_per_step': round(cv[nn + i], 4)}
+                               for i, n in enumerate(names)},
+            'collective_ms_per_step': round(sum(cv[nn:2 * nn]), 4),
+            'weights_broadcast_ms': round(cv[2 * nn], 3),
+            'weights_broadcast_calls': bc['calls'],
+            'ms_per_step_blocking_gather': round(cv[2 * nn + 1] / args.steps * 1e3, 3),
+            'rank_ms_per_step': [round(v, 3) for v in rank_ms.tolist()],
+            'gather_overlapped': overlap,
+            'what': ('HIP events on the issuing stream around each blocking RCCL collective '
+                     '(the interval includes the wait for the slowest peer), max over ranks, '
+                     'from one extra loop of `steps` calls after the timed region with the '
+                     'rank-0 gather blocking; ms_per_step_blocking_gather is that loop\'s '
+                     'wall time (events included); rank_ms_per_step: each rank\'s timed loop '
+                     '(ms_per_step is their max)'),
+        }
         t = torch.tensor([elapsed, host_elapsed or 0.0, host_serial or 0.0], device=cdev,
                          dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -613,7 +693,8 @@ def main():
                                     if world == 1 else
                                     f'c4: {"FastPitch" if fp else "ForwardTacotron"} generate of one '
                                     f'global batch sharded over {world} GPUs (global padding, '
-                                    f'fill rule and T_mel by RCCL all-reduce, mel all-gather), ')
+                                    f'fill rule and T_mel by RCCL all-reduce, the result gathered to '
+                                    f'rank 0{" on its own communicator, pipelined with the next step" if overlap else ""}), ')
                                    + f'batch={args.batch} per GPU, '
                                    f'phoneme lengths U{{{args.tmin}..{args.tmax}}}',
                        'global_batch': args.batch * world, 'T_phonemes': int(x_np.shape[1]),
@@ -645,6 +726,13 @@ def main():
                                            'energy_function = lambda x: x')
         if prenet is not None:
             line['prenet_bank'] = prenet
+        if world > 1:
+            gb = sum(v.numel() * v.element_size() for k, v in out.items()
+                     if not (k == 'mel_post' and v is out['mel']))
+            comm_line['gather_bytes_per_step'] = int(gb)
+            comm_line['gather_bytes_what'] = ('bytes rank 0 collects per step (mel, mel_post, dur, '
+                                              'pitch, energy of the global batch)')
+            line['collectives'] = comm_line
         if voc is not None:
             line['with_vocoder'] = voc
         if world == 1 and not args.no_cpu_baseline:

@@ -267,3 +267,98 @@ def test_generate_sharded_rccl_single_rank():
                                        rtol=0, err_msg=k)
     finally:
         dist.destroy_process_group()
+
+
+class _StubModel:
+    """generate() with the batch hooks a model calls (T_mel all-reduce, status word) and
+    rows that depend on the step, so a pipelined gather that mixed steps up would show."""
+
+    def __init__(self) -> None:
+        self.calls = 0
+
+    def generate(self, x, alpha, pitch_function, energy_function, batch):
+        self.calls += 1
+        totals = (x != 0).sum(1) * 3
+        T_mel = batch.t_mel(totals)
+        batch.status(torch.zeros(1, dtype=torch.int32))
+        mel = x.float()[:, None, :1].expand(x.size(0), 4, T_mel) + 1000 * self.calls
+        return {'mel': mel.contiguous(), 'mel_post': mel.contiguous() * 2,
+                'dur': x.float() * self.calls}
+
+
+def _pipelined(rank, world, port):
+    from forwardtacotron_amd import sharded as S
+    _init(rank, world, port)
+    try:
+        gg = dist.new_group()  # the result collection's own communicator
+        x = torch.randint(1, 9, (rank + 1, 3 + 2 * rank))
+        sync_model, pipe_model = _StubModel(), _StubModel()
+        timer = S.CollectiveTimer()
+        ref = [S.generate_sharded(sync_model, x, gather='rank0', timer=timer) for _ in range(3)]
+        summ = timer.summary()
+        for name in ('shard_sizes all_gather', 't_mel all_reduce MAX', 'status all_reduce MAX',
+                     'result gather to rank 0'):
+            assert name in summ, (name, summ)
+            assert summ[name]['avg_ms'] >= 0
+        assert summ['shard_sizes all_gather']['calls'] == 3
+        assert summ['result gather to rank 0']['calls'] == 3 * 3  # mel, mel_post, dur
+        # pipelined: step i's gather waited on after step i + 1 has been issued
+        got, pending = [], None
+        for _ in range(3):
+            p = S.generate_sharded(pipe_model, x, gather='rank0', gather_group=gg, async_gather=True)
+            if pending is not None:
+                got.append(pending.wait())
+            pending = p
+        got.append(pending.wait())
+        for r, g in zip(ref, got):
+            if rank == 0:
+                assert r.keys() == g.keys()
+                for k in r:
+                    assert torch.equal(r[k], g[k]), k
+                assert r['mel'].size(0) == world * (world + 1) // 2
+            else:
+                assert r is None and g is None
+        with pytest.raises(ValueError):
+            S.generate_sharded(pipe_model, x, gather='all', async_gather=True)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_rank0_gather_gloo():
+    """the rank-0 gather on its own communicator, left in flight while
+    the next step runs, collects exactly what the blocking gather does (3 ranks, uneven
+    shards, 3 steps); the CollectiveTimer records every collective of the protocol."""
+    mp.spawn(_pipelined, args=(3, _port()), nprocs=3, join=True)
+
+
+@pytest.mark.gpu
+def test_generate_sharded_rccl_async_gather():
+    """The pipelined result collection through RCCL on the device (one rank): the gather on
+    a second communicator, in flight while the next generate runs, equals the blocking one;
+    the collective timer's HIP-event spans are positive."""
+    from forwardtacotron_amd import sharded as S
+    from forwardtacotron_amd.forward_tacotron import ForwardTacotron
+    from forwardtacotron_amd.synthetic import default_config, load_synthetic, synthetic_tokens
+    dev = torch.device('cuda', torch.cuda.current_device())
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{_port()}', rank=0,
+                            world_size=1, device_id=dev)
+    try:
+        gg = dist.new_group()
+        m = load_synthetic(ForwardTacotron.from_config(default_config()), 0).cuda().eval()
+        timer = S.CollectiveTimer()
+        S.broadcast_state(m, src=0, timer=timer)
+        xs = [torch.from_numpy(synthetic_tokens(4, 30, seed=s, min_len=8)).cuda() for s in (1, 2)]
+        ref = [S.generate_sharded(m, x, gather='rank0', timer=timer) for x in xs]
+        p0 = S.generate_sharded(m, xs[0], gather='rank0', gather_group=gg, async_gather=True)
+        p1 = S.generate_sharded(m, xs[1], gather='rank0', gather_group=gg, async_gather=True)
+        got = [p0.wait(), p1.wait()]
+        torch.cuda.synchronize()
+        for r, g in zip(ref, got):
+            for k in ('mel_post', 'mel', 'pitch', 'energy', 'dur'):
+                assert torch.equal(r[k], g[k]), k
+        summ = timer.summary()
+        for name in ('weights broadcast', 'shard_sizes all_gather', 'fill_rule all_reduce SUM',
+                     't_mel all_reduce MAX', 'result gather to rank 0'):
+            assert summ[name]['avg_ms'] > 0, (name, summ)
+    finally:
+        dist.destroy_process_group()

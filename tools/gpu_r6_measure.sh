@@ -43,4 +43,9 @@ if [ "$PART" = mfma ] || [ "$PART" = all ]; then
   step mfma_c2 300 rocprofv3 --pmc $MF --output-format csv -d $O/mfma_c2 -o run -- python3 bench.py --config c2 --callbacks gen_forward --steps 3 --warmup 2 --no-cpu-baseline --no-host-loop
   step mfma_c5 400 rocprofv3 --pmc $MF --output-format csv -d $O/mfma_c5 -o run -- python3 bench.py --model fast_pitch --steps 2 --warmup 1 --no-cpu-baseline --no-host-loop
 fi
+if [ "$PART" = c4 ]; then  # the N > 1 path: RCCL tests at world 1, gloo rehearsal at world 2 on one GPU
+  step c4_tests 300 python -u -m pytest tests/test_sharded.py -m gpu -x -v --timeout 200 --timeout-method thread
+  step c4_gloo2 500 env FTMI_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-host-loop
+  step c4_gloo2_pipe 500 env FTMI_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 2 --no-host-loop --gather-overlap on
+fi
 echo ALLOK
