@@ -85,12 +85,12 @@ PEAK_X3_TFLOPS = PEAK_BF16_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 
-PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r5_pmc_traffic.json')        # c3
-PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r5c2_pmc_traffic.json')   # c2 (--config c2)
-PMC_PROFILE_C5 = os.path.join(ROOT, 'profiles', 'r5c5_pmc_traffic.json')   # c5 (--model fast_pitch)
+PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r6_pmc_traffic.json')        # c3
+PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r6c2_pmc_traffic.json')   # c2 (--config c2)
+PMC_PROFILE_C5 = os.path.join(ROOT, 'profiles', 'r6c5_pmc_traffic.json')   # c5 (--model fast_pitch)
 # the PMC files are a prior run of the same workload (separate FETCH_SIZE / WRITE_SIZE passes
 # cannot share the timed run), taken on this tree
-PMC_TREE = '6eb8293 (round 5, tools/gpu_r5_measure.sh pmc / mfma)'
+PMC_TREE = '3e61c87 (round 6, tools/gpu_r6_measure.sh pmc / mfma)'
 
 
 def rocprof_name(label: str):
@@ -148,7 +148,7 @@ def pmc_traffic_slab(label: str, path: str):
             'note': 'a prior PMC run of this workload, not this run'}
 
 
-PMC_MFMA = os.path.join(ROOT, 'profiles', 'r5_pmc_mfma.json')  # tools/pmc_mfma.py
+PMC_MFMA = os.path.join(ROOT, 'profiles', 'r6_pmc_mfma.json')  # tools/pmc_mfma.py
 
 
 def pmc_mfma(label: str, cfg: str):
