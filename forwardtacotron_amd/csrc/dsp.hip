@@ -593,7 +593,9 @@ __device__ __forceinline__ void gl_dft16(double2 (&v)[16]) {
       for (int j = 0; j < h; ++j) {
         const double2 u = v[b + j], t = v[b + j + h];
         v[b + j] = cadd(u, t);
-        v[b + j + h] = (j == 0) ? csub(u, t) : gl_cmul(csub(u, t), W[j * (8 / h)]);
+        const double2 d = csub(u, t);
+        // W[4] = -i: 7 of the 17 products are a swap (the value gl_cmul rounds to)
+        v[b + j + h] = (j == 0) ? d : (j * (8 / h) == 4) ? make_double2(d.y, -d.x) : gl_cmul(d, W[j * (8 / h)]);
       }
     }
   }
@@ -615,6 +617,21 @@ __device__ __forceinline__ double gl_dpp(double x) {
 template <int CTRL>
 __device__ __forceinline__ double2 gl_dpp2(double2 v) {
   return make_double2(gl_dpp<CTRL>(v.x), gl_dpp<CTRL>(v.y));
+}
+
+// 1 / x in float64 to within ~2^-52 (v_rcp_f64 and two Newton steps; inf -> 0).  A float32
+// quotient a / b of float32 values is never within 2^-49 (relative) of a float32 rounding
+// midpoint — b * m for a 25-bit midpoint m differs from a by at least one unit of the
+// product's 49-bit grid — so (float)(a * gl_rcp64(b)) IS the correctly rounded a / b that
+// numpy computes.  The IEEE float32 division sequence reads VCC in v_div_fmas, which keeps
+// independent divisions from overlapping.
+__device__ __forceinline__ double gl_rcp64(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = __fma_rn(-x, r, 1.0);
+  r = __fma_rn(r, e, r);
+  e = __fma_rn(-x, r, 1.0);
+  r = __fma_rn(r, e, r);
+  return __builtin_isinf(x) ? 0.0 : r;
 }
 
 // natural-order index k of the FFT output in a wave buffer (a 4-element gap every 256)
@@ -676,8 +693,26 @@ struct GlParams {
   int64_t y_stride, y_len;
 };
 
+#ifdef FTMI_GL_STAMPS
+// diagnostic build only (libftmi_stamps.so): wave 0's s_memtime at the phase boundaries
+__device__ unsigned long long ftmi_gl_stamps[4096 * 8];
+#define GLSTAMP(i)                                                                 \
+  do {                                                                             \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {                                   \
+      __builtin_amdgcn_sched_barrier(0);                                           \
+      ftmi_gl_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime();         \
+      __builtin_amdgcn_sched_barrier(0);                                           \
+    }                                                                              \
+  } while (0)
+#else
+#define GLSTAMP(i) \
+  do {             \
+  } while (0)
+#endif
+
 template <int W, int TF, bool FINAL>
 __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
+  GLSTAMP(0);
   __shared__ float seg[gl_seg(TF)];
   __shared__ double2 bufs[W][GL_BUF];
   __shared__ double win[GLN];
@@ -698,6 +733,23 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const double scale = 1.0 / GLN;
   double2 *buf = bufs[w];
+  // the first round's spectra are requested before the setup, so their latency hides behind it
+  const int nsyn = a1 - a0;
+  float2 xa[16], xb[16];
+  auto load_pair = [&](int r0) {
+    const int fa = a0 + r0 + 2 * w, fb = fa + 1;
+    const bool va = fa < a1, vb = fb < a1;
+    const float2 *XA = p.Xin + ((int64_t)b * p.F + fa) * GLNB;
+    const float2 *XB = XA + GLNB;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int k = lane + 64 * m;
+      const int kk = k > GLN / 2 ? GLN - k : k;
+      xa[m] = va ? XA[kk] : make_float2(0.f, 0.f);
+      xb[m] = vb ? XB[kk] : make_float2(0.f, 0.f);
+    }
+  };
+  load_pair(0);
   for (int i = threadIdx.x; i < slen; i += 64 * W) seg[i] = 0.f;
   for (int i = threadIdx.x; i < GLN; i += 64 * W) win[i] = p.window[i];
   for (int i = threadIdx.x; i < GL_TWA + GL_TWB; i += 64 * W) {
@@ -718,25 +770,14 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
     }
     wss_int[r] = w2;
   }
+  GLSTAMP(1);
+  static_assert(64 * W == GLHOP, "the overlap-add maps one thread to each sample of a hop");
+  double wr[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wr[j] = win[threadIdx.x + GLHOP * j];
 
   // ---- 1 + 2: synthesis and overlap-add, W frame pairs per round.  The next round's spectra
   // are loaded (registers) while this round's frames are overlap-added.
-  const int nsyn = a1 - a0;
-  float2 xa[16], xb[16];
-  auto load_pair = [&](int r0) {
-    const int fa = a0 + r0 + 2 * w, fb = fa + 1;
-    const bool va = fa < a1, vb = fb < a1;
-    const float2 *XA = p.Xin + ((int64_t)b * p.F + fa) * GLNB;
-    const float2 *XB = XA + GLNB;
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const int k = lane + 64 * m;
-      const int kk = k > GLN / 2 ? GLN - k : k;
-      xa[m] = va ? XA[kk] : make_float2(0.f, 0.f);
-      xb[m] = vb ? XB[kk] : make_float2(0.f, 0.f);
-    }
-  };
-  load_pair(0);
   for (int r0 = 0; r0 < nsyn; r0 += 2 * W) {
     double2 v[16];
 #pragma unroll
@@ -753,43 +794,78 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
       // conj(A_full + i B_full): the inverse FFT as conj(FFT(conj z))
       v[m] = make_double2(ar - bi, -(ai + br));
     }
+    if (r0 == 0) GLSTAMP(2);
     gl_fft1024(v, buf, twA, twB);
+    if (r0 == 0) GLSTAMP(3);
     __syncthreads();
     if (r0 + 2 * W < nsyn) load_pair(r0 + 2 * W);
-    // overlap-add of this round's frames, each sample's frames in increasing order
-    const int rf0 = a0 + r0, rf1 = min(a1, rf0 + 2 * W);
-    const int s_lo = rf0 * GLHOP, s_hi = (rf1 - 1) * GLHOP + GLN;
-    for (int s = s_lo + threadIdx.x; s < s_hi; s += 64 * W) {
-      float acc = seg[s - sb];
-      const int ihi = min(rf1 - 1, s / GLHOP);
-      const int ilo = max(rf0, (s - GLN + GLHOP) / GLHOP);
-      for (int i = ilo; i <= ihi; ++i) {
-        const int off = s - i * GLHOP;
-        const double *zc = (const double *)&bufs[(i - rf0) >> 1][gl_pk(off)];
-        const double part = ((i - rf0) & 1) ? -zc[1] : zc[0];
-        acc = (float)((double)acc + win[off] * (part * scale));
+    // overlap-add of this round's frames, each sample's frames in increasing order.  Thread
+    // r (64 W = one hop of threads) owns the samples (rf0 + q) hop + r: frame rf0 + q - j
+    // reaches them at offset r + j hop, so the thread's four window values sit in registers,
+    // a frame's value is at r + 260 j of its wave's buffer (gl_pk), and which (q, j) pairs
+    // exist depends only on the round's frame count — compile-time in a full round.  The
+    // q's dependent float32-rounded chains are independent and interleave.
+    const int rf0 = a0 + r0, nf = min(a1 - rf0, 2 * W);
+    const int base = r0 * GLHOP + threadIdx.x;  // segment index of (q = 0, r)
+    auto tap = [&](int fi, int j) -> double {
+      const double *zc = (const double *)&bufs[fi >> 1][threadIdx.x + (GLHOP + 4) * j];
+      return (fi & 1) ? -zc[1] : zc[0];
+    };
+    if (nf == 2 * W) {
+#pragma unroll
+      for (int q = 0; q < 2 * W + 3; ++q) {
+        float acc = seg[base + q * GLHOP];
+#pragma unroll
+        for (int j = 3; j >= 0; --j) {
+          const int fi = q - j;
+          if (fi >= 0 && fi < 2 * W) acc = (float)((double)acc + wr[j] * (tap(fi, j) * scale));
+        }
+        seg[base + q * GLHOP] = acc;
       }
-      seg[s - sb] = acc;
+    } else {
+      for (int q = 0; q < nf + 3; ++q) {
+        float acc = seg[base + q * GLHOP];
+#pragma unroll
+        for (int j = 3; j >= 0; --j) {
+          const int fi = q - j;
+          if (fi >= 0 && fi < nf) acc = (float)((double)acc + wr[j] * (tap(fi, j) * scale));
+        }
+        seg[base + q * GLHOP] = acc;
+      }
     }
     __syncthreads();
   }
-  // window sum-square (float32, frame order over every frame of the item), division
-  for (int i = threadIdx.x; i < slen; i += 64 * W) {
-    const int s = sb + i;
-    const int ihi = min(Fb - 1, s / GLHOP);
-    const int ilo = max(0, (s - GLN + GLHOP) / GLHOP);
-    float w2;
-    if (ihi - ilo == 3) {
-      w2 = wss_int[s & (GLHOP - 1)];
-    } else {
-      w2 = 0.f;
-      for (int k = ilo; k <= ihi; ++k) {
-        const double wv = win[s - k * GLHOP];
-        w2 = (float)((double)w2 + wv * wv);
-      }
+  GLSTAMP(4);
+  // window sum-square (float32, frame order over every frame of the item), division.  A
+  // segment clear of the item's first 3 hops and its end has four frames at every sample:
+  // the table, 4 samples per thread (independent divisions interleave); else per sample
+  if (sb >= GLN - GLHOP && sb + slen <= Fb * GLHOP) {
+    // thread r's samples all sit at hop offset r (sb is a multiple of the hop): one divisor
+    const float w2 = wss_int[threadIdx.x];
+    const double rw = gl_rcp64((double)w2);
+    const bool div = w2 > 1.17549435e-38f;
+    for (int i = threadIdx.x; i < slen; i += 64 * W) {
+      const float v = seg[i];
+      seg[i] = div ? (float)((double)v * rw) : v;  // == v / w2 (gl_rcp64)
     }
-    const float v = seg[i];
-    seg[i] = (w2 > 1.17549435e-38f) ? (v / w2) : v;
+  } else {
+    for (int i = threadIdx.x; i < slen; i += 64 * W) {
+      const int s = sb + i;
+      const int ihi = min(Fb - 1, s / GLHOP);
+      const int ilo = max(0, (s - GLN + GLHOP) / GLHOP);
+      float w2;
+      if (ihi - ilo == 3) {
+        w2 = wss_int[s & (GLHOP - 1)];
+      } else {
+        w2 = 0.f;
+        for (int k = ilo; k <= ihi; ++k) {
+          const double wv = win[s - k * GLHOP];
+          w2 = (float)((double)w2 + wv * wv);
+        }
+      }
+      const float v = seg[i];
+      seg[i] = (w2 > 1.17549435e-38f) ? (float)((double)v * gl_rcp64((double)w2)) : v;
+    }
   }
   __syncthreads();
 
@@ -839,34 +915,59 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
           tp[fr][u] = (ok && !p.first) ? p.tprev[ob + k] : make_float2(0.f, 0.f);
         }
       }
+      if (r0 == 0) GLSTAMP(5);
       gl_fft1024(v, buf, twA, twB);
+      if (r0 == 0) GLSTAMP(6);
+      // the update of all 18 bins straight-line (a clamped bin for the lanes past Nyquist),
+      // then the stores: no branch between the bins' sqrt / division chains, so they
+      // interleave (bin by bin behind the branches they ran ~500 cycles each)
+      float2 xo[2][9];
 #pragma unroll
       for (int u = 0; u < 9; ++u) {
-        const int k = lane + 64 * u;
-        if (k >= GLNB) continue;
+        const int k = min(lane + 64 * u, GLNB - 1);
         const double2 zk = buf[gl_pk(k)], zn = buf[gl_pk((GLN - k) & (GLN - 1))];
         const float2 A = make_float2((float)(0.5 * (zk.x + zn.x)), (float)(0.5 * (zk.y - zn.y)));
         const float2 Bq = make_float2((float)(0.5 * (zk.y + zn.y)), (float)(-0.5 * (zk.x - zn.x)));
 #pragma unroll
         for (int fr = 0; fr < 2; ++fr) {
-          if (!(fr ? vb : va)) continue;
           const float2 vv = fr ? Bq : A;
-          const int64_t o = ((int64_t)b * p.F + fa + fr) * GLNB + k;
           float2 an = vv;
           if (!p.first) {
             an.x = (vv.x - (p.c * tp[fr][u].x));
             an.y = (vv.y - (p.c * tp[fr][u].y));
           }
           const float d = (cabs_rn(an.x, an.y) + 1e-16f);
-          const float scl = (1.0f / d);
+          const float scl = (float)gl_rcp64((double)d);  // == 1.0f / d (see gl_rcp64)
           an.x = (an.x * scl);
           an.y = (an.y * scl);
-          p.tprev[o] = vv;
-          p.Xout[o] = make_float2((sv[fr][u] * an.x), (sv[fr][u] * an.y));
+          tp[fr][u] = vv;
+          xo[fr][u] = make_float2((sv[fr][u] * an.x), (sv[fr][u] * an.y));
+        }
+      }
+      // every bin's result exists before the first store: vmcnt counts stores too, and with
+      // both pending each wait becomes vmcnt(0) — one store acknowledgement per bin (the
+      // empty asm takes the results as operands, so no computation sinks into a store's
+      // branch)
+#pragma unroll
+      for (int u = 0; u < 9; ++u)
+#pragma unroll
+        for (int fr = 0; fr < 2; ++fr)
+          asm volatile("" ::"v"(xo[fr][u].x), "v"(xo[fr][u].y), "v"(tp[fr][u].x), "v"(tp[fr][u].y));
+#pragma unroll
+      for (int u = 0; u < 9; ++u) {
+        const int k = lane + 64 * u;
+#pragma unroll
+        for (int fr = 0; fr < 2; ++fr) {
+          if (k < GLNB && (fr ? vb : va)) {
+            const int64_t o = ((int64_t)b * p.F + fa + fr) * GLNB + k;
+            p.tprev[o] = tp[fr][u];
+            p.Xout[o] = xo[fr][u];
+          }
         }
       }
       gl_wave_sync();  // buf is this wave's next FFT buffer
     }
+    GLSTAMP(7);
   }
 }
 
@@ -908,6 +1009,13 @@ int gl_check(int32_t n_fft, int32_t hop, const double *window, const double *win
 }
 
 }  // namespace
+
+#ifdef FTMI_GL_STAMPS
+extern "C" int ftmi_debug_gl_stamps(unsigned long long *host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ftmi_gl_stamps),
+                                  sizeof(unsigned long long) * (size_t)n, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 extern "C" int ftmi_griffinlim_iter(const void *Xin, void *Xout, const float *S, void *tprev,
                                     int32_t B, int32_t F, const int32_t *frames, int32_t n_fft,
