@@ -493,6 +493,32 @@ def main():
             vstep()
             torch.cuda.synchronize()
         voc['kernels'] = dsp_kernel_table(vprobe.summary())
+        # the vocoder leg's dominant audio kernel against the HBM roofline (the fused GL
+        # iteration by default), with its PMC traffic from the committed passes of c5
+        audio = {k: v for k, v in voc['kernels'].items()
+                 if k.split('[')[0] in ('gl_iter', 'gl_stft', 'istft', 'istft_fused', 'mel_nnls',
+                                        'nnls_lbfgsb', 'unit_phases', 'spec_mul')}
+        if audio:
+            lab, v = max(audio.items(), key=lambda kv: kv[1]['avg_ms'] * kv[1]['launches'])
+            vr = {'kernel': lab, 'bound': 'hbm', 'achieved': v['hbm_GBs'], 'peak': PEAK_HBM_GBS,
+                  'unit': 'GB/s', 'frac': v['hbm_frac'],
+                  'algorithmic_per_launch': v['algorithmic_bytes'], 'avg_launch_ms': v['avg_ms'],
+                  'launches': v['launches'], 'traffic': None,
+                  'algorithmic_basis': ('gl_iter: 36 B per bin (X read + written as complex64, '
+                                        'S read, tprev read + written)'
+                                        if lab.startswith('gl_iter') else 'inputs + outputs once')}
+            if lab.startswith('gl_iter') and args.model == 'fast_pitch' and shape == (64, 50, 200) \
+                    and os.path.exists(PMC_PROFILE_C5):
+                hit = json.load(open(PMC_PROFILE_C5))['kernels'].get('gl_fused_kernel<4, 32, false>')
+                if hit:
+                    vr['traffic'] = hit['hbm_bytes_per_launch']
+                    vr['traffic_detail'] = {
+                        'read_bytes_corrected': hit['read_bytes_corrected'],
+                        'write_bytes': hit['write_bytes'],
+                        'vs_algorithmic': round(hit['hbm_bytes_per_launch'] / v['algorithmic_bytes'], 3),
+                        'source': os.path.relpath(PMC_PROFILE_C5, ROOT), 'measured_on_tree': PMC_TREE,
+                        'note': 'a prior PMC run of this workload, not this run'}
+            voc['roofline'] = vr
         if 'wav' in last:
             from forwardtacotron_amd.dsp import mel_spectrogram
             wav = last['wav'].contiguous()

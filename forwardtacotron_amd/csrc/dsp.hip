@@ -712,45 +712,15 @@ __device__ unsigned long long ftmi_gl_stamps[4096 * 8];
 
 template <int W, int TF, bool FINAL>
 __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
-  GLSTAMP(0);
   __shared__ float seg[gl_seg(TF)];
   __shared__ double2 bufs[W][GL_BUF];
   __shared__ double win[GLN];
   __shared__ double2 twA[GL_TWA], twB[GL_TWB];
   __shared__ float wss_int[GLHOP];
-  const int b = blockIdx.x / p.tiles, t = blockIdx.x - b * p.tiles;
-  const int Fb = p.frames ? min(p.frames[b], p.F) : p.F;
-  const int f0 = t * TF;
-  if (f0 >= Fb) return;
-  const int f1 = min(f0 + TF, Fb);
-  // synthesis frames whose support reaches the tile's analysis windows: [f0 - 3, f1 + 3);
-  // the reflect padding at the item's end reaches frame Fb - 5 from the last frame
-  const int a0 = max(0, f0 - GL_HALO - ((f1 == Fb && f1 - f0 < 2) ? 1 : 0));
-  const int a1 = min(Fb, f1 + GL_HALO);
-  const int sb = a0 * GLHOP;                  // segment start (uncropped samples)
-  const int slen = (a1 - 1 - a0) * GLHOP + GLN;
-  const int L = GLHOP * (Fb - 1);             // istft length of item b
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const double scale = 1.0 / GLN;
   double2 *buf = bufs[w];
-  // the first round's spectra are requested before the setup, so their latency hides behind it
-  const int nsyn = a1 - a0;
-  float2 xa[16], xb[16];
-  auto load_pair = [&](int r0) {
-    const int fa = a0 + r0 + 2 * w, fb = fa + 1;
-    const bool va = fa < a1, vb = fb < a1;
-    const float2 *XA = p.Xin + ((int64_t)b * p.F + fa) * GLNB;
-    const float2 *XB = XA + GLNB;
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const int k = lane + 64 * m;
-      const int kk = k > GLN / 2 ? GLN - k : k;
-      xa[m] = va ? XA[kk] : make_float2(0.f, 0.f);
-      xb[m] = vb ? XB[kk] : make_float2(0.f, 0.f);
-    }
-  };
-  load_pair(0);
-  for (int i = threadIdx.x; i < slen; i += 64 * W) seg[i] = 0.f;
+  // the tables, once per workgroup (it walks tiles blockIdx.x, + gridDim.x, ...)
   for (int i = threadIdx.x; i < GLN; i += 64 * W) win[i] = p.window[i];
   for (int i = threadIdx.x; i < GL_TWA + GL_TWB; i += 64 * W) {
     const int j = i < GL_TWA ? (i & 63) * (i / 64 + 1) : 16 * ((i - GL_TWA) >> 4) * ((i - GL_TWA) & 15);
@@ -770,11 +740,45 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
     }
     wss_int[r] = w2;
   }
-  GLSTAMP(1);
   static_assert(64 * W == GLHOP, "the overlap-add maps one thread to each sample of a hop");
   double wr[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) wr[j] = win[threadIdx.x + GLHOP * j];
+
+  for (int tile = blockIdx.x; tile < p.B * p.tiles; tile += gridDim.x) {
+  GLSTAMP(0);
+  const int b = tile / p.tiles, t = tile - b * p.tiles;
+  const int Fb = p.frames ? min(p.frames[b], p.F) : p.F;
+  const int f0 = t * TF;
+  if (f0 >= Fb) continue;
+  const int f1 = min(f0 + TF, Fb);
+  // synthesis frames whose support reaches the tile's analysis windows: [f0 - 3, f1 + 3);
+  // the reflect padding at the item's end reaches frame Fb - 5 from the last frame
+  const int a0 = max(0, f0 - GL_HALO - ((f1 == Fb && f1 - f0 < 2) ? 1 : 0));
+  const int a1 = min(Fb, f1 + GL_HALO);
+  const int sb = a0 * GLHOP;                  // segment start (uncropped samples)
+  const int slen = (a1 - 1 - a0) * GLHOP + GLN;
+  const int L = GLHOP * (Fb - 1);             // istft length of item b
+  // the first round's spectra are requested before the segment is cleared
+  const int nsyn = a1 - a0;
+  float2 xa[16], xb[16];
+  auto load_pair = [&](int r0) {
+    const int fa = a0 + r0 + 2 * w, fb = fa + 1;
+    const bool va = fa < a1, vb = fb < a1;
+    const float2 *XA = p.Xin + ((int64_t)b * p.F + fa) * GLNB;
+    const float2 *XB = XA + GLNB;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int k = lane + 64 * m;
+      const int kk = k > GLN / 2 ? GLN - k : k;
+      xa[m] = va ? XA[kk] : make_float2(0.f, 0.f);
+      xb[m] = vb ? XB[kk] : make_float2(0.f, 0.f);
+    }
+  };
+  load_pair(0);
+  __syncthreads();  // the previous tile's last reads of seg and the wave buffers are done
+  for (int i = threadIdx.x; i < slen; i += 64 * W) seg[i] = 0.f;
+  GLSTAMP(1);
 
   // ---- 1 + 2: synthesis and overlap-add, W frame pairs per round.  The next round's spectra
   // are loaded (registers) while this round's frames are overlap-added.
@@ -876,7 +880,6 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
     float *yb = p.y + (int64_t)b * p.y_stride;
     for (int64_t j = j0 + threadIdx.x; j < j1; j += 64 * W)
       yb[j] = (j < L) ? seg[j + GLN / 2 - sb] : 0.f;
-    return;
   } else {
     // ---- 3: analysis of the tile's frames and the fast-GL update (each wave its own pairs)
     for (int r0 = 0; r0 < f1 - f0; r0 += 2 * W) {
@@ -969,6 +972,7 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
     }
     GLSTAMP(7);
   }
+  }  // tile
 }
 
 // the tile shape: W waves (one FFT pair each at a time), TF analysis frames per tile.  c5
@@ -987,16 +991,34 @@ __global__ __launch_bounds__(64 * W) void gl_fused_kernel(const GlParams p) {
 // tile per CU (c2's 821-frame sentence: 26 tiles of 32 would leave 230 CUs idle; 103 of 8)
 constexpr int GL_SMALL_TF = 8;
 
+// workgroups that fit the chip at once (0: unknown); each walks tiles with a stride of the
+// grid, so the tables are staged once per workgroup instead of once per tile
+template <int TF, bool FINAL>
+int gl_grid(int64_t tiles) {
+  static int cap = -1;
+  if (cap < 0) {
+    int per = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gl_fused_kernel<GL_IW, TF, FINAL>, 64 * GL_IW, 0) !=
+            hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      per = cus = 0;
+    cap = per * cus;
+  }
+  return (int)((cap > 0 && tiles > cap) ? cap : tiles);
+}
+
 template <bool FINAL>
 int gl_launch(GlParams p, hipStream_t s) {
   const int big = (p.F + GL_ITF - 1) / GL_ITF;
   if ((int64_t)p.B * big >= 256) {
     p.tiles = big;
-    hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_ITF, FINAL>), dim3(p.B * p.tiles), dim3(64 * GL_IW), 0, s, p);
+    hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_ITF, FINAL>), dim3(gl_grid<GL_ITF, FINAL>((int64_t)p.B * p.tiles)),
+                       dim3(64 * GL_IW), 0, s, p);
   } else {
     p.tiles = (p.F + GL_SMALL_TF - 1) / GL_SMALL_TF;
-    hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_SMALL_TF, FINAL>), dim3(p.B * p.tiles), dim3(64 * GL_IW), 0, s,
-                       p);
+    hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_SMALL_TF, FINAL>),
+                       dim3(gl_grid<GL_SMALL_TF, FINAL>((int64_t)p.B * p.tiles)), dim3(64 * GL_IW), 0, s, p);
   }
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;

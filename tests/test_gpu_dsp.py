@@ -373,3 +373,35 @@ def test_unit_phases_match_numpy_draw(dsp):
     w2 = dsp.griffinlim(REF_MEL, angles=np.exp(2j * np.pi * np.random.RandomState(3).rand(plan.nb, T)))
     np.testing.assert_array_equal(w1, w2)
 
+
+
+@pytest.mark.parametrize('B,F,frames', [(1, 40, None), (1, 821, None), (3, 300, (300, 113, 33)),
+                                        (16, 1000, None), (5, 517, (517, 9, 2, 258, 33))],
+                         ids=['b1-40', 'c2-821', 'ragged-3', 'b16-32frame-tiles', 'ragged-tiny'])
+def test_fused_gl_iteration_matches_three_kernel_path(dsp, B, F, frames, monkeypatch):
+    """The fused Griffin-Lim iteration (ftmi_griffinlim_iter + ftmi_istft_fused: overlap-add in
+    LDS, the FFT in one wave, tiles of 8 or 32 frames with a 3-frame halo, the grid-stride
+    tile loop) against the three-kernel path (istft frames -> overlap-add -> analysis) on
+    the same magnitudes and phases: 8-frame tiles (B * ceil(F / 32) < 256), 32-frame tiles
+    (b16), ragged items down to 2 frames (reflect padding inside one tile, a 1-frame last
+    tile).  Both are float64 FFTs rounded to float32; they differ only in the FFT's internal
+    rounding (FMA complex products here): max |diff| <= 1e-6 x peak, and the tail past each
+    item's length exactly zero in both."""
+    from forwardtacotron_amd import dsp as G
+    plan = dsp.plan()
+    rng = np.random.Generator(np.random.PCG64(F + B))
+    S = torch.from_numpy(rng.random((B, F, plan.nb), dtype=np.float32)).cuda()
+    ang = torch.polar(torch.ones(B, F, plan.nb, dtype=torch.float64, device='cuda'),
+                      torch.from_numpy(rng.random((B, F, plan.nb)) * 6.283).cuda()).to(torch.complex64)
+    fr = None if frames is None else torch.tensor(frames, dtype=torch.int32, device='cuda')
+    out = {}
+    for mode in ('1', '0'):
+        monkeypatch.setenv('FTMI_GL_FUSED', mode)
+        out[mode] = G.griffinlim_from_stft(plan, S, ang, 8, fr).cpu().numpy()
+    a, b = out['1'], out['0']
+    assert a.shape == b.shape == (B, 256 * (F - 1))
+    peak = np.abs(b).max()
+    assert np.abs(a - b).max() <= 1e-6 * peak, (np.abs(a - b).max(), peak)
+    if frames is not None:
+        for i, f in enumerate(frames):
+            assert not a[i, 256 * (f - 1):].any() and not b[i, 256 * (f - 1):].any()
