@@ -272,6 +272,32 @@ def test_c4_global_batch_vs_torch_cpu(gpu_model, synth_sd):
         assert d.mean() < 1e-4 and d.max() < 5e-4, (k, d.mean(), d.max())
 
 
+def test_mid_batch_prenet_rows_stay_concurrent(gpu_model, synth_sd):
+    """at ~900 prenet rows (B = 8, T = 120: 960 rows) the spread CBHG
+    tail alone would take 240 workgroups; the phase must then give the tail to the stack
+    kernel and stay on its concurrent streams (not serialise), and the result must still be
+    the reference's (torch-CPU restatement: LengthRegulator counts equal, mel_post mean |d|
+    < 1e-4, max < 5e-4)."""
+    from forwardtacotron_amd import ops
+    from forwardtacotron_amd.synthetic import synthetic_tokens
+    from oracle import ft_torch_cpu as TC
+    x = synthetic_tokens(8, 120, seed=21, min_len=110)
+    dev = torch.device('cuda', torch.cuda.current_device())
+    streams = gpu_model._side_streams(dev, 8, 120)
+    main = torch.cuda.current_stream(dev)
+    assert not all(s == main for s in streams), 'phoneme phase serialised at 960 rows'
+    if gpu_model.prenet.allow_spread:
+        preds = (gpu_model.dur_pred.rnn, gpu_model.pitch_pred.rnn, gpu_model.energy_pred.rnn)
+        need = sum(ops.rnn_blocks(r.cell, 8, r.hidden) for r in preds)
+        assert need + gpu_model.prenet.spread_blocks(960) <= ops._num_cus()
+    out = gpu_model.generate(torch.from_numpy(x).cuda())
+    ref = TC.generate(TC.to_torch(synth_sd), torch.from_numpy(x))
+    assert np.array_equal(O.duration_counts(out['dur'].cpu().numpy()),
+                          O.duration_counts(ref['dur'].numpy()))
+    d = np.abs(out['mel_post'].cpu().numpy() - ref['mel_post'].numpy())
+    assert d.mean() < 1e-4 and d.max() < 5e-4, (d.mean(), d.max())
+
+
 def _fresh_graphs(model):
     for k in ('_ftmi_graphs', '_ftmi_graph_seen'):
         model.__dict__.pop(k, None)
