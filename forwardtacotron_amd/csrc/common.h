@@ -29,9 +29,11 @@ __attribute__((visibility("hidden"))) int ftmi_resident_cus(void);
 // relying on a spin bound to turn the deadlock into a status bit).
 static inline int ftmi_resident_ok(const void *kernel, int grid, int block, size_t smem) {
   int per = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, smem) != hipSuccess ||
-      per <= 0)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, smem) != hipSuccess) {
+    (void)hipGetLastError();  // a failed query must not surface in the caller's next HIP call
     return FTMI_E_UNSUPPORTED;
+  }
+  if (per <= 0) return FTMI_E_UNSUPPORTED;
   return (int64_t)per * ftmi_resident_cus() >= grid ? FTMI_OK : FTMI_E_UNSUPPORTED;
 }
 

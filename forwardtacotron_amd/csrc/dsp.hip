@@ -993,18 +993,22 @@ constexpr int GL_SMALL_TF = 8;
 
 // workgroups that fit the chip at once (0: unknown); each walks tiles with a stride of the
 // grid, so the tables are staged once per workgroup instead of once per tile
-template <int TF, bool FINAL>
+// (workgroups per CU from the kernel's static LDS, which is what limits it: one per CU)
+template <int TF>
 int gl_grid(int64_t tiles) {
-  static int cap = -1;
-  if (cap < 0) {
-    int per = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gl_fused_kernel<GL_IW, TF, FINAL>, 64 * GL_IW, 0) !=
-            hipSuccess ||
-        hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      per = cus = 0;
-    cap = per * cus;
+  constexpr int lds = gl_seg(TF) * 4 + GL_IW * GL_BUF * 16 + GLN * 8 + (GL_TWA + GL_TWB) * 16 + GLHOP * 4;
+  constexpr int per = (160 * 1024) / lds;
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+      (void)hipGetLastError();
+      n = 0;
+    }
+    cus = n;
   }
+  const int64_t cap = (int64_t)per * cus;
   return (int)((cap > 0 && tiles > cap) ? cap : tiles);
 }
 
@@ -1013,12 +1017,12 @@ int gl_launch(GlParams p, hipStream_t s) {
   const int big = (p.F + GL_ITF - 1) / GL_ITF;
   if ((int64_t)p.B * big >= 256) {
     p.tiles = big;
-    hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_ITF, FINAL>), dim3(gl_grid<GL_ITF, FINAL>((int64_t)p.B * p.tiles)),
+    hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_ITF, FINAL>), dim3(gl_grid<GL_ITF>((int64_t)p.B * p.tiles)),
                        dim3(64 * GL_IW), 0, s, p);
   } else {
     p.tiles = (p.F + GL_SMALL_TF - 1) / GL_SMALL_TF;
     hipLaunchKernelGGL((gl_fused_kernel<GL_IW, GL_SMALL_TF, FINAL>),
-                       dim3(gl_grid<GL_SMALL_TF, FINAL>((int64_t)p.B * p.tiles)), dim3(64 * GL_IW), 0, s, p);
+                       dim3(gl_grid<GL_SMALL_TF>((int64_t)p.B * p.tiles)), dim3(64 * GL_IW), 0, s, p);
   }
   FTMI_CHECK_LAUNCH();
   return FTMI_OK;

@@ -1280,6 +1280,10 @@ extern "C" int ftmi_rnn_bidir(int32_t cell, int32_t B, int32_t T, int32_t H, con
   if (!index && T_src != T) return FTMI_E_SHAPE;
   if (!ftmi_aligned16(w_hh) || !ftmi_aligned16(sync)) return FTMI_E_ALIGN;
   if (!ftmi_aligned16(y) || (y_stride & 3)) return FTMI_E_ALIGN;  // float4 row stores
+  // the kernel forms below: GRU H 64 / 128 / 256, LSTM H 512 — refused before any HIP call
+  // (the workspace memset), so an unsupported shape leaves no HIP error behind
+  if (cell == 1 ? H != 512 : (cell != 0 || (H != 64 && H != 128 && H != 256)))
+    return FTMI_E_UNSUPPORTED;
   hipStream_t s = ftmi_hs(stream);
   RnnParams p = {};
   int nchunks = 0;

@@ -83,7 +83,8 @@ enum { FTMI_BANK_COUNTERS = 4096 };
  * ftmi_conv_bank_halves_image[_bytes]; 17: FTMI_BANK_PAIR, ftmi_conv_args.x_plane / x_fin;
  * 18: rejected variants removed — FTMI_BANK_LAST, FTMI_BANK_PAIR, ftmi_conv_args.x_plane /
  * x_fin, ftmi_gru_bidir_fused; ftmi_highway_stack_spread[_ws_bytes|_blocks] added;
- * 19: ftmi_nnls_lbfgsb_*, ftmi_set_resident_cu_limit, the persistent-launch guard). */
+ * 19: ftmi_nnls_lbfgsb_*, ftmi_set_resident_cu_limit, the persistent-launch guard,
+ * ftmi_griffinlim_iter, ftmi_istft_fused). */
 int ftmi_abi_version(void);
 /* sha256 (hex) of the sources this library was built from (the .hip and .h files of
  * forwardtacotron_amd/csrc and include/ftmi.h): the Python binding refuses a library whose
