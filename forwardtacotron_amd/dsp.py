@@ -448,9 +448,11 @@ class DSP:
     def draw_uniforms(self, T: int, random_state=None) -> np.ndarray:
         """The U[0, 1) draw behind griffinlim's initial phases for a T-frame mel, taken from
         the reference's stream (librosa: np.random.rand(n_bins, T), or RandomState
-        (random_state)).  Drawn ahead — e.g. while the GPU still decodes the mel, as
-        gen_forward does — and passed as griffinlim(..., uniforms=u), it is the same draw in
-        the same stream order."""
+        (random_state)).  Drawn ahead by a caller that has other work to overlap, and passed
+        as griffinlim(..., uniforms=u), it is the same draw in the same stream order.
+        (gen_forward does not: generate() returns after its end-of-call status read, so no
+        device work is left to hide the draw behind; griffinlim queues the NNLS first and
+        draws while it runs.)"""
         rng = np.random if random_state is None else np.random.RandomState(random_state)
         return rng.rand(self.n_fft // 2 + 1, T)
 
