@@ -625,8 +625,11 @@ __device__ __forceinline__ double2 gl_dpp2(double2 v) {
 // product's 49-bit grid — so (float)(a * gl_rcp64(b)) IS the correctly rounded a / b that
 // numpy computes.  The IEEE float32 division sequence reads VCC in v_div_fmas, which keeps
 // independent divisions from overlapping.
+// x is a float32 value at every call (|an| + 1e-16, the window sum-square), so the seed is
+// the float32 reciprocal (~2^-22, the fast transcendental unit): two Newton steps reach
+// ~2^-88.
 __device__ __forceinline__ double gl_rcp64(double x) {
-  double r = __builtin_amdgcn_rcp(x);
+  double r = (double)__builtin_amdgcn_rcpf((float)x);
   double e = __fma_rn(-x, r, 1.0);
   r = __fma_rn(r, e, r);
   e = __fma_rn(-x, r, 1.0);

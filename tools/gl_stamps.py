@@ -48,6 +48,7 @@ for cfg in (sys.argv[1:] or ['c2', 'c5']):
     buf = (ctypes.c_ulonglong * n)()
     assert fn(buf, n) == 0
     st = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8)[:min(nblk, 4096)].astype(np.float64)
+    st = st[st[:, 7] > 0]  # the workgroups that ran (a grid-stride grid is <= the tiles)
     rel = st - st[:, :1]
     print(f'{cfg}: B={B} F={F} {nblk} workgroups, {a.elapsed_time(b) / 20 * 1e3:.1f} us per '
           f'iteration (events, 20 back to back); cycles from each workgroup start, median (max):')
