@@ -90,7 +90,7 @@ PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r6c2_pmc_traffic.json')   # c2 
 PMC_PROFILE_C5 = os.path.join(ROOT, 'profiles', 'r6c5_pmc_traffic.json')   # c5 (--model fast_pitch)
 # the PMC files are a prior run of the same workload (separate FETCH_SIZE / WRITE_SIZE passes
 # cannot share the timed run), taken on this tree
-PMC_TREE = '3e61c87 (round 6, tools/gpu_r6_measure.sh pmc / mfma)'
+PMC_TREE = '16e443f (round 6 final: tools/gpu_r6_measure.sh pmc; MFMA-busy pass 3e61c87, GEMM kernels unchanged since)'
 
 
 def rocprof_name(label: str):
