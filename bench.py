@@ -190,7 +190,11 @@ def time_prenet_bank(model, x, reps: int = 20):
               Infinity-Cache resident, as in a generate() loop;
       eager — the same calls issued from the host one by one (ctypes + argument packing);
       cold  — each call behind a 512 MiB overwrite of another buffer (the weights come from
-              HBM): graph [overwrite, call] x reps minus graph [overwrite] x reps;
+              HBM): graph [overwrite, call] x reps minus graph [overwrite] x reps; the
+              overwrite's dirty lines are still draining to HBM while the call reads;
+      cold_read — each call behind a 1 GiB streaming READ of another buffer (the weights
+              evicted from L2 and the 256 MB Infinity Cache by clean lines: weights from HBM,
+              no write-back in flight): graph [read, call] x reps minus graph [read] x reps;
       planes — A/B in the same process: the halves kernel reading the split planes."""
     from forwardtacotron_amd import ops
     cb = model.prenet
@@ -218,9 +222,11 @@ def time_prenet_bank(model, x, reps: int = 20):
         call()
     eager = timed(lambda: [call() for _ in range(reps)]) / reps
     flush = torch.empty(512 << 20, dtype=torch.uint8, device=x.device)
+    rflush = torch.zeros(1 << 28, dtype=torch.float32, device=x.device)  # 1 GiB, read only
     graphs = {}
     bodies = [('warm', lambda: call()), ('flush', lambda: flush.fill_(1)),
-              ('cold', lambda: (flush.fill_(1), call()))]
+              ('cold', lambda: (flush.fill_(1), call())),
+              ('rflush', lambda: rflush.sum()), ('cold_read', lambda: (rflush.sum(), call()))]
     if img is not None:  # A/B: the same kernel on the split planes
         bodies += [('planes', lambda: call(None))]
     for name, body in bodies:
@@ -232,11 +238,12 @@ def time_prenet_bank(model, x, reps: int = 20):
         graphs[name] = g
     res = {'warm': timed(graphs['warm'].replay) / reps, 'eager': eager,
            'cold': (timed(graphs['cold'].replay) - timed(graphs['flush'].replay)) / reps,
+           'cold_read': (timed(graphs['cold_read'].replay) - timed(graphs['rflush'].replay)) / reps,
            'weights': ('stream-order image' if img is not None
                        else 'split planes (no few-row kernel at this size)')}
     if img is not None:
         res['planes'] = timed(graphs['planes'].replay) / reps
-    del graphs, flush
+    del graphs, flush, rflush
     return res
 
 
@@ -681,6 +688,13 @@ def main():
                 prenet['cold_basis'] = ('each call behind a 512 MiB overwrite of another buffer '
                                         '(weights from HBM): graph [overwrite, call] minus graph '
                                         '[overwrite], per call')
+                prenet['cold_read_ms'] = round(pb['cold_read'], 4)
+                prenet['hbm_frac_cold_read'] = frac(pb['cold_read'])
+                prenet['cold_read_basis'] = ('each call behind a 1 GiB streaming read of another '
+                                             'buffer (weights evicted from L2 and the Infinity '
+                                             'Cache by clean lines: from HBM, no dirty write-back '
+                                             'competing): graph [read, call] minus graph [read], '
+                                             'per call')
                 prenet['weights_read'] = pb['weights']
                 # PMC traffic of the bank kernel from the committed passes of this workload
                 if pmc_path and os.path.exists(pmc_path) and pb['weights'] == 'stream-order image':

@@ -4,7 +4,10 @@
 // against a contiguous per-block stream?  No compute: each lane sums what it loaded.
 //   hipcc -O3 --offload-arch=gfx950 tools/probe_stream.hip -o /tmp/probe_stream
 // Prints per-variant us per launch (HIP events over back-to-back launches, warm Infinity
-// Cache) and per launch behind a 512 MiB overwrite (cold).
+// Cache), per launch behind a 512 MiB overwrite (cold: the overwrite's dirty lines are
+// still being written back while the launch reads), and per launch behind a 1 GiB streaming
+// READ of another buffer (cold-read: the weights evicted from L2 and the Infinity Cache by
+// clean lines, so the launch pays HBM reads only).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -107,6 +110,17 @@ __global__ __launch_bounds__(NT, 1) void contig(const f32x4 *buf, size_t per16, 
   out[blockIdx.x * NT + threadIdx.x] = s.x + s.y + s.z + s.w;
 }
 
+// evicts every cache level by reading n16 x 16 B (clean lines); one float per block out
+__global__ __launch_bounds__(256) void evict_read(const f32x4 *buf, size_t n16, float *out) {
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) s += buf[i];
+  if (s.x == 12345.f) out[blockIdx.x] = s.y;  // never true for the zero buffer: keeps the loads
+}
+
+static f32x4 *g_rflush = nullptr;
+static size_t g_rbytes = 0;
+static float *g_rout = nullptr;
+
 template <typename F>
 static void timeit(const char *name, F launch, void *flush, size_t fbytes, double bytes) {
   hipEvent_t a, b;
@@ -132,8 +146,18 @@ static void timeit(const char *name, F launch, void *flush, size_t fbytes, doubl
     CK(hipEventElapsedTime(&ms, a, b));
     cold += ms * 1e3 / 10;
   }
-  printf("%-28s warm %7.2f us (%5.2f TB/s) | cold %7.2f us (%5.2f TB/s)\n", name, warm,
-         bytes / warm / 1e6, cold, bytes / cold / 1e6);
+  double cold_r = 0;
+  for (int i = 0; i < 10; ++i) {
+    evict_read<<<4096, 256>>>(g_rflush, g_rbytes / 16, g_rout);
+    CK(hipEventRecord(a));
+    launch();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    CK(hipEventElapsedTime(&ms, a, b));
+    cold_r += ms * 1e3 / 10;
+  }
+  printf("%-28s warm %7.2f us (%5.2f TB/s) | cold %7.2f us (%5.2f TB/s) | cold-read %7.2f us (%5.2f TB/s)\n",
+         name, warm, bytes / warm / 1e6, cold, bytes / cold / 1e6, cold_r, bytes / cold_r / 1e6);
   fflush(stdout);
 }
 
@@ -158,6 +182,10 @@ int main() {
   const size_t fb = (size_t)512 << 20;
   void *flush;
   CK(hipMalloc(&flush, fb));
+  g_rbytes = (size_t)1 << 30;
+  CK(hipMalloc(&g_rflush, g_rbytes));
+  CK(hipMemset(g_rflush, 0, g_rbytes));
+  CK(hipMalloc(&g_rout, 1 << 16));
   printf("bank weight planes: %.2f MB\n", total / 1e6);
   const double B = (double)total;
   timeit("bank 8w ring4", [&] { bank_pattern<8, false><<<256, 512>>>(P, out); }, flush, fb, B);
