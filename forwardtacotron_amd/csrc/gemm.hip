@@ -4117,8 +4117,8 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
   case D_:                                                                                        \
     hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, D_, 16, 16, true>), grid, block, 0, s, p);    \
     break;
-      FTMI_BH_DIAG(1) FTMI_BH_DIAG(2) FTMI_BH_DIAG(4) FTMI_BH_DIAG(32) FTMI_BH_DIAG(128)
-      FTMI_BH_DIAG(256) FTMI_BH_DIAG(512)
+      FTMI_BH_DIAG(1) FTMI_BH_DIAG(2) FTMI_BH_DIAG(3) FTMI_BH_DIAG(4) FTMI_BH_DIAG(16)
+      FTMI_BH_DIAG(18) FTMI_BH_DIAG(32) FTMI_BH_DIAG(128) FTMI_BH_DIAG(256) FTMI_BH_DIAG(512)
 #undef FTMI_BH_DIAG
       default:
         hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16, true>), grid, block, 0, s, p);
