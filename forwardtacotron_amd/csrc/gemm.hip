@@ -2574,7 +2574,15 @@ constexpr int BH_MAXCH = 4;  // 32-channel chunks per half: Cin <= 256
 // is one contiguous 1 KB run (from the planes it touches 16 half-used 128-B lines, their
 // other halves loaded by the next step).  Measured with the bit-3 timing variant's layout
 // (r4c stamps): 17.8 vs 20.4 us per call.
-template <int MI, int NCH, int DIAG = 0, int KT = 0, int NCT = 0, bool PK = false>
+//
+// NM (one sequence in the row tile, B = 1: the c2 prenet bank): no tap masks.  The slab rows
+// outside the sequence are staged as zeros (the conv's zero padding), so every tap reads its
+// row directly: a fragment's LDS address is the lane's base + a per-step scalar + a
+// compile-time row-block offset (the instruction's immediate), instead of a mask test, a
+// select and a quarter-rate multiply per fragment (measured in the ISA: ~7 VALU per
+// fragment, 56 per step and wave on the MFMA loop's issue path).  The products of the masked
+// taps were +0 x w either way: bit-identical.
+template <int MI, int NCH, int DIAG = 0, int KT = 0, int NCT = 0, bool PK = false, bool NM = false>
 __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmParams p) {
   BHSTAMP(0, 0);
   constexpr int RM = MI * 16;
@@ -2613,8 +2621,11 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
   for (int i = 0; i < ASLOTS; ++i) {  // past the slab: a clamped (unused) reload
     const int r = min((tid >> 3) + 64 * i, NCH * SRM - 1), c = r / SRM, sr = r - c * SRM;
     int m = sr - padh;  // one row tile: m0 = 0
+    const bool inseq = m >= 0 && m < p.M;
     m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
     av[i] = *(const f32x4 *)(p.x + (int64_t)m * p.x_stride + c_half + c * 32 + seg * 4);
+    if constexpr (NM)  // the zero padding itself (applied after the load issues: no wait here)
+      av[i] = inseq ? av[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
   }
   // ---- the weight fragments of this wave's CONTIGUOUS step range [q0, q1) of the unit's
   // (group, tap, chunk) list, heavy group first, chunks fastest (consecutive steps of a wave
@@ -2741,8 +2752,9 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
 #pragma unroll
       for (int mm = 0; mm < MB; ++mm) {
         const int mi = m0 + mm;
-        const bool ok = ((msk[mi] >> sh_j) & 1u) != 0;
-        const int o = (ok ? mi * 16 + fr + dr : SRM) * SL_P + fs * 8;
+        const bool ok = NM || ((msk[mi] >> sh_j) & 1u) != 0;
+        const int o = NM ? (fr + dr) * SL_P + fs * 8 + mi * 16 * SL_P
+                         : (ok ? mi * 16 + fr + dr : SRM) * SL_P + fs * 8;
         if constexpr (DIAG & 2) {
           ah[mm] = b1;
           at[mm] = bh;
@@ -4110,7 +4122,7 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
 #ifdef FTMI_DIAG
   // timing variants of the c2 prenet bank (results invalid for some bits): diagnostic build only
   const char *dg = getenv("FTMI_BANK_HALVES_DIAG");
-  const int diag = dg && prenet && p.M > 64 ? atoi(dg) : 0;
+  const int diag = dg && prenet && p.M > 64 ? atoi(dg) : 0;  // any other value: the masked form
   if (diag && p.wimg) {
     switch (diag) {
 #define FTMI_BH_DIAG(D_)                                                                          \
@@ -4137,6 +4149,8 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
   if (p.wimg) {  // the stream-order weight image
     if (p.M <= 64) {
       FTMI_BH_NCH(4, true)
+    } else if (prenet && p.T == p.M) {  // one sequence: the mask-free form
+      hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16, true, true>), grid, block, 0, s, p);
     } else if (prenet) {
       hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16, true>), grid, block, 0, s, p);
     } else {
@@ -4144,6 +4158,8 @@ static int launch_bank_halves(const GemmParams &p, hipStream_t s) {
     }
   } else if (p.M <= 64) {
     FTMI_BH_NCH(4, false)
+  } else if (prenet && p.T == p.M) {
+    hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16, false, true>), grid, block, 0, s, p);
   } else if (prenet) {
     hipLaunchKernelGGL((conv_bank_halves_kernel<8, 4, 0, 16, 16>), grid, block, 0, s, p);
   } else {
