@@ -2830,8 +2830,15 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
     const int e = tid + 512 * r, ug = e / (MI * 64);
     eo[r] = e;
     const int w0 = ug ? wfirst_l : 0, w1 = ug ? 7 : wlast_h;
-    f32x4 s = red[w0 * NIT + e];
-    for (int w = w0 + 1; w <= w1; ++w) s += red[w * NIT + e];
+    // every partial read at once (slots past w1 re-read w1's, never added), then summed in
+    // wave order: one LDS round trip instead of one per wave, the same additions
+    f32x4 pv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pv[k] = red[min(w0 + k, w1) * NIT + e];
+    f32x4 s = pv[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+      if (w0 + k <= w1) s += pv[k];  // wave-uniform
     v[r] = s;
   }
   BHSTAMP(4, 0);
