@@ -1378,14 +1378,20 @@ __global__ __launch_bounds__(WS ? 768 : 512, 1) void conv_gemm_slab_kernel(const
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (f32x4){0.f, 0.f, 0.f, 0.f};
   };
+  // A-fragment addresses without a multiply per fragment: the row (wm 64 + mi 16 + fr + j)
+  // is the lane's base + j SL_P (per step) + mi 16 SL_P (the instruction's immediate), and a
+  // masked tap's zero row is selected as an offset from that same immediate (the select
+  // before a multiply cost a quarter-rate v_mul_lo_u32 per fragment; the same addresses)
+  const int a_row0 = (wm * 64 + fr) * SL_P + fs * 8, a_zrow = SL_ZROW * SL_P + fs * 8;
   auto mfma_step = [&](f32x4 (&acc)[4][4], int abuf, int bbuf, int j) {
     const _Float16 *Ab = lds_a + abuf * 2 * SL_AIMG;
     const _Float16 *Bb = lds_b + bbuf * 2 * SL_BIMG;
     f16x8 ah[4], at[4];
+    const int a_rowj = a_row0 + j * SL_P;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       const bool ok = (vmask[mi] >> j) & 1u;
-      const int o = (ok ? wm * 64 + mi * 16 + fr + j : SL_ZROW) * SL_P + fs * 8;
+      const int o = (ok ? a_rowj : a_zrow - mi * 16 * SL_P) + mi * 16 * SL_P;
       ah[mi] = *(const f16x8 *)(Ab + o);
       at[mi] = *(const f16x8 *)(Ab + SL_AIMG + o);
     }
@@ -2419,8 +2425,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
               ah[mi] = dh[mi];
               at[mi] = dt[mi];
             } else {
+              // the slab kernel's multiply-free address form (same addresses)
               const bool ok = (vmask[mi] >> j) & 1u;
-              const int o = (ok ? mi * 16 + fr + j + dp : SK_ZROW) * SL_P + fs * 8;
+              const int o = (ok ? fr * SL_P + fs * 8 + (j + dp) * SL_P
+                                : SK_ZROW * SL_P + fs * 8 - mi * 16 * SL_P) + mi * 16 * SL_P;
               ah[mi] = *(const f16x8 *)(Ab + o);
               at[mi] = *(const f16x8 *)(Ab + SK_AIMG + o);
             }
