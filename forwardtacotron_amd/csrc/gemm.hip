@@ -1724,10 +1724,14 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_slabp_kernel(const GemmParam
   auto read_frags = [&](Frag &f, int c, int j, int bbuf) {
     const _Float16 *Ab = lds_a + (c % SP_NBUF) * 2 * SP_AIMG;
     const _Float16 *Bb = lds_b + bbuf * 2 * SP_BIMG;
+    // row wm 64 + mi 16 + fr + j: mi 16 changes neither the swizzle bit (row bit 2) nor
+    // anything but the immediate, so one sp_off per step and a select per fragment (the
+    // zero row as an offset from the same immediate): the same addresses
+    const int o_j = sp_off(wm * 64 + fr + j, fs), o_z = sp_off(SL_ZROW, fs);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       const bool ok = (vmask[mi] >> j) & 1u;
-      const int o = sp_off(ok ? wm * 64 + mi * 16 + fr + j : SL_ZROW, fs);
+      const int o = (ok ? o_j : o_z - mi * 16 * SP_ROW) + mi * 16 * SP_ROW;
       f.ah[mi] = *(const f16x8 *)(Ab + o);
       f.at[mi] = *(const f16x8 *)(Ab + SP_AIMG + o);
     }
@@ -1998,10 +2002,12 @@ __global__ __launch_bounds__(512, 1) void conv_bank_walk_kernel(const GemmParams
     const int d = j - k / 2;  // the tap's row offset
     const _Float16 *Ab = lds_a + c * 2 * BW_AIMG;
     const _Float16 *Bb = lds_b + bbuf * 2 * SP_BIMG;
+    // one sp_off per step, a select per fragment (the slabp kernel's form: same addresses)
+    const int o_d = sp_off(wm * 64 + fr + d + PMAX, fs), o_z = sp_off(BW_ZROW, fs);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       const bool ok = (unsigned)(tfr[mi] + d) < (unsigned)p.T;
-      const int o = sp_off(ok ? wm * 64 + mi * 16 + fr + d + PMAX : BW_ZROW, fs);
+      const int o = (ok ? o_d : o_z - mi * 16 * SP_ROW) + mi * 16 * SP_ROW;
       f.ah[mi] = *(const f16x8 *)(Ab + o);
       f.at[mi] = *(const f16x8 *)(Ab + BW_AIMG + o);
     }
