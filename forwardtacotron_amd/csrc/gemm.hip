@@ -2767,8 +2767,11 @@ __global__ __launch_bounds__(512, 1) void conv_bank_halves_kernel(const GemmPara
       for (int mm = 0; mm < MB; ++mm) {
         const int mi = m0 + mm;
         const bool ok = NM || ((msk[mi] >> sh_j) & 1u) != 0;
+        // masked form: the zero row selected as an offset from the same immediate (the slab
+        // kernel's multiply-free address, the same addresses)
         const int o = NM ? (fr + dr) * SL_P + fs * 8 + mi * 16 * SL_P
-                         : (ok ? mi * 16 + fr + dr : SRM) * SL_P + fs * 8;
+                         : (ok ? (fr + dr) * SL_P + fs * 8 : SRM * SL_P + fs * 8 - mi * 16 * SL_P) +
+                               mi * 16 * SL_P;
         if constexpr (DIAG & 2) {
           ah[mm] = b1;
           at[mm] = bh;
