@@ -2270,7 +2270,9 @@ __device__ unsigned long long ftmi_skinny_stamps[4096 * 8];
 // bit 0 = the A fragments read once before the loop (no LDS reads in it), bit 1 = no MFMAs
 // (the loaded weights feed one VALU add), bit 2 = every weight load from one L2-hot line.
 // Instantiated only in the diagnostic build (-DFTMI_DIAG, libftmi_stamps.so).
-template <bool MAXPOOL, bool BANK = false, int DIAG = 0>
+// NM (one sequence in the rows, B = 1: c2): no tap masks — the slab rows outside the sequence
+// are staged as zeros (conv_bank_halves_kernel's mask-free form; bit-identical).
+template <bool MAXPOOL, bool BANK = false, int DIAG = 0, bool NM = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmParams p) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[SK_CPB * 2 * SK_AIMG];
   SKSTAMP(0);
@@ -2311,11 +2313,16 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
     const int r = min((tid >> 3) + 64 * i, nch * SK_SR - 1), c = r / SK_SR, sr = r - c * SK_SR;
     const int ch0 = (c_begin + c) * 32 + seg * 4, ch = ch0 < Cin ? ch0 : 0;
     int m = m0 - pad + sr;
+    const bool inseq = m >= 0 && m < p.M;
     m = m < 0 ? 0 : (m >= p.M ? p.M - 1 : m);  // clamped rows only feed masked taps
     const float *src = p.x + (int64_t)m * p.x_stride + ch;
     av[i] = *(const f32x4 *)src;
     // CBHG maxpool(2, 1) fused: max(x[t - 1], x[t]); x[0] at t = 0
     if constexpr (MAXPOOL) au[i] = *(const f32x4 *)(src - (m % p.T > 0 ? p.x_stride : 0));
+    if constexpr (NM) {  // the zero padding itself (the pooled padding is zero too)
+      av[i] = inseq ? av[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
+      if constexpr (MAXPOOL) au[i] = inseq ? au[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
   }
   float amax = 0.f;
 #pragma unroll
@@ -2432,7 +2439,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_skinny_kernel(const GemmPara
               at[mi] = dt[mi];
             } else {
               // the slab kernel's multiply-free address form (same addresses)
-              const bool ok = (vmask[mi] >> j) & 1u;
+              const bool ok = NM || ((vmask[mi] >> j) & 1u) != 0;
               const int o = (ok ? fr * SL_P + fs * 8 + (j + dp) * SL_P
                                 : SK_ZROW * SL_P + fs * 8 - mi * 16 * SL_P) + mi * 16 * SL_P;
               ah[mi] = *(const f16x8 *)(Ab + o);
@@ -4087,12 +4094,20 @@ static int launch_skinny(const GemmParams &p, int epi, bool maxpool, hipStream_t
         hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true>), grid, block, 0, s, q);
     }
 #else
-    hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true>), grid, block, 0, s, q);
+    if (q.T == q.M)  // one sequence: the mask-free form
+      hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true, 0, true>), grid, block, 0, s, q);
+    else
+      hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, true>), grid, block, 0, s, q);
 #endif
   } else {
     dim3 grid(MT * q.ngroups * NT, q.split), block(512);
-    if (maxpool)
+    const bool nm = q.T == q.M;  // one sequence: the mask-free form
+    if (maxpool && nm)
+      hipLaunchKernelGGL((conv_gemm_skinny_kernel<true, false, 0, true>), grid, block, 0, s, q);
+    else if (maxpool)
       hipLaunchKernelGGL(conv_gemm_skinny_kernel<true>, grid, block, 0, s, q);
+    else if (nm)
+      hipLaunchKernelGGL((conv_gemm_skinny_kernel<false, false, 0, true>), grid, block, 0, s, q);
     else
       hipLaunchKernelGGL(conv_gemm_skinny_kernel<false>, grid, block, 0, s, q);
   }
