@@ -86,11 +86,12 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 
 PMC_PROFILE = os.path.join(ROOT, 'profiles', 'r6_pmc_traffic.json')        # c3
-PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r6c2_pmc_traffic.json')   # c2 (--config c2)
+PMC_PROFILE_C2 = os.path.join(ROOT, 'profiles', 'r6final_c2_pmc_traffic.json')   # c2 (--config c2)
 PMC_PROFILE_C5 = os.path.join(ROOT, 'profiles', 'r6c5_pmc_traffic.json')   # c5 (--model fast_pitch)
 # the PMC files are a prior run of the same workload (separate FETCH_SIZE / WRITE_SIZE passes
 # cannot share the timed run), taken on this tree
-PMC_TREE = '16e443f (round 6 final: tools/gpu_r6_measure.sh pmc; MFMA-busy pass 3e61c87, GEMM kernels unchanged since)'
+PMC_TREE = '16e443f (round 6: tools/gpu_r6_measure.sh pmc; MFMA-busy pass 3e61c87, GEMM kernels unchanged since)'
+PMC_TREE_C2 = 'fcdfa17 (round 6 final tree: the mask-free prenet bank; FETCH_SIZE / WRITE_SIZE passes)'
 
 
 def rocprof_name(label: str):
@@ -122,7 +123,8 @@ def pmc_traffic(label: str, path: str = PMC_PROFILE):
     return {'bytes_per_launch': hit[0]['hbm_bytes_per_launch'],
             'read_bytes_corrected': hit[0]['read_bytes_corrected'],
             'write_bytes': hit[0]['write_bytes'],
-            'source': os.path.relpath(path, ROOT), 'measured_on_tree': PMC_TREE,
+            'source': os.path.relpath(path, ROOT),
+            'measured_on_tree': PMC_TREE_C2 if path == PMC_PROFILE_C2 else PMC_TREE,
             'note': 'a prior PMC run of this workload, not this run'}
 
 
@@ -144,7 +146,8 @@ def pmc_traffic_slab(label: str, path: str):
     k, v = hit[0]
     return {'bytes_per_launch': v['hbm_bytes_per_launch'],
             'read_bytes_corrected': v['read_bytes_corrected'], 'write_bytes': v['write_bytes'],
-            'kernel_grid': k, 'source': os.path.relpath(path, ROOT), 'measured_on_tree': PMC_TREE,
+            'kernel_grid': k, 'source': os.path.relpath(path, ROOT),
+            'measured_on_tree': PMC_TREE_C2 if path == PMC_PROFILE_C2 else PMC_TREE,
             'note': 'a prior PMC run of this workload, not this run'}
 
 
@@ -304,6 +307,7 @@ def main():
         args.batch, args.tmin, args.tmax = 1, 120, 120
     shape = (args.batch, args.tmin, args.tmax)
     pmc_path = {(64, 50, 200): PMC_PROFILE, (1, 120, 120): PMC_PROFILE_C2}.get(shape)
+    pmc_tree = PMC_TREE_C2 if pmc_path == PMC_PROFILE_C2 else PMC_TREE
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -699,8 +703,11 @@ def main():
                 # PMC traffic of the bank kernel from the committed passes of this workload
                 if pmc_path and os.path.exists(pmc_path) and pb['weights'] == 'stream-order image':
                     ks = json.load(open(pmc_path))['kernels']
-                    hit = [v_ for k_, v_ in ks.items()
-                           if k_.startswith('conv_bank_halves_kernel<8, 4, 0, 16, 16, true>')]
+                    # the mask-free single-sequence form (B = 1) when the PMC run has it, else
+                    # the masked image kernel of earlier runs
+                    hit = [ks[k_] for k_ in ('conv_bank_halves_kernel<8, 4, 0, 16, 16, true, true>',
+                                             'conv_bank_halves_kernel<8, 4, 0, 16, 16, true>')
+                           if k_ in ks][:1]
                     if len(hit) == 1:
                         prenet['traffic'] = hit[0]['hbm_bytes_per_launch']
                         prenet['traffic_detail'] = {
@@ -709,7 +716,7 @@ def main():
                             'vs_algorithmic': round(hit[0]['hbm_bytes_per_launch'] / v['bytes'], 3),
                             'what': 'FETCH_SIZE x 2 + WRITE_SIZE per launch (writes include the '
                                     'halves\' 4 MB exchange and the counters)',
-                            'source': os.path.relpath(pmc_path, ROOT), 'measured_on_tree': PMC_TREE,
+                            'source': os.path.relpath(pmc_path, ROOT), 'measured_on_tree': pmc_tree,
                             'note': 'a prior PMC run of this workload, not this run'}
                 if 'planes' in pb:
                     prenet['warm_ms_split_planes'] = round(pb['planes'], 4)
